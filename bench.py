@@ -1,0 +1,97 @@
+"""Headline benchmark: whole-node sequences/sec, BERT-base seq_len 128, bf16, DP over RCCL.
+
+Contract (driver): ``python bench.py --gpus N --steps K --warmup W``; for N>1 launched by
+``torch.distributed.run`` with one rank per GPU. W untimed warmup steps, then EXACTLY K timed full
+training steps (forward + backward + bucketed all-reduce + fused Adam), bracketed by barrier +
+device synchronize on both sides; the max over ranks is reported. Rank 0 prints ONE JSON line.
+
+Data: synthetic full-length sequences of the reference's tensor shapes (offline box, no IMDB);
+weights: random-init bert-base-uncased architecture (no hub). Dropout on, as in training.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+from huggingface_sagemaker_tensorflow_distributed_amd import data as hdata  # noqa: E402
+from huggingface_sagemaker_tensorflow_distributed_amd.parallel import backend  # noqa: E402
+from huggingface_sagemaker_tensorflow_distributed_amd.train.runner import build  # noqa: E402
+from huggingface_sagemaker_tensorflow_distributed_amd.utils.args import build_parser  # noqa: E402
+
+METRIC = "sequences/sec (whole node) BERT-base seq128 at 1/2/4/8 MI355X"
+BASELINE_VALUE = None  # the reference publishes no number
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--batch_size", type=int, default=int(os.environ.get("HSD_BENCH_BATCH", "256")),
+                    help="per-GPU batch")
+    ap.add_argument("--seq_len", type=int, default=128)
+    ap.add_argument("--model", default="bert-base-uncased")
+    ap.add_argument("--bucket_mb", type=float, default=None)
+    ap.add_argument("--grad_dtype", default=None)
+    a = ap.parse_args()
+
+    world_env = int(os.environ.get("WORLD_SIZE", "1"))
+    if a.gpus != world_env:
+        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world_env}; using WORLD_SIZE", file=sys.stderr)
+    targs, _ = build_parser("train").parse_known_args(
+        ["--model_name_or_path", a.model, "--train_batch_size", str(a.batch_size), "--dtype", "bf16",
+         "--learning_rate", "5e-5", "--log_every", "0"]
+        + (["--bucket_mb", str(a.bucket_mb)] if a.bucket_mb else [])
+        + (["--grad_dtype", a.grad_dtype] if a.grad_dtype else []))
+    parts = build(targs, "train")
+    trainer, dev, world, rank = parts["trainer"], parts["device"], parts["world"], parts["rank"]
+    cfg = parts["model"].cfg
+    n_batches = 4
+    ds = hdata.synthetic_classification(a.batch_size * n_batches, a.seq_len, cfg.vocab_size,
+                                        seed=1234 + rank, full_length=True)
+    batches = []
+    for i in range(n_batches):
+        sl = slice(i * a.batch_size, (i + 1) * a.batch_size)
+        batches.append({"input_ids": torch.from_numpy(ds.input_ids[sl]).long().to(dev),
+                        "attention_mask": torch.from_numpy(ds.attention_mask[sl]).long().to(dev),
+                        "labels": torch.from_numpy(ds.labels[sl]).long().to(dev)})
+
+    def sync():
+        backend.barrier()
+        if dev.type == "cuda":
+            torch.cuda.synchronize(dev)
+
+    for i in range(a.warmup):
+        trainer.train_step([batches[i % n_batches]])
+    sync()
+    t0 = time.perf_counter()
+    for i in range(a.steps):
+        trainer.train_step([batches[i % n_batches]])
+    sync()
+    dt = time.perf_counter() - t0
+    t = torch.tensor([dt], dtype=torch.float64, device=dev)
+    if backend.is_distributed():
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+    dt = float(t.item())
+    ms = dt * 1e3 / a.steps
+    value = a.batch_size * world * a.steps / dt
+    if rank == 0:
+        print(json.dumps({
+            "metric": METRIC, "value": round(value, 2), "unit": "sequences/sec", "n_gpus": world,
+            "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
+            "dtype": "bf16", "data": "synthetic (random-init weights, full-length seq, dropout on)",
+            "config": {"model": a.model, "global_batch": a.batch_size * world, "per_gpu_batch": a.batch_size,
+                       "seq_len": a.seq_len, "parallelism": f"dp{world}",
+                       "ops": "torch-reference" if os.environ.get("HSD_OPS") == "torch" else "hip"},
+        }), flush=True)
+    backend.shutdown()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,107 @@
+// Shared device helpers for the gfx950 (CDNA4) kernels.
+//
+// * bf16 is carried as raw 16-bit words (`bf16_t`); conversions go through the compiler's
+//   f32->bf16 cast (v_cvt_pk_bf16_f32 on gfx950, RNE, NaN-preserving — MI355X_MICROARCH.md
+//   'Correctness boundaries').
+// * 16-byte vector types for every memory-bound kernel (cdna_hip_programming.md Guideline 13).
+// * wave64 reductions (never 32-lane warp idioms).
+// * the counter-based dropout hash, bit-identical to ops/rng.py.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_bf16.h>
+#include <stdint.h>
+
+namespace hsd {
+
+typedef uint16_t bf16_t;
+typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(16))) float f32x16;
+typedef __attribute__((ext_vector_type(8))) short bf16x8;   // MFMA A/B fragment (8 bf16)
+typedef __attribute__((ext_vector_type(4))) short bf16x4;
+typedef __attribute__((ext_vector_type(4))) uint32_t u32x4;
+typedef __attribute__((ext_vector_type(2))) uint32_t u32x2;
+
+constexpr int kWave = 64;
+
+__device__ __forceinline__ float bf2f(bf16_t v) { return __uint_as_float(((uint32_t)v) << 16); }
+
+__device__ __forceinline__ bf16_t f2bf(float f) {
+  __hip_bfloat16 b = __float2bfloat16(f);
+  return *reinterpret_cast<bf16_t*>(&b);
+}
+
+// two floats -> packed bf16x2 in one u32 (lo = a, hi = b)
+__device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
+  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+}
+__device__ __forceinline__ float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }
+__device__ __forceinline__ float hi_bf(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
+
+// ---- wave64 reductions ---------------------------------------------------------------
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+__device__ __forceinline__ float wave_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// ---- dropout hash (ops/rng.py) -------------------------------------------------------
+__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+  x ^= x >> 16;
+  x *= 0x7FEB352Du;
+  x ^= x >> 15;
+  x *= 0x846CA68Bu;
+  x ^= x >> 16;
+  return x;
+}
+// 32 random bits for element pair j: lo16 -> element 2j, hi16 -> element 2j+1
+__device__ __forceinline__ uint32_t dropout_bits(uint32_t pair, uint32_t seed_lo, uint32_t seed_hi) {
+  return mix32(mix32(pair ^ seed_lo) ^ seed_hi);
+}
+
+struct DropoutParams {
+  uint32_t seed_lo, seed_hi;
+  uint32_t thr;     // keep iff bits16 >= thr
+  float scale;      // 1/(1-p)
+  int enabled;
+};
+
+__host__ inline DropoutParams make_dropout(double p, uint64_t seed) {
+  DropoutParams d;
+  d.seed_lo = (uint32_t)(seed & 0xFFFFFFFFull);
+  d.seed_hi = (uint32_t)(seed >> 32);
+  double t = p * 65536.0;
+  d.thr = (uint32_t)(t + 0.5);
+  d.scale = p > 0.0 ? (float)(1.0 / (1.0 - p)) : 1.0f;
+  d.enabled = p > 0.0 ? 1 : 0;
+  return d;
+}
+
+// keep factor (0 or scale) for element `e` given its pair's bits
+__device__ __forceinline__ float keep_factor(uint32_t bits, int e, const DropoutParams& d) {
+  uint32_t b16 = (e & 1) ? (bits >> 16) : (bits & 0xFFFFu);
+  return b16 >= d.thr ? d.scale : 0.0f;
+}
+
+__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+__device__ __forceinline__ float gelu_erf_grad(float x) {
+  // d/dx [0.5 x (1+erf(x/√2))] = 0.5(1+erf(x/√2)) + x·φ(x)
+  const float kInvSqrt2Pi = 0.3989422804014327f;
+  return 0.5f * (1.0f + erff(x * 0.70710678118654752f)) + x * kInvSqrt2Pi * __expf(-0.5f * x * x);
+}
+
+}  // namespace hsd
+
+#define HSD_CHECK_LAUNCH()                                                                    \
+  do {                                                                                        \
+    hipError_t e__ = hipGetLastError();                                                       \
+    if (e__ != hipSuccess) {                                                                  \
+      fprintf(stderr, "HIP launch error %s at %s:%d\n", hipGetErrorString(e__), __FILE__, __LINE__); \
+      abort();                                                                                \
+    }                                                                                         \
+  } while (0)

@@ -1,0 +1,40 @@
+"""MI355X-native data-parallel transformer fine-tuning framework.
+
+Capabilities of ``philschmid/huggingface_sagemaker_tensorflow_distributed`` (a SageMaker/TF2/Horovod
+BERT fine-tuning job), re-designed for AMD Instinct MI355X (gfx950): PyTorch-ROCm framework layer,
+hand-written HIP/CDNA4 kernels for the BERT hot path, RCCL-over-xGMI bucketed all-reduce.
+
+The top level doubles as the ``hvd``-style facade the reference script programs against
+(``scripts/train.py:16-31,112-133``)::
+
+    import huggingface_sagemaker_tensorflow_distributed_amd as hvd
+    hvd.init(); hvd.rank(); hvd.size(); hvd.local_rank()
+"""
+from __future__ import annotations
+
+__version__ = "0.1.0"
+
+from .parallel.backend import barrier, init, is_distributed, local_rank, local_size, rank, shutdown, size
+
+
+def DistributedOptimizer(optimizer, store=None, bucket_mb=None):
+    """Horovod-compatible spelling: returns ``(optimizer, bucketer)`` wired to the flat store.
+
+    In this framework gradient averaging lives in :class:`parallel.GradBucketer` (all-reduce overlapped
+    with backward) and the ``1/N`` scale is folded into :class:`optim.FusedAdam`; this helper exists so
+    code written against ``hvd.DistributedOptimizer`` has a direct equivalent.
+    """
+    from .parallel.ddp import GradBucketer
+
+    store = store or optimizer.store
+    return optimizer, (GradBucketer(store, bucket_mb=bucket_mb) if size() > 1 else None)
+
+
+def broadcast_parameters(store, optimizer=None, root_rank: int = 0):
+    from .parallel.collectives import broadcast_parameters as _b
+
+    _b(store, optimizer, src=root_rank)
+
+
+__all__ = ["init", "rank", "size", "local_rank", "local_size", "barrier", "is_distributed", "shutdown",
+           "DistributedOptimizer", "broadcast_parameters", "__version__"]

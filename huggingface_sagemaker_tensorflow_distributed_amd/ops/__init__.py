@@ -1,0 +1,88 @@
+"""Op dispatch: one API, two implementations.
+
+* CUDA (=HIP on ROCm) tensors -> hand-written gfx950 kernels in ``csrc/kernels`` via
+  :mod:`.hip` (custom autograd Functions). If the compiled extension is missing on a GPU box this
+  raises — there is no silent eager fallback.
+* CPU tensors -> :mod:`.reference` (plain torch; also the numerics oracle for the kernel tests).
+
+``HSD_OPS=torch`` forces the reference path on GPU (only for A/B measurements of the kernels).
+"""
+from __future__ import annotations
+
+import os
+from typing import Optional
+
+import torch
+
+from . import reference as _ref
+
+_FORCE_TORCH = os.environ.get("HSD_OPS", "").lower() == "torch"
+
+
+def _hip(x: torch.Tensor) -> bool:
+    return x.is_cuda and not _FORCE_TORCH
+
+
+def _hipmod():
+    from . import hip  # noqa: WPS433 (lazy: imports the compiled extension)
+
+    return hip
+
+
+def key_mask_bias(attention_mask: Optional[torch.Tensor]):
+    return _ref.key_mask_bias(attention_mask)
+
+
+def dropout(x: torch.Tensor, p: float, seed: int):
+    if p <= 0.0:
+        return x
+    if _hip(x):
+        return _hipmod().dropout(x, p, seed)
+    return _ref.dropout(x, p, seed, True)
+
+
+def embed_ln(input_ids, position_ids, token_type_ids, word_w, pos_w, type_w, ln_w, ln_b, eps, p, seed):
+    if _hip(word_w):
+        return _hipmod().embed_ln(input_ids, position_ids, token_type_ids, word_w, pos_w, type_w, ln_w, ln_b,
+                                  eps, p, seed)
+    return _ref.embed_ln(input_ids, position_ids, token_type_ids, word_w, pos_w, type_w, ln_w, ln_b, eps, p, seed,
+                         p > 0)
+
+
+def linear(x, w, b):
+    if _hip(x):
+        return _hipmod().linear(x, w, b)
+    return _ref.linear(x, w, b)
+
+
+def linear_gelu(x, w, b):
+    if _hip(x):
+        return _hipmod().linear_gelu(x, w, b)
+    return _ref.linear_gelu(x, w, b)
+
+
+def layer_norm(x, w, b, eps):
+    if _hip(x):
+        return _hipmod().layer_norm(x, w, b, eps)
+    return _ref.layer_norm(x, w, b, eps)
+
+
+def dense_residual_ln(x, w, b, residual, ln_w, ln_b, eps, p, seed):
+    """``LN(dropout(x Wᵀ + b) + residual)`` — the post-LN block tail."""
+    if _hip(x):
+        return _hipmod().dense_residual_ln(x, w, b, residual, ln_w, ln_b, eps, p, seed)
+    return _ref.layer_norm(_ref.linear_dropout_residual(x, w, b, residual, p, seed, p > 0), ln_w, ln_b, eps)
+
+
+def attention(qkv, mask_bias, batch, seq, heads, p, seed):
+    if _hip(qkv):
+        return _hipmod().attention(qkv, mask_bias, batch, seq, heads, p, seed)
+    return _ref.attention(qkv, mask_bias, batch, seq, heads, p, seed, p > 0)
+
+
+def cross_entropy(logits, labels):
+    return _ref.cross_entropy(logits, labels)
+
+
+def accuracy_count(logits, labels):
+    return _ref.accuracy_count(logits, labels)

@@ -1,0 +1,89 @@
+"""Plain-PyTorch reference implementations of every fused op.
+
+These are (a) the CPU execution path (tests, gloo plumbing runs) and (b) the numerics oracle the
+HIP kernels are tested against. Math follows HF PyTorch BERT
+([dep: transformers/models/bert/modeling_bert.py]) which is what the reference's TF model computes
+(``scripts/train.py:117``): post-LN residual blocks, exact-erf GELU, additive key-padding mask.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import torch
+import torch.nn.functional as F
+
+from .rng import keep_mask
+
+
+def dropout(x: torch.Tensor, p: float, seed: int, training: bool = True) -> torch.Tensor:
+    if not training or p <= 0.0:
+        return x
+    m = keep_mask(seed, x.numel(), p, device=x.device).view_as(x)
+    return x * m.to(x.dtype) * (1.0 / (1.0 - p))
+
+
+def embed_ln(input_ids, position_ids, token_type_ids, word_w, pos_w, type_w, ln_w, ln_b,
+             eps: float, p: float, seed: int, training: bool) -> torch.Tensor:
+    """``dropout(LN(word[ids] + pos[pos_ids] + type[tt]))`` (modeling_bert.py BertEmbeddings)."""
+    h = F.embedding(input_ids, word_w) + F.embedding(position_ids, pos_w)
+    if type_w is not None:
+        h = h + F.embedding(token_type_ids, type_w)
+    h = F.layer_norm(h.float(), (h.shape[-1],), ln_w.float(), ln_b.float(), eps).to(word_w.dtype)
+    return dropout(h, p, seed, training)
+
+
+def linear(x, w, b):
+    return F.linear(x, w, b)
+
+
+def gelu(x):
+    return F.gelu(x.float(), approximate="none").to(x.dtype)
+
+
+def linear_gelu(x, w, b):
+    return gelu(F.linear(x, w, b))
+
+
+def linear_dropout_residual(x, w, b, residual, p: float, seed: int, training: bool):
+    return dropout(F.linear(x, w, b), p, seed, training) + residual
+
+
+def layer_norm(x, w, b, eps: float):
+    return F.layer_norm(x.float(), (x.shape[-1],), w.float(), b.float(), eps).to(x.dtype)
+
+
+def key_mask_bias(attention_mask: Optional[torch.Tensor], dtype=torch.float32) -> Optional[torch.Tensor]:
+    """[B,S] 0/1 mask -> additive fp32 bias [B,S] (0 keep, -inf-like mask)."""
+    if attention_mask is None:
+        return None
+    return (1.0 - attention_mask.to(torch.float32)) * torch.finfo(torch.float32).min
+
+
+def attention(qkv: torch.Tensor, mask_bias: Optional[torch.Tensor], batch: int, seq: int, heads: int,
+              p: float, seed: int, training: bool) -> torch.Tensor:
+    """Self-attention over a packed ``[B*S, 3H]`` QKV tensor -> ``[B*S, H]`` context.
+
+    Dropout on the probabilities indexes element ``((b*heads + h)*S + i)*S + j``.
+    """
+    H3 = qkv.shape[-1]
+    H = H3 // 3
+    d = H // heads
+    x = qkv.view(batch, seq, 3, heads, d).permute(2, 0, 3, 1, 4).float()  # [3,B,h,S,d]
+    q, k, v = x[0], x[1], x[2]
+    s = torch.matmul(q, k.transpose(-1, -2)) * (1.0 / math.sqrt(d))
+    if mask_bias is not None:
+        s = s + mask_bias.view(batch, 1, 1, seq).float()
+    pr = torch.softmax(s, dim=-1)
+    pr = dropout(pr, p, seed, training)
+    o = torch.matmul(pr, v)  # [B,h,S,d]
+    return o.permute(0, 2, 1, 3).reshape(batch * seq, H).to(qkv.dtype)
+
+
+def cross_entropy(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+    """SparseCategoricalCrossentropy(from_logits=True), SUM_OVER_BATCH_SIZE (``scripts/train.py:118``)."""
+    return F.cross_entropy(logits.float(), labels.long())
+
+
+def accuracy_count(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
+    return (logits.argmax(dim=-1) == labels.long()).sum()

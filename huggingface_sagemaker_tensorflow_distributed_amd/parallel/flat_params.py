@@ -1,0 +1,131 @@
+"""Flat parameter / gradient / optimizer-state storage.
+
+MI355X-first memory layout: every parameter of the model lives inside ONE flat fp32 master buffer,
+ONE flat compute-dtype (bf16) buffer whose views the kernels read, and ONE flat gradient buffer
+(``main_grad`` views) that the backward kernels write directly (no per-parameter allocation, no
+``AccumulateGrad`` pass, no bucket pack copy: a gradient bucket is a contiguous slice). The
+optimizer is then a single launch over flat buffers, and broadcast/all-reduce are single
+collectives over slices — the replacement for Horovod's 64 MiB fusion buffer.
+
+Layout order is *reverse* declaration order (== approximately backward order), so gradient buckets
+complete front-to-back while backward is still running.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass
+from typing import Dict, List, Optional
+
+import torch
+import torch.nn as nn
+
+ALIGN = 64  # elements; keeps every view 128-B (bf16) / 256-B (fp32) aligned for 16-B vector IO
+
+
+def _round_up(x: int, a: int) -> int:
+    return (x + a - 1) // a * a
+
+
+@dataclass
+class Segment:
+    name: str
+    offset: int
+    numel: int
+    shape: tuple
+    decay: bool
+
+
+def _no_decay(name: str) -> bool:
+    leaf = name.rsplit(".", 1)[-1]
+    toks = leaf.split("_")
+    return leaf.endswith("bias") or any(t in ("ln", "ln1", "ln2") for t in toks)
+
+
+class FlatParamStore:
+    def __init__(self, model: nn.Module, device: torch.device, compute_dtype: torch.dtype = torch.float32,
+                 grad_dtype: torch.dtype = torch.float32):
+        self.device = torch.device(device)
+        self.compute_dtype = compute_dtype
+        self.grad_dtype = grad_dtype
+        named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
+        named = list(reversed(named))
+        self.params: List[nn.Parameter] = [p for _, p in named]
+        self.names: List[str] = [n for n, _ in named]
+        self.segments: List[Segment] = []
+        off = 0
+        for n, p in named:
+            self.segments.append(Segment(n, off, p.numel(), tuple(p.shape), not _no_decay(n)))
+            off = _round_up(off + p.numel(), ALIGN)
+        self.numel = _round_up(off, 1024)
+        # ---- buffers
+        self.master = torch.zeros(self.numel, dtype=torch.float32, device=self.device)
+        with torch.no_grad():
+            for seg, p in zip(self.segments, self.params):
+                self.master[seg.offset:seg.offset + seg.numel].copy_(p.detach().reshape(-1).to(torch.float32))
+        if compute_dtype == torch.float32:
+            self.compute = self.master
+        else:
+            self.compute = self.master.to(compute_dtype)
+        self.grad = torch.zeros(self.numel, dtype=grad_dtype, device=self.device)
+        # decay mask per 64-element block (optimizer segment table)
+        for seg, p in zip(self.segments, self.params):
+            p.data = self.compute[seg.offset:seg.offset + seg.numel].view(seg.shape)
+            p.main_grad = self.grad[seg.offset:seg.offset + seg.numel].view(seg.shape)
+            p.grad = None
+        self._index: Dict[int, int] = {id(p): i for i, p in enumerate(self.params)}
+        # gradient-ready notification: HIP backward kernels write main_grad directly and call
+        # p._hsd_ready(); torch-autograd gradients (CPU path, small torch-op heads) are folded into
+        # main_grad by a post-accumulate hook first.
+        self.ready_callback = None
+        self._hooks = []
+        for i, p in enumerate(self.params):
+            p._hsd_ready = self._make_ready(i)
+            self._hooks.append(p.register_post_accumulate_grad_hook(self._make_accum_hook(i)))
+
+    def _make_ready(self, i: int):
+        def ready():
+            cb = self.ready_callback
+            if cb is not None:
+                cb(i)
+        return ready
+
+    def _make_accum_hook(self, i: int):
+        def hook(p):
+            if p.grad is not None:
+                p.main_grad.add_(p.grad.to(p.main_grad.dtype))
+                p.grad = None
+            p._hsd_ready()
+        return hook
+
+    # ----------------------------------------------------------------------------------
+    def index_of(self, p: torch.Tensor) -> int:
+        return self._index[id(p)]
+
+    def segment_of(self, p: torch.Tensor) -> Segment:
+        return self.segments[self._index[id(p)]]
+
+    def zero_grad(self) -> None:
+        self.grad.zero_()
+
+    @torch.no_grad()
+    def sync_compute_from_master(self) -> None:
+        if self.compute is not self.master:
+            self.compute.copy_(self.master)
+
+    def decay_block_mask(self, block: int) -> torch.Tensor:
+        """uint8 per ``block`` elements: 1 = apply weight decay. Segments are ALIGN-aligned."""
+        assert block % ALIGN == 0 or ALIGN % block == 0
+        nb = self.numel // block
+        m = torch.zeros(nb, dtype=torch.uint8)
+        for s in self.segments:
+            if s.decay:
+                m[s.offset // block: (s.offset + s.numel + block - 1) // block] = 1
+        return m.to(self.device)
+
+    def state_dict(self) -> dict:
+        return {"master": self.master.detach().cpu(), "names": list(self.names),
+                "offsets": [s.offset for s in self.segments]}
+
+    @torch.no_grad()
+    def load_master(self, master: torch.Tensor) -> None:
+        self.master.copy_(master.to(self.device))
+        self.sync_compute_from_master()

@@ -1,0 +1,152 @@
+"""End-to-end entry logic shared by ``scripts/train.py`` and ``scripts/singe_node_train.py``.
+
+Two batch/LR semantics, exactly as the two reference scripts differ:
+
+* ``mode="train"`` (Horovod/SMDDP, ``scripts/train.py``): ``--train_batch_size`` is PER RANK,
+  learning rate is scaled ×N (``scripts/train.py:112``), ``train_results.txt`` gets a
+  ``train_runtime`` line (``:165``).
+* ``mode="single_node"`` (MirroredStrategy, ``scripts/singe_node_train.py``): ``--train_batch_size``
+  is the GLOBAL batch split across replicas, no LR scaling (``:78``), no runtime line (``:96-101``).
+
+Reference fixes applied: Q3 data sharded by rank, Q4 params broadcast before
+step 1, Q5 rank-0-only save + barrier, Q6 global metrics.
+"""
+from __future__ import annotations
+
+import logging
+import os
+import time
+from typing import List, Optional, Sequence
+
+import torch
+
+from .. import data as hdata
+from ..models import from_pretrained, save_pretrained
+from ..optim import FusedAdam
+from ..parallel import FlatParamStore, GradBucketer, ShardSampler, backend, broadcast_parameters
+from ..utils.args import parse_args
+from ..utils.env import is_sagemaker_dp_enabled
+from ..utils.logging import setup_logging
+from ..utils.results_io import write_eval_results, write_train_results
+from .callbacks import FaultInjection, ModelCheckpoint, load_checkpoint, master_state_dict
+from .trainer import Trainer
+
+logger = logging.getLogger("__main__")
+
+_DTYPES = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp8": torch.bfloat16}
+
+
+def _datasets(args, cfg, tokenizer, max_len: int):
+    n_train = args.num_train_examples
+    n_eval = args.num_eval_examples
+    if args.dataset == "synthetic":
+        tr = hdata.synthetic_classification(n_train or 2048, max_len, cfg.vocab_size, seed=args.seed,
+                                            num_labels=cfg.num_labels)
+        te = hdata.synthetic_classification(n_eval or 512, max_len, cfg.vocab_size, seed=args.seed + 1,
+                                            num_labels=cfg.num_labels)
+        return tr, te
+    texts, labels = hdata.load_text_split(args.dataset, "train", args.dataset_dir)
+    if n_train:
+        texts, labels = texts[:n_train], labels[:n_train]
+    tr = hdata.tokenize_dataset(tokenizer, texts, labels, max_len)
+    texts, labels = hdata.load_text_split(args.dataset, "test", args.dataset_dir)
+    if n_eval:
+        texts, labels = texts[:n_eval], labels[:n_eval]
+    te = hdata.tokenize_dataset(tokenizer, texts, labels, max_len)
+    return tr, te
+
+
+def build(args, mode: str):
+    """Construct model/store/optimizer/bucketer/trainer for ``args``. Returns a dict of parts."""
+    st = backend.init(device=args.device, timeout_s=args.dist_timeout)
+    dev = st.device
+    world, rank = st.world_size, st.rank
+    on_gpu = dev.type == "cuda"
+    dtype_name = args.dtype or ("bf16" if on_gpu else "fp32")
+    compute_dtype = _DTYPES[dtype_name]
+    grad_dtype = {"fp32": torch.float32, "bf16": torch.bfloat16}[args.grad_dtype or "fp32"]
+    torch.manual_seed(args.seed)
+
+    model = from_pretrained(args.model_name_or_path or "bert-base-uncased", num_labels=args.num_labels,
+                            seed=args.seed)
+    model.to(dev)
+    model.rng.base_seed = args.seed
+    model.rng.rank = rank
+    store = FlatParamStore(model, dev, compute_dtype=compute_dtype, grad_dtype=grad_dtype)
+    base_lr = float(args.learning_rate)
+    lr = base_lr * world if mode == "train" else base_lr  # scripts/train.py:112 vs singe_node_train.py:78
+    opt = FusedAdam(store, lr=lr, eps=args.adam_epsilon, eps_mode=args.adam_eps_mode,
+                    weight_decay=args.weight_decay if args.optimizer == "adamw" else 0.0)
+    bucketer = GradBucketer(store, bucket_mb=args.bucket_mb) if world > 1 else None
+    trainer = Trainer(model, store, opt, bucketer, dev, grad_accum=args.gradient_accumulation_steps,
+                      check_sync=args.check_sync, log_every=args.log_every, step_watchdog=args.step_watchdog)
+    if args.resume_from:
+        load_checkpoint(args.resume_from, trainer)
+    broadcast_parameters(store, opt if args.resume_from else None)
+    return {"model": model, "store": store, "optimizer": opt, "bucketer": bucketer, "trainer": trainer,
+            "device": dev, "world": world, "rank": rank, "lr": lr, "dtype": dtype_name}
+
+
+def run(argv: Optional[Sequence[str]] = None, mode: str = "train") -> dict:
+    args, _unknown = parse_args(argv, "train" if mode == "train" else "single_node")
+    env_rank = int(os.environ.get("RANK", "0"))
+    setup_logging(env_rank)
+    if mode == "train":
+        logger.info(args)  # scripts/train.py:63
+        if is_sagemaker_dp_enabled():
+            logger.info("SMDDP requested via SM_FRAMEWORK_PARAMS: served by the RCCL data-parallel engine")
+    parts = build(args, mode)
+    model, trainer, dev = parts["model"], parts["trainer"], parts["device"]
+    world, rank = parts["world"], parts["rank"]
+    cfg = model.cfg
+
+    tokenizer = hdata.load_tokenizer(args.model_name_or_path, cfg.vocab_size, cfg.model_max_length)
+    max_len = args.max_seq_length or min(tokenizer.model_max_length, cfg.max_position_embeddings)
+    train_ds, test_ds = _datasets(args, cfg, tokenizer, max_len)
+
+    if mode == "train":
+        per_rank_train = args.train_batch_size
+    else:  # MirroredStrategy: global batch split over replicas
+        if args.train_batch_size % world:
+            raise ValueError(f"global train_batch_size {args.train_batch_size} not divisible by {world} replicas")
+        per_rank_train = args.train_batch_size // world
+    per_rank_eval = args.eval_batch_size if mode == "train" else max(1, args.eval_batch_size // world)
+
+    train_loader = hdata.BatchLoader(train_ds, ShardSampler(len(train_ds), rank, world, shuffle=False, seed=args.seed,
+                                                             batch_size=per_rank_train), dev)
+    test_loader = hdata.BatchLoader(test_ds, ShardSampler(len(test_ds), rank, world, shuffle=False, seed=args.seed,
+                                                           drop_last=True, batch_size=per_rank_eval), dev)
+    out = {"args": args}
+    callbacks = [FaultInjection()]
+    if args.save_every_epoch:
+        callbacks.append(ModelCheckpoint(os.path.join(args.model_dir, "checkpoint-{epoch}")))
+
+    if args.do_train:
+        if mode == "train":
+            logger.info("*** Train ***")
+        start = time.time()
+        hist = trainer.fit(train_loader, args.epochs, callbacks=callbacks, verbose=(rank == 0),
+                           max_steps=args.max_steps)
+        train_runtime = {"train_runtime": round(time.time() - start, 4)}
+        if mode == "train":
+            logger.info(f"train_runtime = {train_runtime}\n")
+        else:
+            logger.info("*** Train ***")  # singe_node_train.py logs it AFTER fit (:92)
+        if rank == 0:
+            write_train_results(args.output_data_dir, hist.history, train_runtime if mode == "train" else None)
+        out["history"] = hist.history
+        out["train_runtime"] = train_runtime
+
+    if args.do_eval:
+        logger.info("*** Evaluate ***")
+        result = trainer.evaluate(test_loader)
+        if rank == 0:
+            write_eval_results(args.output_data_dir, result)
+        out["eval"] = result
+
+    # Q5: rank-0-only save, then barrier
+    if rank == 0:
+        save_pretrained(model, args.model_dir, state_dict=master_state_dict(model, parts["store"]))
+        tokenizer.save_pretrained(args.model_dir)
+    backend.barrier()
+    return out

@@ -1,0 +1,174 @@
+"""Keras-equivalent ``fit`` / ``evaluate`` loop (reference L6: ``model.compile/fit/evaluate``,
+``scripts/train.py:123,145,170``).
+
+One training step (SURVEY.md §3.3 'Our step'):
+
+1. new dropout seeds for the step, gradient buffer zeroed (one memset of the flat buffer);
+2. forward through the fused HIP kernels, ``SparseCategoricalCrossentropy(from_logits)`` mean loss;
+3. backward: kernels write parameter gradients straight into the flat ``main_grad`` buffer and each
+   completed bucket starts its RCCL all-reduce while backward continues;
+4. wait for the buckets, one fused-Adam launch (``1/N`` folded in) that also refreshes the bf16
+   weights.
+
+Metrics stay on the device (no host sync per step) and are all-reduced at epoch end so the
+reported history is global.
+"""
+from __future__ import annotations
+
+import logging
+import math
+import time
+from dataclasses import dataclass, field
+from typing import Callable, Dict, Iterable, List, Optional
+
+import torch
+
+from .. import ops
+from ..parallel import backend
+from ..parallel.collectives import allreduce_sums, params_in_sync
+
+logger = logging.getLogger(__name__)
+
+
+@dataclass
+class History:
+    history: Dict[str, List[float]] = field(default_factory=dict)
+    epoch: List[int] = field(default_factory=list)
+
+    def append(self, epoch: int, logs: Dict[str, float]) -> None:
+        self.epoch.append(epoch)
+        for k, v in logs.items():
+            self.history.setdefault(k, []).append(v)
+
+    def __repr__(self) -> str:  # mirrors the keras object repr that the reference logs
+        return f"<History epochs={len(self.epoch)} keys={list(self.history)}>"
+
+
+class _Meter:
+    """Device-side running sums: loss·n, correct, n."""
+
+    def __init__(self, device):
+        self.t = torch.zeros(3, dtype=torch.float64, device=device)
+
+    def update(self, loss: torch.Tensor, logits: torch.Tensor, labels: torch.Tensor) -> None:
+        n = labels.numel() if logits.dim() == 2 else labels.ne(-100).sum()
+        if logits.dim() == 2 and logits.shape[0] == labels.numel():
+            correct = ops.accuracy_count(logits, labels)
+        else:
+            correct = torch.zeros((), device=logits.device)
+        upd = torch.stack([loss.detach().double() * n, correct.double(), torch.as_tensor(n, device=self.t.device).double()])
+        self.t += upd
+
+    def result(self, global_: bool = True) -> Dict[str, float]:
+        vals = self.t.tolist()
+        if global_:
+            vals = allreduce_sums(vals, self.t.device)
+        loss_sum, correct, n = vals
+        n = max(n, 1.0)
+        return {"loss": loss_sum / n, "sparse_categorical_accuracy": correct / n}
+
+
+class Trainer:
+    def __init__(self, model, store, optimizer, bucketer=None, device=None, grad_accum: int = 1,
+                 check_sync: int = 0, log_every: int = 50, step_watchdog: float = 0.0):
+        self.model = model
+        self.store = store
+        self.optimizer = optimizer
+        self.bucketer = bucketer
+        self.device = torch.device(device) if device is not None else store.device
+        self.grad_accum = max(1, int(grad_accum))
+        self.check_sync = int(check_sync)
+        self.log_every = int(log_every)
+        self.step_watchdog = float(step_watchdog)
+        self.global_step = 0
+        self.world = backend.size()
+        self.rank = backend.rank()
+
+    # -------------------------------------------------------------------------- step
+    def _forward_loss(self, batch):
+        loss, logits = self.model(batch["input_ids"], attention_mask=batch["attention_mask"],
+                                  labels=batch["labels"])
+        return loss, logits
+
+    def train_step(self, micro_batches: List[Dict[str, torch.Tensor]], meter: Optional[_Meter] = None) -> torch.Tensor:
+        """One optimizer step over ``len(micro_batches)`` accumulation micro-steps."""
+        self.model.train()
+        self.model.rng.new_step(self.global_step)
+        self.store.zero_grad()
+        if self.bucketer is not None:
+            self.bucketer.begin()
+        k = len(micro_batches)
+        loss = None
+        for i, mb in enumerate(micro_batches):
+            last = i == k - 1
+            if self.bucketer is not None and not last:
+                with self.bucketer.no_sync():
+                    loss, logits = self._forward_loss(mb)
+                    loss.backward()
+            else:
+                loss, logits = self._forward_loss(mb)
+                loss.backward()
+            if meter is not None:
+                meter.update(loss, logits, mb["labels"])
+        if self.bucketer is not None:
+            self.bucketer.finish()
+        self.optimizer.step(grad_scale=1.0 / (self.world * k))
+        self.global_step += 1
+        if self.check_sync and self.global_step % self.check_sync == 0:
+            if not params_in_sync(self.store):
+                raise RuntimeError(f"ranks diverged at step {self.global_step} (--check_sync)")
+        return loss
+
+    # -------------------------------------------------------------------------- fit
+    def fit(self, loader, epochs: int, callbacks: Iterable = (), verbose: bool = True,
+            max_steps: Optional[int] = None) -> History:
+        hist = History()
+        callbacks = list(callbacks)
+        for cb in callbacks:
+            cb.on_train_begin(self)
+        for epoch in range(epochs):
+            if hasattr(loader, "sampler"):
+                loader.sampler.set_epoch(epoch)
+            meter = _Meter(self.device)
+            nsteps = len(loader) // self.grad_accum
+            if max_steps:
+                nsteps = min(nsteps, max_steps)
+            t0 = time.time()
+            it = iter(loader)
+            for step in range(nsteps):
+                mbs = [next(it) for _ in range(self.grad_accum)]
+                ts = time.time()
+                self.train_step(mbs, meter)
+                if self.step_watchdog and time.time() - ts > self.step_watchdog:
+                    raise RuntimeError(f"step {self.global_step} exceeded watchdog {self.step_watchdog}s")
+                if verbose and self.rank == 0 and self.log_every and (step + 1) % self.log_every == 0:
+                    r = meter.result(global_=False)
+                    logger.info("epoch %d step %d/%d - loss: %.4f - sparse_categorical_accuracy: %.4f - %.1f ms/step",
+                                epoch + 1, step + 1, nsteps, r["loss"], r["sparse_categorical_accuracy"],
+                                (time.time() - t0) * 1e3 / (step + 1))
+                for cb in callbacks:
+                    cb.on_batch_end(self, step)
+            for _ in it:  # drain the prefetch thread
+                pass
+            logs = meter.result(global_=True)
+            hist.append(epoch, logs)
+            if verbose and self.rank == 0:
+                logger.info("Epoch %d/%d - %.1fs - loss: %.4f - sparse_categorical_accuracy: %.4f", epoch + 1, epochs,
+                            time.time() - t0, logs["loss"], logs["sparse_categorical_accuracy"])
+            for cb in callbacks:
+                cb.on_epoch_end(self, epoch, logs)
+        for cb in callbacks:
+            cb.on_train_end(self)
+        return hist
+
+    # -------------------------------------------------------------------------- evaluate
+    @torch.no_grad()
+    def evaluate(self, loader, max_steps: Optional[int] = None) -> Dict[str, float]:
+        self.model.eval()
+        meter = _Meter(self.device)
+        for i, b in enumerate(loader):
+            if max_steps and i >= max_steps:
+                continue  # drain
+            loss, logits = self._forward_loss(b)
+            meter.update(loss, logits, b["labels"])
+        return meter.result(global_=True)
