@@ -1,0 +1,274 @@
+// Embedding gather + add + LayerNorm + dropout, and its backward.
+//
+// forward : e = word[id] + pos[pos_id] + type[type_id];  out = dropout(LN(e))   -> saves mean/rstd
+// backward: recompute e by re-gathering (cheaper than storing it), LN backward, then
+//           word_grad[id] += de      (fp32 atomics, 256-B-contiguous per wave instruction)
+//           pos_grad / type_grad     (reduced in registers per block first: each block owns ONE
+//                                     position and walks the batch, so the position row gets one
+//                                     atomic per block and the type rows are not hammered by
+//                                     every token — MI355X_MICROARCH.md 'Global float atomics',
+//                                     one-row contention is 14x slower)
+//           dgamma / dbeta           (register partials, one atomic per column per block)
+#include "common.h"
+
+namespace hsd {
+
+template <int NCH>
+__device__ __forceinline__ void gather_row(float (&e)[NCH][4], const bf16_t* __restrict__ w, const bf16_t* __restrict__ p,
+                                           const bf16_t* __restrict__ t, int64_t wid_, int64_t pid, int64_t tid, int H,
+                                           int lane) {
+  const int nq = H >> 2;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    int c = lane + 64 * i;
+    if (c < nq) {
+      u32x2 a = *reinterpret_cast<const u32x2*>(w + wid_ * H + 4 * c);
+      u32x2 b = *reinterpret_cast<const u32x2*>(p + pid * H + 4 * c);
+      e[i][0] = lo_bf(a.x) + lo_bf(b.x);
+      e[i][1] = hi_bf(a.x) + hi_bf(b.x);
+      e[i][2] = lo_bf(a.y) + lo_bf(b.y);
+      e[i][3] = hi_bf(a.y) + hi_bf(b.y);
+      if (t) {
+        u32x2 d = *reinterpret_cast<const u32x2*>(t + tid * H + 4 * c);
+        e[i][0] += lo_bf(d.x); e[i][1] += hi_bf(d.x); e[i][2] += lo_bf(d.y); e[i][3] += hi_bf(d.y);
+      }
+    } else {
+      e[i][0] = e[i][1] = e[i][2] = e[i][3] = 0.f;
+    }
+  }
+}
+
+template <int NCH>
+__global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restrict__ ids, const int64_t* __restrict__ pos_ids,
+                                                        const int64_t* __restrict__ type_ids, const bf16_t* __restrict__ word,
+                                                        const bf16_t* __restrict__ pos, const bf16_t* __restrict__ type,
+                                                        const bf16_t* __restrict__ gamma, const bf16_t* __restrict__ beta,
+                                                        bf16_t* __restrict__ out, float* __restrict__ mean_out,
+                                                        float* __restrict__ rstd_out, int rows, int H, float eps,
+                                                        DropoutParams dp) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nq = H >> 2;
+  float e[NCH][4];
+  gather_row<NCH>(e, word, pos, type, ids[row], pos_ids[row], type ? type_ids[row] : 0, H, lane);
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) s += e[i][0] + e[i][1] + e[i][2] + e[i][3];
+  const float mean = wave_sum(s) / (float)H;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i)
+    if (lane + 64 * i < nq)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { float d = e[i][k] - mean; ss += d * d; }
+  const float rstd = rsqrtf(wave_sum(ss) / (float)H + eps);
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    int c = lane + 64 * i;
+    if (c < nq) {
+      size_t off = (size_t)row * H + 4 * c;
+      u32x2 gw = *reinterpret_cast<const u32x2*>(gamma + 4 * c);
+      u32x2 bw = *reinterpret_cast<const u32x2*>(beta + 4 * c);
+      float o[4] = {(e[i][0] - mean) * rstd * lo_bf(gw.x) + lo_bf(bw.x), (e[i][1] - mean) * rstd * hi_bf(gw.x) + hi_bf(bw.x),
+                    (e[i][2] - mean) * rstd * lo_bf(gw.y) + lo_bf(bw.y), (e[i][3] - mean) * rstd * hi_bf(gw.y) + hi_bf(bw.y)};
+      if (dp.enabled) {
+        // dropout is applied to the bf16-rounded LN output (matches the reference op order)
+        uint32_t pair0 = (uint32_t)(off >> 1);
+        uint32_t b0 = dropout_bits(pair0, dp.seed_lo, dp.seed_hi);
+        uint32_t b1 = dropout_bits(pair0 + 1, dp.seed_lo, dp.seed_hi);
+        o[0] = bf2f(f2bf(o[0])) * keep_factor(b0, 0, dp);
+        o[1] = bf2f(f2bf(o[1])) * keep_factor(b0, 1, dp);
+        o[2] = bf2f(f2bf(o[2])) * keep_factor(b1, 0, dp);
+        o[3] = bf2f(f2bf(o[3])) * keep_factor(b1, 1, dp);
+      }
+      u32x2 w;
+      w.x = pack_bf2(o[0], o[1]);
+      w.y = pack_bf2(o[2], o[3]);
+      *reinterpret_cast<u32x2*>(out + off) = w;
+    }
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// grid: (S positions) x (batch chunks). Block = 4 waves; wave w handles batch rows b = chunk*bpc + w, +4, ...
+template <int NCH>
+__global__ __launch_bounds__(256) void embed_bwd_kernel(const bf16_t* __restrict__ dout, const int64_t* __restrict__ ids,
+                                                        const int64_t* __restrict__ pos_ids, const int64_t* __restrict__ type_ids,
+                                                        const bf16_t* __restrict__ word, const bf16_t* __restrict__ pos,
+                                                        const bf16_t* __restrict__ type, const bf16_t* __restrict__ gamma,
+                                                        const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+                                                        float* __restrict__ gword, float* __restrict__ gpos,
+                                                        float* __restrict__ gtype, float* __restrict__ ggamma,
+                                                        float* __restrict__ gbeta, int B, int S, int H, int bpc,
+                                                        int pos_is_arange, DropoutParams dp) {
+  __shared__ float red[4][4][256];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int s = blockIdx.x;
+  const int b0 = blockIdx.y * bpc;
+  const int b1 = min(B, b0 + bpc);
+  const int nq = H >> 2;
+  float gam[NCH][4], acc_g[NCH][4], acc_b[NCH][4], acc_p[NCH][4], acc_t0[NCH][4];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    int c = lane + 64 * i;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc_g[i][k] = acc_b[i][k] = acc_p[i][k] = acc_t0[i][k] = gam[i][k] = 0.f;
+    if (c < nq) {
+      u32x2 gw = *reinterpret_cast<const u32x2*>(gamma + 4 * c);
+      gam[i][0] = lo_bf(gw.x); gam[i][1] = hi_bf(gw.x); gam[i][2] = lo_bf(gw.y); gam[i][3] = hi_bf(gw.y);
+    }
+  }
+  for (int b = b0 + wid; b < b1; b += 4) {
+    const int row = b * S + s;
+    const int64_t id = ids[row], pid = pos_ids[row];
+    const int64_t tid = type ? type_ids[row] : 0;
+    float e[NCH][4];
+    gather_row<NCH>(e, word, pos, type, id, pid, tid, H, lane);
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float g[NCH][4], xh[NCH][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      int c = lane + 64 * i;
+      if (c < nq) {
+        size_t off = (size_t)row * H + 4 * c;
+        u32x2 dw = *reinterpret_cast<const u32x2*>(dout + off);
+        float d[4] = {lo_bf(dw.x), hi_bf(dw.x), lo_bf(dw.y), hi_bf(dw.y)};
+        if (dp.enabled) {
+          uint32_t pair0 = (uint32_t)(off >> 1);
+          uint32_t bb0 = dropout_bits(pair0, dp.seed_lo, dp.seed_hi);
+          uint32_t bb1 = dropout_bits(pair0 + 1, dp.seed_lo, dp.seed_hi);
+          d[0] *= keep_factor(bb0, 0, dp);
+          d[1] *= keep_factor(bb0, 1, dp);
+          d[2] *= keep_factor(bb1, 0, dp);
+          d[3] *= keep_factor(bb1, 1, dp);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          xh[i][k] = (e[i][k] - mean) * rstd;
+          g[i][k] = d[k] * gam[i][k];
+          s1 += g[i][k];
+          s2 += g[i][k] * xh[i][k];
+          acc_g[i][k] += d[k] * xh[i][k];
+          acc_b[i][k] += d[k];
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) g[i][k] = xh[i][k] = 0.f;
+      }
+    }
+    s1 = wave_sum(s1) / (float)H;
+    s2 = wave_sum(s2) / (float)H;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      int c = lane + 64 * i;
+      if (c < nq) {
+        float de[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) de[k] = rstd * (g[i][k] - s1 - xh[i][k] * s2);
+        float* gw = gword + id * H + 4 * c;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) atomicAdd(gw + k, de[k]);
+        if (pos_is_arange) {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) acc_p[i][k] += de[k];
+        } else {
+          float* gp = gpos + pid * H + 4 * c;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) atomicAdd(gp + k, de[k]);
+        }
+        if (gtype) {
+          if (tid == 0) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) acc_t0[i][k] += de[k];
+          } else {
+            float* gt = gtype + tid * H + 4 * c;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) atomicAdd(gt + k, de[k]);
+          }
+        }
+      }
+    }
+  }
+  // block reduction of the 4 register partials (gamma, beta, pos row s, type row 0)
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    int c = lane + 64 * i;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      red[wid][0][lane * 4 + k] = acc_g[i][k];
+      red[wid][1][lane * 4 + k] = acc_b[i][k];
+      red[wid][2][lane * 4 + k] = acc_p[i][k];
+      red[wid][3][lane * 4 + k] = acc_t0[i][k];
+    }
+    __syncthreads();
+    if (c < nq) {
+      float* dst = wid == 0 ? ggamma : wid == 1 ? gbeta : wid == 2 ? (pos_is_arange ? gpos + (size_t)s * H : nullptr)
+                                                                   : gtype;
+      if (dst) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float t = red[0][wid][lane * 4 + k] + red[1][wid][lane * 4 + k] + red[2][wid][lane * 4 + k] +
+                    red[3][wid][lane * 4 + k];
+          atomicAdd(dst + 4 * c + k, t);
+        }
+      }
+    }
+  }
+}
+
+template <int NCH>
+static void embed_fwd_t(const int64_t* ids, const int64_t* pos_ids, const int64_t* type_ids, const bf16_t* word,
+                        const bf16_t* pos, const bf16_t* type, const bf16_t* gamma, const bf16_t* beta, bf16_t* out,
+                        float* mean, float* rstd, int rows, int H, float eps, const DropoutParams& dp, hipStream_t st) {
+  hipLaunchKernelGGL((embed_fwd_kernel<NCH>), dim3((rows + 3) / 4), dim3(256), 0, st, ids, pos_ids, type_ids, word, pos,
+                     type, gamma, beta, out, mean, rstd, rows, H, eps, dp);
+}
+
+void launch_embed_fwd(const int64_t* ids, const int64_t* pos_ids, const int64_t* type_ids, const bf16_t* word,
+                      const bf16_t* pos, const bf16_t* type, const bf16_t* gamma, const bf16_t* beta, bf16_t* out,
+                      float* mean, float* rstd, int rows, int H, float eps, double p, uint64_t seed, hipStream_t st) {
+  DropoutParams dp = make_dropout(p, seed);
+  int nch = (H / 4 + 63) / 64;
+  if (nch <= 1) embed_fwd_t<1>(ids, pos_ids, type_ids, word, pos, type, gamma, beta, out, mean, rstd, rows, H, eps, dp, st);
+  else if (nch <= 2) embed_fwd_t<2>(ids, pos_ids, type_ids, word, pos, type, gamma, beta, out, mean, rstd, rows, H, eps, dp, st);
+  else if (nch <= 3) embed_fwd_t<3>(ids, pos_ids, type_ids, word, pos, type, gamma, beta, out, mean, rstd, rows, H, eps, dp, st);
+  else if (nch <= 4) embed_fwd_t<4>(ids, pos_ids, type_ids, word, pos, type, gamma, beta, out, mean, rstd, rows, H, eps, dp, st);
+  else abort();
+  HSD_CHECK_LAUNCH();
+}
+
+template <int NCH>
+static void embed_bwd_t(const bf16_t* dout, const int64_t* ids, const int64_t* pos_ids, const int64_t* type_ids,
+                        const bf16_t* word, const bf16_t* pos, const bf16_t* type, const bf16_t* gamma,
+                        const float* mean, const float* rstd, float* gword, float* gpos, float* gtype, float* ggamma,
+                        float* gbeta, int B, int S, int H, int pos_is_arange, const DropoutParams& dp, hipStream_t st) {
+  // enough blocks to fill 256 CUs: S * chunks >= ~1024
+  int chunks = max(1, min(B, (1024 + S - 1) / S));
+  int bpc = (B + chunks - 1) / chunks;
+  chunks = (B + bpc - 1) / bpc;
+  hipLaunchKernelGGL((embed_bwd_kernel<NCH>), dim3(S, chunks), dim3(256), 0, st, dout, ids, pos_ids, type_ids, word,
+                     pos, type, gamma, mean, rstd, gword, gpos, gtype, ggamma, gbeta, B, S, H, bpc, pos_is_arange, dp);
+}
+
+void launch_embed_bwd(const bf16_t* dout, const int64_t* ids, const int64_t* pos_ids, const int64_t* type_ids,
+                      const bf16_t* word, const bf16_t* pos, const bf16_t* type, const bf16_t* gamma,
+                      const float* mean, const float* rstd, float* gword, float* gpos, float* gtype, float* ggamma,
+                      float* gbeta, int B, int S, int H, int pos_is_arange, double p, uint64_t seed, hipStream_t st) {
+  DropoutParams dp = make_dropout(p, seed);
+  int nch = (H / 4 + 63) / 64;
+  if (nch <= 1) embed_bwd_t<1>(dout, ids, pos_ids, type_ids, word, pos, type, gamma, mean, rstd, gword, gpos, gtype, ggamma, gbeta, B, S, H, pos_is_arange, dp, st);
+  else if (nch <= 2) embed_bwd_t<2>(dout, ids, pos_ids, type_ids, word, pos, type, gamma, mean, rstd, gword, gpos, gtype, ggamma, gbeta, B, S, H, pos_is_arange, dp, st);
+  else if (nch <= 3) embed_bwd_t<3>(dout, ids, pos_ids, type_ids, word, pos, type, gamma, mean, rstd, gword, gpos, gtype, ggamma, gbeta, B, S, H, pos_is_arange, dp, st);
+  else if (nch <= 4) embed_bwd_t<4>(dout, ids, pos_ids, type_ids, word, pos, type, gamma, mean, rstd, gword, gpos, gtype, ggamma, gbeta, B, S, H, pos_is_arange, dp, st);
+  else abort();
+  HSD_CHECK_LAUNCH();
+}
+
+}  // namespace hsd

@@ -14,3 +14,32 @@ void launch_adam(float* p, float* m, float* v, const void* g, bool grad_bf16, bf
                  float lr_wd, hipStream_t stream);
 
 }  // namespace hsd
+
+namespace hsd {
+// layernorm.hip
+void launch_ln_fwd(const bf16_t* y, const bf16_t* res, const bf16_t* gamma, const bf16_t* beta, bf16_t* z,
+                   bf16_t* out, float* mean, float* rstd, int rows, int H, float eps, double p, uint64_t seed,
+                   hipStream_t st);
+void launch_ln_bwd(const bf16_t* dout, const bf16_t* z, const float* mean, const float* rstd, const bf16_t* gamma,
+                   bf16_t* dz, bf16_t* dy, const bf16_t* dres_add, float* dgamma, float* dbeta, float* dbias,
+                   int rows, int H, double p, uint64_t seed, hipStream_t st);
+// embedding.hip
+void launch_embed_fwd(const int64_t* ids, const int64_t* pos_ids, const int64_t* type_ids, const bf16_t* word,
+                      const bf16_t* pos, const bf16_t* type, const bf16_t* gamma, const bf16_t* beta, bf16_t* out,
+                      float* mean, float* rstd, int rows, int H, float eps, double p, uint64_t seed, hipStream_t st);
+void launch_embed_bwd(const bf16_t* dout, const int64_t* ids, const int64_t* pos_ids, const int64_t* type_ids,
+                      const bf16_t* word, const bf16_t* pos, const bf16_t* type, const bf16_t* gamma,
+                      const float* mean, const float* rstd, float* gword, float* gpos, float* gtype, float* ggamma,
+                      float* gbeta, int B, int S, int H, int pos_is_arange, double p, uint64_t seed, hipStream_t st);
+// elementwise.hip
+void launch_gelu_fwd(const bf16_t* y, bf16_t* g, int64_t n, hipStream_t st);
+void launch_gelu_bwd_colsum(const bf16_t* dg, const bf16_t* y, bf16_t* da, float* dbias, int rows, int N,
+                            hipStream_t st);
+void launch_colsum(const bf16_t* x, float* dbias, int rows, int N, hipStream_t st);
+void launch_dropout(const bf16_t* x, bf16_t* out, int64_t n, double p, uint64_t seed, hipStream_t st);
+// attention.hip
+void launch_attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse2, int B, int S, int heads,
+                     double p, uint64_t seed, hipStream_t st);
+void launch_attn_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
+                     bf16_t* dqkv, float* dq_acc, int B, int S, int heads, double p, uint64_t seed, hipStream_t st);
+}  // namespace hsd

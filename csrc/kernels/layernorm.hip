@@ -1,0 +1,267 @@
+// LayerNorm with the BERT post-LN block tail fused in.
+//
+// forward : z = dropout(y) + residual   (y = GEMM output incl. bias)
+//           out = (z - mean) * rstd * gamma + beta       (fp32 statistics, eps 1e-12 / 1e-5)
+//           saves z (bf16) + mean/rstd (fp32) for backward
+// backward: dz   = rstd * (g - mean(g) - xhat * mean(g * xhat)),   g = dout * gamma
+//           dy   = dz * keep * scale          (gradient into the GEMM output, dropout regenerated)
+//           dgamma += Σ dout * xhat ; dbeta += Σ dout ; dbias += Σ dy   (fp32 atomics into main_grad,
+//           after a per-block register/LDS reduction — one atomic per column per block)
+//
+// One wave64 per row; each lane owns columns {4·(lane + 64·i)} (8-byte vector IO), so column
+// partial sums for the weight/bias gradients accumulate in registers across the rows a block
+// walks, with no atomics until the block ends.
+#include "common.h"
+
+namespace hsd {
+
+constexpr int kLnWaves = 4;
+
+template <int NCH>  // 4-element chunks per lane: ceil(H / 256)
+__global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ y, const bf16_t* __restrict__ res,
+                                                     const bf16_t* __restrict__ gamma, const bf16_t* __restrict__ beta,
+                                                     bf16_t* __restrict__ z_out, bf16_t* __restrict__ out,
+                                                     float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                     int rows, int H, float eps, DropoutParams dp) {
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * kLnWaves + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nq = H >> 2;  // 4-element chunks in the row
+  float v[NCH][4];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    int c = lane + 64 * i;
+    if (c < nq) {
+      size_t off = (size_t)row * H + 4 * c;
+      u32x2 w = *reinterpret_cast<const u32x2*>(y + off);
+      float a[4] = {lo_bf(w.x), hi_bf(w.x), lo_bf(w.y), hi_bf(w.y)};
+      if (dp.enabled) {
+        // element index within the site tensor = off + k ; pairs (off+0,off+1), (off+2,off+3)
+        uint32_t pair0 = (uint32_t)(off >> 1);
+        uint32_t b0 = dropout_bits(pair0, dp.seed_lo, dp.seed_hi);
+        uint32_t b1 = dropout_bits(pair0 + 1, dp.seed_lo, dp.seed_hi);
+        a[0] *= keep_factor(b0, 0, dp);
+        a[1] *= keep_factor(b0, 1, dp);
+        a[2] *= keep_factor(b1, 0, dp);
+        a[3] *= keep_factor(b1, 1, dp);
+      }
+      if (res) {
+        u32x2 r = *reinterpret_cast<const u32x2*>(res + off);
+        a[0] += lo_bf(r.x); a[1] += hi_bf(r.x); a[2] += lo_bf(r.y); a[3] += hi_bf(r.y);
+      }
+      // round z to bf16 now: backward recomputes xhat from the stored bf16 z
+      u32x2 zw;
+      zw.x = pack_bf2(a[0], a[1]);
+      zw.y = pack_bf2(a[2], a[3]);
+      if (z_out) *reinterpret_cast<u32x2*>(z_out + off) = zw;
+      v[i][0] = lo_bf(zw.x); v[i][1] = hi_bf(zw.x); v[i][2] = lo_bf(zw.y); v[i][3] = hi_bf(zw.y);
+      s += v[i][0] + v[i][1] + v[i][2] + v[i][3];
+    } else {
+      v[i][0] = v[i][1] = v[i][2] = v[i][3] = 0.f;
+    }
+  }
+  const float mean = wave_sum(s) / (float)H;
+  float ss = 0.f;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    int c = lane + 64 * i;
+    if (c < nq) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) { float d = v[i][k] - mean; ss += d * d; }
+    }
+  }
+  const float rstd = rsqrtf(wave_sum(ss) / (float)H + eps);
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    int c = lane + 64 * i;
+    if (c < nq) {
+      size_t off = (size_t)row * H + 4 * c;
+      u32x2 gw = *reinterpret_cast<const u32x2*>(gamma + 4 * c);
+      u32x2 bw = *reinterpret_cast<const u32x2*>(beta + 4 * c);
+      float g[4] = {lo_bf(gw.x), hi_bf(gw.x), lo_bf(gw.y), hi_bf(gw.y)};
+      float b[4] = {lo_bf(bw.x), hi_bf(bw.x), lo_bf(bw.y), hi_bf(bw.y)};
+      u32x2 o;
+      o.x = pack_bf2((v[i][0] - mean) * rstd * g[0] + b[0], (v[i][1] - mean) * rstd * g[1] + b[1]);
+      o.y = pack_bf2((v[i][2] - mean) * rstd * g[2] + b[2], (v[i][3] - mean) * rstd * g[3] + b[3]);
+      *reinterpret_cast<u32x2*>(out + off) = o;
+    }
+  }
+  if (lane == 0) {
+    mean_out[row] = mean;
+    rstd_out[row] = rstd;
+  }
+}
+
+// Block = 4 waves; block walks `rows_per_block` rows (wave-strided) accumulating column partials.
+template <int NCH>
+__global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ z,
+                                                     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
+                                                     const bf16_t* __restrict__ gamma,
+                                                     bf16_t* __restrict__ dz_out,    // residual grad (may be null)
+                                                     bf16_t* __restrict__ dy_out,    // grad into GEMM output (may alias dz_out if no dropout)
+                                                     const bf16_t* __restrict__ dres_add,  // extra grad to add to dz (may be null)
+                                                     float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                     float* __restrict__ dbias,      // may be null
+                                                     int rows, int H, int rows_per_block, DropoutParams dp) {
+  __shared__ float red[kLnWaves][3][256 * 4 / 4];  // per wave: 3 x (H up to 1024 per pass) -> reuse below
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int nq = H >> 2;
+  float gam[NCH][4];
+  float acc_g[NCH][4], acc_b[NCH][4], acc_db[NCH][4];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    int c = lane + 64 * i;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { acc_g[i][k] = acc_b[i][k] = acc_db[i][k] = 0.f; gam[i][k] = 0.f; }
+    if (c < nq) {
+      u32x2 gw = *reinterpret_cast<const u32x2*>(gamma + 4 * c);
+      gam[i][0] = lo_bf(gw.x); gam[i][1] = hi_bf(gw.x); gam[i][2] = lo_bf(gw.y); gam[i][3] = hi_bf(gw.y);
+    }
+  }
+  const int row0 = blockIdx.x * rows_per_block;
+  const int row_end = min(rows, row0 + rows_per_block);
+  for (int row = row0 + wid; row < row_end; row += kLnWaves) {
+    const float mean = mean_in[row], rstd = rstd_in[row];
+    float xh[NCH][4], g[NCH][4], d[NCH][4];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      int c = lane + 64 * i;
+      if (c < nq) {
+        size_t off = (size_t)row * H + 4 * c;
+        u32x2 zw = *reinterpret_cast<const u32x2*>(z + off);
+        u32x2 dw = *reinterpret_cast<const u32x2*>(dout + off);
+        float zz[4] = {lo_bf(zw.x), hi_bf(zw.x), lo_bf(zw.y), hi_bf(zw.y)};
+        d[i][0] = lo_bf(dw.x); d[i][1] = hi_bf(dw.x); d[i][2] = lo_bf(dw.y); d[i][3] = hi_bf(dw.y);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          xh[i][k] = (zz[k] - mean) * rstd;
+          g[i][k] = d[i][k] * gam[i][k];
+          s1 += g[i][k];
+          s2 += g[i][k] * xh[i][k];
+          acc_g[i][k] += d[i][k] * xh[i][k];
+          acc_b[i][k] += d[i][k];
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) xh[i][k] = g[i][k] = d[i][k] = 0.f;
+      }
+    }
+    s1 = wave_sum(s1) / (float)H;
+    s2 = wave_sum(s2) / (float)H;
+#pragma unroll
+    for (int i = 0; i < NCH; ++i) {
+      int c = lane + 64 * i;
+      if (c < nq) {
+        size_t off = (size_t)row * H + 4 * c;
+        float dz[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) dz[k] = rstd * (g[i][k] - s1 - xh[i][k] * s2);
+        if (dres_add) {
+          u32x2 r = *reinterpret_cast<const u32x2*>(dres_add + off);
+          dz[0] += lo_bf(r.x); dz[1] += hi_bf(r.x); dz[2] += lo_bf(r.y); dz[3] += hi_bf(r.y);
+        }
+        u32x2 o;
+        o.x = pack_bf2(dz[0], dz[1]);
+        o.y = pack_bf2(dz[2], dz[3]);
+        if (dz_out) *reinterpret_cast<u32x2*>(dz_out + off) = o;
+        if (dy_out) {
+          float dy[4] = {dz[0], dz[1], dz[2], dz[3]};
+          if (dp.enabled) {
+            uint32_t pair0 = (uint32_t)(off >> 1);
+            uint32_t b0 = dropout_bits(pair0, dp.seed_lo, dp.seed_hi);
+            uint32_t b1 = dropout_bits(pair0 + 1, dp.seed_lo, dp.seed_hi);
+            dy[0] *= keep_factor(b0, 0, dp);
+            dy[1] *= keep_factor(b0, 1, dp);
+            dy[2] *= keep_factor(b1, 0, dp);
+            dy[3] *= keep_factor(b1, 1, dp);
+          }
+          u32x2 yo;
+          yo.x = pack_bf2(dy[0], dy[1]);
+          yo.y = pack_bf2(dy[2], dy[3]);
+          *reinterpret_cast<u32x2*>(dy_out + off) = yo;
+          // bias grad sums the bf16-rounded dy that the dgrad GEMM consumes
+          acc_db[i][0] += lo_bf(yo.x); acc_db[i][1] += hi_bf(yo.x);
+          acc_db[i][2] += lo_bf(yo.y); acc_db[i][3] += hi_bf(yo.y);
+        }
+      }
+    }
+  }
+  // cross-wave reduction through LDS, one column chunk-pass at a time (H up to 256*NCH*... )
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    int c = lane + 64 * i;
+    __syncthreads();
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      red[wid][0][lane * 4 + k] = acc_g[i][k];
+      red[wid][1][lane * 4 + k] = acc_b[i][k];
+      red[wid][2][lane * 4 + k] = acc_db[i][k];
+    }
+    __syncthreads();
+    if (c < nq) {
+      // wave w reduces quantity w (w < 3), all 4 elements of this lane's chunk
+      if (wid < 3 && (wid < 2 || dbias != nullptr)) {
+        float* dst = wid == 0 ? dgamma : (wid == 1 ? dbeta : dbias);
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          float t = red[0][wid][lane * 4 + k] + red[1][wid][lane * 4 + k] + red[2][wid][lane * 4 + k] +
+                    red[3][wid][lane * 4 + k];
+          atomicAdd(dst + 4 * c + k, t);
+        }
+      }
+    }
+  }
+}
+
+template <int NCH>
+static void ln_fwd_t(const bf16_t* y, const bf16_t* res, const bf16_t* gamma, const bf16_t* beta, bf16_t* z,
+                     bf16_t* out, float* mean, float* rstd, int rows, int H, float eps, const DropoutParams& dp,
+                     hipStream_t st) {
+  dim3 grid((rows + kLnWaves - 1) / kLnWaves);
+  hipLaunchKernelGGL((ln_fwd_kernel<NCH>), grid, dim3(256), 0, st, y, res, gamma, beta, z, out, mean, rstd, rows,
+                     H, eps, dp);
+}
+
+void launch_ln_fwd(const bf16_t* y, const bf16_t* res, const bf16_t* gamma, const bf16_t* beta, bf16_t* z,
+                   bf16_t* out, float* mean, float* rstd, int rows, int H, float eps, double p, uint64_t seed,
+                   hipStream_t st) {
+  DropoutParams dp = make_dropout(p, seed);
+  int nch = (H / 4 + 63) / 64;
+  if (nch <= 1) ln_fwd_t<1>(y, res, gamma, beta, z, out, mean, rstd, rows, H, eps, dp, st);
+  else if (nch <= 2) ln_fwd_t<2>(y, res, gamma, beta, z, out, mean, rstd, rows, H, eps, dp, st);
+  else if (nch <= 3) ln_fwd_t<3>(y, res, gamma, beta, z, out, mean, rstd, rows, H, eps, dp, st);
+  else if (nch <= 4) ln_fwd_t<4>(y, res, gamma, beta, z, out, mean, rstd, rows, H, eps, dp, st);
+  else if (nch <= 8) ln_fwd_t<8>(y, res, gamma, beta, z, out, mean, rstd, rows, H, eps, dp, st);
+  else abort();
+  HSD_CHECK_LAUNCH();
+}
+
+template <int NCH>
+static void ln_bwd_t(const bf16_t* dout, const bf16_t* z, const float* mean, const float* rstd, const bf16_t* gamma,
+                     bf16_t* dz, bf16_t* dy, const bf16_t* dres_add, float* dgamma, float* dbeta, float* dbias,
+                     int rows, int H, const DropoutParams& dp, hipStream_t st) {
+  int rpb = 128;
+  int blocks = (rows + rpb - 1) / rpb;
+  if (blocks < 512 && rows > 512 * 8) { rpb = (rows + 511) / 512; blocks = (rows + rpb - 1) / rpb; }
+  if (blocks < 256) { rpb = max(kLnWaves, (rows + 255) / 256); blocks = (rows + rpb - 1) / rpb; }
+  hipLaunchKernelGGL((ln_bwd_kernel<NCH>), dim3(blocks), dim3(256), 0, st, dout, z, mean, rstd, gamma, dz, dy,
+                     dres_add, dgamma, dbeta, dbias, rows, H, rpb, dp);
+}
+
+void launch_ln_bwd(const bf16_t* dout, const bf16_t* z, const float* mean, const float* rstd, const bf16_t* gamma,
+                   bf16_t* dz, bf16_t* dy, const bf16_t* dres_add, float* dgamma, float* dbeta, float* dbias,
+                   int rows, int H, double p, uint64_t seed, hipStream_t st) {
+  DropoutParams dp = make_dropout(p, seed);
+  int nch = (H / 4 + 63) / 64;
+  if (nch <= 1) ln_bwd_t<1>(dout, z, mean, rstd, gamma, dz, dy, dres_add, dgamma, dbeta, dbias, rows, H, dp, st);
+  else if (nch <= 2) ln_bwd_t<2>(dout, z, mean, rstd, gamma, dz, dy, dres_add, dgamma, dbeta, dbias, rows, H, dp, st);
+  else if (nch <= 3) ln_bwd_t<3>(dout, z, mean, rstd, gamma, dz, dy, dres_add, dgamma, dbeta, dbias, rows, H, dp, st);
+  else if (nch <= 4) ln_bwd_t<4>(dout, z, mean, rstd, gamma, dz, dy, dres_add, dgamma, dbeta, dbias, rows, H, dp, st);
+  else abort();
+  HSD_CHECK_LAUNCH();
+}
+
+}  // namespace hsd

@@ -49,7 +49,7 @@ class Embeddings(nn.Module):
         p = c.hidden_dropout_prob if training else 0.0
         return ops.embed_ln(input_ids, pos, token_type_ids, self.word_embeddings, self.position_embeddings,
                             self.token_type_embeddings, self.ln_weight, self.ln_bias, c.layer_norm_eps,
-                            p, rng.next() if p else 0)
+                            p, rng.next() if p else 0, pos_is_arange=c.model_type != "roberta")
 
 
 class Encoder(nn.Module):

@@ -41,10 +41,11 @@ def dropout(x: torch.Tensor, p: float, seed: int):
     return _ref.dropout(x, p, seed, True)
 
 
-def embed_ln(input_ids, position_ids, token_type_ids, word_w, pos_w, type_w, ln_w, ln_b, eps, p, seed):
+def embed_ln(input_ids, position_ids, token_type_ids, word_w, pos_w, type_w, ln_w, ln_b, eps, p, seed,
+             pos_is_arange=False):
     if _hip(word_w):
         return _hipmod().embed_ln(input_ids, position_ids, token_type_ids, word_w, pos_w, type_w, ln_w, ln_b,
-                                  eps, p, seed)
+                                  eps, p, seed, pos_is_arange)
     return _ref.embed_ln(input_ids, position_ids, token_type_ids, word_w, pos_w, type_w, ln_w, ln_b, eps, p, seed,
                          p > 0)
 

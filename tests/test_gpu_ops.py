@@ -1,0 +1,173 @@
+"""HIP kernel numerics vs the plain-PyTorch fp32 reference of the same op (SURVEY.md §4 'kernel / GPU').
+
+Dropout masks are bit-identical between the kernels and ops/reference.py (shared hash), so every
+test also runs with dropout on.
+"""
+import math
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+from huggingface_sagemaker_tensorflow_distributed_amd.ops import reference as ref  # noqa: E402
+from huggingface_sagemaker_tensorflow_distributed_amd.ops.rng import keep_mask  # noqa: E402
+
+
+def _hip():
+    from huggingface_sagemaker_tensorflow_distributed_amd.ops import hip
+
+    return hip
+
+
+def _close(a, b, atol, rtol, what=""):
+    a = a.float()
+    b = b.float()
+    err = (a - b).abs()
+    tol = atol + rtol * b.abs()
+    bad = (err > tol).float().mean().item()
+    assert bad <= 1e-3, f"{what}: {bad*100:.3f}% elements out of tol, max err {err.max().item():.4g}"
+
+
+def test_extension_loaded(gpu):
+    hip = _hip()
+    assert hip._C.__file__.endswith(".so")
+
+
+def test_dropout_mask_matches_reference(gpu):
+    hip = _hip()
+    x = torch.ones(4096 * 3, device=gpu, dtype=torch.bfloat16)
+    seed = 0xDEADBEEF12345678
+    y = hip.dropout(x, 0.1, seed)
+    m = keep_mask(seed, x.numel(), 0.1, device=gpu)
+    assert torch.equal(y.float() != 0, m)
+    frac = m.float().mean().item()
+    assert abs(frac - 0.9) < 0.02
+
+
+@pytest.mark.parametrize("H", [64, 768, 1024])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_dense_residual_ln(gpu, H, p):
+    hip = _hip()
+    torch.manual_seed(0)
+    T, K = 512, 256
+    x = torch.randn(T, K, device=gpu, dtype=torch.bfloat16)
+    w = (torch.randn(H, K, device=gpu) * 0.05).bfloat16().requires_grad_()
+    b = (torch.randn(H, device=gpu) * 0.1).bfloat16().requires_grad_()
+    res = torch.randn(T, H, device=gpu, dtype=torch.bfloat16)
+    g = (1 + 0.1 * torch.randn(H, device=gpu)).bfloat16().requires_grad_()
+    be = (0.1 * torch.randn(H, device=gpu)).bfloat16().requires_grad_()
+    xr = x.clone().requires_grad_()
+    rr = res.clone().requires_grad_()
+    out = hip.dense_residual_ln(xr, w, b, rr, g, be, 1e-12, p, 1234)
+    # reference in fp32
+    x32, w32, b32, r32, g32, be32 = [t.detach().float().requires_grad_() for t in (x, w, b, res, g, be)]
+    ref_out = ref.layer_norm(ref.linear_dropout_residual(x32, w32, b32, r32, p, 1234, p > 0), g32, be32, 1e-12)
+    _close(out, ref_out, 3e-2, 2e-2, "fwd")
+    dout = torch.randn_like(out)
+    out.backward(dout)
+    ref_out.backward(dout.float())
+    _close(xr.grad, x32.grad, 5e-2, 5e-2, "dx")
+    _close(rr.grad, r32.grad, 5e-2, 5e-2, "dres")
+    _close(w.grad, w32.grad, 5e-2, 5e-2, "dw")
+    _close(b.grad, b32.grad, 1e-1, 2e-2, "db")
+    _close(g.grad, g32.grad, 1e-1, 2e-2, "dgamma")
+    _close(be.grad, be32.grad, 1e-1, 2e-2, "dbeta")
+
+
+def test_linear_gelu(gpu):
+    hip = _hip()
+    torch.manual_seed(1)
+    T, K, N = 1024, 256, 512
+    x = torch.randn(T, K, device=gpu, dtype=torch.bfloat16).requires_grad_()
+    w = (torch.randn(N, K, device=gpu) * 0.05).bfloat16().requires_grad_()
+    b = (torch.randn(N, device=gpu) * 0.1).bfloat16().requires_grad_()
+    y = hip.linear_gelu(x, w, b)
+    x32, w32, b32 = [t.detach().float().requires_grad_() for t in (x, w, b)]
+    yr = ref.linear_gelu(x32, w32, b32)
+    _close(y, yr, 2e-2, 2e-2, "fwd")
+    d = torch.randn_like(y)
+    y.backward(d)
+    yr.backward(d.float())
+    _close(x.grad, x32.grad, 5e-2, 5e-2, "dx")
+    _close(w.grad, w32.grad, 1e-1, 5e-2, "dw")
+    _close(b.grad, b32.grad, 2e-1, 2e-2, "db")
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+@pytest.mark.parametrize("type_vocab", [2, 0])
+def test_embed_ln(gpu, p, type_vocab):
+    hip = _hip()
+    torch.manual_seed(2)
+    B, S, H, V = 8, 64, 768, 1000
+    ids = torch.randint(0, V, (B, S), device=gpu)
+    pos = torch.arange(S, device=gpu).unsqueeze(0).expand(B, S)
+    tt = torch.randint(0, 2, (B, S), device=gpu) if type_vocab else None
+    word = (torch.randn(V, H, device=gpu) * 0.02).bfloat16().requires_grad_()
+    pw = (torch.randn(S, H, device=gpu) * 0.02).bfloat16().requires_grad_()
+    tw = (torch.randn(2, H, device=gpu) * 0.02).bfloat16().requires_grad_() if type_vocab else None
+    g = (1 + 0.1 * torch.randn(H, device=gpu)).bfloat16().requires_grad_()
+    be = (0.1 * torch.randn(H, device=gpu)).bfloat16().requires_grad_()
+    out = hip.embed_ln(ids, pos, tt, word, pw, tw, g, be, 1e-12, p, 99, True)
+    f = lambda t: t.detach().float().requires_grad_() if t is not None else None  # noqa: E731
+    word32, pw32, tw32, g32, be32 = f(word), f(pw), f(tw), f(g), f(be)
+    r = ref.embed_ln(ids, pos, tt, word32, pw32, tw32, g32, be32, 1e-12, 0.0, 0, False)
+    if p > 0:
+        # kernel applies dropout to the bf16-rounded LN output
+        r = r.bfloat16().float() * keep_mask(99, r.numel(), p, device=gpu).view_as(r).float() / (1 - p)
+    _close(out, r, 3e-2, 2e-2, "fwd")
+    d = torch.randn_like(out)
+    out.backward(d)
+    r.backward(d.float())
+    _close(word.grad, word32.grad, 1e-2, 5e-2, "dword")
+    _close(pw.grad, pw32.grad, 1e-1, 5e-2, "dpos")
+    if type_vocab:
+        _close(tw.grad, tw32.grad, 5e-1, 5e-2, "dtype")
+    _close(g.grad, g32.grad, 2e-1, 5e-2, "dgamma")
+    _close(be.grad, be32.grad, 2e-1, 5e-2, "dbeta")
+
+
+@pytest.mark.parametrize("S", [32, 128, 256])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+@pytest.mark.parametrize("masked", [False, True])
+def test_attention(gpu, S, p, masked):
+    hip = _hip()
+    torch.manual_seed(3)
+    B, heads = 4, 4
+    H = heads * 64
+    qkv = torch.randn(B * S, 3 * H, device=gpu, dtype=torch.bfloat16).requires_grad_()
+    mb = None
+    if masked:
+        lens = torch.randint(S // 4, S + 1, (B,), device=gpu)
+        am = (torch.arange(S, device=gpu)[None, :] < lens[:, None]).long()
+        mb = ref.key_mask_bias(am)
+    out = hip.attention(qkv, mb, B, S, heads, p, 777)
+    q32 = qkv.detach().float().requires_grad_()
+    r = ref.attention(q32, mb, B, S, heads, p, 777, p > 0)
+    _close(out, r, 2e-2, 2e-2, "fwd")
+    d = torch.randn_like(out)
+    out.backward(d)
+    r.backward(d.float())
+    g, gr = qkv.grad.float(), q32.grad
+    for i, name in enumerate("qkv"):
+        _close(g[:, i * H:(i + 1) * H], gr[:, i * H:(i + 1) * H], 3e-2, 3e-2, f"d{name}")
+
+
+def test_adam_kernel_matches_reference(gpu):
+    hip = _hip()
+    torch.manual_seed(4)
+    n = 4096
+    p = torch.randn(n, device=gpu)
+    m = torch.randn(n, device=gpu).abs() * 0.1
+    v = torch.randn(n, device=gpu).abs() * 0.1
+    g = torch.randn(n, device=gpu)
+    out = torch.empty(n, device=gpu, dtype=torch.bfloat16)
+    pr, mr, vr = p.clone(), m.clone(), v.clone()
+    step, eps, b1, b2, gs = 1e-3, 1e-7, 0.9, 0.999, 0.5
+    hip.adam_step(p, m, v, g, out, None, step, eps, b1, b2, gs, 0.0)
+    gg = g * gs
+    mr = b1 * mr + (1 - b1) * gg
+    vr = b2 * vr + (1 - b2) * gg * gg
+    pr = pr - step * mr / (vr.sqrt() + eps)
+    torch.testing.assert_close(p, pr, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(out.float(), pr.bfloat16().float())
