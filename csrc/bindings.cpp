@@ -176,6 +176,43 @@ void attn_bwd(torch::Tensor qkv, c10::optional<torch::Tensor> mask, torch::Tenso
                        (int)B, (int)S, (int)heads, p, (uint64_t)seed, cur_stream());
 }
 
+// C[M,N] (+)= A·B with fused epilogue. la=0: A [M,K]; la=1: A [K,M]. lb=0: B [N,K]; lb=1: B [K,N].
+void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int64_t la, int64_t lb, int64_t epi,
+          c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> aux, c10::optional<torch::Tensor> C2,
+          double p, int64_t seed, int64_t splits) {
+  TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda(), "gemm operands must be GPU tensors");
+  TORCH_CHECK(A.scalar_type() == torch::kBFloat16 && B.scalar_type() == torch::kBFloat16, "gemm inputs must be bf16");
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "gemm operands must be 2-D");
+  TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && C.stride(1) == 1, "gemm operands need unit inner stride");
+  const int64_t M = la == 0 ? A.size(0) : A.size(1);
+  const int64_t K = la == 0 ? A.size(1) : A.size(0);
+  const int64_t N = lb == 0 ? B.size(0) : B.size(1);
+  const int64_t KB = lb == 0 ? B.size(1) : B.size(0);
+  TORCH_CHECK(K == KB, "gemm K mismatch");
+  TORCH_CHECK(C.size(0) == M && C.size(1) == N, "gemm C shape");
+  TORCH_CHECK(M % 8 == 0 && N % 8 == 0 && K % 8 == 0, "gemm dims must be multiples of 8");
+  TORCH_CHECK(A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0 && C.stride(0) % 4 == 0, "gemm leading dims alignment");
+  const bool f32out = epi == 6;
+  TORCH_CHECK(C.scalar_type() == (f32out ? torch::kFloat32 : torch::kBFloat16), "gemm C dtype");
+  if (epi == 1 || epi == 2 || epi == 3) {
+    TORCH_CHECK(bias.has_value() && bias->numel() == N && bias->scalar_type() == torch::kBFloat16 &&
+                bias->is_contiguous(), "gemm bias");
+  }
+  if (epi == 3 || epi == 4 || epi == 5) {
+    TORCH_CHECK(aux.has_value() && aux->dim() == 2 && aux->size(0) == M && aux->size(1) == N &&
+                aux->stride(1) == 1 && aux->scalar_type() == torch::kBFloat16, "gemm aux");
+  }
+  if (epi == 2) {
+    TORCH_CHECK(C2.has_value() && C2->sizes() == C.sizes() && C2->strides() == C.strides() &&
+                C2->scalar_type() == torch::kBFloat16, "gemm C2");
+  }
+  TORCH_CHECK(epi == 6 || splits == 1, "split-K only with the fp32 atomic epilogue");
+  hsd::launch_gemm((int)la, (int)lb, (int)epi, CBF(A), A.stride(0), CBF(B), B.stride(0), (int)M, (int)N, (int)K,
+                   C.data_ptr(), C.stride(0), bias.has_value() ? CBF(*bias) : nullptr,
+                   aux.has_value() ? CBF(*aux) : nullptr, aux.has_value() ? aux->stride(0) : 0,
+                   C2.has_value() ? BF(*C2) : nullptr, p, (uint64_t)seed, (int)splits, cur_stream());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -191,4 +228,5 @@ PYBIND11_MODULE(_C, m) {
   m.def("dropout", &dropout);
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
+  m.def("gemm", &gemm);
 }

@@ -43,3 +43,10 @@ void launch_attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* l
 void launch_attn_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
                      bf16_t* dqkv, float* dq_acc, int B, int S, int heads, double p, uint64_t seed, hipStream_t st);
 }  // namespace hsd
+
+namespace hsd {
+// gemm.hip — la: 0 A[M][K], 1 A[K][M];  lb: 0 B[N][K], 1 B[K][N];  epi: see gemm.hip Epi
+void launch_gemm(int la, int lb, int epi, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, int M, int N,
+                 int K, void* C, int64_t ldc, const bf16_t* bias, const bf16_t* aux, int64_t ldaux, bf16_t* C2,
+                 double p_drop, uint64_t seed, int splits, hipStream_t st);
+}  // namespace hsd

@@ -1,0 +1,159 @@
+"""Multi-process data parallelism on gloo (CPU): the RCCL code path with a CPU backend (SURVEY.md §4 'dist')."""
+import os
+import socket
+import sys
+
+import pytest
+import torch
+import torch.multiprocessing as mp
+
+pytestmark = pytest.mark.dist
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+
+
+def _port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _setenv(rank, world, port):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "LOCAL_WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+
+
+def _make(seed_init, bucket_mb=0.05):
+    from huggingface_sagemaker_tensorflow_distributed_amd.models import build_model, resolve_config
+    from huggingface_sagemaker_tensorflow_distributed_amd.optim import FusedAdam
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel import FlatParamStore, GradBucketer, backend
+    from huggingface_sagemaker_tensorflow_distributed_amd.train.trainer import Trainer
+
+    cfg = resolve_config("hsd-tiny-bert").replace(hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    model = build_model(cfg, seed=seed_init)
+    store = FlatParamStore(model, torch.device("cpu"))
+    opt = FusedAdam(store, lr=1e-3)
+    buck = GradBucketer(store, bucket_mb=bucket_mb) if backend.size() > 1 else None
+    return model, store, opt, Trainer(model, store, opt, buck, torch.device("cpu"))
+
+
+def _data(n, S=16, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    ids = torch.randint(5, 1024, (n, S), generator=g)
+    am = torch.ones(n, S, dtype=torch.long)
+    am[::3, S // 2:] = 0
+    lab = torch.randint(0, 2, (n,), generator=g)
+    return ids, am, lab
+
+
+def _worker_dp(rank, world, port, out_path):
+    _setenv(rank, world, port)
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel import backend, broadcast_parameters
+
+    backend.init(device="cpu")
+    # different init per rank: broadcast must make them identical (Q4)
+    model, store, opt, tr = _make(seed_init=100 + rank)
+    broadcast_parameters(store)
+    ids, am, lab = _data(8 * world)
+    per = 8
+    for step in range(3):
+        sl = slice(rank * per, (rank + 1) * per)
+        tr.train_step([{"input_ids": ids[sl], "attention_mask": am[sl], "labels": lab[sl]}])
+    if rank == 0:
+        torch.save(store.master.clone(), out_path)
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel.collectives import params_in_sync
+
+    assert params_in_sync(store)
+    backend.shutdown()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_dp_equals_single_process_global_batch(tmp_path, world):
+    """N ranks x per-rank batch 8 with grad averaging == 1 process on the 8N global batch."""
+    out = str(tmp_path / "dp.pt")
+    mp.spawn(_worker_dp, args=(world, _port(), out), nprocs=world, join=True)
+    dp_master = torch.load(out)
+
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE"):
+        os.environ.pop(k, None)
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel import backend
+
+    backend.init(device="cpu")
+    model, store, opt, tr = _make(seed_init=100)  # rank 0's init (what broadcast distributes)
+    ids, am, lab = _data(8 * world)
+    for step in range(3):
+        tr.train_step([{"input_ids": ids, "attention_mask": am, "labels": lab}])
+    torch.testing.assert_close(store.master, dp_master, atol=2e-6, rtol=1e-5)
+
+
+def _worker_buckets(rank, world, port):
+    _setenv(rank, world, port)
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel import backend
+
+    backend.init(device="cpu")
+    model, store, opt, tr = _make(seed_init=0, bucket_mb=0.01)
+    assert len(tr.bucketer.buckets) > 3
+    # gradients with rank-dependent values, marked ready in backward order -> buckets fire early
+    tr.bucketer.begin()
+    store.grad.copy_(torch.arange(store.numel, dtype=torch.float32) * (rank + 1))
+    for i in range(len(store.params)):
+        store.params[i]._hsd_ready()
+    launched_before_finish = sum(b.launched for b in tr.bucketer.buckets)
+    tr.bucketer.finish()
+    expect = torch.arange(store.numel, dtype=torch.float32) * sum(r + 1 for r in range(world))
+    torch.testing.assert_close(store.grad, expect)
+    assert launched_before_finish == len(tr.bucketer.buckets)
+    backend.shutdown()
+
+
+def test_bucketed_allreduce_sums_and_overlaps():
+    mp.spawn(_worker_buckets, args=(2, _port()), nprocs=2, join=True)
+
+
+def test_shard_sampler_disjoint_complete():
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel.sampler import ShardSampler
+
+    n, world = 103, 4
+    parts = [ShardSampler(n, r, world, shuffle=True, seed=3).indices() for r in range(world)]
+    flat = sum(parts, [])
+    assert len(set(flat)) == len(flat) == (n // world) * world
+    assert all(len(p) == n // world for p in parts)
+
+
+def test_launcher_failure_propagates(tmp_path):
+    from huggingface_sagemaker_tensorflow_distributed_amd.launcher.spawn import launch
+
+    script = tmp_path / "s.py"
+    script.write_text("import os, sys, time\n"
+                      "r = int(os.environ['RANK'])\n"
+                      "print('rank', r, os.environ['SM_MODEL_DIR'], flush=True)\n"
+                      "if r == 1: sys.exit(3)\n"
+                      "time.sleep(60)\n")
+    import io
+
+    buf = io.StringIO()
+    rc = launch([sys.executable, str(script)], 2, output_data_dir=str(tmp_path / "d"), model_dir=str(tmp_path / "m"),
+                stdout=buf, kill_grace_s=2)
+    assert rc == 3
+    assert "rank 1 exited with 3" in buf.getvalue()
+
+
+def test_train_script_two_ranks_end_to_end(tmp_path):
+    """scripts/train.py under the local launcher: world 2 (gloo), rank-0 save, results files."""
+    from huggingface_sagemaker_tensorflow_distributed_amd.launcher.spawn import launch
+
+    import io
+
+    buf = io.StringIO()
+    rc = launch([sys.executable, os.path.join(ROOT, "scripts", "train.py"), "--model_name_or_path", "hsd-tiny-bert",
+                 "--epochs", "1", "--train_batch_size", "8", "--eval_batch_size", "8", "--max_seq_length", "32",
+                 "--num_train_examples", "64", "--num_eval_examples", "32", "--device", "cpu"], 2,
+                output_data_dir=str(tmp_path / "data"), model_dir=str(tmp_path / "model"), stdout=buf)
+    assert rc == 0, buf.getvalue()[-3000:]
+    txt = (tmp_path / "data" / "train_results.txt").read_text()
+    assert txt.startswith("loss = [") and "train_runtime = {'train_runtime':" in txt
+    assert (tmp_path / "data" / "eval_results.txt").read_text().count(" = ") == 2
+    assert (tmp_path / "model" / "model.safetensors").exists()
+    assert (tmp_path / "model" / "tokenizer.json").exists()

@@ -1,0 +1,101 @@
+"""MFMA GEMM (csrc/kernels/gemm.hip) vs a plain fp32 PyTorch reference: all layouts and epilogues."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+EPI_STORE, EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_DROP_RES, EPI_RES, EPI_DGELU, EPI_F32_ATOMIC = range(7)
+
+
+def _C():
+    from huggingface_sagemaker_tensorflow_distributed_amd.ops import hip
+
+    return hip._C
+
+
+def _mk(shape, dev, scale=1.0):
+    return (torch.randn(shape, device=dev) * scale).bfloat16()
+
+
+def _ref(A, B, la, lb):
+    a = A.float() if la == 0 else A.float().t()
+    b = B.float() if lb == 1 else B.float().t()
+    return a @ b  # [M, N]
+
+
+def _check(out, ref, tol=2e-2):
+    err = (out.float() - ref).abs().max().item()
+    scale = ref.abs().max().item() + 1e-6
+    assert err <= tol * scale, f"max err {err:.4g} vs scale {scale:.4g}"
+
+
+SHAPES = [(256, 256, 128), (200, 136, 72), (1024, 768, 768), (512, 2304, 64), (96, 64, 3072)]
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+@pytest.mark.parametrize("la,lb", [(0, 0), (0, 1)])
+def test_gemm_store(gpu, M, N, K, la, lb):
+    torch.manual_seed(0)
+    A = _mk((M, K) if la == 0 else (K, M), gpu)
+    B = _mk((N, K) if lb == 0 else (K, N), gpu)
+    C = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    _C().gemm(A, B, C, la, lb, EPI_STORE, None, None, None, 0.0, 0, 1)
+    _check(C, _ref(A, B, la, lb))
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+@pytest.mark.parametrize("la,lb", [(1, 1), (0, 0), (0, 1)])
+@pytest.mark.parametrize("splits", [1, 3])
+def test_gemm_f32_atomic_accumulates(gpu, M, N, K, la, lb, splits):
+    torch.manual_seed(1)
+    A = _mk((M, K) if la == 0 else (K, M), gpu)
+    B = _mk((N, K) if lb == 0 else (K, N), gpu)
+    C0 = torch.randn(M, N, device=gpu)
+    C = C0.clone()
+    _C().gemm(A, B, C, la, lb, EPI_F32_ATOMIC, None, None, None, 0.0, 0, splits)
+    _check(C, C0 + _ref(A, B, la, lb), 1e-3)
+
+
+def test_gemm_bias_epilogues(gpu):
+    torch.manual_seed(2)
+    M, N, K = 384, 512, 256
+    A, B = _mk((M, K), gpu), _mk((N, K), gpu, 0.1)
+    bias = _mk((N,), gpu)
+    ref = _ref(A, B, 0, 0) + bias.float()
+    C = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    _C().gemm(A, B, C, 0, 0, EPI_BIAS, bias, None, None, 0.0, 0, 1)
+    _check(C, ref)
+    C2 = torch.empty_like(C)
+    _C().gemm(A, B, C, 0, 0, EPI_BIAS_GELU, bias, None, C2, 0.0, 0, 1)
+    _check(C, ref)
+    _check(C2, torch.nn.functional.gelu(ref))
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_gemm_bias_dropout_residual(gpu, p):
+    from huggingface_sagemaker_tensorflow_distributed_amd.ops.reference import dropout
+
+    torch.manual_seed(3)
+    M, N, K = 256, 768, 512
+    A, B = _mk((M, K), gpu), _mk((N, K), gpu, 0.05)
+    bias, res = _mk((N,), gpu), _mk((M, N), gpu)
+    y = (_ref(A, B, 0, 0) + bias.float()).bfloat16()
+    ref = dropout(y, p, 4242, True).float() + res.float()
+    C = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    _C().gemm(A, B, C, 0, 0, EPI_BIAS_DROP_RES, bias, res, None, p, 4242, 1)
+    _check(C, ref)
+
+
+def test_gemm_dgrad_epilogues(gpu):
+    torch.manual_seed(4)
+    M, N, K = 512, 768, 1024  # dX[M,N] = dY[M,K] . W[K,N]
+    A, B = _mk((M, K), gpu), _mk((K, N), gpu, 0.05)
+    aux = _mk((M, N), gpu)
+    ref = _ref(A, B, 0, 1)
+    C = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    _C().gemm(A, B, C, 0, 1, EPI_RES, None, aux, None, 0.0, 0, 1)
+    _check(C, ref + aux.float())
+    _C().gemm(A, B, C, 0, 1, EPI_DGELU, None, aux, None, 0.0, 0, 1)
+    x = aux.float().requires_grad_()
+    torch.nn.functional.gelu(x).backward(torch.ones_like(x))
+    _check(C, ref.bfloat16().float() * x.grad, 3e-2)
