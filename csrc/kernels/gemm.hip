@@ -22,6 +22,7 @@
 //   F32_ATOMIC (wgrad straight into the fp32 main_grad buffer; split-K partials add atomically —
 //   n on the lane so every atomic wave instruction is two contiguous 128-B row segments).
 #include "common.h"
+#include <stdlib.h>
 
 namespace hsd {
 
@@ -56,12 +57,13 @@ __device__ __forceinline__ int swz0(int row) {  // [rows][64] image: chunk ^ bre
 }
 __device__ __forceinline__ int off0(int row, int chunk) { return row * 64 + ((chunk ^ swz0(row)) << 3); }
 __device__ __forceinline__ int swz1(int krow) { return (((krow & 1) << 1) | ((krow >> 1) & 1)) << 2; }
-__device__ __forceinline__ int off1(int krow, int col) {  // [64 k][128] image, col = element column
-  return krow * 128 + ((((col >> 3) ^ swz1(krow))) << 3) + (col & 7);
+template <int R = 128>
+__device__ __forceinline__ int off1(int krow, int col) {  // [64 k][R] image, col = element column
+  return krow * R + ((((col >> 3) ^ swz1(krow))) << 3) + (col & 7);
 }
 
 // fragment (8 consecutive-k bf16 for lane row r = lane&31, k = 16ks + 8h + j) of rows [rbase, rbase+32)
-template <int L>
+template <int L, int R = 128>
 __device__ __forceinline__ bf16x8 frag(const bf16_t* tile, int rbase, int ks, int lane) {
   if constexpr (L == 0) {
     const int r = lane & 31, h = lane >> 5;
@@ -70,8 +72,8 @@ __device__ __forceinline__ bf16x8 frag(const bf16_t* tile, int rbase, int ks, in
     const int g = lane >> 4, i = lane & 15, h = g >> 1, q = i >> 2, p = i & 3;
     const int col = rbase + 16 * (g & 1) + 4 * p;
     const int k0 = 16 * ks + 8 * h + q;
-    bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4_t*)(tile + off1(k0, col)));
-    bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4_t*)(tile + off1(k0 + 4, col)));
+    bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4_t*)(tile + off1<R>(k0, col)));
+    bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4_t*)(tile + off1<R>(k0 + 4, col)));
     bf16x8 r;
     r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
     r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
@@ -112,6 +114,205 @@ __device__ __forceinline__ void swrite(bf16_t* tile, const u32x4 (&st)[4], int t
       *reinterpret_cast<u32x4*>(tile + off1(c >> 4, (c & 15) * 8)) = st[i];
     }
   }
+}
+
+
+// One 32x32 accumulator block. SWAP: D[n][m] (m on the lane, regs walk n); else D[m][n] (n on the lane).
+template <int EPI, bool SWAP>
+__device__ __forceinline__ void epi_block(const f32x16& a, int mb, int nb, int lane, const GemmParams& p) {
+  const int r = lane & 31, h = lane >> 5;
+  if constexpr (!SWAP) {
+    float* C = reinterpret_cast<float*>(p.C);
+    const int n = nb + r;
+    if (n >= p.N) return;
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const int m = mb + (reg & 3) + 8 * (reg >> 2) + 4 * h;
+      if (m < p.M) atomicAdd(C + (int64_t)m * p.ldc + n, a[reg]);
+    }
+  } else {
+    bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
+    const int m = mb + r;
+    if (m >= p.M) return;
+    constexpr bool kBias = EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_DROP_RES;
+    constexpr bool kAux = EPI == EPI_BIAS_DROP_RES || EPI == EPI_RES || EPI == EPI_DGELU;
+    // phase 1: issue every load of the block (bias / residual / pre-activation) before any store
+    u32x2 bw[4], xw[4];
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+      const int n = min(nb + 8 * q4 + 4 * h, p.N - 4);
+      if constexpr (kBias) bw[q4] = *reinterpret_cast<const u32x2*>(p.bias + n);
+      if constexpr (kAux) xw[q4] = *reinterpret_cast<const u32x2*>(p.aux + (int64_t)m * p.ldaux + n);
+    }
+    // phase 2: math + stores
+#pragma unroll
+    for (int q4 = 0; q4 < 4; ++q4) {
+      const int n = nb + 8 * q4 + 4 * h;
+      if (n >= p.N) continue;
+      float v[4] = {a[4 * q4], a[4 * q4 + 1], a[4 * q4 + 2], a[4 * q4 + 3]};
+      const int64_t co = (int64_t)m * p.ldc + n;
+      if constexpr (kBias) {
+        v[0] += lo_bf(bw[q4].x); v[1] += hi_bf(bw[q4].x); v[2] += lo_bf(bw[q4].y); v[3] += hi_bf(bw[q4].y);
+      }
+      u32x2 o;
+      if constexpr (EPI == EPI_BIAS_GELU) {
+        o.x = pack_bf2(v[0], v[1]);
+        o.y = pack_bf2(v[2], v[3]);
+        *reinterpret_cast<u32x2*>(C + co) = o;  // pre-activation (saved for backward)
+        u32x2 g;
+        g.x = pack_bf2(gelu_erf(lo_bf(o.x)), gelu_erf(hi_bf(o.x)));
+        g.y = pack_bf2(gelu_erf(lo_bf(o.y)), gelu_erf(hi_bf(o.y)));
+        *reinterpret_cast<u32x2*>(p.C2 + co) = g;
+        continue;
+      } else if constexpr (EPI == EPI_BIAS_DROP_RES) {
+        // y = bf16(acc + b); yd = bf16(y * keep * scale); z = bf16(yd + residual)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = bf2f(f2bf(v[e]));
+        if (p.dp.enabled) {
+          const uint32_t pair0 = (uint32_t)(((int64_t)m * p.N + n) >> 1);
+          const uint32_t b0 = dropout_bits(pair0, p.dp.seed_lo, p.dp.seed_hi);
+          const uint32_t b1 = dropout_bits(pair0 + 1, p.dp.seed_lo, p.dp.seed_hi);
+          v[0] = bf2f(f2bf(v[0] * keep_factor(b0, 0, p.dp)));
+          v[1] = bf2f(f2bf(v[1] * keep_factor(b0, 1, p.dp)));
+          v[2] = bf2f(f2bf(v[2] * keep_factor(b1, 0, p.dp)));
+          v[3] = bf2f(f2bf(v[3] * keep_factor(b1, 1, p.dp)));
+        }
+        v[0] += lo_bf(xw[q4].x); v[1] += hi_bf(xw[q4].x); v[2] += lo_bf(xw[q4].y); v[3] += hi_bf(xw[q4].y);
+      } else if constexpr (EPI == EPI_RES) {
+        v[0] += lo_bf(xw[q4].x); v[1] += hi_bf(xw[q4].x); v[2] += lo_bf(xw[q4].y); v[3] += hi_bf(xw[q4].y);
+      } else if constexpr (EPI == EPI_DGELU) {
+        v[0] = bf2f(f2bf(v[0])) * gelu_erf_grad(lo_bf(xw[q4].x));
+        v[1] = bf2f(f2bf(v[1])) * gelu_erf_grad(hi_bf(xw[q4].x));
+        v[2] = bf2f(f2bf(v[2])) * gelu_erf_grad(lo_bf(xw[q4].y));
+        v[3] = bf2f(f2bf(v[3])) * gelu_erf_grad(hi_bf(xw[q4].y));
+      }
+      o.x = pack_bf2(v[0], v[1]);
+      o.y = pack_bf2(v[2], v[3]);
+      *reinterpret_cast<u32x2*>(C + co) = o;
+    }
+  }
+}
+
+// ================================================================================================
+// v2 main loop: direct global->LDS DMA (global_load_lds_dwordx4, 1 KiB per wave instruction, swizzle
+// applied on the SOURCE address so the LDS image stays lane-linear — cdna_hip_programming.md rule 21),
+// 8 waves, BMxBNx64 tiles, 2 LDS stages, next stage's DMA in flight across the raw s_barrier with a
+// counted vmcnt (never a drain to 0 inside the loop).
+template <int L, int R>
+__device__ __forceinline__ void dma_tile(bf16_t* tile, const bf16_t* __restrict__ X, int64_t ld, int r0, int Rmax,
+                                         int k0, int wave, int lane) {
+  constexpr int PER_WAVE = R / 64;  // 1-KiB instructions per wave
+#pragma unroll
+  for (int j = 0; j < PER_WAVE; ++j) {
+    const int g = wave * PER_WAVE + j;
+    int row, lc;
+    const bf16_t* src;
+    if constexpr (L == 0) {  // [R rows][64 k], 8 rows per KiB
+      row = g * 8 + (lane >> 3);
+      lc = (lane & 7) ^ swz0(row);
+      const int rr = min(r0 + row, Rmax - 1);
+      src = X + (int64_t)rr * ld + k0 + lc * 8;
+    } else {  // [64 k][R cols], 512/R k-rows per KiB
+      constexpr int RPK = 512 / R;
+      row = g * RPK + (lane * 8) / R;
+      const int pc = ((lane * 8) % R) >> 3;
+      lc = pc ^ swz1(row);
+      const int cc = min(r0 + lc * 8, Rmax - 8);
+      src = X + (int64_t)(k0 + row) * ld + cc;
+    }
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(tile + g * 512), 16, 0, 0);
+  }
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int LA, int LB, int EPI, int BM_, int BN_, int WM, int WN>
+__global__ __launch_bounds__(512, 1) void gemm_dma_kernel(GemmParams p) {
+  constexpr bool SWAP = EPI != EPI_F32_ATOMIC;
+  constexpr int TA = BM_ * 64, TB = BN_ * 64, STAGE = TA + TB;
+  constexpr int MB = BM_ / WM / 32, NB = BN_ / WN / 32;
+  constexpr int G = BM_ / 64 + BN_ / 64;
+  static_assert(WM * WN == 8, "8 waves");
+  static_assert(LA == 0 || BM_ == 128 || BM_ == 256, "k-strided tiles are 128 or 256 wide");
+  static_assert(LB == 0 || BN_ == 128 || BN_ == 256, "k-strided tiles are 128 or 256 wide");
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;
+
+  const int nwg = gridDim.x;
+  const int bid = blockIdx.x;
+  const int xcd = bid & 7;
+  const int q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tm = wg / p.tiles_n, tn = wg % p.tiles_n;
+  const int m0 = tm * BM_, n0 = tn * BN_;
+  const int kbeg = blockIdx.y * p.kps;
+  const int kend = min(p.K, kbeg + p.kps);
+  const int nt = (kend - kbeg) / BK;
+
+  f32x16 acc[MB][NB];
+#pragma unroll
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j) acc[i][j] = f32x16{};
+
+  dma_tile<LA, BM_>(smem, p.A, p.lda, m0, p.M, kbeg, wave, lane);
+  dma_tile<LB, BN_>(smem + TA, p.B, p.ldb, n0, p.N, kbeg, wave, lane);
+  for (int t = 0; t < nt; ++t) {
+    bf16_t* cur = smem + (t & 1) * STAGE;
+    if (t + 1 < nt) {
+      bf16_t* nxt = smem + ((t + 1) & 1) * STAGE;
+      dma_tile<LA, BM_>(nxt, p.A, p.lda, m0, p.M, kbeg + (t + 1) * BK, wave, lane);
+      dma_tile<LB, BN_>(nxt + TA, p.B, p.ldb, n0, p.N, kbeg + (t + 1) * BK, wave, lane);
+      wait_vmcnt<G>();
+    } else {
+      wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    const bf16_t* tA = cur;
+    const bf16_t* tB = cur + TA;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      bf16x8 fa[MB], fb[NB];
+#pragma unroll
+      for (int i = 0; i < MB; ++i) fa[i] = frag<LA, BM_>(tA, wm * (BM_ / WM) + 32 * i, ks, lane);
+#pragma unroll
+      for (int j = 0; j < NB; ++j) fb[j] = frag<LB, BN_>(tB, wn * (BN_ / WN) + 32 * j, ks, lane);
+#pragma unroll
+      for (int i = 0; i < MB; ++i)
+#pragma unroll
+        for (int j = 0; j < NB; ++j) {
+          if constexpr (SWAP) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+          else acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
+        }
+    }
+    __builtin_amdgcn_s_barrier();
+  }
+#pragma unroll
+  for (int i = 0; i < MB; ++i)
+#pragma unroll
+    for (int j = 0; j < NB; ++j)
+      epi_block<EPI, SWAP>(acc[i][j], m0 + wm * (BM_ / WM) + 32 * i, n0 + wn * (BN_ / WN) + 32 * j, lane, p);
+}
+
+template <int LA, int LB, int EPI, int BM_, int BN_, int WM, int WN>
+static void gemm_dma_launch(const GemmParams& p0, int splits, hipStream_t st) {
+  GemmParams p = p0;
+  p.tiles_m = (p.M + BM_ - 1) / BM_;
+  p.tiles_n = (p.N + BN_ - 1) / BN_;
+  if (splits < 1) splits = 1;
+  int kps = (p.K + splits - 1) / splits;
+  kps = (kps + BK - 1) / BK * BK;
+  splits = (p.K + kps - 1) / kps;
+  p.kps = kps;
+  dim3 grid(p.tiles_m * p.tiles_n, splits);
+  hipLaunchKernelGGL((gemm_dma_kernel<LA, LB, EPI, BM_, BN_, WM, WN>), grid, dim3(512), 0, st, p);
+  HSD_CHECK_LAUNCH();
 }
 
 template <int LA, int LB, int EPI>
@@ -182,82 +383,13 @@ __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmParams p) {
   }
 
   // ------------------------------------------------------------------ epilogue
-  const int r = lane & 31, h = lane >> 5;
-  if constexpr (!SWAP) {
-    // acc[i][j]: rows m = m0 + wm*64 + 32i + (reg&3) + 8(reg>>2) + 4h ; col n = n0 + wn*64 + 32j + r
-    float* C = reinterpret_cast<float*>(p.C);
 #pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < 2; ++j) {
-        const int n = n0 + wn * 64 + 32 * j + r;
-        if (n >= p.N) continue;
-#pragma unroll
-        for (int reg = 0; reg < 16; ++reg) {
-          const int m = m0 + wm * 64 + 32 * i + (reg & 3) + 8 * (reg >> 2) + 4 * h;
-          if (m < p.M) atomicAdd(C + (int64_t)m * p.ldc + n, acc[i][j][reg]);
-        }
-      }
-  } else {
-    // acc[i][j]: D[n][m]; lane m = m0 + wm*64 + 32j + r ; n = n0 + wn*64 + 32i + 8*q4 + 4h + e
-    bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
+  for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
-      const int m = m0 + wm * 64 + 32 * j + r;
-      if (m >= p.M) continue;
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int q4 = 0; q4 < 4; ++q4) {
-          const int n = n0 + wn * 64 + 32 * i + 8 * q4 + 4 * h;
-          if (n >= p.N) continue;
-          float v[4] = {acc[i][j][4 * q4], acc[i][j][4 * q4 + 1], acc[i][j][4 * q4 + 2], acc[i][j][4 * q4 + 3]};
-          const int64_t co = (int64_t)m * p.ldc + n;
-          if constexpr (EPI == EPI_BIAS || EPI == EPI_BIAS_GELU || EPI == EPI_BIAS_DROP_RES) {
-            u32x2 bw = *reinterpret_cast<const u32x2*>(p.bias + n);
-            v[0] += lo_bf(bw.x); v[1] += hi_bf(bw.x); v[2] += lo_bf(bw.y); v[3] += hi_bf(bw.y);
-          }
-          u32x2 o;
-          if constexpr (EPI == EPI_BIAS_GELU) {
-            o.x = pack_bf2(v[0], v[1]);
-            o.y = pack_bf2(v[2], v[3]);
-            *reinterpret_cast<u32x2*>(C + co) = o;  // pre-activation (saved for backward)
-            u32x2 g;
-            g.x = pack_bf2(gelu_erf(lo_bf(o.x)), gelu_erf(hi_bf(o.x)));
-            g.y = pack_bf2(gelu_erf(lo_bf(o.y)), gelu_erf(hi_bf(o.y)));
-            *reinterpret_cast<u32x2*>(p.C2 + co) = g;
-            continue;
-          } else if constexpr (EPI == EPI_BIAS_DROP_RES) {
-            // y = bf16(acc + b); yd = bf16(y * keep * scale); z = bf16(yd + residual)
-#pragma unroll
-            for (int e = 0; e < 4; ++e) v[e] = bf2f(f2bf(v[e]));
-            if (p.dp.enabled) {
-              const uint32_t pair0 = (uint32_t)(((int64_t)m * p.N + n) >> 1);
-              const uint32_t b0 = dropout_bits(pair0, p.dp.seed_lo, p.dp.seed_hi);
-              const uint32_t b1 = dropout_bits(pair0 + 1, p.dp.seed_lo, p.dp.seed_hi);
-              v[0] = bf2f(f2bf(v[0] * keep_factor(b0, 0, p.dp)));
-              v[1] = bf2f(f2bf(v[1] * keep_factor(b0, 1, p.dp)));
-              v[2] = bf2f(f2bf(v[2] * keep_factor(b1, 0, p.dp)));
-              v[3] = bf2f(f2bf(v[3] * keep_factor(b1, 1, p.dp)));
-            }
-            u32x2 rw = *reinterpret_cast<const u32x2*>(p.aux + (int64_t)m * p.ldaux + n);
-            v[0] += lo_bf(rw.x); v[1] += hi_bf(rw.x); v[2] += lo_bf(rw.y); v[3] += hi_bf(rw.y);
-          } else if constexpr (EPI == EPI_RES) {
-            u32x2 rw = *reinterpret_cast<const u32x2*>(p.aux + (int64_t)m * p.ldaux + n);
-            v[0] += lo_bf(rw.x); v[1] += hi_bf(rw.x); v[2] += lo_bf(rw.y); v[3] += hi_bf(rw.y);
-          } else if constexpr (EPI == EPI_DGELU) {
-            u32x2 yw = *reinterpret_cast<const u32x2*>(p.aux + (int64_t)m * p.ldaux + n);
-            v[0] = bf2f(f2bf(v[0])) * gelu_erf_grad(lo_bf(yw.x));
-            v[1] = bf2f(f2bf(v[1])) * gelu_erf_grad(hi_bf(yw.x));
-            v[2] = bf2f(f2bf(v[2])) * gelu_erf_grad(lo_bf(yw.y));
-            v[3] = bf2f(f2bf(v[3])) * gelu_erf_grad(hi_bf(yw.y));
-          }
-          o.x = pack_bf2(v[0], v[1]);
-          o.y = pack_bf2(v[2], v[3]);
-          *reinterpret_cast<u32x2*>(C + co) = o;
-        }
+      if constexpr (SWAP) epi_block<EPI, true>(acc[i][j], m0 + wm * 64 + 32 * j, n0 + wn * 64 + 32 * i, lane, p);
+      else epi_block<EPI, false>(acc[i][j], m0 + wm * 64 + 32 * i, n0 + wn * 64 + 32 * j, lane, p);
     }
-  }
 }
 
 template <int LA, int LB, int EPI>
@@ -283,6 +415,29 @@ void launch_gemm(int la, int lb, int epi, const bf16_t* A, int64_t lda, const bf
   p.A = A; p.lda = lda; p.B = B; p.ldb = ldb; p.M = M; p.N = N; p.K = K; p.C = C; p.ldc = ldc;
   p.bias = bias; p.aux = aux; p.ldaux = ldaux; p.C2 = C2;
   p.dp = make_dropout(p_drop, seed);
+  const bool dma = (K % 64 == 0) && (M >= 128) && (N >= 128) && !getenv("HSD_GEMM_V1");
+  if (dma) {
+    if (epi == EPI_F32_ATOMIC) {
+      if (la == 1 && lb == 1) { gemm_dma_launch<1, 1, EPI_F32_ATOMIC, 256, 128, 4, 2>(p, splits, st); return; }
+      if (la == 0 && lb == 0) { gemm_dma_launch<0, 0, EPI_F32_ATOMIC, 256, 128, 4, 2>(p, splits, st); return; }
+      if (la == 0 && lb == 1) { gemm_dma_launch<0, 1, EPI_F32_ATOMIC, 256, 128, 4, 2>(p, splits, st); return; }
+    } else if (la == 0 && lb == 0) {
+      switch (epi) {
+        case EPI_STORE: gemm_dma_launch<0, 0, EPI_STORE, 256, 192, 4, 2>(p, 1, st); return;
+        case EPI_BIAS: gemm_dma_launch<0, 0, EPI_BIAS, 256, 192, 4, 2>(p, 1, st); return;
+        case EPI_BIAS_GELU: gemm_dma_launch<0, 0, EPI_BIAS_GELU, 256, 192, 4, 2>(p, 1, st); return;
+        case EPI_BIAS_DROP_RES: gemm_dma_launch<0, 0, EPI_BIAS_DROP_RES, 256, 192, 4, 2>(p, 1, st); return;
+        default: break;
+      }
+    } else if (la == 0 && lb == 1) {
+      switch (epi) {
+        case EPI_STORE: gemm_dma_launch<0, 1, EPI_STORE, 256, 128, 4, 2>(p, 1, st); return;
+        case EPI_RES: gemm_dma_launch<0, 1, EPI_RES, 256, 128, 4, 2>(p, 1, st); return;
+        case EPI_DGELU: gemm_dma_launch<0, 1, EPI_DGELU, 256, 128, 4, 2>(p, 1, st); return;
+        default: break;
+      }
+    }
+  }
   if (epi == EPI_F32_ATOMIC) {
     if (la == 1 && lb == 1) gemm_launch<1, 1, EPI_F32_ATOMIC>(p, splits, st);
     else if (la == 0 && lb == 0) gemm_launch<0, 0, EPI_F32_ATOMIC>(p, splits, st);
