@@ -213,6 +213,17 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int64_t la, int64_t
                    C2.has_value() ? BF(*C2) : nullptr, p, (uint64_t)seed, (int)splits, cur_stream());
 }
 
+void gemm_variant(torch::Tensor A, torch::Tensor B, torch::Tensor C, int64_t la, int64_t lb, int64_t variant) {
+  const int64_t M = la == 0 ? A.size(0) : A.size(1);
+  const int64_t K = la == 0 ? A.size(1) : A.size(0);
+  const int64_t N = lb == 0 ? B.size(0) : B.size(1);
+  TORCH_CHECK(C.size(0) == M && C.size(1) == N && K % 64 == 0 && M >= 256 && N >= 256, "gemm_variant shapes");
+  TORCH_CHECK(A.scalar_type() == torch::kBFloat16 && B.scalar_type() == torch::kBFloat16 &&
+              C.scalar_type() == torch::kBFloat16, "bf16");
+  hsd::launch_gemm_variant((int)la, (int)lb, (int)variant, CBF(A), A.stride(0), CBF(B), B.stride(0), (int)M, (int)N,
+                           (int)K, BF(C), C.stride(0), cur_stream());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -229,4 +240,5 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_fwd", &attn_fwd);
   m.def("attn_bwd", &attn_bwd);
   m.def("gemm", &gemm);
+  m.def("gemm_variant", &gemm_variant);
 }

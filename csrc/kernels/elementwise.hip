@@ -20,43 +20,64 @@ __global__ __launch_bounds__(256) void gelu_fwd_kernel(const bf16_t* __restrict_
   }
 }
 
-// block: 256 threads; thread t owns columns [8t, 8t+8) of a 2048-column group (blockIdx.y);
-// blockIdx.x walks `rows_per_block` rows.
+// Column sums (bias gradients). Block = 256 threads = 64 column chunks (8 columns each, 512 columns)
+// x 4 row groups; each thread walks rows rg, rg+4, ... of the block's row range with 4 rows' loads in
+// flight, then the 4 row groups are reduced through LDS -> one atomic per column per block.
+// kGelu: also writes da = dg * gelu'(y) (the FFN1 dgrad input) and sums da instead of x.
 template <bool kGelu>
 __global__ __launch_bounds__(256) void colsum_kernel(const bf16_t* __restrict__ x, const bf16_t* __restrict__ y,
                                                      bf16_t* __restrict__ out, float* __restrict__ dbias, int rows,
                                                      int N, int rows_per_block) {
-  const int col = (blockIdx.y * 256 + threadIdx.x) * 8;
-  if (col >= N) return;
-  const int r0 = blockIdx.x * rows_per_block;
+  __shared__ float red[4][512 + 8];
+  const int cc = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int col = blockIdx.x * 512 + cc * 8;
+  const bool active = col < N;
+  const int r0 = blockIdx.y * rows_per_block;
   const int r1 = min(rows, r0 + rows_per_block);
   float acc[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  for (int r = r0; r < r1; ++r) {
-    size_t off = (size_t)r * N + col;
-    u32x4 w = *reinterpret_cast<const u32x4*>(x + off);
-    if constexpr (kGelu) {
-      u32x4 yy = *reinterpret_cast<const u32x4*>(y + off);
-      u32x4 o;
+  if (active) {
+    for (int rb = r0 + rg; rb < r1; rb += 16) {
+      u32x4 w[4], yy[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float a = lo_bf(w[k]) * gelu_erf_grad(lo_bf(yy[k]));
-        float b = hi_bf(w[k]) * gelu_erf_grad(hi_bf(yy[k]));
-        o[k] = pack_bf2(a, b);
-        acc[2 * k] += lo_bf(o[k]);
-        acc[2 * k + 1] += hi_bf(o[k]);
+      for (int u = 0; u < 4; ++u) {
+        const int r = rb + 4 * u;
+        if (r < r1) {
+          w[u] = *reinterpret_cast<const u32x4*>(x + (size_t)r * N + col);
+          if constexpr (kGelu) yy[u] = *reinterpret_cast<const u32x4*>(y + (size_t)r * N + col);
+        }
       }
-      *reinterpret_cast<u32x4*>(out + off) = o;
-    } else {
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        acc[2 * k] += lo_bf(w[k]);
-        acc[2 * k + 1] += hi_bf(w[k]);
+      for (int u = 0; u < 4; ++u) {
+        const int r = rb + 4 * u;
+        if (r >= r1) continue;
+        if constexpr (kGelu) {
+          u32x4 o;
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            o[k] = pack_bf2(lo_bf(w[u][k]) * gelu_erf_grad(lo_bf(yy[u][k])),
+                            hi_bf(w[u][k]) * gelu_erf_grad(hi_bf(yy[u][k])));
+            acc[2 * k] += lo_bf(o[k]);
+            acc[2 * k + 1] += hi_bf(o[k]);
+          }
+          *reinterpret_cast<u32x4*>(out + (size_t)r * N + col) = o;
+        } else {
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            acc[2 * k] += lo_bf(w[u][k]);
+            acc[2 * k + 1] += hi_bf(w[u][k]);
+          }
+        }
       }
     }
   }
-  if (dbias) {
+  if (dbias == nullptr) return;
 #pragma unroll
-    for (int k = 0; k < 8; ++k) atomicAdd(dbias + col + k, acc[k]);
+  for (int k = 0; k < 8; ++k) red[rg][cc * 8 + k] = acc[k];
+  __syncthreads();
+  // 256 threads x 2 columns each
+  for (int c = threadIdx.x; c < 512; c += 256) {
+    const int gc = blockIdx.x * 512 + c;
+    if (gc < N) atomicAdd(dbias + gc, red[0][c] + red[1][c] + red[2][c] + red[3][c]);
   }
 }
 
@@ -90,11 +111,12 @@ void launch_gelu_fwd(const bf16_t* y, bf16_t* g, int64_t n, hipStream_t st) {
 
 static void colsum_launch(bool gelu, const bf16_t* x, const bf16_t* y, bf16_t* out, float* dbias, int rows, int N,
                           hipStream_t st) {
-  int gy = (N + 2047) / 2048;
-  // aim for ~1024 blocks total
-  int want_x = max(1, 1024 / gy);
-  int rpb = max(16, (rows + want_x - 1) / want_x);
-  int gx = (rows + rpb - 1) / rpb;
+  const int gx = (N + 511) / 512;
+  // ~2048 blocks (8 per CU); rows per block a multiple of 16 (4 row groups x 4 rows in flight)
+  int want_y = max(1, 2048 / gx);
+  int rpb = max(16, (rows + want_y - 1) / want_y);
+  rpb = (rpb + 15) / 16 * 16;
+  const int gy = (rows + rpb - 1) / rpb;
   if (gelu)
     hipLaunchKernelGGL((colsum_kernel<true>), dim3(gx, gy), dim3(256), 0, st, x, y, out, dbias, rows, N, rpb);
   else

@@ -230,16 +230,17 @@ __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int LA, int LB, int EPI, int BM_, int BN_, int WM, int WN>
+template <int LA, int LB, int EPI, int BM_, int BN_, int WM, int WN, int NS>
 __global__ __launch_bounds__(512, 1) void gemm_dma_kernel(GemmParams p) {
   constexpr bool SWAP = EPI != EPI_F32_ATOMIC;
   constexpr int TA = BM_ * 64, TB = BN_ * 64, STAGE = TA + TB;
   constexpr int MB = BM_ / WM / 32, NB = BN_ / WN / 32;
-  constexpr int G = BM_ / 64 + BN_ / 64;
+  constexpr int G = BM_ / 64 + BN_ / 64;  // DMA instructions per wave per stage
   static_assert(WM * WN == 8, "8 waves");
   static_assert(LA == 0 || BM_ == 128 || BM_ == 256, "k-strided tiles are 128 or 256 wide");
   static_assert(LB == 0 || BN_ == 128 || BN_ == 256, "k-strided tiles are 128 or 256 wide");
-  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * STAGE];
+  static_assert(NS >= 2 && NS <= 4, "2..4 LDS stages");
+  __shared__ __attribute__((aligned(16))) bf16_t smem[NS * STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
@@ -261,21 +262,32 @@ __global__ __launch_bounds__(512, 1) void gemm_dma_kernel(GemmParams p) {
 #pragma unroll
     for (int j = 0; j < NB; ++j) acc[i][j] = f32x16{};
 
-  dma_tile<LA, BM_>(smem, p.A, p.lda, m0, p.M, kbeg, wave, lane);
-  dma_tile<LB, BN_>(smem + TA, p.B, p.ldb, n0, p.N, kbeg, wave, lane);
+  // prologue: NS-1 stages in flight
+#pragma unroll
+  for (int s = 0; s < NS - 1; ++s) {
+    if (s < nt) {
+      dma_tile<LA, BM_>(smem + s * STAGE, p.A, p.lda, m0, p.M, kbeg + s * BK, wave, lane);
+      dma_tile<LB, BN_>(smem + s * STAGE + TA, p.B, p.ldb, n0, p.N, kbeg + s * BK, wave, lane);
+    }
+  }
+  int slot = 0;
   for (int t = 0; t < nt; ++t) {
-    bf16_t* cur = smem + (t & 1) * STAGE;
-    if (t + 1 < nt) {
-      bf16_t* nxt = smem + ((t + 1) & 1) * STAGE;
-      dma_tile<LA, BM_>(nxt, p.A, p.lda, m0, p.M, kbeg + (t + 1) * BK, wave, lane);
-      dma_tile<LB, BN_>(nxt + TA, p.B, p.ldb, n0, p.N, kbeg + (t + 1) * BK, wave, lane);
-      wait_vmcnt<G>();
+    const int ahead = t + NS - 1;
+    if (ahead < nt) {
+      const int ns = ahead % NS;
+      dma_tile<LA, BM_>(smem + ns * STAGE, p.A, p.lda, m0, p.M, kbeg + ahead * BK, wave, lane);
+      dma_tile<LB, BN_>(smem + ns * STAGE + TA, p.B, p.ldb, n0, p.N, kbeg + ahead * BK, wave, lane);
+      wait_vmcnt<(NS - 1) * G>();
     } else {
-      wait_vmcnt<0>();
+      // stages newer than t still in flight: nt-1-t (< NS-1)
+      const int newer = nt - 1 - t;
+      if constexpr (NS >= 4) { if (newer == 2) wait_vmcnt<2 * G>(); }
+      if constexpr (NS >= 3) { if (newer == 1) wait_vmcnt<G>(); }
+      if (newer == 0) wait_vmcnt<0>();
     }
     __builtin_amdgcn_s_barrier();
-    const bf16_t* tA = cur;
-    const bf16_t* tB = cur + TA;
+    const bf16_t* tA = smem + slot * STAGE;
+    const bf16_t* tB = tA + TA;
 #pragma unroll
     for (int ks = 0; ks < 4; ++ks) {
       bf16x8 fa[MB], fb[NB];
@@ -292,6 +304,7 @@ __global__ __launch_bounds__(512, 1) void gemm_dma_kernel(GemmParams p) {
         }
     }
     __builtin_amdgcn_s_barrier();
+    slot = slot + 1 == NS ? 0 : slot + 1;
   }
 #pragma unroll
   for (int i = 0; i < MB; ++i)
@@ -300,7 +313,7 @@ __global__ __launch_bounds__(512, 1) void gemm_dma_kernel(GemmParams p) {
       epi_block<EPI, SWAP>(acc[i][j], m0 + wm * (BM_ / WM) + 32 * i, n0 + wn * (BN_ / WN) + 32 * j, lane, p);
 }
 
-template <int LA, int LB, int EPI, int BM_, int BN_, int WM, int WN>
+template <int LA, int LB, int EPI, int BM_, int BN_, int WM, int WN, int NS = 2>
 static void gemm_dma_launch(const GemmParams& p0, int splits, hipStream_t st) {
   GemmParams p = p0;
   p.tiles_m = (p.M + BM_ - 1) / BM_;
@@ -311,7 +324,7 @@ static void gemm_dma_launch(const GemmParams& p0, int splits, hipStream_t st) {
   splits = (p.K + kps - 1) / kps;
   p.kps = kps;
   dim3 grid(p.tiles_m * p.tiles_n, splits);
-  hipLaunchKernelGGL((gemm_dma_kernel<LA, LB, EPI, BM_, BN_, WM, WN>), grid, dim3(512), 0, st, p);
+  hipLaunchKernelGGL((gemm_dma_kernel<LA, LB, EPI, BM_, BN_, WM, WN, NS>), grid, dim3(512), 0, st, p);
   HSD_CHECK_LAUNCH();
 }
 
@@ -405,6 +418,37 @@ static void gemm_launch(const GemmParams& p0, int splits, hipStream_t st) {
   dim3 grid(p.tiles_m * p.tiles_n, splits);
   hipLaunchKernelGGL((gemm_kernel<LA, LB, EPI>), grid, dim3(256), 0, st, p);
   HSD_CHECK_LAUNCH();
+}
+
+// Sweep entry (tools/bench_gemm.py): fixed EPI_STORE, config chosen by `variant`.
+void launch_gemm_variant(int la, int lb, int variant, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb,
+                         int M, int N, int K, bf16_t* C, int64_t ldc, hipStream_t st) {
+  GemmParams p{};
+  p.A = A; p.lda = lda; p.B = B; p.ldb = ldb; p.M = M; p.N = N; p.K = K; p.C = C; p.ldc = ldc;
+  p.dp = make_dropout(0.0, 0);
+  if (la == 0 && lb == 0) {
+    switch (variant) {
+      case 0: gemm_dma_launch<0, 0, EPI_STORE, 256, 192, 4, 2, 2>(p, 1, st); break;
+      case 1: gemm_dma_launch<0, 0, EPI_STORE, 256, 128, 4, 2, 3>(p, 1, st); break;
+      case 2: gemm_dma_launch<0, 0, EPI_STORE, 256, 128, 4, 2, 2>(p, 1, st); break;
+      case 3: gemm_dma_launch<0, 0, EPI_STORE, 256, 256, 2, 4, 2>(p, 1, st); break;
+      case 4: gemm_dma_launch<0, 0, EPI_STORE, 128, 256, 2, 4, 3>(p, 1, st); break;
+      case 5: gemm_dma_launch<0, 0, EPI_STORE, 192, 256, 2, 4, 2>(p, 1, st); break;
+      default: abort();
+    }
+  } else if (la == 0 && lb == 1) {
+    switch (variant) {
+      case 0: gemm_dma_launch<0, 1, EPI_STORE, 256, 128, 4, 2, 2>(p, 1, st); break;
+      case 1: gemm_dma_launch<0, 1, EPI_STORE, 256, 128, 4, 2, 3>(p, 1, st); break;
+      case 2: gemm_dma_launch<0, 1, EPI_STORE, 128, 256, 2, 4, 3>(p, 1, st); break;
+      case 3: gemm_dma_launch<0, 1, EPI_STORE, 256, 256, 2, 4, 2>(p, 1, st); break;
+      case 4: gemm_dma_launch<0, 1, EPI_STORE, 192, 256, 2, 4, 2>(p, 1, st); break;
+      case 5: gemm_dma_launch<0, 1, EPI_STORE, 128, 256, 2, 4, 2>(p, 1, st); break;
+      default: abort();
+    }
+  } else {
+    abort();
+  }
 }
 
 // Public entry: layouts + epilogue chosen at run time.

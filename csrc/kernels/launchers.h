@@ -49,4 +49,6 @@ namespace hsd {
 void launch_gemm(int la, int lb, int epi, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, int M, int N,
                  int K, void* C, int64_t ldc, const bf16_t* bias, const bf16_t* aux, int64_t ldaux, bf16_t* C2,
                  double p_drop, uint64_t seed, int splits, hipStream_t st);
+void launch_gemm_variant(int la, int lb, int variant, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb,
+                         int M, int N, int K, bf16_t* C, int64_t ldc, hipStream_t st);
 }  // namespace hsd

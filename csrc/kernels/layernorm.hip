@@ -93,18 +93,101 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
   }
 }
 
-// Block = 4 waves; block walks `rows_per_block` rows (wave-strided) accumulating column partials.
+// Block = 4 waves; block walks `rows_per_block` rows (wave-strided, TWO rows in flight per wave so the
+// second row's loads overlap the first row's reductions) accumulating column partials in registers.
+template <int NCH>
+__device__ __forceinline__ void ln_bwd_load(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ z, int row,
+                                            int H, int lane, u32x2 (&zw)[NCH], u32x2 (&dw)[NCH]) {
+  const int nq = H >> 2;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int c = lane + 64 * i;
+    if (c < nq) {
+      const size_t off = (size_t)row * H + 4 * c;
+      zw[i] = *reinterpret_cast<const u32x2*>(z + off);
+      dw[i] = *reinterpret_cast<const u32x2*>(dout + off);
+    } else {
+      zw[i] = u32x2{0, 0};
+      dw[i] = u32x2{0, 0};
+    }
+  }
+}
+
+template <int NCH>
+__device__ __forceinline__ void ln_bwd_row(const u32x2 (&zw)[NCH], const u32x2 (&dw)[NCH], float mean, float rstd,
+                                           const float (&gam)[NCH][4], int row, int H, int lane,
+                                           bf16_t* __restrict__ dz_out, bf16_t* __restrict__ dy_out,
+                                           const bf16_t* __restrict__ dres_add, const DropoutParams& dp,
+                                           float (&acc_g)[NCH][4], float (&acc_b)[NCH][4], float (&acc_db)[NCH][4]) {
+  const int nq = H >> 2;
+  float xh[NCH][4], g[NCH][4];
+  float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const float zz[4] = {lo_bf(zw[i].x), hi_bf(zw[i].x), lo_bf(zw[i].y), hi_bf(zw[i].y)};
+    const float d[4] = {lo_bf(dw[i].x), hi_bf(dw[i].x), lo_bf(dw[i].y), hi_bf(dw[i].y)};
+    const bool ok = lane + 64 * i < nq;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      xh[i][k] = ok ? (zz[k] - mean) * rstd : 0.f;
+      g[i][k] = d[k] * gam[i][k];
+      s1 += g[i][k];
+      s2 += g[i][k] * xh[i][k];
+      acc_g[i][k] += d[k] * xh[i][k];
+      acc_b[i][k] += d[k];
+    }
+  }
+  s1 = wave_sum(s1) / (float)H;
+  s2 = wave_sum(s2) / (float)H;
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int c = lane + 64 * i;
+    if (c >= nq) continue;
+    const size_t off = (size_t)row * H + 4 * c;
+    float dz[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) dz[k] = rstd * (g[i][k] - s1 - xh[i][k] * s2);
+    if (dres_add) {
+      u32x2 r = *reinterpret_cast<const u32x2*>(dres_add + off);
+      dz[0] += lo_bf(r.x); dz[1] += hi_bf(r.x); dz[2] += lo_bf(r.y); dz[3] += hi_bf(r.y);
+    }
+    u32x2 o;
+    o.x = pack_bf2(dz[0], dz[1]);
+    o.y = pack_bf2(dz[2], dz[3]);
+    if (dz_out) *reinterpret_cast<u32x2*>(dz_out + off) = o;
+    if (dy_out) {
+      float dy[4] = {dz[0], dz[1], dz[2], dz[3]};
+      if (dp.enabled) {
+        const uint32_t pair0 = (uint32_t)(off >> 1);
+        const uint32_t b0 = dropout_bits(pair0, dp.seed_lo, dp.seed_hi);
+        const uint32_t b1 = dropout_bits(pair0 + 1, dp.seed_lo, dp.seed_hi);
+        dy[0] *= keep_factor(b0, 0, dp);
+        dy[1] *= keep_factor(b0, 1, dp);
+        dy[2] *= keep_factor(b1, 0, dp);
+        dy[3] *= keep_factor(b1, 1, dp);
+      }
+      u32x2 yo;
+      yo.x = pack_bf2(dy[0], dy[1]);
+      yo.y = pack_bf2(dy[2], dy[3]);
+      *reinterpret_cast<u32x2*>(dy_out + off) = yo;
+      // bias grad sums the bf16-rounded dy that the dgrad GEMM consumes
+      acc_db[i][0] += lo_bf(yo.x); acc_db[i][1] += hi_bf(yo.x);
+      acc_db[i][2] += lo_bf(yo.y); acc_db[i][3] += hi_bf(yo.y);
+    }
+  }
+}
+
 template <int NCH>
 __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ z,
                                                      const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
                                                      const bf16_t* __restrict__ gamma,
                                                      bf16_t* __restrict__ dz_out,    // residual grad (may be null)
-                                                     bf16_t* __restrict__ dy_out,    // grad into GEMM output (may alias dz_out if no dropout)
-                                                     const bf16_t* __restrict__ dres_add,  // extra grad to add to dz (may be null)
+                                                     bf16_t* __restrict__ dy_out,    // grad into GEMM output (may be null)
+                                                     const bf16_t* __restrict__ dres_add,  // extra grad added to dz
                                                      float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                      float* __restrict__ dbias,      // may be null
                                                      int rows, int H, int rows_per_block, DropoutParams dp) {
-  __shared__ float red[kLnWaves][3][256 * 4 / 4];  // per wave: 3 x (H up to 1024 per pass) -> reuse below
+  __shared__ float red[kLnWaves][3][256];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int nq = H >> 2;
@@ -112,7 +195,7 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
   float acc_g[NCH][4], acc_b[NCH][4], acc_db[NCH][4];
 #pragma unroll
   for (int i = 0; i < NCH; ++i) {
-    int c = lane + 64 * i;
+    const int c = lane + 64 * i;
 #pragma unroll
     for (int k = 0; k < 4; ++k) { acc_g[i][k] = acc_b[i][k] = acc_db[i][k] = 0.f; gam[i][k] = 0.f; }
     if (c < nq) {
@@ -122,77 +205,25 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
   }
   const int row0 = blockIdx.x * rows_per_block;
   const int row_end = min(rows, row0 + rows_per_block);
-  for (int row = row0 + wid; row < row_end; row += kLnWaves) {
-    const float mean = mean_in[row], rstd = rstd_in[row];
-    float xh[NCH][4], g[NCH][4], d[NCH][4];
-    float s1 = 0.f, s2 = 0.f;
-#pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      int c = lane + 64 * i;
-      if (c < nq) {
-        size_t off = (size_t)row * H + 4 * c;
-        u32x2 zw = *reinterpret_cast<const u32x2*>(z + off);
-        u32x2 dw = *reinterpret_cast<const u32x2*>(dout + off);
-        float zz[4] = {lo_bf(zw.x), hi_bf(zw.x), lo_bf(zw.y), hi_bf(zw.y)};
-        d[i][0] = lo_bf(dw.x); d[i][1] = hi_bf(dw.x); d[i][2] = lo_bf(dw.y); d[i][3] = hi_bf(dw.y);
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          xh[i][k] = (zz[k] - mean) * rstd;
-          g[i][k] = d[i][k] * gam[i][k];
-          s1 += g[i][k];
-          s2 += g[i][k] * xh[i][k];
-          acc_g[i][k] += d[i][k] * xh[i][k];
-          acc_b[i][k] += d[i][k];
-        }
-      } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) xh[i][k] = g[i][k] = d[i][k] = 0.f;
-      }
+  for (int row = row0 + wid; row < row_end; row += 2 * kLnWaves) {
+    const int row2 = row + kLnWaves;
+    const bool two = row2 < row_end;
+    u32x2 za[NCH], da[NCH], zb[NCH], db[NCH];
+    ln_bwd_load<NCH>(dout, z, row, H, lane, za, da);
+    const float ma = mean_in[row], ra = rstd_in[row];
+    float mb = 0.f, rb = 0.f;
+    if (two) {
+      ln_bwd_load<NCH>(dout, z, row2, H, lane, zb, db);
+      mb = mean_in[row2];
+      rb = rstd_in[row2];
     }
-    s1 = wave_sum(s1) / (float)H;
-    s2 = wave_sum(s2) / (float)H;
-#pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      int c = lane + 64 * i;
-      if (c < nq) {
-        size_t off = (size_t)row * H + 4 * c;
-        float dz[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) dz[k] = rstd * (g[i][k] - s1 - xh[i][k] * s2);
-        if (dres_add) {
-          u32x2 r = *reinterpret_cast<const u32x2*>(dres_add + off);
-          dz[0] += lo_bf(r.x); dz[1] += hi_bf(r.x); dz[2] += lo_bf(r.y); dz[3] += hi_bf(r.y);
-        }
-        u32x2 o;
-        o.x = pack_bf2(dz[0], dz[1]);
-        o.y = pack_bf2(dz[2], dz[3]);
-        if (dz_out) *reinterpret_cast<u32x2*>(dz_out + off) = o;
-        if (dy_out) {
-          float dy[4] = {dz[0], dz[1], dz[2], dz[3]};
-          if (dp.enabled) {
-            uint32_t pair0 = (uint32_t)(off >> 1);
-            uint32_t b0 = dropout_bits(pair0, dp.seed_lo, dp.seed_hi);
-            uint32_t b1 = dropout_bits(pair0 + 1, dp.seed_lo, dp.seed_hi);
-            dy[0] *= keep_factor(b0, 0, dp);
-            dy[1] *= keep_factor(b0, 1, dp);
-            dy[2] *= keep_factor(b1, 0, dp);
-            dy[3] *= keep_factor(b1, 1, dp);
-          }
-          u32x2 yo;
-          yo.x = pack_bf2(dy[0], dy[1]);
-          yo.y = pack_bf2(dy[2], dy[3]);
-          *reinterpret_cast<u32x2*>(dy_out + off) = yo;
-          // bias grad sums the bf16-rounded dy that the dgrad GEMM consumes
-          acc_db[i][0] += lo_bf(yo.x); acc_db[i][1] += hi_bf(yo.x);
-          acc_db[i][2] += lo_bf(yo.y); acc_db[i][3] += hi_bf(yo.y);
-        }
-      }
-    }
+    ln_bwd_row<NCH>(za, da, ma, ra, gam, row, H, lane, dz_out, dy_out, dres_add, dp, acc_g, acc_b, acc_db);
+    if (two) ln_bwd_row<NCH>(zb, db, mb, rb, gam, row2, H, lane, dz_out, dy_out, dres_add, dp, acc_g, acc_b, acc_db);
   }
-  // cross-wave reduction through LDS, one column chunk-pass at a time (H up to 256*NCH*... )
+  // cross-wave reduction through LDS, one 256-column pass at a time; one atomic per column per block
 #pragma unroll
   for (int i = 0; i < NCH; ++i) {
-    int c = lane + 64 * i;
+    const int c = lane + 64 * i;
     __syncthreads();
 #pragma unroll
     for (int k = 0; k < 4; ++k) {
@@ -201,16 +232,13 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
       red[wid][2][lane * 4 + k] = acc_db[i][k];
     }
     __syncthreads();
-    if (c < nq) {
-      // wave w reduces quantity w (w < 3), all 4 elements of this lane's chunk
-      if (wid < 3 && (wid < 2 || dbias != nullptr)) {
-        float* dst = wid == 0 ? dgamma : (wid == 1 ? dbeta : dbias);
+    if (c < nq && wid < 3 && (wid < 2 || dbias != nullptr)) {
+      float* dst = wid == 0 ? dgamma : (wid == 1 ? dbeta : dbias);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          float t = red[0][wid][lane * 4 + k] + red[1][wid][lane * 4 + k] + red[2][wid][lane * 4 + k] +
-                    red[3][wid][lane * 4 + k];
-          atomicAdd(dst + 4 * c + k, t);
-        }
+      for (int k = 0; k < 4; ++k) {
+        const float t = red[0][wid][lane * 4 + k] + red[1][wid][lane * 4 + k] + red[2][wid][lane * 4 + k] +
+                        red[3][wid][lane * 4 + k];
+        atomicAdd(dst + 4 * c + k, t);
       }
     }
   }
@@ -243,10 +271,10 @@ template <int NCH>
 static void ln_bwd_t(const bf16_t* dout, const bf16_t* z, const float* mean, const float* rstd, const bf16_t* gamma,
                      bf16_t* dz, bf16_t* dy, const bf16_t* dres_add, float* dgamma, float* dbeta, float* dbias,
                      int rows, int H, const DropoutParams& dp, hipStream_t st) {
-  int rpb = 128;
+  // ~1024 blocks (4 per CU, 16 waves/CU) of 4 waves x 2 rows in flight; one atomic per column per block
+  int rpb = max(2 * kLnWaves, (rows + 1023) / 1024);
+  rpb = (rpb + 2 * kLnWaves - 1) / (2 * kLnWaves) * (2 * kLnWaves);
   int blocks = (rows + rpb - 1) / rpb;
-  if (blocks < 512 && rows > 512 * 8) { rpb = (rows + 511) / 512; blocks = (rows + rpb - 1) / rpb; }
-  if (blocks < 256) { rpb = max(kLnWaves, (rows + 255) / 256); blocks = (rows + rpb - 1) / rpb; }
   hipLaunchKernelGGL((ln_bwd_kernel<NCH>), dim3(blocks), dim3(256), 0, st, dout, z, mean, rstd, gamma, dz, dy,
                      dres_add, dgamma, dbeta, dbias, rows, H, rpb, dp);
 }

@@ -47,6 +47,9 @@ for name, (N, K) in {"qkv": (2304, 768), "out": (768, 768), "ffn1": (3072, 768),
         if tiles * sp > 4096:
             break
         r[f"wgrad_hsd_s{sp}"] = fl / bench(lambda: C_.gemm(dy, x, gw, 1, 1, 6, None, None, None, 0.0, 0, sp)) / 1e12
+    for v in range(6):
+        r[f"fwd_v{v}"] = fl / bench(lambda: C_.gemm_variant(x, w, y, 0, 0, v)) / 1e12
+        r[f"dgrad_v{v}"] = fl / bench(lambda: C_.gemm_variant(dy, w, dx, 0, 1, v)) / 1e12
     import os
     os.environ["HSD_GEMM_V1"] = "1"
     r["fwd_hsd_v1"] = fl / bench(lambda: C_.gemm(x, w, y, 0, 0, 1, b, None, None, 0.0, 0, 1)) / 1e12
