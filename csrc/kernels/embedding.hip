@@ -95,7 +95,10 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
 }
 
 // grid: (S positions) x (batch chunks). Block = 4 waves; wave w handles batch rows b = chunk*bpc + w, +4, ...
-template <int NCH>
+// Element mapping in the backward is e = lane + 64*i (NE = H/64 elements per lane) so each fp32 atomic
+// wave instruction into the word-gradient row is 256 contiguous bytes (full atomic rate,
+// MI355X_MICROARCH.md 'Global float atomics' access-shape row).
+template <int NE>
 __global__ __launch_bounds__(256) void embed_bwd_kernel(const bf16_t* __restrict__ dout, const int64_t* __restrict__ ids,
                                                         const int64_t* __restrict__ pos_ids, const int64_t* __restrict__ type_ids,
                                                         const bf16_t* __restrict__ word, const bf16_t* __restrict__ pos,
@@ -105,120 +108,76 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const bf16_t* __restrict
                                                         float* __restrict__ gtype, float* __restrict__ ggamma,
                                                         float* __restrict__ gbeta, int B, int S, int H, int bpc,
                                                         int pos_is_arange, DropoutParams dp) {
-  __shared__ float red[4][4][256];
+  __shared__ float red[4][4][NE * 64];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int s = blockIdx.x;
   const int b0 = blockIdx.y * bpc;
   const int b1 = min(B, b0 + bpc);
-  const int nq = H >> 2;
-  float gam[NCH][4], acc_g[NCH][4], acc_b[NCH][4], acc_p[NCH][4], acc_t0[NCH][4];
+  float gam[NE], acc_g[NE], acc_b[NE], acc_p[NE], acc_t0[NE];
 #pragma unroll
-  for (int i = 0; i < NCH; ++i) {
-    int c = lane + 64 * i;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) acc_g[i][k] = acc_b[i][k] = acc_p[i][k] = acc_t0[i][k] = gam[i][k] = 0.f;
-    if (c < nq) {
-      u32x2 gw = *reinterpret_cast<const u32x2*>(gamma + 4 * c);
-      gam[i][0] = lo_bf(gw.x); gam[i][1] = hi_bf(gw.x); gam[i][2] = lo_bf(gw.y); gam[i][3] = hi_bf(gw.y);
-    }
+  for (int i = 0; i < NE; ++i) {
+    const int e = lane + 64 * i;
+    acc_g[i] = acc_b[i] = acc_p[i] = acc_t0[i] = 0.f;
+    gam[i] = e < H ? bf2f(gamma[e]) : 0.f;
   }
   for (int b = b0 + wid; b < b1; b += 4) {
     const int row = b * S + s;
     const int64_t id = ids[row], pid = pos_ids[row];
     const int64_t tid = type ? type_ids[row] : 0;
-    float e[NCH][4];
-    gather_row<NCH>(e, word, pos, type, id, pid, tid, H, lane);
     const float mean = mean_in[row], rstd = rstd_in[row];
-    float g[NCH][4], xh[NCH][4];
+    float xh[NE], g[NE], d[NE];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      int c = lane + 64 * i;
-      if (c < nq) {
-        size_t off = (size_t)row * H + 4 * c;
-        u32x2 dw = *reinterpret_cast<const u32x2*>(dout + off);
-        float d[4] = {lo_bf(dw.x), hi_bf(dw.x), lo_bf(dw.y), hi_bf(dw.y)};
-        if (dp.enabled) {
-          uint32_t pair0 = (uint32_t)(off >> 1);
-          uint32_t bb0 = dropout_bits(pair0, dp.seed_lo, dp.seed_hi);
-          uint32_t bb1 = dropout_bits(pair0 + 1, dp.seed_lo, dp.seed_hi);
-          d[0] *= keep_factor(bb0, 0, dp);
-          d[1] *= keep_factor(bb0, 1, dp);
-          d[2] *= keep_factor(bb1, 0, dp);
-          d[3] *= keep_factor(bb1, 1, dp);
-        }
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          xh[i][k] = (e[i][k] - mean) * rstd;
-          g[i][k] = d[k] * gam[i][k];
-          s1 += g[i][k];
-          s2 += g[i][k] * xh[i][k];
-          acc_g[i][k] += d[k] * xh[i][k];
-          acc_b[i][k] += d[k];
-        }
+    for (int i = 0; i < NE; ++i) {
+      const int e = lane + 64 * i;
+      if (e < H) {
+        float ev = bf2f(word[id * H + e]) + bf2f(pos[pid * H + e]);
+        if (type) ev += bf2f(type[tid * H + e]);
+        const size_t off = (size_t)row * H + e;
+        float dv = bf2f(dout[off]);
+        if (dp.enabled) dv *= keep_factor(dropout_bits((uint32_t)(off >> 1), dp.seed_lo, dp.seed_hi), (int)(off & 1), dp);
+        d[i] = dv;
+        xh[i] = (ev - mean) * rstd;
+        g[i] = dv * gam[i];
+        s1 += g[i];
+        s2 += g[i] * xh[i];
+        acc_g[i] += dv * xh[i];
+        acc_b[i] += dv;
       } else {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) g[i][k] = xh[i][k] = 0.f;
+        d[i] = xh[i] = g[i] = 0.f;
       }
     }
     s1 = wave_sum(s1) / (float)H;
     s2 = wave_sum(s2) / (float)H;
 #pragma unroll
-    for (int i = 0; i < NCH; ++i) {
-      int c = lane + 64 * i;
-      if (c < nq) {
-        float de[4];
-#pragma unroll
-        for (int k = 0; k < 4; ++k) de[k] = rstd * (g[i][k] - s1 - xh[i][k] * s2);
-        float* gw = gword + id * H + 4 * c;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) atomicAdd(gw + k, de[k]);
-        if (pos_is_arange) {
-#pragma unroll
-          for (int k = 0; k < 4; ++k) acc_p[i][k] += de[k];
-        } else {
-          float* gp = gpos + pid * H + 4 * c;
-#pragma unroll
-          for (int k = 0; k < 4; ++k) atomicAdd(gp + k, de[k]);
-        }
-        if (gtype) {
-          if (tid == 0) {
-#pragma unroll
-            for (int k = 0; k < 4; ++k) acc_t0[i][k] += de[k];
-          } else {
-            float* gt = gtype + tid * H + 4 * c;
-#pragma unroll
-            for (int k = 0; k < 4; ++k) atomicAdd(gt + k, de[k]);
-          }
-        }
+    for (int i = 0; i < NE; ++i) {
+      const int e = lane + 64 * i;
+      if (e >= H) continue;
+      const float de = rstd * (g[i] - s1 - xh[i] * s2);
+      atomicAdd(gword + id * H + e, de);
+      if (pos_is_arange) acc_p[i] += de;
+      else atomicAdd(gpos + pid * H + e, de);
+      if (gtype) {
+        if (tid == 0) acc_t0[i] += de;
+        else atomicAdd(gtype + tid * H + e, de);
       }
     }
   }
-  // block reduction of the 4 register partials (gamma, beta, pos row s, type row 0)
 #pragma unroll
-  for (int i = 0; i < NCH; ++i) {
-    int c = lane + 64 * i;
-    __syncthreads();
+  for (int i = 0; i < NE; ++i) {
+    red[wid][0][lane + 64 * i] = acc_g[i];
+    red[wid][1][lane + 64 * i] = acc_b[i];
+    red[wid][2][lane + 64 * i] = acc_p[i];
+    red[wid][3][lane + 64 * i] = acc_t0[i];
+  }
+  __syncthreads();
+  float* dst = wid == 0 ? ggamma : wid == 1 ? gbeta : wid == 2 ? (pos_is_arange ? gpos + (size_t)s * H : nullptr) : gtype;
+  if (dst) {
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      red[wid][0][lane * 4 + k] = acc_g[i][k];
-      red[wid][1][lane * 4 + k] = acc_b[i][k];
-      red[wid][2][lane * 4 + k] = acc_p[i][k];
-      red[wid][3][lane * 4 + k] = acc_t0[i][k];
-    }
-    __syncthreads();
-    if (c < nq) {
-      float* dst = wid == 0 ? ggamma : wid == 1 ? gbeta : wid == 2 ? (pos_is_arange ? gpos + (size_t)s * H : nullptr)
-                                                                   : gtype;
-      if (dst) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          float t = red[0][wid][lane * 4 + k] + red[1][wid][lane * 4 + k] + red[2][wid][lane * 4 + k] +
-                    red[3][wid][lane * 4 + k];
-          atomicAdd(dst + 4 * c + k, t);
-        }
-      }
+    for (int i = 0; i < NE; ++i) {
+      const int e = lane + 64 * i;
+      if (e < H) atomicAdd(dst + e, red[0][wid][e] + red[1][wid][e] + red[2][wid][e] + red[3][wid][e]);
     }
   }
 }
@@ -244,16 +203,16 @@ void launch_embed_fwd(const int64_t* ids, const int64_t* pos_ids, const int64_t*
   HSD_CHECK_LAUNCH();
 }
 
-template <int NCH>
+template <int NE>
 static void embed_bwd_t(const bf16_t* dout, const int64_t* ids, const int64_t* pos_ids, const int64_t* type_ids,
                         const bf16_t* word, const bf16_t* pos, const bf16_t* type, const bf16_t* gamma,
                         const float* mean, const float* rstd, float* gword, float* gpos, float* gtype, float* ggamma,
                         float* gbeta, int B, int S, int H, int pos_is_arange, const DropoutParams& dp, hipStream_t st) {
-  // enough blocks to fill 256 CUs: S * chunks >= ~1024
-  int chunks = max(1, min(B, (1024 + S - 1) / S));
+  // enough blocks to fill 256 CUs: S * chunks >= ~2048
+  int chunks = max(1, min(B, (2048 + S - 1) / S));
   int bpc = (B + chunks - 1) / chunks;
   chunks = (B + bpc - 1) / bpc;
-  hipLaunchKernelGGL((embed_bwd_kernel<NCH>), dim3(S, chunks), dim3(256), 0, st, dout, ids, pos_ids, type_ids, word,
+  hipLaunchKernelGGL((embed_bwd_kernel<NE>), dim3(S, chunks), dim3(256), 0, st, dout, ids, pos_ids, type_ids, word,
                      pos, type, gamma, mean, rstd, gword, gpos, gtype, ggamma, gbeta, B, S, H, bpc, pos_is_arange, dp);
 }
 
@@ -262,11 +221,11 @@ void launch_embed_bwd(const bf16_t* dout, const int64_t* ids, const int64_t* pos
                       const float* mean, const float* rstd, float* gword, float* gpos, float* gtype, float* ggamma,
                       float* gbeta, int B, int S, int H, int pos_is_arange, double p, uint64_t seed, hipStream_t st) {
   DropoutParams dp = make_dropout(p, seed);
-  int nch = (H / 4 + 63) / 64;
-  if (nch <= 1) embed_bwd_t<1>(dout, ids, pos_ids, type_ids, word, pos, type, gamma, mean, rstd, gword, gpos, gtype, ggamma, gbeta, B, S, H, pos_is_arange, dp, st);
-  else if (nch <= 2) embed_bwd_t<2>(dout, ids, pos_ids, type_ids, word, pos, type, gamma, mean, rstd, gword, gpos, gtype, ggamma, gbeta, B, S, H, pos_is_arange, dp, st);
-  else if (nch <= 3) embed_bwd_t<3>(dout, ids, pos_ids, type_ids, word, pos, type, gamma, mean, rstd, gword, gpos, gtype, ggamma, gbeta, B, S, H, pos_is_arange, dp, st);
-  else if (nch <= 4) embed_bwd_t<4>(dout, ids, pos_ids, type_ids, word, pos, type, gamma, mean, rstd, gword, gpos, gtype, ggamma, gbeta, B, S, H, pos_is_arange, dp, st);
+  const int ne = (H + 63) / 64;
+  if (ne <= 1) embed_bwd_t<1>(dout, ids, pos_ids, type_ids, word, pos, type, gamma, mean, rstd, gword, gpos, gtype, ggamma, gbeta, B, S, H, pos_is_arange, dp, st);
+  else if (ne <= 2) embed_bwd_t<2>(dout, ids, pos_ids, type_ids, word, pos, type, gamma, mean, rstd, gword, gpos, gtype, ggamma, gbeta, B, S, H, pos_is_arange, dp, st);
+  else if (ne <= 12) embed_bwd_t<12>(dout, ids, pos_ids, type_ids, word, pos, type, gamma, mean, rstd, gword, gpos, gtype, ggamma, gbeta, B, S, H, pos_is_arange, dp, st);
+  else if (ne <= 16) embed_bwd_t<16>(dout, ids, pos_ids, type_ids, word, pos, type, gamma, mean, rstd, gword, gpos, gtype, ggamma, gbeta, B, S, H, pos_is_arange, dp, st);
   else abort();
   HSD_CHECK_LAUNCH();
 }

@@ -177,17 +177,20 @@ __device__ __forceinline__ void ln_bwd_row(const u32x2 (&zw)[NCH], const u32x2 (
   }
 }
 
-template <int NCH>
-__global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ z,
-                                                     const float* __restrict__ mean_in, const float* __restrict__ rstd_in,
-                                                     const bf16_t* __restrict__ gamma,
-                                                     bf16_t* __restrict__ dz_out,    // residual grad (may be null)
-                                                     bf16_t* __restrict__ dy_out,    // grad into GEMM output (may be null)
-                                                     const bf16_t* __restrict__ dres_add,  // extra grad added to dz
-                                                     float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                     float* __restrict__ dbias,      // may be null
-                                                     int rows, int H, int rows_per_block, DropoutParams dp) {
-  __shared__ float red[kLnWaves][3][256];
+template <int NCH, int NW>
+__global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ z,
+                                                         const float* __restrict__ mean_in,
+                                                         const float* __restrict__ rstd_in,
+                                                         const bf16_t* __restrict__ gamma,
+                                                         bf16_t* __restrict__ dz_out,    // residual grad (may be null)
+                                                         bf16_t* __restrict__ dy_out,    // grad into GEMM output
+                                                         const bf16_t* __restrict__ dres_add,  // added to dz
+                                                         float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                         float* __restrict__ dbias,      // may be null
+                                                         int rows, int H, int rows_per_wave, DropoutParams dp) {
+  // NW waves per block (many waves resident hide the row latency, like ln_fwd), each wave owns
+  // `rows_per_wave` consecutive rows; column partials reduced through LDS: one atomic per column per block.
+  __shared__ float red[NW][3][256];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;
   const int nq = H >> 2;
@@ -203,24 +206,15 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
       gam[i][0] = lo_bf(gw.x); gam[i][1] = hi_bf(gw.x); gam[i][2] = lo_bf(gw.y); gam[i][3] = hi_bf(gw.y);
     }
   }
-  const int row0 = blockIdx.x * rows_per_block;
-  const int row_end = min(rows, row0 + rows_per_block);
-  for (int row = row0 + wid; row < row_end; row += 2 * kLnWaves) {
-    const int row2 = row + kLnWaves;
-    const bool two = row2 < row_end;
-    u32x2 za[NCH], da[NCH], zb[NCH], db[NCH];
+  const int row0 = (blockIdx.x * NW + wid) * rows_per_wave;
+  for (int rr = 0; rr < rows_per_wave; ++rr) {
+    const int row = row0 + rr;
+    if (row >= rows) break;
+    u32x2 za[NCH], da[NCH];
     ln_bwd_load<NCH>(dout, z, row, H, lane, za, da);
-    const float ma = mean_in[row], ra = rstd_in[row];
-    float mb = 0.f, rb = 0.f;
-    if (two) {
-      ln_bwd_load<NCH>(dout, z, row2, H, lane, zb, db);
-      mb = mean_in[row2];
-      rb = rstd_in[row2];
-    }
-    ln_bwd_row<NCH>(za, da, ma, ra, gam, row, H, lane, dz_out, dy_out, dres_add, dp, acc_g, acc_b, acc_db);
-    if (two) ln_bwd_row<NCH>(zb, db, mb, rb, gam, row2, H, lane, dz_out, dy_out, dres_add, dp, acc_g, acc_b, acc_db);
+    ln_bwd_row<NCH>(za, da, mean_in[row], rstd_in[row], gam, row, H, lane, dz_out, dy_out, dres_add, dp, acc_g,
+                    acc_b, acc_db);
   }
-  // cross-wave reduction through LDS, one 256-column pass at a time; one atomic per column per block
 #pragma unroll
   for (int i = 0; i < NCH; ++i) {
     const int c = lane + 64 * i;
@@ -236,8 +230,9 @@ __global__ __launch_bounds__(256) void ln_bwd_kernel(const bf16_t* __restrict__ 
       float* dst = wid == 0 ? dgamma : (wid == 1 ? dbeta : dbias);
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
-        const float t = red[0][wid][lane * 4 + k] + red[1][wid][lane * 4 + k] + red[2][wid][lane * 4 + k] +
-                        red[3][wid][lane * 4 + k];
+        float t = 0.f;
+#pragma unroll
+        for (int w = 0; w < NW; ++w) t += red[w][wid][lane * 4 + k];
         atomicAdd(dst + 4 * c + k, t);
       }
     }
@@ -271,12 +266,12 @@ template <int NCH>
 static void ln_bwd_t(const bf16_t* dout, const bf16_t* z, const float* mean, const float* rstd, const bf16_t* gamma,
                      bf16_t* dz, bf16_t* dy, const bf16_t* dres_add, float* dgamma, float* dbeta, float* dbias,
                      int rows, int H, const DropoutParams& dp, hipStream_t st) {
-  // ~1024 blocks (4 per CU, 16 waves/CU) of 4 waves x 2 rows in flight; one atomic per column per block
-  int rpb = max(2 * kLnWaves, (rows + 1023) / 1024);
-  rpb = (rpb + 2 * kLnWaves - 1) / (2 * kLnWaves) * (2 * kLnWaves);
-  int blocks = (rows + rpb - 1) / rpb;
-  hipLaunchKernelGGL((ln_bwd_kernel<NCH>), dim3(blocks), dim3(256), 0, st, dout, z, mean, rstd, gamma, dz, dy,
-                     dres_add, dgamma, dbeta, dbias, rows, H, rpb, dp);
+  // 16-wave blocks, 2 rows per wave: ~1024 blocks at 32k rows, one atomic per column per block
+  constexpr int NW = 16;
+  const int rpw = rows >= NW * 2 * 512 ? 2 : 1;
+  const int blocks = (rows + NW * rpw - 1) / (NW * rpw);
+  hipLaunchKernelGGL((ln_bwd_kernel<NCH, NW>), dim3(blocks), dim3(NW * 64), 0, st, dout, z, mean, rstd, gamma, dz,
+                     dy, dres_add, dgamma, dbeta, dbias, rows, H, rpw, dp);
 }
 
 void launch_ln_bwd(const bf16_t* dout, const bf16_t* z, const float* mean, const float* rstd, const bf16_t* gamma,

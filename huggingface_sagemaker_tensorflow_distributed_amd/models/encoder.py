@@ -51,14 +51,14 @@ class EncoderLayer(nn.Module):
         c = self.cfg
         p_h = c.hidden_dropout_prob if training else 0.0
         p_a = c.attention_probs_dropout_prob if training else 0.0
-        qkv = ops.linear(h, self.qkv_weight, self.qkv_bias)
-        ctx = ops.attention(qkv, mask_bias, batch, seq, c.num_attention_heads, p_a, rng.next() if p_a else 0)
-        h1 = ops.dense_residual_ln(ctx, self.attn_out_weight, self.attn_out_bias, h, self.ln1_weight,
-                                   self.ln1_bias, c.layer_norm_eps, p_h, rng.next() if p_h else 0)
-        a = ops.linear_gelu(h1, self.ffn1_weight, self.ffn1_bias)
-        h2 = ops.dense_residual_ln(a, self.ffn2_weight, self.ffn2_bias, h1, self.ln2_weight, self.ln2_bias,
-                                   c.layer_norm_eps, p_h, rng.next() if p_h else 0)
-        return h2
+        seed_a = rng.next() if p_a else 0
+        seed_h1 = rng.next() if p_h else 0
+        h1 = ops.attn_block(h, self.qkv_weight, self.qkv_bias, self.attn_out_weight, self.attn_out_bias,
+                            self.ln1_weight, self.ln1_bias, c.layer_norm_eps, mask_bias, batch, seq,
+                            c.num_attention_heads, p_a, seed_a, p_h, seed_h1)
+        seed_h2 = rng.next() if p_h else 0
+        return ops.ffn_block(h1, self.ffn1_weight, self.ffn1_bias, self.ffn2_weight, self.ffn2_bias,
+                             self.ln2_weight, self.ln2_bias, c.layer_norm_eps, p_h, seed_h2)
 
 
 # name tables: internal name -> list of (hf suffix, row-slice or None)

@@ -75,6 +75,25 @@ def dense_residual_ln(x, w, b, residual, ln_w, ln_b, eps, p, seed):
     return _ref.layer_norm(_ref.linear_dropout_residual(x, w, b, residual, p, seed, p > 0), ln_w, ln_b, eps)
 
 
+def attn_block(h, qkv_w, qkv_b, out_w, out_b, ln_w, ln_b, eps, mask_bias, batch, seq, heads, p_attn, seed_attn,
+               p_hidden, seed_hidden):
+    """Self-attention sub-block: ``LN(dropout(attn(h Wqkvᵀ + b) Woᵀ + bo) + h)``."""
+    if _hip(h) and h.dtype == torch.bfloat16 and qkv_w.shape[0] == 3 * heads * 64:
+        return _hipmod().attn_block(h, qkv_w, qkv_b, out_w, out_b, ln_w, ln_b, eps, mask_bias, batch, seq, heads,
+                                    p_attn, seed_attn, p_hidden, seed_hidden)
+    qkv = linear(h, qkv_w, qkv_b)
+    ctx = attention(qkv, mask_bias, batch, seq, heads, p_attn, seed_attn)
+    return dense_residual_ln(ctx, out_w, out_b, h, ln_w, ln_b, eps, p_hidden, seed_hidden)
+
+
+def ffn_block(h, w1, b1, w2, b2, ln_w, ln_b, eps, p, seed):
+    """Feed-forward sub-block: ``LN(dropout(gelu(h W1ᵀ + b1) W2ᵀ + b2) + h)``."""
+    if _hip(h) and h.dtype == torch.bfloat16:
+        return _hipmod().ffn_block(h, w1, b1, w2, b2, ln_w, ln_b, eps, p, seed)
+    a = linear_gelu(h, w1, b1)
+    return dense_residual_ln(a, w2, b2, h, ln_w, ln_b, eps, p, seed)
+
+
 def attention(qkv, mask_bias, batch, seq, heads, p, seed):
     if _hip(qkv):
         return _hipmod().attention(qkv, mask_bias, batch, seq, heads, p, seed)

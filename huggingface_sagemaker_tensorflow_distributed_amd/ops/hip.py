@@ -276,3 +276,159 @@ def attention(qkv, mask_bias, batch, seq, heads, p, seed):
 
         return ref(qkv, mask_bias, batch, seq, heads, p, seed, p > 0)
     return _Attention.apply(qkv, mask_bias, batch, seq, heads, p, seed)
+
+
+# ------------------------------------------------------------------------------------------ GEMM helpers
+EPI_STORE, EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_DROP_RES, EPI_RES, EPI_DGELU, EPI_F32_ATOMIC = range(7)
+
+# split-K factors for the wgrad GEMM (fp32 atomic epilogue), measured with tools/bench_gemm.py at
+# T = 32768 tokens; key = (out_features, in_features)
+_WGRAD_SPLITS = {(2304, 768): 4, (768, 768): 8, (3072, 768): 8, (768, 3072): 8,
+                 (3072, 1024): 8, (1024, 4096): 8, (1024, 1024): 8, (4096, 1024): 8}
+
+
+def _wgrad_splits(n_out: int, k_in: int, tokens: int) -> int:
+    s = _WGRAD_SPLITS.get((n_out, k_in))
+    if s is None:
+        tiles = -(-n_out // 256) * -(-k_in // 128)
+        s = 1
+        while tiles * s * 2 <= 512 and s < 16:
+            s *= 2
+    # keep >= 2 k-tiles (64 tokens each) per split
+    while s > 1 and tokens // s < 128:
+        s //= 2
+    return s
+
+
+def gemm_fwd(x, w, epi, bias=None, aux=None, out2=None, p=0.0, seed=0):
+    """y[T, N] = x[T, K] · w[N, K]ᵀ with epilogue."""
+    y = torch.empty((x.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)
+    _C.gemm(x, w, y, 0, 0, epi, bias, aux, out2, float(p), _s64(seed), 1)
+    return y
+
+
+def gemm_dgrad(dy, w, epi=EPI_STORE, aux=None):
+    """dx[T, K] = dy[T, N] · w[N, K]."""
+    dx = torch.empty((dy.shape[0], w.shape[1]), dtype=dy.dtype, device=dy.device)
+    _C.gemm(dy, w, dx, 0, 1, epi, None, aux, None, 0.0, 0, 1)
+    return dx
+
+
+def gemm_wgrad_(g: "_Grad", dy, x):
+    """g.buf[N, K] += dy[T, N]ᵀ · x[T, K]   (fp32, atomics, split-K over tokens)."""
+    splits = _wgrad_splits(dy.shape[1], x.shape[1], dy.shape[0])
+    _C.gemm(dy, x, g.buf, 1, 1, EPI_F32_ATOMIC, None, None, None, 0.0, 0, splits)
+
+
+def _ln_fwd(z, w, b, eps):
+    rows, H = z.shape
+    out = torch.empty_like(z)
+    mean = torch.empty(rows, dtype=torch.float32, device=z.device)
+    rstd = torch.empty_like(mean)
+    _C.ln_fwd(z, None, w, b, None, out, mean, rstd, float(eps), 0.0, 0)
+    return out, mean, rstd
+
+
+# ------------------------------------------------------------------------------------------ fused blocks
+class _AttnBlock(torch.autograd.Function):
+    """h1 = LN(dropout(attn(h Wqkvᵀ + b) Woᵀ + bo) + h) with a hand-written backward:
+    LN-bwd (+dropout, + out-proj bias grad) -> Wo wgrad / dgrad -> flash-attn bwd -> bias colsum ->
+    Wqkv wgrad -> dgrad with the residual gradient added in the GEMM epilogue."""
+
+    @staticmethod
+    def forward(ctx, h, qkv_w, qkv_b, out_w, out_b, ln_w, ln_b, eps, mask_bias, B, S, heads, p_a, seed_a, p_h,
+                seed_h):
+        h2d = h.reshape(-1, h.shape[-1])
+        qkv = gemm_fwd(h2d, qkv_w, EPI_BIAS, bias=qkv_b)
+        H = out_w.shape[0]
+        actx = torch.empty((h2d.shape[0], H), dtype=h.dtype, device=h.device)
+        lse = torch.empty(B * heads * S, dtype=torch.float32, device=h.device)
+        mb = mask_bias.contiguous().float() if mask_bias is not None else None
+        _C.attn_fwd(qkv, mb, actx, lse, B, S, heads, float(p_a), _s64(seed_a))
+        z = gemm_fwd(actx, out_w, EPI_BIAS_DROP_RES, bias=out_b, aux=h2d, p=p_h, seed=seed_h)
+        out, mean, rstd = _ln_fwd(z, ln_w, ln_b, eps)
+        ctx.save_for_backward(h2d, qkv_w, qkv_b, out_w, out_b, ln_w, ln_b, qkv, actx, lse, z, mean, rstd,
+                              mb if mb is not None else lse)
+        ctx.cfg = (B, S, heads, float(p_a), seed_a, float(p_h), seed_h, mb is not None)
+        return out.view(h.shape)
+
+    @staticmethod
+    def backward(ctx, dout):
+        (h2d, qkv_w, qkv_b, out_w, out_b, ln_w, ln_b, qkv, actx, lse, z, mean, rstd, mb) = ctx.saved_tensors
+        B, S, heads, p_a, seed_a, p_h, seed_h, has_mask = ctx.cfg
+        dout2 = dout.reshape(z.shape).contiguous()
+        g_lnw, g_lnb, g_ow, g_ob = _Grad(ln_w), _Grad(ln_b), _Grad(out_w), _Grad(out_b)
+        dy = torch.empty_like(z)
+        if p_h > 0:
+            dz = torch.empty_like(z)
+            _C.ln_bwd(dout2, z, mean, rstd, ln_w, dz, dy, None, g_lnw.buf, g_lnb.buf, g_ob.buf, p_h, _s64(seed_h))
+        else:
+            _C.ln_bwd(dout2, z, mean, rstd, ln_w, None, dy, None, g_lnw.buf, g_lnb.buf, g_ob.buf, 0.0, 0)
+            dz = dy
+        r_lnw, r_lnb, r_ob = g_lnw.done(), g_lnb.done(), g_ob.done()
+        gemm_wgrad_(g_ow, dy, actx)
+        r_ow = g_ow.done()
+        dctx = gemm_dgrad(dy, out_w)
+        dqkv = torch.empty_like(qkv)
+        dq_acc = torch.zeros(actx.shape, dtype=torch.float32, device=actx.device) if S > 128 else None
+        _C.attn_bwd(qkv, mb if has_mask else None, actx, dctx, lse, dqkv, dq_acc, B, S, heads, p_a, _s64(seed_a))
+        g_qw, g_qb = _Grad(qkv_w), _Grad(qkv_b)
+        _C.colsum(dqkv, g_qb.buf)
+        r_qb = g_qb.done()
+        gemm_wgrad_(g_qw, dqkv, h2d)
+        r_qw = g_qw.done()
+        dh = gemm_dgrad(dqkv, qkv_w, EPI_RES, aux=dz) if ctx.needs_input_grad[0] else None
+        return (dh.view(dout.shape) if dh is not None else None, r_qw, r_qb, r_ow, r_ob, r_lnw, r_lnb,
+                None, None, None, None, None, None, None, None, None)
+
+
+def attn_block(h, qkv_w, qkv_b, out_w, out_b, ln_w, ln_b, eps, mask_bias, B, S, heads, p_a, seed_a, p_h, seed_h):
+    return _AttnBlock.apply(h, qkv_w, qkv_b, out_w, out_b, ln_w, ln_b, eps, mask_bias, B, S, heads, p_a, seed_a,
+                            p_h, seed_h)
+
+
+class _FFNBlock(torch.autograd.Function):
+    """h2 = LN(dropout(gelu(h W1ᵀ + b1) W2ᵀ + b2) + h). Forward: 2 GEMMs (bias+GELU epilogue writing
+    pre-activation and activation; bias+dropout+residual epilogue) + LN. Backward: LN-bwd (+dropout,
+    + b2 grad) -> W2 wgrad -> dgrad with gelu' epilogue -> b1 colsum -> W1 wgrad -> dgrad + residual."""
+
+    @staticmethod
+    def forward(ctx, h, w1, b1, w2, b2, ln_w, ln_b, eps, p, seed):
+        h2d = h.reshape(-1, h.shape[-1])
+        act = torch.empty((h2d.shape[0], w1.shape[0]), dtype=h.dtype, device=h.device)
+        pre = gemm_fwd(h2d, w1, EPI_BIAS_GELU, bias=b1, out2=act)
+        z = gemm_fwd(act, w2, EPI_BIAS_DROP_RES, bias=b2, aux=h2d, p=p, seed=seed)
+        out, mean, rstd = _ln_fwd(z, ln_w, ln_b, eps)
+        ctx.save_for_backward(h2d, w1, b1, w2, b2, ln_w, ln_b, pre, act, z, mean, rstd)
+        ctx.cfg = (float(p), seed)
+        return out.view(h.shape)
+
+    @staticmethod
+    def backward(ctx, dout):
+        h2d, w1, b1, w2, b2, ln_w, ln_b, pre, act, z, mean, rstd = ctx.saved_tensors
+        p, seed = ctx.cfg
+        dout2 = dout.reshape(z.shape).contiguous()
+        g_lnw, g_lnb, g_w2, g_b2 = _Grad(ln_w), _Grad(ln_b), _Grad(w2), _Grad(b2)
+        dy = torch.empty_like(z)
+        if p > 0:
+            dz = torch.empty_like(z)
+            _C.ln_bwd(dout2, z, mean, rstd, ln_w, dz, dy, None, g_lnw.buf, g_lnb.buf, g_b2.buf, p, _s64(seed))
+        else:
+            _C.ln_bwd(dout2, z, mean, rstd, ln_w, None, dy, None, g_lnw.buf, g_lnb.buf, g_b2.buf, 0.0, 0)
+            dz = dy
+        r_lnw, r_lnb, r_b2 = g_lnw.done(), g_lnb.done(), g_b2.done()
+        gemm_wgrad_(g_w2, dy, act)
+        r_w2 = g_w2.done()
+        da = gemm_dgrad(dy, w2, EPI_DGELU, aux=pre)
+        g_w1, g_b1 = _Grad(w1), _Grad(b1)
+        _C.colsum(da, g_b1.buf)
+        r_b1 = g_b1.done()
+        gemm_wgrad_(g_w1, da, h2d)
+        r_w1 = g_w1.done()
+        dh = gemm_dgrad(da, w1, EPI_RES, aux=dz) if ctx.needs_input_grad[0] else None
+        return (dh.view(dout.shape) if dh is not None else None, r_w1, r_b1, r_w2, r_b2, r_lnw, r_lnb,
+                None, None, None)
+
+
+def ffn_block(h, w1, b1, w2, b2, ln_w, ln_b, eps, p, seed):
+    return _FFNBlock.apply(h, w1, b1, w2, b2, ln_w, ln_b, eps, p, seed)

@@ -172,3 +172,51 @@ def test_adam_kernel_matches_reference(gpu):
     pr = pr - step * mr / (vr.sqrt() + eps)
     torch.testing.assert_close(p, pr, rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(out.float(), pr.bfloat16().float())
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_fused_blocks_vs_reference(gpu, p):
+    """attn_block / ffn_block (GEMM epilogues + fused backward) vs composed fp32 reference ops."""
+    from huggingface_sagemaker_tensorflow_distributed_amd import ops
+
+    hip = _hip()
+    torch.manual_seed(5)
+    B, S, heads, H, I = 4, 128, 4, 256, 512
+    T = B * S
+    mk = lambda *s, sc=0.05: (torch.randn(*s, device=gpu) * sc).bfloat16().requires_grad_()  # noqa: E731
+    h = torch.randn(T, H, device=gpu).bfloat16().requires_grad_()
+    qw, qb, ow, ob = mk(3 * H, H), mk(3 * H), mk(H, H), mk(H)
+    lw, lb = (1 + 0.1 * torch.randn(H, device=gpu)).bfloat16().requires_grad_(), mk(H)
+    w1, b1, w2, b2 = mk(I, H), mk(I), mk(H, I), mk(H)
+    l2w, l2b = (1 + 0.1 * torch.randn(H, device=gpu)).bfloat16().requires_grad_(), mk(H)
+    am = torch.ones(B, S, dtype=torch.long, device=gpu)
+    am[2, 100:] = 0
+    mb = ref.key_mask_bias(am)
+    params = [h, qw, qb, ow, ob, lw, lb, w1, b1, w2, b2, l2w, l2b]
+
+    def run(hip_path):
+        for t in params:
+            t.grad = None
+        if hip_path:
+            h1 = hip.attn_block(h, qw, qb, ow, ob, lw, lb, 1e-12, mb, B, S, heads, p, 11, p, 12)
+            out = hip.ffn_block(h1, w1, b1, w2, b2, l2w, l2b, 1e-12, p, 13)
+        else:
+            f = [t.detach().float().requires_grad_() for t in params]
+            qkv = ref.linear(f[0], f[1], f[2])
+            ctx_ = ref.attention(qkv, mb, B, S, heads, p, 11, p > 0)
+            h1 = ref.layer_norm(ref.linear_dropout_residual(ctx_, f[3], f[4], f[0], p, 12, p > 0), f[5], f[6], 1e-12)
+            a = ref.linear_gelu(h1, f[7], f[8])
+            out = ref.layer_norm(ref.linear_dropout_residual(a, f[9], f[10], h1, p, 13, p > 0), f[11], f[12], 1e-12)
+            params_f = f
+        g = torch.randn(out.shape, device=gpu, generator=torch.Generator(device=gpu).manual_seed(9))
+        out.backward(g.to(out.dtype))
+        grads = [t.grad.float() for t in (params if hip_path else params_f)]
+        return out.float(), grads
+
+    o1, g1 = run(True)
+    o2, g2 = run(False)
+    _close(o1, o2, 3e-2, 3e-2, "out")
+    names = ["h", "qw", "qb", "ow", "ob", "lw", "lb", "w1", "b1", "w2", "b2", "l2w", "l2b"]
+    for n, a, b in zip(names, g1, g2):
+        rel = (a - b).norm() / (b.norm() + 1e-6)
+        assert rel < 4e-2, f"{n}: rel err {rel:.3g}"
