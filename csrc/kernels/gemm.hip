@@ -225,6 +225,30 @@ __device__ __forceinline__ void dma_tile(bf16_t* tile, const bf16_t* __restrict_
   }
 }
 
+// piece j (0..R/64-1) of this wave's share of one operand tile
+template <int L, int R>
+__device__ __forceinline__ void dma_piece(int j, bf16_t* tile, const bf16_t* __restrict__ X, int64_t ld, int r0,
+                                          int Rmax, int k0, int wave, int lane) {
+  constexpr int PER_WAVE = R / 64;
+  const int g = wave * PER_WAVE + j;
+  const bf16_t* src;
+  if constexpr (L == 0) {
+    const int row = g * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ swz0(row);
+    const int rr = min(r0 + row, Rmax - 1);
+    src = X + (int64_t)rr * ld + k0 + lc * 8;
+  } else {
+    constexpr int RPK = 512 / R;
+    const int row = g * RPK + (lane * 8) / R;
+    const int pc = ((lane * 8) % R) >> 3;
+    const int lc = pc ^ swz1(row);
+    const int cc = min(r0 + lc * 8, Rmax - 8);
+    src = X + (int64_t)(k0 + row) * ld + cc;
+  }
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)(tile + g * 512), 16, 0, 0);
+}
+
 template <int N>
 __device__ __forceinline__ void wait_vmcnt() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
@@ -270,22 +294,24 @@ __global__ __launch_bounds__(512, 1) void gemm_dma_kernel(GemmParams p) {
       dma_tile<LB, BN_>(smem + s * STAGE + TA, p.B, p.ldb, n0, p.N, kbeg + s * BK, wave, lane);
     }
   }
+  // Main loop, ONE barrier per K-tile: at the top of iteration t the outstanding DMA stages are
+  // t .. t+NS-2; wait until stage t landed (counted vmcnt), barrier (stage t visible to every wave AND
+  // every wave finished reading stage t-1, whose buffer stage t+NS-1 now overwrites), then compute
+  // stage t while the DMA pieces of stage t+NS-1 are issued between the MFMA groups.
+  constexpr int GA = BM_ / 64;
   int slot = 0;
   for (int t = 0; t < nt; ++t) {
-    const int ahead = t + NS - 1;
-    if (ahead < nt) {
-      const int ns = ahead % NS;
-      dma_tile<LA, BM_>(smem + ns * STAGE, p.A, p.lda, m0, p.M, kbeg + ahead * BK, wave, lane);
-      dma_tile<LB, BN_>(smem + ns * STAGE + TA, p.B, p.ldb, n0, p.N, kbeg + ahead * BK, wave, lane);
-      wait_vmcnt<(NS - 1) * G>();
-    } else {
-      // stages newer than t still in flight: nt-1-t (< NS-1)
-      const int newer = nt - 1 - t;
-      if constexpr (NS >= 4) { if (newer == 2) wait_vmcnt<2 * G>(); }
-      if constexpr (NS >= 3) { if (newer == 1) wait_vmcnt<G>(); }
-      if (newer == 0) wait_vmcnt<0>();
-    }
+    const int newer = min(NS - 2, nt - 1 - t);  // stages issued after t and still possibly in flight
+    if constexpr (NS >= 4) { if (newer == 2) wait_vmcnt<2 * G>(); }
+    if constexpr (NS >= 3) { if (newer == 1) wait_vmcnt<G>(); }
+    if (newer == 0) wait_vmcnt<0>();
     __builtin_amdgcn_s_barrier();
+    const int ahead = t + NS - 1;
+    const bool issue = ahead < nt;
+    int nslot = slot + NS - 1;
+    nslot = nslot >= NS ? nslot - NS : nslot;
+    bf16_t* nA = smem + nslot * STAGE;
+    const int kn = kbeg + ahead * BK;
     const bf16_t* tA = smem + slot * STAGE;
     const bf16_t* tB = tA + TA;
 #pragma unroll
@@ -295,6 +321,15 @@ __global__ __launch_bounds__(512, 1) void gemm_dma_kernel(GemmParams p) {
       for (int i = 0; i < MB; ++i) fa[i] = frag<LA, BM_>(tA, wm * (BM_ / WM) + 32 * i, ks, lane);
 #pragma unroll
       for (int j = 0; j < NB; ++j) fb[j] = frag<LB, BN_>(tB, wn * (BN_ / WN) + 32 * j, ks, lane);
+      if (issue) {
+#pragma unroll
+        for (int j = 0; j < G; ++j) {
+          if ((j * 4) / G == ks) {
+            if (j < GA) dma_piece<LA, BM_>(j, nA, p.A, p.lda, m0, p.M, kn, wave, lane);
+            else dma_piece<LB, BN_>(j - GA, nA + TA, p.B, p.ldb, n0, p.N, kn, wave, lane);
+          }
+        }
+      }
 #pragma unroll
       for (int i = 0; i < MB; ++i)
 #pragma unroll
@@ -303,7 +338,6 @@ __global__ __launch_bounds__(512, 1) void gemm_dma_kernel(GemmParams p) {
           else acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
         }
     }
-    __builtin_amdgcn_s_barrier();
     slot = slot + 1 == NS ? 0 : slot + 1;
   }
 #pragma unroll
@@ -433,7 +467,7 @@ void launch_gemm_variant(int la, int lb, int variant, const bf16_t* A, int64_t l
       case 2: gemm_dma_launch<0, 0, EPI_STORE, 256, 128, 4, 2, 2>(p, 1, st); break;
       case 3: gemm_dma_launch<0, 0, EPI_STORE, 256, 256, 2, 4, 2>(p, 1, st); break;
       case 4: gemm_dma_launch<0, 0, EPI_STORE, 128, 256, 2, 4, 3>(p, 1, st); break;
-      case 5: gemm_dma_launch<0, 0, EPI_STORE, 192, 256, 2, 4, 2>(p, 1, st); break;
+      case 5: gemm_dma_launch<0, 0, EPI_STORE, 128, 128, 2, 4, 4>(p, 1, st); break;
       default: abort();
     }
   } else if (la == 0 && lb == 1) {
@@ -443,7 +477,7 @@ void launch_gemm_variant(int la, int lb, int variant, const bf16_t* A, int64_t l
       case 2: gemm_dma_launch<0, 1, EPI_STORE, 128, 256, 2, 4, 3>(p, 1, st); break;
       case 3: gemm_dma_launch<0, 1, EPI_STORE, 256, 256, 2, 4, 2>(p, 1, st); break;
       case 4: gemm_dma_launch<0, 1, EPI_STORE, 192, 256, 2, 4, 2>(p, 1, st); break;
-      case 5: gemm_dma_launch<0, 1, EPI_STORE, 128, 256, 2, 4, 2>(p, 1, st); break;
+      case 5: gemm_dma_launch<0, 1, EPI_STORE, 128, 128, 2, 4, 4>(p, 1, st); break;
       default: abort();
     }
   } else {
