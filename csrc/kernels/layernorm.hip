@@ -177,65 +177,101 @@ __device__ __forceinline__ void ln_bwd_row(const u32x2 (&zw)[NCH], const u32x2 (
   }
 }
 
-template <int NCH, int NW>
-__global__ __launch_bounds__(NW * 64) void ln_bwd_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ z,
-                                                         const float* __restrict__ mean_in,
-                                                         const float* __restrict__ rstd_in,
-                                                         const bf16_t* __restrict__ gamma,
-                                                         bf16_t* __restrict__ dz_out,    // residual grad (may be null)
-                                                         bf16_t* __restrict__ dy_out,    // grad into GEMM output
-                                                         const bf16_t* __restrict__ dres_add,  // added to dz
-                                                         float* __restrict__ dgamma, float* __restrict__ dbeta,
-                                                         float* __restrict__ dbias,      // may be null
-                                                         int rows, int H, int rows_per_wave, DropoutParams dp) {
-  // NW waves per block (many waves resident hide the row latency, like ln_fwd), each wave owns
-  // `rows_per_wave` consecutive rows; column partials reduced through LDS: one atomic per column per block.
-  __shared__ float red[NW][3][256];
+// Pass 1: one wave per row, 4 rows per block (high occupancy, like ln_fwd): dz (+dres_add) and dy.
+template <int NCH>
+__global__ __launch_bounds__(256) void ln_bwd_rows_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ z,
+                                                          const float* __restrict__ mean_in,
+                                                          const float* __restrict__ rstd_in,
+                                                          const bf16_t* __restrict__ gamma, bf16_t* __restrict__ dz_out,
+                                                          bf16_t* __restrict__ dy_out,
+                                                          const bf16_t* __restrict__ dres_add, int rows, int H,
+                                                          DropoutParams dp) {
   const int lane = threadIdx.x & 63;
-  const int wid = threadIdx.x >> 6;
+  const int row = blockIdx.x * kLnWaves + (threadIdx.x >> 6);
+  if (row >= rows) return;
   const int nq = H >> 2;
-  float gam[NCH][4];
-  float acc_g[NCH][4], acc_b[NCH][4], acc_db[NCH][4];
+  float gam[NCH][4], dummy_g[NCH][4], dummy_b[NCH][4], dummy_db[NCH][4];
 #pragma unroll
   for (int i = 0; i < NCH; ++i) {
     const int c = lane + 64 * i;
 #pragma unroll
-    for (int k = 0; k < 4; ++k) { acc_g[i][k] = acc_b[i][k] = acc_db[i][k] = 0.f; gam[i][k] = 0.f; }
+    for (int k = 0; k < 4; ++k) gam[i][k] = dummy_g[i][k] = dummy_b[i][k] = dummy_db[i][k] = 0.f;
     if (c < nq) {
       u32x2 gw = *reinterpret_cast<const u32x2*>(gamma + 4 * c);
       gam[i][0] = lo_bf(gw.x); gam[i][1] = hi_bf(gw.x); gam[i][2] = lo_bf(gw.y); gam[i][3] = hi_bf(gw.y);
     }
   }
-  const int row0 = (blockIdx.x * NW + wid) * rows_per_wave;
-  for (int rr = 0; rr < rows_per_wave; ++rr) {
-    const int row = row0 + rr;
-    if (row >= rows) break;
-    u32x2 za[NCH], da[NCH];
-    ln_bwd_load<NCH>(dout, z, row, H, lane, za, da);
-    ln_bwd_row<NCH>(za, da, mean_in[row], rstd_in[row], gam, row, H, lane, dz_out, dy_out, dres_add, dp, acc_g,
-                    acc_b, acc_db);
-  }
+  u32x2 za[NCH], da[NCH];
+  ln_bwd_load<NCH>(dout, z, row, H, lane, za, da);
+  // the accumulators are dead here (column sums are pass 2); the compiler drops them
+  ln_bwd_row<NCH>(za, da, mean_in[row], rstd_in[row], gam, row, H, lane, dz_out, dy_out, dres_add, dp, dummy_g,
+                  dummy_b, dummy_db);
+}
+
+// Pass 2: column sums dgamma += Σ dout·xhat, dbeta += Σ dout, dbias += Σ dy. Block = 64 column chunks
+// (8 columns) x 4 row groups, 4 rows' loads in flight per thread, LDS reduction, one atomic per column.
+__global__ __launch_bounds__(256) void ln_bwd_cols_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ z,
+                                                          const float* __restrict__ mean_in,
+                                                          const float* __restrict__ rstd_in,
+                                                          const bf16_t* __restrict__ dy, float* __restrict__ dgamma,
+                                                          float* __restrict__ dbeta, float* __restrict__ dbias,
+                                                          int rows, int H, int rows_per_block) {
+  __shared__ float red[3][4][512 + 4];
+  const int cc = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int col = blockIdx.x * 512 + cc * 8;
+  const bool active = col < H;
+  const int r0 = blockIdx.y * rows_per_block;
+  const int r1 = min(rows, r0 + rows_per_block);
+  float ag[8], ab[8], ad[8];
 #pragma unroll
-  for (int i = 0; i < NCH; ++i) {
-    const int c = lane + 64 * i;
-    __syncthreads();
+  for (int k = 0; k < 8; ++k) ag[k] = ab[k] = ad[k] = 0.f;
+  if (active) {
+    for (int rb = r0 + rg; rb < r1; rb += 16) {
+      u32x4 dw[4], zw[4], yw[4];
+      float mu[4], rs[4];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      red[wid][0][lane * 4 + k] = acc_g[i][k];
-      red[wid][1][lane * 4 + k] = acc_b[i][k];
-      red[wid][2][lane * 4 + k] = acc_db[i][k];
-    }
-    __syncthreads();
-    if (c < nq && wid < 3 && (wid < 2 || dbias != nullptr)) {
-      float* dst = wid == 0 ? dgamma : (wid == 1 ? dbeta : dbias);
+      for (int u = 0; u < 4; ++u) {
+        const int r = rb + 4 * u;
+        if (r < r1) {
+          const size_t off = (size_t)r * H + col;
+          dw[u] = *reinterpret_cast<const u32x4*>(dout + off);
+          zw[u] = *reinterpret_cast<const u32x4*>(z + off);
+          if (dbias) yw[u] = *reinterpret_cast<const u32x4*>(dy + off);
+          mu[u] = mean_in[r];
+          rs[u] = rstd_in[r];
+        }
+      }
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        float t = 0.f;
+      for (int u = 0; u < 4; ++u) {
+        if (rb + 4 * u >= r1) continue;
 #pragma unroll
-        for (int w = 0; w < NW; ++w) t += red[w][wid][lane * 4 + k];
-        atomicAdd(dst + 4 * c + k, t);
+        for (int k = 0; k < 4; ++k) {
+          const float d0 = lo_bf(dw[u][k]), d1 = hi_bf(dw[u][k]);
+          ag[2 * k] += d0 * (lo_bf(zw[u][k]) - mu[u]) * rs[u];
+          ag[2 * k + 1] += d1 * (hi_bf(zw[u][k]) - mu[u]) * rs[u];
+          ab[2 * k] += d0;
+          ab[2 * k + 1] += d1;
+          if (dbias) {
+            ad[2 * k] += lo_bf(yw[u][k]);
+            ad[2 * k + 1] += hi_bf(yw[u][k]);
+          }
+        }
       }
     }
+  }
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    red[0][rg][cc * 8 + k] = ag[k];
+    red[1][rg][cc * 8 + k] = ab[k];
+    red[2][rg][cc * 8 + k] = ad[k];
+  }
+  __syncthreads();
+  for (int c = threadIdx.x; c < 512; c += 256) {
+    const int gc = blockIdx.x * 512 + c;
+    if (gc >= H) continue;
+    atomicAdd(dgamma + gc, red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c]);
+    atomicAdd(dbeta + gc, red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c]);
+    if (dbias) atomicAdd(dbias + gc, red[2][0][c] + red[2][1][c] + red[2][2][c] + red[2][3][c]);
   }
 }
 
@@ -266,12 +302,17 @@ template <int NCH>
 static void ln_bwd_t(const bf16_t* dout, const bf16_t* z, const float* mean, const float* rstd, const bf16_t* gamma,
                      bf16_t* dz, bf16_t* dy, const bf16_t* dres_add, float* dgamma, float* dbeta, float* dbias,
                      int rows, int H, const DropoutParams& dp, hipStream_t st) {
-  // 16-wave blocks, 2 rows per wave: ~1024 blocks at 32k rows, one atomic per column per block
-  constexpr int NW = 16;
-  const int rpw = rows >= NW * 2 * 512 ? 2 : 1;
-  const int blocks = (rows + NW * rpw - 1) / (NW * rpw);
-  hipLaunchKernelGGL((ln_bwd_kernel<NCH, NW>), dim3(blocks), dim3(NW * 64), 0, st, dout, z, mean, rstd, gamma, dz,
-                     dy, dres_add, dgamma, dbeta, dbias, rows, H, rpw, dp);
+  hipLaunchKernelGGL((ln_bwd_rows_kernel<NCH>), dim3((rows + kLnWaves - 1) / kLnWaves), dim3(256), 0, st, dout, z,
+                     mean, rstd, gamma, dz, dy, dres_add, rows, H, dp);
+  const int gx = (H + 511) / 512;
+  int want_y = max(1, 2048 / gx);
+  int rpb = max(16, (rows + want_y - 1) / want_y);
+  rpb = (rpb + 15) / 16 * 16;
+  const int gy = (rows + rpb - 1) / rpb;
+  // dbias sums the gradient that enters the GEMM (dy, or dz when dy is not materialised separately)
+  const bf16_t* ysrc = dy ? dy : dz;
+  hipLaunchKernelGGL(ln_bwd_cols_kernel, dim3(gx, gy), dim3(256), 0, st, dout, z, mean, rstd, ysrc, dgamma, dbeta,
+                     ysrc ? dbias : nullptr, rows, H, rpb);
 }
 
 void launch_ln_bwd(const bf16_t* dout, const bf16_t* z, const float* mean, const float* rstd, const bf16_t* gamma,
