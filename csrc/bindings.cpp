@@ -224,6 +224,13 @@ void gemm_variant(torch::Tensor A, torch::Tensor B, torch::Tensor C, int64_t la,
                            (int)K, BF(C), C.stride(0), cur_stream());
 }
 
+void gemm_wgrad_variant(torch::Tensor dy, torch::Tensor x, torch::Tensor C, int64_t splits) {
+  TORCH_CHECK(dy.size(0) == x.size(0) && C.size(0) == dy.size(1) && C.size(1) == x.size(1), "shapes");
+  TORCH_CHECK(C.scalar_type() == torch::kFloat32 && dy.size(0) % 64 == 0, "wgrad variant");
+  hsd::launch_gemm_wgrad_variant(CBF(dy), dy.stride(0), CBF(x), x.stride(0), (int)dy.size(1), (int)x.size(1),
+                                 (int)dy.size(0), C.data_ptr<float>(), C.stride(0), (int)splits, cur_stream());
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -241,4 +248,5 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_bwd", &attn_bwd);
   m.def("gemm", &gemm);
   m.def("gemm_variant", &gemm_variant);
+  m.def("gemm_wgrad_variant", &gemm_wgrad_variant);
 }

@@ -51,4 +51,6 @@ void launch_gemm(int la, int lb, int epi, const bf16_t* A, int64_t lda, const bf
                  double p_drop, uint64_t seed, int splits, hipStream_t st);
 void launch_gemm_variant(int la, int lb, int variant, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb,
                          int M, int N, int K, bf16_t* C, int64_t ldc, hipStream_t st);
+void launch_gemm_wgrad_variant(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, int M, int N, int K, float* C,
+                               int64_t ldc, int splits, hipStream_t st);
 }  // namespace hsd

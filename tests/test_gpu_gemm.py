@@ -99,3 +99,26 @@ def test_gemm_dgrad_epilogues(gpu):
     x = aux.float().requires_grad_()
     torch.nn.functional.gelu(x).backward(torch.ones_like(x))
     _check(C, ref.bfloat16().float() * x.grad, 3e-2)
+
+
+@pytest.mark.parametrize("variant", range(8))
+@pytest.mark.parametrize("la,lb", [(0, 0), (0, 1)])
+def test_gemm_variants(gpu, variant, la, lb):
+    torch.manual_seed(6)
+    M, N, K = 640, 768, 512
+    A = _mk((M, K), gpu)
+    B = _mk((N, K) if lb == 0 else (K, N), gpu)
+    C = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    _C().gemm_variant(A, B, C, la, lb, variant)
+    _check(C, _ref(A, B, la, lb))
+
+
+@pytest.mark.parametrize("splits", [1, 4])
+def test_gemm_wgrad_big(gpu, splits):
+    torch.manual_seed(7)
+    T, N, K = 1024, 768, 320
+    dy, x = _mk((T, N), gpu), _mk((T, K), gpu)
+    C0 = torch.randn(N, K, device=gpu)
+    C = C0.clone()
+    _C().gemm_wgrad_variant(dy, x, C, splits)
+    _check(C, C0 + dy.float().t() @ x.float(), 1e-3)

@@ -42,12 +42,14 @@ for name, (N, K) in {"qkv": (2304, 768), "out": (768, 768), "ffn1": (3072, 768),
     r["dgrad_torch"] = fl / bench(lambda: dy @ w) / 1e12
     r["dgrad_hsd"] = fl / bench(lambda: C_.gemm(dy, w, dx, 0, 1, 0, None, None, None, 0.0, 0, 1)) / 1e12
     r["wgrad_torch"] = fl / bench(lambda: dy.t() @ x) / 1e12
+    for sp in (2, 4, 8):
+        r[f"wgrad_big_s{sp}"] = fl / bench(lambda: C_.gemm_wgrad_variant(dy, x, gw, sp)) / 1e12
     tiles = ((N + 127) // 128) * ((K + 127) // 128)
     for sp in (1, 2, 4, 8, 16):
         if tiles * sp > 4096:
             break
         r[f"wgrad_hsd_s{sp}"] = fl / bench(lambda: C_.gemm(dy, x, gw, 1, 1, 6, None, None, None, 0.0, 0, sp)) / 1e12
-    for v in range(6):
+    for v in range(8):
         r[f"fwd_v{v}"] = fl / bench(lambda: C_.gemm_variant(x, w, y, 0, 0, v)) / 1e12
         r[f"dgrad_v{v}"] = fl / bench(lambda: C_.gemm_variant(dy, w, dx, 0, 1, v)) / 1e12
     import os
