@@ -5,6 +5,8 @@ cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
 mkdir -p gpurun_out
 python -m huggingface_sagemaker_tensorflow_distributed_amd._build > gpurun_out/build.log 2>&1 || { tail -20 gpurun_out/build.log; exit 1; }
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { tail -20 gpurun_out/smoke.log; exit 1; }
+tail -1 gpurun_out/smoke.log
 timeout -k 10 900 python -m pytest tests -x -q -m gpu ${PYTEST_ARGS} > gpurun_out/gpu_tests.log 2>&1
 rc=$?; tail -25 gpurun_out/gpu_tests.log
 [ $rc -eq 0 ] || exit $rc
