@@ -231,6 +231,59 @@ void gemm_wgrad_variant(torch::Tensor dy, torch::Tensor x, torch::Tensor C, int6
                                  (int)dy.size(0), C.data_ptr<float>(), C.stride(0), (int)splits, cur_stream());
 }
 
+// gemm2: la=lb=0 -> NT (A [M,K], B [N,K]) bf16 C with epilogue 0..5;
+//        la=lb=1 -> TT (A [K,M], B [K,N]) fp32 C += A^T B, epi 6 atomics / 7 slabs in ws.
+void gemm2(torch::Tensor A, torch::Tensor B, torch::Tensor C, int64_t la, int64_t lb, int64_t epi,
+           c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> aux, c10::optional<torch::Tensor> C2,
+           double p, int64_t seed, int64_t splits, c10::optional<torch::Tensor> ws) {
+  TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda(), "gemm2 operands must be GPU tensors");
+  TORCH_CHECK(A.scalar_type() == torch::kBFloat16 && B.scalar_type() == torch::kBFloat16, "gemm2 inputs must be bf16");
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "gemm2 operands must be 2-D");
+  TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && C.stride(1) == 1, "gemm2 operands need unit inner stride");
+  TORCH_CHECK(la == lb, "gemm2 layouts: NT (0,0) or TT (1,1)");
+  const int64_t M = la == 0 ? A.size(0) : A.size(1);
+  const int64_t K = la == 0 ? A.size(1) : A.size(0);
+  const int64_t N = lb == 0 ? B.size(0) : B.size(1);
+  const int64_t KB = lb == 0 ? B.size(1) : B.size(0);
+  TORCH_CHECK(K == KB, "gemm2 K mismatch");
+  TORCH_CHECK(C.size(0) == M && C.size(1) == N, "gemm2 C shape");
+  TORCH_CHECK(hsd::gemm2_supported((int)la, (int)lb, (int)epi, (int)M, (int)N, (int)K), "gemm2: unsupported shape/epilogue");
+  TORCH_CHECK(A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0 && C.stride(0) % 8 == 0, "gemm2 leading dims alignment");
+  const bool f32out = epi >= 6;
+  TORCH_CHECK(C.scalar_type() == (f32out ? torch::kFloat32 : torch::kBFloat16), "gemm2 C dtype");
+  if (epi == 1 || epi == 2 || epi == 3) {
+    TORCH_CHECK(bias.has_value() && bias->numel() == N && bias->scalar_type() == torch::kBFloat16 &&
+                bias->is_contiguous(), "gemm2 bias");
+  }
+  if (epi == 3 || epi == 4 || epi == 5) {
+    TORCH_CHECK(aux.has_value() && aux->dim() == 2 && aux->size(0) == M && aux->size(1) == N &&
+                aux->stride(1) == 1 && aux->stride(0) % 8 == 0 && aux->scalar_type() == torch::kBFloat16, "gemm2 aux");
+  }
+  if (epi == 2) {
+    TORCH_CHECK(C2.has_value() && C2->sizes() == C.sizes() && C2->strides() == C.strides() &&
+                C2->scalar_type() == torch::kBFloat16, "gemm2 C2");
+  }
+  float* wsp = nullptr;
+  int sp = (int)splits;
+  if (f32out && sp <= 0) sp = hsd::gemm2_wgrad_splits((int)M, (int)N, (int)K);
+  if (epi == 7) {
+    TORCH_CHECK(C.is_contiguous() || C.stride(0) % 4 == 0, "gemm2 slab C");
+    TORCH_CHECK(ws.has_value() && ws->scalar_type() == torch::kFloat32 && ws->is_contiguous() &&
+                ws->numel() >= (int64_t)sp * M * N, "gemm2 slab workspace too small");
+    wsp = ws->data_ptr<float>();
+  }
+  if (!f32out) TORCH_CHECK(sp == 1, "split-K only with fp32 output");
+  hsd::launch_gemm2((int)la, (int)lb, (int)epi, CBF(A), A.stride(0), CBF(B), B.stride(0), (int)M, (int)N, (int)K,
+                    C.data_ptr(), C.stride(0), bias.has_value() ? CBF(*bias) : nullptr,
+                    aux.has_value() ? CBF(*aux) : nullptr, aux.has_value() ? aux->stride(0) : 0,
+                    C2.has_value() ? BF(*C2) : nullptr, p, (uint64_t)seed, sp, wsp, cur_stream());
+}
+
+int64_t gemm2_splits(int64_t M, int64_t N, int64_t K) { return hsd::gemm2_wgrad_splits((int)M, (int)N, (int)K); }
+bool gemm2_supported(int64_t la, int64_t lb, int64_t epi, int64_t M, int64_t N, int64_t K) {
+  return la == lb && hsd::gemm2_supported((int)la, (int)lb, (int)epi, (int)M, (int)N, (int)K);
+}
+
 }  // namespace
 
 PYBIND11_MODULE(_C, m) {
@@ -248,5 +301,8 @@ PYBIND11_MODULE(_C, m) {
   m.def("attn_bwd", &attn_bwd);
   m.def("gemm", &gemm);
   m.def("gemm_variant", &gemm_variant);
+  m.def("gemm2", &gemm2);
+  m.def("gemm2_splits", &gemm2_splits);
+  m.def("gemm2_supported", &gemm2_supported);
   m.def("gemm_wgrad_variant", &gemm_wgrad_variant);
 }

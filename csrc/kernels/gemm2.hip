@@ -1,0 +1,506 @@
+// bf16 MFMA GEMM, 256-row tiles, 8-phase-style schedule (cdna_hip_programming.md §5 "256² 8-phase
+// template": T1 XCD remap, T2 source-swizzled LDS images, T3/T4 phase interleave with counted vmcnt
+// across raw s_barriers, T5 s_setprio around the MFMA clusters).
+//
+//   C[m][n] = Σ_k A(m,k) · B(n,k)        fp32 accumulate, v_mfma_f32_16x16x32_bf16
+//
+// Operand layouts (template LA / LB):
+//   0 = k-contiguous   A[M][K] / B[N][K]  -> LDS image [rows][64 k], 128-B rows, 16-B chunk ^ ((row>>1)&7),
+//                                            fragments by ds_read_b128
+//   1 = k-strided      A[K][M] / B[K][N]  -> LDS image [64 k][256], 512-B rows,
+//                                            16-B chunk ^ 2·((k&3) | ((k>>3)&1)<<2), fragments by the
+//                                            transposing ds_read_b64_tr_b16
+// (both images bank-conflict-free for their fragment reads: tools/lds_banks.py model).
+//
+// Uses in the BERT step:
+//   forward  Y  = X · Wᵀ    NT  (LA=0, LB=0)   bf16 out + fused epilogue
+//   dgrad    dX = dY · W    NT with Wᵀ stored [K][N] -> B(n,k) = Wᵀ[n][k]  (LA=0, LB=0)
+//   wgrad    dW += dYᵀ · X  TT  (LA=1, LB=1)   fp32 out, split-K over tokens into slabs + reduce
+//
+// Block = 512 threads = 8 waves as 2 (M) x 4 (N); tile 256 x BN x 64; wave tile 128 x BN/4.
+// Per K-tile a wave runs 4 phases over its output quadrants (A rows 0-63 / 64-127 of the wave,
+// B cols first / second half): P1 reads A-sub0 + B-sub0, P2 B-sub1, P3 A-sub1, P4 no reads. The
+// next K-tile's LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave instruction) is spread over
+// P4(prev) / P1 / P2 / P3 into the other LDS stage and retired by ONE counted vmcnt at the end of P4.
+#include "common.h"
+#include <stdlib.h>
+
+namespace hsd {
+
+enum Epi2 : int { E2_STORE = 0, E2_BIAS = 1, E2_BIAS_GELU = 2, E2_BIAS_DROP_RES = 3, E2_RES = 4, E2_DGELU = 5,
+                  E2_F32_ATOMIC = 6, E2_F32_SLAB = 7 };
+
+struct G2Params {
+  const bf16_t* A;
+  int64_t lda;
+  const bf16_t* B;
+  int64_t ldb;
+  int M, N, K;
+  void* C;  // bf16 [M][ldc], or fp32 (atomic: [M][ldc]; slab: [splits][M][N])
+  int64_t ldc;
+  const bf16_t* bias;
+  const bf16_t* aux;
+  int64_t ldaux;
+  bf16_t* C2;
+  DropoutParams dp;
+  int kps;  // K elements per split (multiple of 64)
+  int tiles_n;
+};
+
+namespace g2 {
+
+constexpr int BM = 256, BK = 64;
+
+__device__ __forceinline__ int f1(int row) { return (row >> 1) & 7; }
+__device__ __forceinline__ int f2(int k) { return ((k & 3) | (((k >> 3) & 1) << 2)) << 1; }
+
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4_t;
+
+#define G2_BARRIER()                       \
+  do {                                     \
+    asm volatile("" ::: "memory");         \
+    __builtin_amdgcn_sched_barrier(0);     \
+    __builtin_amdgcn_s_barrier();          \
+    __builtin_amdgcn_sched_barrier(0);     \
+    asm volatile("" ::: "memory");         \
+  } while (0)
+
+template <int N>
+__device__ __forceinline__ void vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// One 1-KiB LDS-DMA wave instruction `g` of an operand tile image (see header for the images).
+template <int L, int R>
+__device__ __forceinline__ void dma(bf16_t* img, const bf16_t* __restrict__ X, int64_t ld, int r0, int Rmax, int k0,
+                                    int g, int lane) {
+  const bf16_t* src;
+  if constexpr (L == 0) {
+    const int row = g * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ f1(row);
+    const int rr = min(r0 + row, Rmax - 1);
+    src = X + (int64_t)rr * ld + k0 + lc * 8;
+  } else {
+    static_assert(R == 256, "k-strided images are 256 wide");
+    const int krow = g * 2 + (lane >> 5);
+    const int lc = (lane & 31) ^ f2(krow);
+    const int cc = min(r0 + lc * 8, Rmax - 8);
+    src = X + (int64_t)(k0 + krow) * ld + cc;
+  }
+  __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                   (__attribute__((address_space(3))) void*)(img + g * 512), 16, 0, 0);
+}
+
+// 16x16x32 operand fragment: lane l holds rows (rbase + (l&15)), k = 32·ks + 8·(l>>4) + 0..7
+template <int L>
+__device__ __forceinline__ bf16x8 frag(const bf16_t* img, int rbase, int ks, int lane) {
+  if constexpr (L == 0) {
+    const int row = rbase + (lane & 15);
+    const int ch = (lane >> 4) + 4 * ks;
+    return *reinterpret_cast<const bf16x8*>(img + row * 64 + ((ch ^ f1(row)) << 3));
+  } else {
+    const int g = lane >> 4, i = lane & 15, q = i >> 2, p = i & 3;
+    const int k = 32 * ks + 8 * g + q;
+    const int m = rbase + 4 * p;
+    const int k2 = k + 4;
+    bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_bf16x4_t*)(img + k * 256 + (((m >> 3) ^ f2(k)) << 3) + (m & 7)));
+    bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
+        (lds_bf16x4_t*)(img + k2 * 256 + (((m >> 3) ^ f2(k2)) << 3) + (m & 7)));
+    bf16x8 r;
+    r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
+    r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
+    return r;
+  }
+}
+
+__device__ __forceinline__ u32x2 pack4(const f32x4& v) {
+  u32x2 o;
+  o.x = pack_bf2(v[0], v[1]);
+  o.y = pack_bf2(v[2], v[3]);
+  return o;
+}
+
+template <int LA, int LB, int EPI, int BN>
+__global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
+  constexpr int WN = BN / 4;       // wave tile columns
+  constexpr int NREP = WN / 16;    // 16-col MFMA blocks per wave
+  constexpr int NB0 = 2;           // B-sub0 blocks (cols 0..31 of the wave)
+  constexpr int NB1 = NREP - NB0;  // B-sub1 blocks
+  static_assert(NREP == 3 || NREP == 4, "BN 192 or 256");
+  static_assert(LB == 0 || BN == 256, "k-strided B needs BN 256");
+  constexpr int TA = BM * 64, TB = BN * 64, STAGE = TA + TB;
+  constexpr int GA = 4;                              // DMA instructions per wave per stage for A
+  constexpr int GB = (LB == 0) ? BN / 64 : 4;        // ... for B
+  constexpr int G = GA + GB;                         // 8 (BN 256) or 7 (BN 192)
+  constexpr int D0 = 2;                              // issued in P4 of the previous tile
+  constexpr bool F32OUT = EPI == E2_F32_ATOMIC || EPI == E2_F32_SLAB;
+
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+
+  // XCD-aware bijective remap: blocks sharing an XCD get consecutive tiles (same A row panel)
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tm = wg / p.tiles_n, tn = wg % p.tiles_n;
+  const int m0 = tm * BM, n0 = tn * BN;
+  const int kbeg = blockIdx.y * p.kps;
+  const int kend = min(p.K, kbeg + p.kps);
+  const int nt = (kend - kbeg) / BK;
+
+  auto dma_slot = [&](int q, bf16_t* stage, int k0) {
+    if (q < GA) dma<LA, BM>(stage, p.A, p.lda, m0, p.M, k0, wave * GA + q, lane);
+    else dma<LB, BN>(stage + TA, p.B, p.ldb, n0, p.N, k0, wave * GB + (q - GA), lane);
+  };
+
+  f32x4 acc[8][NREP];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < NREP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  // prologue: tile 0 whole, first D0 slots of tile 1
+#pragma unroll
+  for (int q = 0; q < G; ++q) dma_slot(q, smem, kbeg);
+  if (nt > 1) {
+#pragma unroll
+    for (int q = 0; q < D0; ++q) dma_slot(q, smem + STAGE, kbeg + BK);
+    vmcnt<D0>();
+  } else {
+    vmcnt<0>();
+  }
+  G2_BARRIER();
+
+  const int arow = wm * 128;
+  const int bcol = wn * WN;
+  bf16x8 fa[4][2], fb0[NB0][2], fb1[NB1][2];
+
+  for (int t = 0; t < nt; ++t) {
+    const bf16_t* cA = smem + (t & 1) * STAGE;
+    const bf16_t* cB = cA + TA;
+    bf16_t* nS = smem + ((t + 1) & 1) * STAGE;
+    const bool n1 = t + 1 < nt, n2 = t + 2 < nt;
+    const int k1 = kbeg + (t + 1) * BK, k2 = kbeg + (t + 2) * BK;
+
+    // ---------------- P1: A-sub0, B-sub0
+#pragma unroll
+    for (int j = 0; j < NB0; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) fb0[j][ks] = frag<LB>(cB, bcol + 16 * j, ks, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<LA>(cA, arow + 16 * i, ks, lane);
+    if (n1) {
+#pragma unroll
+      for (int q = D0; q < D0 + 2; ++q) dma_slot(q, nS, k1);
+    }
+    G2_BARRIER();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NB0; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][ks], fa[i][ks], acc[i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    G2_BARRIER();
+
+    // ---------------- P2: B-sub1
+#pragma unroll
+    for (int j = 0; j < NB1; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) fb1[j][ks] = frag<LB>(cB, bcol + 16 * (NB0 + j), ks, lane);
+    if (n1) {
+#pragma unroll
+      for (int q = D0 + 2; q < D0 + 4; ++q) dma_slot(q, nS, k1);
+    }
+    G2_BARRIER();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NB1; ++j)
+          acc[i][NB0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][ks], fa[i][ks], acc[i][NB0 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    G2_BARRIER();
+
+    // ---------------- P3: A-sub1
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<LA>(cA, arow + 64 + 16 * i, ks, lane);
+    if (n1) {
+#pragma unroll
+      for (int q = D0 + 4; q < G; ++q) dma_slot(q, nS, k1);
+    }
+    G2_BARRIER();
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NB1; ++j)
+          acc[4 + i][NB0 + j] =
+              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][ks], fa[i][ks], acc[4 + i][NB0 + j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    G2_BARRIER();
+
+    // ---------------- P4: registers only; first D0 slots of tile t+2 into this (now free) stage
+    if (n2) {
+#pragma unroll
+      for (int q = 0; q < D0; ++q) dma_slot(q, const_cast<bf16_t*>(cA), k2);
+    }
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NB0; ++j)
+          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][ks], fa[i][ks], acc[4 + i][j], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    if (n2) vmcnt<D0>();
+    else vmcnt<0>();
+    G2_BARRIER();
+  }
+
+  // ================================================================ epilogue
+  // acc[i][j] = D[n][m] block: lane l holds m = 16i + (l&15), n = 16j + 4(l>>4) + r (r = 0..3)
+  const int mw = m0 + arow, nw = n0 + bcol;
+  const int q4 = lane >> 4, lr = lane & 15;
+  if constexpr (F32OUT) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int m = mw + 16 * i + lr;
+      if (m >= p.M) continue;
+#pragma unroll
+      for (int j = 0; j < NREP; ++j) {
+        const int n = nw + 16 * j + 4 * q4;
+        if (n >= p.N) continue;
+        if constexpr (EPI == E2_F32_ATOMIC) {
+          float* c = reinterpret_cast<float*>(p.C) + (int64_t)m * p.ldc + n;
+          atomicAdd(c + 0, acc[i][j][0]);
+          atomicAdd(c + 1, acc[i][j][1]);
+          atomicAdd(c + 2, acc[i][j][2]);
+          atomicAdd(c + 3, acc[i][j][3]);
+        } else {
+          float* c = reinterpret_cast<float*>(p.C) + (int64_t)blockIdx.y * p.M * p.N + (int64_t)m * p.N + n;
+          *reinterpret_cast<f32x4*>(c) = acc[i][j];
+        }
+      }
+    }
+  } else {
+    // stage bf16(acc [+ bias]) through a wave-private LDS slice ([64 rows][WN + 8]), then write whole
+    // rows with 16-B lanes: each lane owns 8 consecutive n of one m.
+    constexpr int SROW = WN + 8;
+    constexpr int CPR = WN / 8;  // 16-B chunks per row
+    constexpr bool kBias = EPI == E2_BIAS || EPI == E2_BIAS_GELU || EPI == E2_BIAS_DROP_RES;
+    constexpr bool kAux = EPI == E2_BIAS_DROP_RES || EPI == E2_RES || EPI == E2_DGELU;
+    bf16_t* stg = smem + wave * (64 * SROW);
+    f32x4 bv[NREP];
+    if constexpr (kBias) {
+#pragma unroll
+      for (int j = 0; j < NREP; ++j) {
+        const int n = min(nw + 16 * j + 4 * q4, p.N - 4);
+        const u32x2 b = *reinterpret_cast<const u32x2*>(p.bias + n);
+        bv[j] = f32x4{lo_bf(b.x), hi_bf(b.x), lo_bf(b.y), hi_bf(b.y)};
+      }
+    }
+    bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NREP; ++j) {
+          f32x4 v = acc[4 * h + i][j];
+          if constexpr (kBias) v += bv[j];
+          *reinterpret_cast<u32x2*>(stg + (16 * i + lr) * SROW + 16 * j + 4 * q4) = pack4(v);
+        }
+      __builtin_amdgcn_wave_barrier();
+      constexpr int ITER = 64 * CPR / 64;
+      u32x4 sv[ITER], xv[ITER];
+#pragma unroll
+      for (int it = 0; it < ITER; ++it) {
+        const int idx = lane + 64 * it;
+        const int row = idx / CPR, c8 = idx % CPR;
+        sv[it] = *reinterpret_cast<const u32x4*>(stg + row * SROW + c8 * 8);
+        if constexpr (kAux) {
+          const int m = min(mw + 64 * h + row, p.M - 1);
+          xv[it] = *reinterpret_cast<const u32x4*>(p.aux + (int64_t)m * p.ldaux + nw + c8 * 8);
+        }
+      }
+#pragma unroll
+      for (int it = 0; it < ITER; ++it) {
+        const int idx = lane + 64 * it;
+        const int row = idx / CPR, c8 = idx % CPR;
+        const int m = mw + 64 * h + row;
+        const int n = nw + c8 * 8;
+        if (m >= p.M) continue;
+        const int64_t co = (int64_t)m * p.ldc + n;
+        u32x4 o = sv[it];
+        if constexpr (EPI == E2_BIAS_GELU) {
+          *reinterpret_cast<u32x4*>(C + co) = o;  // pre-activation (kept for backward)
+          u32x4 g;
+          g.x = pack_bf2(gelu_erf(lo_bf(o.x)), gelu_erf(hi_bf(o.x)));
+          g.y = pack_bf2(gelu_erf(lo_bf(o.y)), gelu_erf(hi_bf(o.y)));
+          g.z = pack_bf2(gelu_erf(lo_bf(o.z)), gelu_erf(hi_bf(o.z)));
+          g.w = pack_bf2(gelu_erf(lo_bf(o.w)), gelu_erf(hi_bf(o.w)));
+          *reinterpret_cast<u32x4*>(p.C2 + co) = g;
+          continue;
+        } else if constexpr (EPI == E2_BIAS_DROP_RES) {
+          // z = bf16(bf16(y · keep · scale) + residual)
+          float v[8] = {lo_bf(o.x), hi_bf(o.x), lo_bf(o.y), hi_bf(o.y), lo_bf(o.z), hi_bf(o.z), lo_bf(o.w), hi_bf(o.w)};
+          if (p.dp.enabled) {
+            const uint32_t pair0 = (uint32_t)(((int64_t)m * p.N + n) >> 1);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) {
+              const uint32_t b = dropout_bits(pair0 + e, p.dp.seed_lo, p.dp.seed_hi);
+              v[2 * e] = bf2f(f2bf(v[2 * e] * keep_factor(b, 0, p.dp)));
+              v[2 * e + 1] = bf2f(f2bf(v[2 * e + 1] * keep_factor(b, 1, p.dp)));
+            }
+          }
+          const u32x4 x = xv[it];
+          o.x = pack_bf2(v[0] + lo_bf(x.x), v[1] + hi_bf(x.x));
+          o.y = pack_bf2(v[2] + lo_bf(x.y), v[3] + hi_bf(x.y));
+          o.z = pack_bf2(v[4] + lo_bf(x.z), v[5] + hi_bf(x.z));
+          o.w = pack_bf2(v[6] + lo_bf(x.w), v[7] + hi_bf(x.w));
+        } else if constexpr (EPI == E2_RES) {
+          const u32x4 x = xv[it];
+          o.x = pack_bf2(lo_bf(o.x) + lo_bf(x.x), hi_bf(o.x) + hi_bf(x.x));
+          o.y = pack_bf2(lo_bf(o.y) + lo_bf(x.y), hi_bf(o.y) + hi_bf(x.y));
+          o.z = pack_bf2(lo_bf(o.z) + lo_bf(x.z), hi_bf(o.z) + hi_bf(x.z));
+          o.w = pack_bf2(lo_bf(o.w) + lo_bf(x.w), hi_bf(o.w) + hi_bf(x.w));
+        } else if constexpr (EPI == E2_DGELU) {
+          const u32x4 x = xv[it];
+          o.x = pack_bf2(lo_bf(o.x) * gelu_erf_grad(lo_bf(x.x)), hi_bf(o.x) * gelu_erf_grad(hi_bf(x.x)));
+          o.y = pack_bf2(lo_bf(o.y) * gelu_erf_grad(lo_bf(x.y)), hi_bf(o.y) * gelu_erf_grad(hi_bf(x.y)));
+          o.z = pack_bf2(lo_bf(o.z) * gelu_erf_grad(lo_bf(x.z)), hi_bf(o.z) * gelu_erf_grad(hi_bf(x.z)));
+          o.w = pack_bf2(lo_bf(o.w) * gelu_erf_grad(lo_bf(x.w)), hi_bf(o.w) * gelu_erf_grad(hi_bf(x.w)));
+        }
+        *reinterpret_cast<u32x4*>(C + co) = o;
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+  }
+}
+
+// main_grad[i] += Σ_s ws[s][i]   (float4 lanes, grid-stride)
+__global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ ws, float* __restrict__ C,
+                                                          int64_t ldc, int M, int N, int splits) {
+  const int64_t n4 = (int64_t)M * N / 4;
+  const int64_t plane = (int64_t)M * N;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const int64_t e = i * 4;
+    f32x4 s = *reinterpret_cast<const f32x4*>(ws + e);
+    for (int k = 1; k < splits; ++k) s += *reinterpret_cast<const f32x4*>(ws + k * plane + e);
+    const int64_t m = e / N, n = e % N;
+    f32x4* c = reinterpret_cast<f32x4*>(C + m * ldc + n);
+    *c = *c + s;
+  }
+}
+
+}  // namespace g2
+
+template <int LA, int LB, int EPI, int BN>
+static void g2_launch(const G2Params& p0, int splits, hipStream_t st) {
+  G2Params p = p0;
+  const int tiles_m = (p.M + g2::BM - 1) / g2::BM;
+  p.tiles_n = (p.N + BN - 1) / BN;
+  if (splits < 1) splits = 1;
+  int kps = (p.K + splits - 1) / splits;
+  kps = (kps + g2::BK - 1) / g2::BK * g2::BK;
+  splits = (p.K + kps - 1) / kps;
+  p.kps = kps;
+  dim3 grid(tiles_m * p.tiles_n, splits);
+  hipLaunchKernelGGL((g2::gemm2_kernel<LA, LB, EPI, BN>), grid, dim3(512), 0, st, p);
+  HSD_CHECK_LAUNCH();
+}
+
+// Tile width for a bf16-output NT GEMM: minimise (rounds of 256 CUs) x (per-tile cost ∝ BN + c).
+int gemm2_pick_bn(int M, int N) {
+  const int tm = (M + 255) / 256;
+  int best = 0;
+  double best_cost = 1e30;
+  for (int bn : {256, 192}) {
+    if (N % bn) continue;
+    const int blocks = tm * (N / bn);
+    const int rounds = (blocks + 255) / 256;
+    const double cost = rounds * (bn + 64.0);
+    if (cost < best_cost) { best_cost = cost; best = bn; }
+  }
+  return best;
+}
+
+bool gemm2_supported(int la, int lb, int epi, int M, int N, int K) {
+  if (K % 64 || M < 1 || N % 8) return false;
+  if (la == 0 && lb == 0) return epi <= E2_DGELU && gemm2_pick_bn(M, N) != 0;
+  if (la == 1 && lb == 1) return (epi == E2_F32_ATOMIC || epi == E2_F32_SLAB) && M % 8 == 0 && N % 256 == 0;
+  return false;
+}
+
+// splits for the TT wgrad: fill ~one wave of 256 CUs with >= 4 K-tiles per block
+int gemm2_wgrad_splits(int M, int N, int K) {
+  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  int s = 256 / tiles;
+  if (s < 1) s = 1;
+  const int kt = K / 64;
+  while (s > 1 && kt / s < 4) --s;
+  return s;
+}
+
+void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, int M, int N,
+                  int K, void* C, int64_t ldc, const bf16_t* bias, const bf16_t* aux, int64_t ldaux, bf16_t* C2,
+                  double p_drop, uint64_t seed, int splits, float* ws, hipStream_t st) {
+  G2Params p{};
+  p.A = A; p.lda = lda; p.B = B; p.ldb = ldb; p.M = M; p.N = N; p.K = K; p.C = C; p.ldc = ldc;
+  p.bias = bias; p.aux = aux; p.ldaux = ldaux; p.C2 = C2;
+  p.dp = make_dropout(p_drop, seed);
+  if (la == 0 && lb == 0) {
+    const int bn = gemm2_pick_bn(M, N);
+#define G2_NT(E)                                                     \
+  case E:                                                            \
+    if (bn == 256) g2_launch<0, 0, E, 256>(p, 1, st);                \
+    else g2_launch<0, 0, E, 192>(p, 1, st);                          \
+    return;
+    switch (epi) {
+      G2_NT(E2_STORE)
+      G2_NT(E2_BIAS)
+      G2_NT(E2_BIAS_GELU)
+      G2_NT(E2_BIAS_DROP_RES)
+      G2_NT(E2_RES)
+      G2_NT(E2_DGELU)
+      default: abort();
+    }
+#undef G2_NT
+  } else if (la == 1 && lb == 1) {
+    if (splits <= 0) splits = gemm2_wgrad_splits(M, N, K);
+    if (epi == E2_F32_SLAB && splits > 1 && ws != nullptr) {
+      G2Params q = p;
+      q.C = ws;
+      g2_launch<1, 1, E2_F32_SLAB, 256>(q, splits, st);
+      int kps = (K + splits - 1) / splits;
+      kps = (kps + 63) / 64 * 64;
+      const int real = (K + kps - 1) / kps;
+      const int64_t n4 = (int64_t)M * N / 4;
+      int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
+      hipLaunchKernelGGL(g2::slab_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, reinterpret_cast<float*>(C), ldc,
+                         M, N, real);
+      HSD_CHECK_LAUNCH();
+    } else {
+      g2_launch<1, 1, E2_F32_ATOMIC, 256>(p, splits, st);
+    }
+  } else {
+    abort();
+  }
+}
+
+}  // namespace hsd

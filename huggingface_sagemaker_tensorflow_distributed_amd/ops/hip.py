@@ -300,24 +300,54 @@ def _wgrad_splits(n_out: int, k_in: int, tokens: int) -> int:
     return s
 
 
+_WS = {}
+
+
+def _workspace(numel: int, device) -> torch.Tensor:
+    """Split-K slab workspace (fp32), grown on demand, reused stream-ordered across wgrad GEMMs."""
+    key = (device.type, device.index)
+    buf = _WS.get(key)
+    if buf is None or buf.numel() < numel:
+        buf = torch.empty(max(numel, 1 << 20), dtype=torch.float32, device=device)
+        _WS[key] = buf
+    return buf
+
+
+def _nt_ok(M, N, K, epi):
+    return _C.gemm2_supported(0, 0, epi, M, N, K)
+
+
 def gemm_fwd(x, w, epi, bias=None, aux=None, out2=None, p=0.0, seed=0):
-    """y[T, N] = x[T, K] · w[N, K]ᵀ with epilogue."""
+    """y[T, N] = x[T, K] · w[N, K]ᵀ with epilogue (gemm2 8-phase kernel; 128-tile kernel for odd shapes)."""
     y = torch.empty((x.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)
-    _C.gemm(x, w, y, 0, 0, epi, bias, aux, out2, float(p), _s64(seed), 1)
+    if _nt_ok(x.shape[0], w.shape[0], x.shape[1], epi):
+        _C.gemm2(x, w, y, 0, 0, epi, bias, aux, out2, float(p), _s64(seed), 1, None)
+    else:
+        _C.gemm(x, w, y, 0, 0, epi, bias, aux, out2, float(p), _s64(seed), 1)
     return y
 
 
 def gemm_dgrad(dy, w, epi=EPI_STORE, aux=None):
-    """dx[T, K] = dy[T, N] · w[N, K]."""
+    """dx[T, K] = dy[T, N] · w[N, K]  (NT kernel on the transposed weight wᵀ [K, N])."""
     dx = torch.empty((dy.shape[0], w.shape[1]), dtype=dy.dtype, device=dy.device)
-    _C.gemm(dy, w, dx, 0, 1, epi, None, aux, None, 0.0, 0, 1)
+    if _nt_ok(dy.shape[0], w.shape[1], dy.shape[1], epi):
+        wt = w.t().contiguous()
+        _C.gemm2(dy, wt, dx, 0, 0, epi, None, aux, None, 0.0, 0, 1, None)
+    else:
+        _C.gemm(dy, w, dx, 0, 1, epi, None, aux, None, 0.0, 0, 1)
     return dx
 
 
 def gemm_wgrad_(g: "_Grad", dy, x):
-    """g.buf[N, K] += dy[T, N]ᵀ · x[T, K]   (fp32, atomics, split-K over tokens)."""
-    splits = _wgrad_splits(dy.shape[1], x.shape[1], dy.shape[0])
-    _C.gemm(dy, x, g.buf, 1, 1, EPI_F32_ATOMIC, None, None, None, 0.0, 0, splits)
+    """g.buf[N, K] += dy[T, N]ᵀ · x[T, K]   (fp32; split-K over tokens into slabs + one reduce)."""
+    N, K, T = dy.shape[1], x.shape[1], dy.shape[0]
+    if _C.gemm2_supported(1, 1, 7, N, K, T):
+        sp = _C.gemm2_splits(N, K, T)
+        ws = _workspace(sp * N * K, dy.device)
+        _C.gemm2(dy, x, g.buf, 1, 1, 7, None, None, None, 0.0, 0, sp, ws)
+    else:
+        splits = _wgrad_splits(N, K, T)
+        _C.gemm(dy, x, g.buf, 1, 1, EPI_F32_ATOMIC, None, None, None, 0.0, 0, splits)
 
 
 def _ln_fwd(z, w, b, eps):
