@@ -235,7 +235,8 @@ void gemm_wgrad_variant(torch::Tensor dy, torch::Tensor x, torch::Tensor C, int6
 //        la=lb=1 -> TT (A [K,M], B [K,N]) fp32 C += A^T B, epi 6 atomics / 7 slabs in ws.
 void gemm2(torch::Tensor A, torch::Tensor B, torch::Tensor C, int64_t la, int64_t lb, int64_t epi,
            c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> aux, c10::optional<torch::Tensor> C2,
-           double p, int64_t seed, int64_t splits, c10::optional<torch::Tensor> ws) {
+           double p, int64_t seed, int64_t splits, c10::optional<torch::Tensor> ws,
+           c10::optional<torch::Tensor> dbias) {
   TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda(), "gemm2 operands must be GPU tensors");
   TORCH_CHECK(A.scalar_type() == torch::kBFloat16 && B.scalar_type() == torch::kBFloat16, "gemm2 inputs must be bf16");
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "gemm2 operands must be 2-D");
@@ -273,10 +274,17 @@ void gemm2(torch::Tensor A, torch::Tensor B, torch::Tensor C, int64_t la, int64_
     wsp = ws->data_ptr<float>();
   }
   if (!f32out) TORCH_CHECK(sp == 1, "split-K only with fp32 output");
+  float* dbp = nullptr;
+  if (dbias.has_value()) {
+    TORCH_CHECK(epi == 5 && N % 256 == 0, "gemm2 fused dbias: DGELU epilogue with N % 256 == 0");
+    check_f32(*dbias, "dbias");
+    TORCH_CHECK(dbias->numel() == N, "dbias size");
+    dbp = dbias->data_ptr<float>();
+  }
   hsd::launch_gemm2((int)la, (int)lb, (int)epi, CBF(A), A.stride(0), CBF(B), B.stride(0), (int)M, (int)N, (int)K,
                     C.data_ptr(), C.stride(0), bias.has_value() ? CBF(*bias) : nullptr,
                     aux.has_value() ? CBF(*aux) : nullptr, aux.has_value() ? aux->stride(0) : 0,
-                    C2.has_value() ? BF(*C2) : nullptr, p, (uint64_t)seed, sp, wsp, cur_stream());
+                    C2.has_value() ? BF(*C2) : nullptr, p, (uint64_t)seed, sp, wsp, dbp, cur_stream());
 }
 
 int64_t gemm2_splits(int64_t M, int64_t N, int64_t K) { return hsd::gemm2_wgrad_splits((int)M, (int)N, (int)K); }

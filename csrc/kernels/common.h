@@ -88,11 +88,35 @@ __device__ __forceinline__ float keep_factor(uint32_t bits, int e, const Dropout
   return b16 >= d.thr ? d.scale : 0.0f;
 }
 
-__device__ __forceinline__ float gelu_erf(float x) { return 0.5f * x * (1.0f + erff(x * 0.70710678118654752f)); }
+// Exact-erf GELU (HF "gelu") with erf from Abramowitz & Stegun 7.1.26 (|err| <= 1.5e-7, far below bf16
+// resolution): one v_rcp_f32 + one v_exp_f32 + ~12 FMA-class ops instead of libm erff's piecewise
+// polynomial — the GELU epilogues of the FFN GEMMs are VALU-bound (cdna_hip_programming.md §5.4 rule 28).
+//   z = |x|/√2,  t = 1/(1 + p·z),  erf(z) = 1 - P(t)·e^{-z²}
+//   gelu(x)  = max(x, 0) - ½|x|·P·E                 with E = e^{-x²/2}
+//   gelu'(x) = ½(1+erf(x/√2)) + x·E/√(2π)
+struct GeluParts {
+  float pe;  // P(t)·E
+  float e;   // E
+};
+__device__ __forceinline__ GeluParts gelu_parts(float x) {
+  const float a = fabsf(x);
+  const float t = __builtin_amdgcn_rcpf(fmaf(0.23164189784f /* p/√2 */, a, 1.0f));
+  float P = fmaf(t, 1.061405429f, -1.453152027f);
+  P = fmaf(t, P, 1.421413741f);
+  P = fmaf(t, P, -0.284496736f);
+  P = fmaf(t, P, 0.254829592f);
+  P *= t;
+  const float e = __builtin_amdgcn_exp2f(x * x * -0.72134752044f /* -½·log2(e) */);
+  return {P * e, e};
+}
+__device__ __forceinline__ float gelu_erf(float x) {
+  const GeluParts g = gelu_parts(x);
+  return fmaf(-0.5f * fabsf(x), g.pe, fmaxf(x, 0.0f));
+}
 __device__ __forceinline__ float gelu_erf_grad(float x) {
-  // d/dx [0.5 x (1+erf(x/√2))] = 0.5(1+erf(x/√2)) + x·φ(x)
-  const float kInvSqrt2Pi = 0.3989422804014327f;
-  return 0.5f * (1.0f + erff(x * 0.70710678118654752f)) + x * kInvSqrt2Pi * __expf(-0.5f * x * x);
+  const GeluParts g = gelu_parts(x);
+  const float half_1p_erf = x >= 0.0f ? fmaf(-0.5f, g.pe, 1.0f) : 0.5f * g.pe;
+  return fmaf(x * 0.3989422804014327f, g.e, half_1p_erf);
 }
 
 }  // namespace hsd

@@ -45,6 +45,7 @@ struct G2Params {
   DropoutParams dp;
   int kps;  // K elements per split (multiple of 64)
   int tiles_n;
+  float* dbias;  // E2_DGELU: optional fp32 column sums of the output (the bias gradient), BN 256 only
 };
 
 namespace g2 {
@@ -315,6 +316,8 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
       }
     }
     bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
+    constexpr bool kColsum = EPI == E2_DGELU && CPR == 8;
+    float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
 #pragma unroll
@@ -385,10 +388,34 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
           o.y = pack_bf2(lo_bf(o.y) * gelu_erf_grad(lo_bf(x.y)), hi_bf(o.y) * gelu_erf_grad(hi_bf(x.y)));
           o.z = pack_bf2(lo_bf(o.z) * gelu_erf_grad(lo_bf(x.z)), hi_bf(o.z) * gelu_erf_grad(hi_bf(x.z)));
           o.w = pack_bf2(lo_bf(o.w) * gelu_erf_grad(lo_bf(x.w)), hi_bf(o.w) * gelu_erf_grad(hi_bf(x.w)));
+          if constexpr (kColsum) {
+            csum[0] += lo_bf(o.x); csum[1] += hi_bf(o.x); csum[2] += lo_bf(o.y); csum[3] += hi_bf(o.y);
+            csum[4] += lo_bf(o.z); csum[5] += hi_bf(o.z); csum[6] += lo_bf(o.w); csum[7] += hi_bf(o.w);
+          }
         }
         *reinterpret_cast<u32x4*>(C + co) = o;
       }
       __builtin_amdgcn_wave_barrier();
+    }
+    if constexpr (kColsum) {
+      // lanes with equal (lane & 7) own the same 8 columns: reduce over lane bits 3..5, then 8 lanes add
+      if (p.dbias != nullptr) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) {
+          float v = csum[e];
+          v += __shfl_xor(v, 8, 64);
+          v += __shfl_xor(v, 16, 64);
+          v += __shfl_xor(v, 32, 64);
+          csum[e] = v;
+        }
+        if (lane < 8) {
+          const int n = nw + lane * 8;
+          if (n < p.N) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) atomicAdd(p.dbias + n + e, csum[e]);
+          }
+        }
+      }
     }
   }
 }
@@ -459,13 +486,18 @@ int gemm2_wgrad_splits(int M, int N, int K) {
 
 void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, int M, int N,
                   int K, void* C, int64_t ldc, const bf16_t* bias, const bf16_t* aux, int64_t ldaux, bf16_t* C2,
-                  double p_drop, uint64_t seed, int splits, float* ws, hipStream_t st) {
+                  double p_drop, uint64_t seed, int splits, float* ws, float* dbias, hipStream_t st) {
   G2Params p{};
+  p.dbias = dbias;
   p.A = A; p.lda = lda; p.B = B; p.ldb = ldb; p.M = M; p.N = N; p.K = K; p.C = C; p.ldc = ldc;
   p.bias = bias; p.aux = aux; p.ldaux = ldaux; p.C2 = C2;
   p.dp = make_dropout(p_drop, seed);
   if (la == 0 && lb == 0) {
-    const int bn = gemm2_pick_bn(M, N);
+    int bn = gemm2_pick_bn(M, N);
+    if (dbias != nullptr) {
+      if (epi != E2_DGELU || N % 256) abort();  // fused bias-grad column sums: 8 columns per lane (BN 256)
+      bn = 256;
+    }
 #define G2_NT(E)                                                     \
   case E:                                                            \
     if (bn == 256) g2_launch<0, 0, E, 256>(p, 1, st);                \

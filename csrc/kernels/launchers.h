@@ -55,7 +55,7 @@ void launch_gemm_variant(int la, int lb, int variant, const bf16_t* A, int64_t l
 // (epi 6 = atomics, 7 = split-K slabs in `ws` [splits][M][N] + reduce into C)
 void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, int M, int N,
                   int K, void* C, int64_t ldc, const bf16_t* bias, const bf16_t* aux, int64_t ldaux, bf16_t* C2,
-                  double p_drop, uint64_t seed, int splits, float* ws, hipStream_t st);
+                  double p_drop, uint64_t seed, int splits, float* ws, float* dbias, hipStream_t st);
 bool gemm2_supported(int la, int lb, int epi, int M, int N, int K);
 int gemm2_wgrad_splits(int M, int N, int K);
 void launch_gemm_wgrad_variant(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, int M, int N, int K, float* C,

@@ -321,20 +321,28 @@ def gemm_fwd(x, w, epi, bias=None, aux=None, out2=None, p=0.0, seed=0):
     """y[T, N] = x[T, K] · w[N, K]ᵀ with epilogue (gemm2 8-phase kernel; 128-tile kernel for odd shapes)."""
     y = torch.empty((x.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)
     if _nt_ok(x.shape[0], w.shape[0], x.shape[1], epi):
-        _C.gemm2(x, w, y, 0, 0, epi, bias, aux, out2, float(p), _s64(seed), 1, None)
+        _C.gemm2(x, w, y, 0, 0, epi, bias, aux, out2, float(p), _s64(seed), 1, None, None)
     else:
         _C.gemm(x, w, y, 0, 0, epi, bias, aux, out2, float(p), _s64(seed), 1)
     return y
 
 
-def gemm_dgrad(dy, w, epi=EPI_STORE, aux=None):
-    """dx[T, K] = dy[T, N] · w[N, K]  (NT kernel on the transposed weight wᵀ [K, N])."""
+def gemm_dgrad(dy, w, epi=EPI_STORE, aux=None, dbias=None):
+    """dx[T, K] = dy[T, N] · w[N, K]  (NT kernel on the transposed weight wᵀ [K, N]).
+
+    ``dbias`` (DGELU only): fp32 [K] buffer that receives the column sums of dx (the bias gradient of
+    the layer that produced ``aux``) from the epilogue; returns ``(dx, fused)``-style via attribute."""
     dx = torch.empty((dy.shape[0], w.shape[1]), dtype=dy.dtype, device=dy.device)
     if _nt_ok(dy.shape[0], w.shape[1], dy.shape[1], epi):
         wt = w.t().contiguous()
-        _C.gemm2(dy, wt, dx, 0, 0, epi, None, aux, None, 0.0, 0, 1, None)
+        fuse = dbias is not None and epi == EPI_DGELU and w.shape[1] % 256 == 0
+        _C.gemm2(dy, wt, dx, 0, 0, epi, None, aux, None, 0.0, 0, 1, None, dbias if fuse else None)
+        if dbias is not None and not fuse:
+            _C.colsum(dx, dbias)
     else:
         _C.gemm(dy, w, dx, 0, 1, epi, None, aux, None, 0.0, 0, 1)
+        if dbias is not None:
+            _C.colsum(dx, dbias)
     return dx
 
 
@@ -344,7 +352,7 @@ def gemm_wgrad_(g: "_Grad", dy, x):
     if _C.gemm2_supported(1, 1, 7, N, K, T):
         sp = _C.gemm2_splits(N, K, T)
         ws = _workspace(sp * N * K, dy.device)
-        _C.gemm2(dy, x, g.buf, 1, 1, 7, None, None, None, 0.0, 0, sp, ws)
+        _C.gemm2(dy, x, g.buf, 1, 1, 7, None, None, None, 0.0, 0, sp, ws, None)
     else:
         splits = _wgrad_splits(N, K, T)
         _C.gemm(dy, x, g.buf, 1, 1, EPI_F32_ATOMIC, None, None, None, 0.0, 0, splits)
@@ -449,9 +457,8 @@ class _FFNBlock(torch.autograd.Function):
         r_lnw, r_lnb, r_b2 = g_lnw.done(), g_lnb.done(), g_b2.done()
         gemm_wgrad_(g_w2, dy, act)
         r_w2 = g_w2.done()
-        da = gemm_dgrad(dy, w2, EPI_DGELU, aux=pre)
         g_w1, g_b1 = _Grad(w1), _Grad(b1)
-        _C.colsum(da, g_b1.buf)
+        da = gemm_dgrad(dy, w2, EPI_DGELU, aux=pre, dbias=g_b1.buf)
         r_b1 = g_b1.done()
         gemm_wgrad_(g_w1, da, h2d)
         r_w1 = g_w1.done()

@@ -41,7 +41,7 @@ for (M, N, K) in [(300, 768, 128), (512, 2304, 768), (1000, 192 * 5, 64 * 3)]:
     w = torch.randn(N, K, device=dev).bfloat16()
     b = torch.randn(N, device=dev).bfloat16()
     y = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
-    C_.gemm2(x, w, y, 0, 0, 1, b, None, None, 0.0, 0, 1, None)
+    C_.gemm2(x, w, y, 0, 0, 1, b, None, None, 0.0, 0, 1, None, None)
     ref = x.float() @ w.float().t() + b.float()
     e = relerr(y, ref)
     print(f"NT bias M={M} N={N} K={K} err={e:.2e}", flush=True)
@@ -54,7 +54,7 @@ for (M, N, K) in [(300, 768, 128), (512, 2304, 768), (1000, 192 * 5, 64 * 3)]:
             g0 = gw.clone()
             sp = C_.gemm2_splits(N, K, M)
             ws = torch.empty(sp * N * K, device=dev)
-            C_.gemm2(dy, x, gw, 1, 1, epi, None, None, None, 0.0, 0, 0, ws)
+            C_.gemm2(dy, x, gw, 1, 1, epi, None, None, None, 0.0, 0, 0, ws, None)
             ref = g0 + dy.float().t() @ x.float()
             e = relerr(gw, ref)
             print(f"TT epi{epi} M={N} N={K} K={M} splits={sp} err={e:.2e}", flush=True)
@@ -76,31 +76,47 @@ for name, (N, K) in {"qkv": (2304, 768), "out": (768, 768), "ffn1": (3072, 768),
     ws = torch.empty(sp * N * K, device=dev)
     r = {}
     # correctness at full size
-    C_.gemm2(x, w, y, 0, 0, 1, b, None, None, 0.0, 0, 1, None)
+    C_.gemm2(x, w, y, 0, 0, 1, b, None, None, 0.0, 0, 1, None, None)
     r["fwd_err"] = relerr(y, x.float() @ w.float().t() + b.float())
-    C_.gemm2(dy, wt, dx, 0, 0, 0, None, None, None, 0.0, 0, 1, None)
+    C_.gemm2(dy, wt, dx, 0, 0, 0, None, None, None, 0.0, 0, 1, None, None)
     r["dgrad_err"] = relerr(dx, dy.float() @ w.float())
     gw.zero_()
-    C_.gemm2(dy, x, gw, 1, 1, 7, None, None, None, 0.0, 0, 0, ws)
+    C_.gemm2(dy, x, gw, 1, 1, 7, None, None, None, 0.0, 0, 0, ws, None)
     r["wgrad_err"] = relerr(gw, dy.float().t() @ x.float())
     # speed
     r["fwd_torch"] = fl / bench(lambda: torch.addmm(b, x, w.t())) / 1e12
-    r["fwd_bias"] = fl / bench(lambda: C_.gemm2(x, w, y, 0, 0, 1, b, None, None, 0.0, 0, 1, None)) / 1e12
-    r["fwd_store"] = fl / bench(lambda: C_.gemm2(x, w, y, 0, 0, 0, None, None, None, 0.0, 0, 1, None)) / 1e12
-    r["fwd_gelu"] = fl / bench(lambda: C_.gemm2(x, w, y, 0, 0, 2, b, None, y2, 0.0, 0, 1, None)) / 1e12
-    r["fwd_droppres"] = fl / bench(lambda: C_.gemm2(x, w, y, 0, 0, 3, b, res_in, None, 0.1, 7, 1, None)) / 1e12
+    r["fwd_bias"] = fl / bench(lambda: C_.gemm2(x, w, y, 0, 0, 1, b, None, None, 0.0, 0, 1, None, None)) / 1e12
+    r["fwd_store"] = fl / bench(lambda: C_.gemm2(x, w, y, 0, 0, 0, None, None, None, 0.0, 0, 1, None, None)) / 1e12
+    r["fwd_gelu"] = fl / bench(lambda: C_.gemm2(x, w, y, 0, 0, 2, b, None, y2, 0.0, 0, 1, None, None)) / 1e12
+    r["fwd_droppres"] = fl / bench(lambda: C_.gemm2(x, w, y, 0, 0, 3, b, res_in, None, 0.1, 7, 1, None, None)) / 1e12
     r["fwd_old"] = fl / bench(lambda: C_.gemm(x, w, y, 0, 0, 1, b, None, None, 0.0, 0, 1)) / 1e12
     r["dgrad_torch"] = fl / bench(lambda: dy @ w) / 1e12
-    r["dgrad_store"] = fl / bench(lambda: C_.gemm2(dy, wt, dx, 0, 0, 0, None, None, None, 0.0, 0, 1, None)) / 1e12
+    r["dgrad_store"] = fl / bench(lambda: C_.gemm2(dy, wt, dx, 0, 0, 0, None, None, None, 0.0, 0, 1, None, None)) / 1e12
+    pre = torch.randn(T, K, device=dev).bfloat16()
+    db = torch.zeros(K, device=dev)
+    if K % 256 == 0:
+        C_.gemm2(dy, wt, dx, 0, 0, 5, None, pre, None, 0.0, 0, 1, None, db)
+        import math
+        ref = (dy.float() @ w.float())
+        pf = pre.float()
+        gp = 0.5 * (1 + torch.erf(pf / math.sqrt(2))) + pf * torch.exp(-0.5 * pf * pf) / math.sqrt(2 * math.pi)
+        ref = (ref.bfloat16().float() * gp)
+        r["dgelu_err"] = relerr(dx, ref)
+        r["dbias_err"] = relerr(db, dx.float().sum(0))
+        r["dgrad_dgelu_dbias"] = fl / bench(lambda: C_.gemm2(dy, wt, dx, 0, 0, 5, None, pre, None, 0.0, 0, 1, None, db)) / 1e12
+    r["dgrad_dgelu"] = fl / bench(lambda: C_.gemm2(dy, wt, dx, 0, 0, 5, None, pre, None, 0.0, 0, 1, None, None)) / 1e12
+    C_.gemm2(x, w, y, 0, 0, 2, b, None, y2, 0.0, 0, 1, None, None)
+    yf = x.float() @ w.float().t() + b.float()
+    r["gelu_err"] = relerr(y2, torch.nn.functional.gelu(y.float()))
     r["dgrad_old"] = fl / bench(lambda: C_.gemm(dy, w, dx, 0, 1, 0, None, None, None, 0.0, 0, 1)) / 1e12
     r["wgrad_torch"] = fl / bench(lambda: dy.t() @ x) / 1e12
-    r["wgrad_slab"] = fl / bench(lambda: C_.gemm2(dy, x, gw, 1, 1, 7, None, None, None, 0.0, 0, 0, ws)) / 1e12
-    r["wgrad_atomic"] = fl / bench(lambda: C_.gemm2(dy, x, gw, 1, 1, 6, None, None, None, 0.0, 0, 0, None)) / 1e12
+    r["wgrad_slab"] = fl / bench(lambda: C_.gemm2(dy, x, gw, 1, 1, 7, None, None, None, 0.0, 0, 0, ws, None)) / 1e12
+    r["wgrad_atomic"] = fl / bench(lambda: C_.gemm2(dy, x, gw, 1, 1, 6, None, None, None, 0.0, 0, 0, None, None)) / 1e12
     for s2 in (sp // 2, sp * 2):
         if s2 >= 1:
             ws2 = torch.empty(s2 * N * K, device=dev)
             r[f"wgrad_slab_s{s2}"] = fl / bench(lambda: C_.gemm2(dy, x, gw, 1, 1, 7, None, None, None, 0.0, 0, s2,
-                                                                  ws2)) / 1e12
+                                                                  ws2, None)) / 1e12
     r["wgrad_old"] = fl / bench(lambda: C_.gemm(dy, x, gw, 1, 1, 6, None, None, None, 0.0, 0, 8)) / 1e12
     r["splits"] = sp
     res[name] = {k: (round(v, 1) if isinstance(v, float) and v > 1 else v) for k, v in r.items()}
