@@ -19,6 +19,7 @@
 // LDS once for dQ. dQ is written directly when one workgroup covers all keys (S <= 128) and
 // accumulated with fp32 atomics otherwise.
 #include "common.h"
+#include <stdlib.h>
 
 namespace hsd {
 
@@ -367,8 +368,18 @@ __global__ __launch_bounds__(256) void dq_convert_kernel(const float* __restrict
   }
 }
 
+bool attn128_supported(int S, int head_dim);
+void launch_attn128_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse2, int B, int heads, double p,
+                        uint64_t seed, hipStream_t st);
+void launch_attn128_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
+                        bf16_t* dqkv, int B, int heads, double p, uint64_t seed, hipStream_t st);
+
 void launch_attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse2, int B, int S, int heads,
                      double p, uint64_t seed, hipStream_t st) {
+  if (attn128_supported(S, kD) && !getenv("HSD_ATTN_GENERIC")) {
+    launch_attn128_fwd(qkv, mask, out, lse2, B, heads, p, seed, st);
+    return;
+  }
   DropoutParams dp = make_dropout(p, seed);
   const float sl2 = kLog2e / sqrtf((float)kD);
   dim3 grid((S + 127) / 128, B * heads);
@@ -378,6 +389,10 @@ void launch_attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* l
 
 void launch_attn_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
                      bf16_t* dqkv, float* dq_acc, int B, int S, int heads, double p, uint64_t seed, hipStream_t st) {
+  if (attn128_supported(S, kD) && !getenv("HSD_ATTN_GENERIC")) {
+    launch_attn128_bwd(qkv, mask, o, dout, lse2, dqkv, B, heads, p, seed, st);
+    return;
+  }
   DropoutParams dp = make_dropout(p, seed);
   const float sl2 = kLog2e / sqrtf((float)kD);
   const float scale = 1.0f / sqrtf((float)kD);

@@ -1,0 +1,362 @@
+// Self-attention for S == 128, head_dim 64 (the headline BERT-base seq-128 config; SURVEY.md §2.10
+// K4-K7 forward, K14 backward): ONE workgroup per (batch, head) holds the whole 128x128 problem, so
+// Q/K/V/dO are read from HBM exactly once, probabilities never leave registers, and the only
+// workgroup-wide synchronisation is one barrier after the operand DMA (forward) or three (backward).
+//
+// * operands are staged HBM -> LDS with global_load_lds_dwordx4 (1 KiB per wave instruction) into
+//   [128][64] bf16 images whose 16-B chunks are XOR-swizzled (chunk ^ bitrev3((row>>1)&7)) — the
+//   swizzle is applied to the per-lane SOURCE address so the DMA destination stays lane-linear
+//   (cdna_hip_programming.md rule 21); the image is conflict-free for ds_read_b128 row reads AND
+//   ds_read_b64_tr_b16 transposed reads.
+// * forward: wave w owns queries 32w..32w+31 on the MFMA lanes ("swapped" Sᵀ = K·Qᵀ), all 128 keys in
+//   its 64 accumulator registers -> exact (not online) softmax in registers, Oᵀ = Vᵀ·Pᵀ with the
+//   accumulator as the B operand, O staged through a wave-private LDS slice to 128-B row stores.
+// * backward: wave w owns keys 32w..32w+31 on the lanes; loops over 4 query blocks recomputing P from
+//   the saved log-sum-exp, accumulates dKᵀ, dVᵀ in registers, writes dS once to a [128 key][128 q] LDS
+//   image (chunk ^ 4((r&3)^((r>>4)&3)) + ((r>>2)&3): conflict-free for its b64 writes and tr reads),
+//   then dQᵀ = Kᵀ·dSᵀ with wave w owning queries 32w..32w+31. The dropout hash of a key pair is
+//   computed once per lane pair and exchanged (keys sit on adjacent lanes here).
+// Dropout / mask / lse conventions are identical to attention.hip (ops/rng.py site indexing).
+#include "common.h"
+
+namespace hsd {
+namespace a128 {
+
+constexpr int S = 128, D = 64;
+constexpr float kLog2e = 1.4426950408889634f;
+
+typedef __attribute__((address_space(3))) bf16x4 lds_bf16x4;
+
+__device__ __forceinline__ int swz(int row) {
+  const int t = (row >> 1) & 7;
+  return ((t & 1) << 2) | (t & 2) | ((t >> 2) & 1);
+}
+// element offset of (row, col) in a [rows][64] bf16 image
+__device__ __forceinline__ int toff(int row, int col) { return row * 64 + (((col >> 3) ^ swz(row)) << 3) + (col & 7); }
+// [128][128] dS image
+__device__ __forceinline__ int fS(int row) { return 4 * ((row & 3) ^ ((row >> 4) & 3)) + ((row >> 2) & 3); }
+__device__ __forceinline__ int soff(int row, int col) { return row * 128 + (((col >> 3) ^ fS(row)) << 3) + (col & 7); }
+// wave-private [32][64] output staging slice
+__device__ __forceinline__ int stoff(int row, int col) { return row * 64 + (((col >> 3) ^ ((row >> 1) & 7)) << 3) + (col & 7); }
+
+__device__ __forceinline__ bf16x4 tr_read(const bf16_t* base, int elem_off) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_bf16x4*)(base + elem_off));
+}
+__device__ __forceinline__ bf16x8 cat8(bf16x4 a, bf16x4 b) {
+  bf16x8 r;
+  r[0] = a[0]; r[1] = a[1]; r[2] = a[2]; r[3] = a[3];
+  r[4] = b[0]; r[5] = b[1]; r[6] = b[2]; r[7] = b[3];
+  return r;
+}
+__device__ __forceinline__ bf16x8 pack8(const f32x16& acc, int s) {
+  bf16x8 r;
+#pragma unroll
+  for (int j = 0; j < 8; ++j) r[j] = (short)f2bf(acc[8 * s + j]);
+  return r;
+}
+// Transposed A operand from a [rows][64] image: rows rb + 16s + 8(j>>2) + 4h + (j&3) (the accumulator's
+// permuted k order), columns colblk*32 + (lane & 31).
+__device__ __forceinline__ bf16x8 trA(const bf16_t* img, int rb, int s, int colblk, int lane) {
+  const int g = lane >> 4, i = lane & 15, h = g >> 1, q = i >> 2, p = i & 3;
+  const int col = colblk * 32 + 16 * (g & 1) + 4 * p;
+  const int r0 = rb + 16 * s + 4 * h + q;
+  return cat8(tr_read(img, toff(r0, col)), tr_read(img, toff(r0 + 8, col)));
+}
+// Same from the [128][128] dS image (columns cb + (lane & 31)).
+__device__ __forceinline__ bf16x8 trS(const bf16_t* img, int rb, int s, int cb, int lane) {
+  const int g = lane >> 4, i = lane & 15, h = g >> 1, q = i >> 2, p = i & 3;
+  const int col = cb + 16 * (g & 1) + 4 * p;
+  const int r0 = rb + 16 * s + 4 * h + q;
+  return cat8(tr_read(img, soff(r0, col)), tr_read(img, soff(r0 + 8, col)));
+}
+
+// DMA rows [0,128) x 64 cols of a qkv / [T][H] column block into a [128][64] image: 16 instructions,
+// wave w issues instructions w*per .. (w+1)*per-1.
+__device__ __forceinline__ void dma_img(bf16_t* img, const bf16_t* __restrict__ src0, int64_t ld, int first, int count,
+                                        int lane) {
+  for (int g = first; g < first + count; ++g) {
+    const int row = g * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ swz(row);
+    const bf16_t* src = src0 + (int64_t)row * ld + lc * 8;
+    __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
+                                     (__attribute__((address_space(3))) void*)(img + g * 512), 16, 0, 0);
+  }
+}
+
+// acc (32 rows on the lane x 64 d in regs: d = 32*blk + (reg&3) + 8(reg>>2) + 4h) * scale -> bf16 rows
+// of `dst` (row stride ld) through the wave-private staging slice `stg` ([32][64]).
+__device__ __forceinline__ void store_rows(bf16_t* stg, const f32x16& a0, const f32x16& a1, float scale,
+                                           bf16_t* __restrict__ dst, int64_t ld, int lane) {
+  const int r = lane & 31, h = lane >> 5;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    u32x2 w0, w1;
+    w0.x = pack_bf2(a0[4 * i] * scale, a0[4 * i + 1] * scale);
+    w0.y = pack_bf2(a0[4 * i + 2] * scale, a0[4 * i + 3] * scale);
+    w1.x = pack_bf2(a1[4 * i] * scale, a1[4 * i + 1] * scale);
+    w1.y = pack_bf2(a1[4 * i + 2] * scale, a1[4 * i + 3] * scale);
+    *reinterpret_cast<u32x2*>(stg + stoff(r, 8 * i + 4 * h)) = w0;
+    *reinterpret_cast<u32x2*>(stg + stoff(r, 32 + 8 * i + 4 * h)) = w1;
+  }
+  __builtin_amdgcn_wave_barrier();
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int row = (lane >> 3) + 8 * it, c = lane & 7;
+    const u32x4 v = *reinterpret_cast<const u32x4*>(stg + stoff(row, c * 8));
+    *reinterpret_cast<u32x4*>(dst + (int64_t)row * ld + c * 8) = v;
+  }
+  __builtin_amdgcn_wave_barrier();
+}
+
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 2) void attn128_fwd_kernel(const bf16_t* __restrict__ qkv,
+                                                             const float* __restrict__ mask, bf16_t* __restrict__ out,
+                                                             float* __restrict__ lse2, int heads, float sl2,
+                                                             DropoutParams dp) {
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * S * D + 4 * 32 * D + 2 * S];
+  bf16_t* Ks = lds;
+  bf16_t* Vs = lds + S * D;
+  bf16_t* stg_all = lds + 2 * S * D;
+  float* mbias = reinterpret_cast<float*>(lds + 2 * S * D + 4 * 32 * D);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, hf = lane >> 5;
+  const int bh = blockIdx.x, b = bh / heads, hh = bh % heads;
+  const int H = heads * D, ld = 3 * H;
+  const bf16_t* base = qkv + (int64_t)b * S * ld + hh * D;
+
+  // K, V -> LDS (8 DMA instructions per wave), Q fragments -> registers, mask bias -> LDS
+  dma_img(Ks, base + H, ld, wave * 4, 4, lane);
+  dma_img(Vs, base + 2 * H, ld, wave * 4, 4, lane);
+  const int q = wave * 32 + r;
+  bf16x8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(base + (int64_t)q * ld + 16 * s + 8 * hf);
+  if (tid < S) mbias[tid] = mask ? fmaxf(mask[(int64_t)b * S + tid] * kLog2e, -1e30f) : 0.f;
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  // Sᵀ[key][q]: 4 key blocks of 32
+  f32x16 st[4];
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb) {
+    st[kb] = f32x16{};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 a = *reinterpret_cast<const bf16x8*>(Ks + toff(kb * 32 + r, 16 * s + 8 * hf));
+      st[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s], st[kb], 0, 0, 0);
+    }
+  }
+  // exact softmax over the 128 keys of this query (64 in-lane + the partner half-wave)
+  float mx = -INFINITY;
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int g4 = 0; g4 < 4; ++g4) {
+      const f32x4 mb = *reinterpret_cast<const f32x4*>(mbias + kb * 32 + 8 * g4 + 4 * hf);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float x = fmaf(st[kb][4 * g4 + e], sl2, mb[e]);
+        st[kb][4 * g4 + e] = x;
+        mx = fmaxf(mx, x);
+      }
+    }
+  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  float l = 0.f;
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      const float p = __builtin_amdgcn_exp2f(st[kb][reg] - mx);
+      l += p;
+      st[kb][reg] = p;
+    }
+  l += __shfl_xor(l, 32, 64);
+  if (dp.enabled) {
+    const uint32_t rowbase = (uint32_t)(((int64_t)bh * S + q) * S);
+#pragma unroll
+    for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+      for (int reg = 0; reg < 16; reg += 2) {
+        const int key = kb * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * hf;
+        const uint32_t bits = dropout_bits((rowbase + key) >> 1, dp.seed_lo, dp.seed_hi);
+        st[kb][reg] *= keep_factor(bits, 0, dp);
+        st[kb][reg + 1] *= keep_factor(bits, 1, dp);
+      }
+  }
+  // Oᵀ[d][q] = Σ_key Vᵀ[d][key] Pᵀ[key][q]
+  f32x16 o0 = {}, o1 = {};
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 pb = pack8(st[kb], s);
+      o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(Vs, kb * 32, s, 0, lane), pb, o0, 0, 0, 0);
+      o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(Vs, kb * 32, s, 1, lane), pb, o1, 0, 0, 0);
+    }
+  if (hf == 0) lse2[(int64_t)bh * S + q] = mx + __log2f(l);
+  store_rows(stg_all + wave * 32 * D, o0, o1, 1.0f / l, out + ((int64_t)b * S + wave * 32) * H + hh * D, H, lane);
+}
+
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 2) void attn128_bwd_kernel(const bf16_t* __restrict__ qkv,
+                                                             const float* __restrict__ mask,
+                                                             const bf16_t* __restrict__ o,
+                                                             const bf16_t* __restrict__ dout,
+                                                             const float* __restrict__ lse2,
+                                                             bf16_t* __restrict__ dqkv, int heads, float sl2,
+                                                             float scale, DropoutParams dp) {
+  // [Q | dO | dS | lse | delta]; after the main loop Q's slot holds K, dO's slot the output staging
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * S * D + S * S + 4 * S];
+  bf16_t* Qs = lds;
+  bf16_t* dOs = lds + S * D;
+  bf16_t* dSt = lds + 2 * S * D;
+  float* lse_s = reinterpret_cast<float*>(lds + 2 * S * D + S * S);
+  float* del_s = lse_s + S;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, hf = lane >> 5;
+  const int bh = blockIdx.x, b = bh / heads, hh = bh % heads;
+  const int H = heads * D, ld = 3 * H;
+  const bf16_t* base = qkv + (int64_t)b * S * ld + hh * D;
+  const bf16_t* obase = o + (int64_t)b * S * H + hh * D;
+  const bf16_t* dobase = dout + (int64_t)b * S * H + hh * D;
+
+  dma_img(Qs, base, ld, wave * 4, 4, lane);
+  dma_img(dOs, dobase, H, wave * 4, 4, lane);
+  const int key = wave * 32 + r;
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    kf[s] = *reinterpret_cast<const bf16x8*>(base + (int64_t)key * ld + H + 16 * s + 8 * hf);
+    vf[s] = *reinterpret_cast<const bf16x8*>(base + (int64_t)key * ld + 2 * H + 16 * s + 8 * hf);
+  }
+  const float kb2 = mask ? fmaxf(mask[(int64_t)b * S + key] * kLog2e, -1e30f) : 0.f;
+  // delta[q] = Σ_d dO[q][d]·O[q][d]: thread handles rows (tid>>3) + 32i, chunk tid&7
+  {
+    float part[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = (tid >> 3) + 32 * i, c = tid & 7;
+      const u32x4 ov = *reinterpret_cast<const u32x4*>(obase + (int64_t)row * H + c * 8);
+      const u32x4 dv = *reinterpret_cast<const u32x4*>(dobase + (int64_t)row * H + c * 8);
+      float acc = 0.f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) acc += lo_bf(dv[k]) * lo_bf(ov[k]) + hi_bf(dv[k]) * hi_bf(ov[k]);
+      acc += __shfl_xor(acc, 1, 64);
+      acc += __shfl_xor(acc, 2, 64);
+      acc += __shfl_xor(acc, 4, 64);
+      part[i] = acc;
+    }
+    if ((tid & 7) == 0) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) del_s[(tid >> 3) + 32 * i] = part[i];
+    }
+    if (tid < S) lse_s[tid] = lse2[(int64_t)bh * S + tid];
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  f32x16 dk0 = {}, dk1 = {}, dv0 = {}, dv1 = {};
+  const bool odd = (lane & 1) != 0;
+#pragma unroll 1
+  for (int qb = 0; qb < 4; ++qb) {
+    f32x16 sacc = {}, dpacc = {};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const bf16x8 aq = *reinterpret_cast<const bf16x8*>(Qs + toff(qb * 32 + r, 16 * s + 8 * hf));
+      sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aq, kf[s], sacc, 0, 0, 0);
+      const bf16x8 ad = *reinterpret_cast<const bf16x8*>(dOs + toff(qb * 32 + r, 16 * s + 8 * hf));
+      dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ad, vf[s], dpacc, 0, 0, 0);
+    }
+    // rows: query qi = (reg&3) + 8(reg>>2) + 4hf of the block; col (lane): key
+    f32x16 pd, ds;
+#pragma unroll
+    for (int reg = 0; reg < 16; reg += 2) {
+      const int qi0 = qb * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * hf;  // rows qi0, qi0 + 1
+      const f32x2 lse = *reinterpret_cast<const f32x2*>(lse_s + qi0);
+      const f32x2 del = *reinterpret_cast<const f32x2*>(del_s + qi0);
+      const float p0 = __builtin_amdgcn_exp2f(fmaf(sacc[reg], sl2, kb2) - lse[0]);
+      const float p1 = __builtin_amdgcn_exp2f(fmaf(sacc[reg + 1], sl2, kb2) - lse[1]);
+      float k0 = 1.f, k1 = 1.f;
+      if (dp.enabled) {
+        // element ((bh*S + q)*S + key): keys 2j, 2j+1 (lanes l, l^1) share one hash per query row.
+        // even lane hashes row qi0, odd lane row qi0+1, then they swap.
+        const int qmine = odd ? qi0 + 1 : qi0;
+        const uint32_t e = (uint32_t)(((int64_t)bh * S + qmine) * S + key);
+        const uint32_t bits = dropout_bits(e >> 1, dp.seed_lo, dp.seed_hi);
+        const uint32_t other = (uint32_t)__shfl_xor((int)bits, 1, 64);
+        const uint32_t b0 = odd ? other : bits;   // hash of row qi0
+        const uint32_t b1 = odd ? bits : other;   // hash of row qi0 + 1
+        k0 = keep_factor(b0, key & 1, dp);
+        k1 = keep_factor(b1, key & 1, dp);
+      }
+      pd[reg] = p0 * k0;
+      pd[reg + 1] = p1 * k1;
+      ds[reg] = p0 * fmaf(dpacc[reg], k0, -del[0]);
+      ds[reg + 1] = p1 * fmaf(dpacc[reg + 1], k1, -del[1]);
+    }
+    // dVᵀ += dOᵀ·Pd, dKᵀ += Qᵀ·dS  (accumulators as B operands, rows of the images in the same order)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 pb = pack8(pd, s);
+      const bf16x8 sb = pack8(ds, s);
+      dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(dOs, qb * 32, s, 0, lane), pb, dv0, 0, 0, 0);
+      dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(dOs, qb * 32, s, 1, lane), pb, dv1, 0, 0, 0);
+      dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(Qs, qb * 32, s, 0, lane), sb, dk0, 0, 0, 0);
+      dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(Qs, qb * 32, s, 1, lane), sb, dk1, 0, 0, 0);
+    }
+    // dS -> [key][q] image
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      u32x2 w;
+      w.x = pack_bf2(ds[4 * i], ds[4 * i + 1]);
+      w.y = pack_bf2(ds[4 * i + 2], ds[4 * i + 3]);
+      *reinterpret_cast<u32x2*>(dSt + soff(key, qb * 32 + 8 * i + 4 * hf)) = w;
+    }
+  }
+  __syncthreads();  // every dS written; Q / dO no longer read
+  // K -> Q's slot for dQ; dK, dV out through this wave's staging slice (dO's slot)
+  dma_img(Qs, base + H, ld, wave * 4, 4, lane);
+  bf16_t* stg = dOs + wave * 32 * D;
+  bf16_t* rowbase = dqkv + ((int64_t)b * S + wave * 32) * ld + hh * D;
+  store_rows(stg, dv0, dv1, 1.0f, rowbase + 2 * H, ld, lane);
+  store_rows(stg, dk0, dk1, scale, rowbase + H, ld, lane);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  // dQᵀ[d][q] = Σ_key Kᵀ[d][key] dSᵀ[key][q], wave w: queries 32w..32w+31
+  f32x16 dq0 = {}, dq1 = {};
+#pragma unroll
+  for (int kb = 0; kb < 4; ++kb)
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      const bf16x8 bs = trS(dSt, kb * 32, s, wave * 32, lane);
+      dq0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(Qs, kb * 32, s, 0, lane), bs, dq0, 0, 0, 0);
+      dq1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(Qs, kb * 32, s, 1, lane), bs, dq1, 0, 0, 0);
+    }
+  store_rows(stg, dq0, dq1, scale, rowbase, ld, lane);
+}
+
+}  // namespace a128
+
+bool attn128_supported(int S, int head_dim) { return S == a128::S && head_dim == a128::D; }
+
+void launch_attn128_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse2, int B, int heads, double p,
+                        uint64_t seed, hipStream_t st) {
+  DropoutParams dp = make_dropout(p, seed);
+  const float sl2 = a128::kLog2e / sqrtf((float)a128::D);
+  hipLaunchKernelGGL(a128::attn128_fwd_kernel, dim3(B * heads), dim3(256), 0, st, qkv, mask, out, lse2, heads, sl2, dp);
+  HSD_CHECK_LAUNCH();
+}
+
+void launch_attn128_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
+                        bf16_t* dqkv, int B, int heads, double p, uint64_t seed, hipStream_t st) {
+  DropoutParams dp = make_dropout(p, seed);
+  const float sl2 = a128::kLog2e / sqrtf((float)a128::D);
+  const float scale = 1.0f / sqrtf((float)a128::D);
+  hipLaunchKernelGGL(a128::attn128_bwd_kernel, dim3(B * heads), dim3(256), 0, st, qkv, mask, o, dout, lse2, dqkv,
+                     heads, sl2, scale, dp);
+  HSD_CHECK_LAUNCH();
+}
+
+}  // namespace hsd

@@ -16,6 +16,7 @@ namespace hsd {
 
 typedef uint16_t bf16_t;
 typedef __attribute__((ext_vector_type(4))) float f32x4;
+typedef __attribute__((ext_vector_type(2))) float f32x2;
 typedef __attribute__((ext_vector_type(16))) float f32x16;
 typedef __attribute__((ext_vector_type(8))) short bf16x8;   // MFMA A/B fragment (8 bf16)
 typedef __attribute__((ext_vector_type(4))) short bf16x4;

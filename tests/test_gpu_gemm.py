@@ -122,3 +122,71 @@ def test_gemm_wgrad_big(gpu, splits):
     C = C0.clone()
     _C().gemm_wgrad_variant(dy, x, C, splits)
     _check(C, C0 + dy.float().t() @ x.float(), 1e-3)
+
+
+# ---------------------------------------------------------------- gemm2 (8-phase 256-row tiles)
+G2_SHAPES = [(256, 768, 768), (300, 768, 128), (1000, 960, 192), (512, 2304, 256), (768, 3072, 512)]
+
+
+def _gelu_grad(x):
+    import math
+
+    return 0.5 * (1 + torch.erf(x / math.sqrt(2))) + x * torch.exp(-0.5 * x * x) / math.sqrt(2 * math.pi)
+
+
+@pytest.mark.parametrize("M,N,K", G2_SHAPES)
+@pytest.mark.parametrize("epi", [0, 1, 2, 3, 4, 5])
+def test_gemm2_nt_epilogues(gpu, M, N, K, epi):
+    from huggingface_sagemaker_tensorflow_distributed_amd.ops import reference as ref
+
+    torch.manual_seed(11 + epi)
+    C_ = _C()
+    A, B = _mk((M, K), gpu), _mk((N, K), gpu, 0.1)
+    bias, aux = _mk((N,), gpu), _mk((M, N), gpu)
+    C = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    C2 = torch.empty_like(C)
+    p = 0.1 if epi == 3 else 0.0
+    C_.gemm2(A, B, C, 0, 0, epi, bias if epi in (1, 2, 3) else None, aux if epi in (3, 4, 5) else None,
+             C2 if epi == 2 else None, p, 99, 1, None, None)
+    acc = A.float() @ B.float().t()
+    if epi in (1, 2, 3):
+        acc = acc + bias.float()
+    if epi == 2:
+        _check(C, acc)
+        _check(C2, torch.nn.functional.gelu(C.float()))
+        return
+    if epi == 3:
+        y = acc.bfloat16().float()
+        keep = ref.dropout(torch.ones(M, N, device=gpu), p, 99, True)
+        acc = (y * keep).bfloat16().float() + aux.float()
+    elif epi == 4:
+        acc = acc.bfloat16().float() + aux.float()
+    elif epi == 5:
+        acc = acc.bfloat16().float() * _gelu_grad(aux.float())
+    _check(C, acc)
+
+
+@pytest.mark.parametrize("M,N,K", [(768, 768, 256), (2304, 768, 512), (256, 1024, 4096)])
+@pytest.mark.parametrize("epi", [6, 7])
+def test_gemm2_tt_wgrad(gpu, M, N, K, epi):
+    torch.manual_seed(12)
+    C_ = _C()
+    A, B = _mk((K, M), gpu), _mk((K, N), gpu)
+    C0 = torch.randn(M, N, device=gpu)
+    C = C0.clone()
+    sp = C_.gemm2_splits(M, N, K)
+    ws = torch.empty(sp * M * N, device=gpu) if epi == 7 else None
+    C_.gemm2(A, B, C, 1, 1, epi, None, None, None, 0.0, 0, sp, ws, None)
+    _check(C, C0 + A.float().t() @ B.float(), 1e-3)
+
+
+def test_gemm2_dgelu_fused_dbias(gpu):
+    torch.manual_seed(13)
+    C_ = _C()
+    M, N, K = 1024, 3072, 768
+    A, B, pre = _mk((M, K), gpu), _mk((N, K), gpu, 0.1), _mk((M, N), gpu)
+    C = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    db = torch.full((N,), 0.5, device=gpu)
+    C_.gemm2(A, B, C, 0, 0, 5, None, pre, None, 0.0, 0, 1, None, db)
+    _check(C, (A.float() @ B.float().t()).bfloat16().float() * _gelu_grad(pre.float()))
+    _check(db, 0.5 + C.float().sum(0), 1e-3)
