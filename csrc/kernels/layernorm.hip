@@ -12,6 +12,8 @@
 // partial sums for the weight/bias gradients accumulate in registers across the rows a block
 // walks, with no atomics until the block ends.
 #include "common.h"
+#include <stdlib.h>
+#include <algorithm>
 
 namespace hsd {
 
@@ -275,6 +277,77 @@ __global__ __launch_bounds__(256) void ln_bwd_cols_kernel(const bf16_t* __restri
   }
 }
 
+// Single pass: every wave walks `rpw` consecutive rows (next row's loads in flight while the current
+// row reduces), keeps dgamma / dbeta / dbias column partials in registers, and the block reduces its 4
+// waves' partials through LDS into one fp32 atomic per column per block. Reads dout, z once; writes
+// dz, dy once (the split rows + cols passes read dout / z twice).
+template <int NCH>
+__global__ __launch_bounds__(256) void ln_bwd_fused_kernel(const bf16_t* __restrict__ dout,
+                                                           const bf16_t* __restrict__ z,
+                                                           const float* __restrict__ mean_in,
+                                                           const float* __restrict__ rstd_in,
+                                                           const bf16_t* __restrict__ gamma, bf16_t* __restrict__ dz_out,
+                                                           bf16_t* __restrict__ dy_out,
+                                                           const bf16_t* __restrict__ dres_add,
+                                                           float* __restrict__ dgamma, float* __restrict__ dbeta,
+                                                           float* __restrict__ dbias, int rows, int H, int rpw,
+                                                           DropoutParams dp) {
+  __shared__ float red[kLnWaves][3][NCH * 256];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int nq = H >> 2;
+  const int r0 = (blockIdx.x * kLnWaves + wave) * rpw;
+  const int r1 = min(rows, r0 + rpw);
+  float gam[NCH][4], ag[NCH][4], ab[NCH][4], ad[NCH][4];
+#pragma unroll
+  for (int i = 0; i < NCH; ++i) {
+    const int c = lane + 64 * i;
+#pragma unroll
+    for (int k = 0; k < 4; ++k) gam[i][k] = ag[i][k] = ab[i][k] = ad[i][k] = 0.f;
+    if (c < nq) {
+      const u32x2 gw = *reinterpret_cast<const u32x2*>(gamma + 4 * c);
+      gam[i][0] = lo_bf(gw.x); gam[i][1] = hi_bf(gw.x); gam[i][2] = lo_bf(gw.y); gam[i][3] = hi_bf(gw.y);
+    }
+  }
+  if (r0 < r1) {
+    u32x2 za[NCH], da[NCH], zb[NCH], db[NCH];
+    ln_bwd_load<NCH>(dout, z, r0, H, lane, za, da);
+    float mu = mean_in[r0], rs = rstd_in[r0];
+    for (int r = r0; r < r1; r += 2) {
+      const bool more = r + 1 < r1;
+      float mu2 = 0.f, rs2 = 0.f;
+      if (more) {
+        ln_bwd_load<NCH>(dout, z, r + 1, H, lane, zb, db);
+        mu2 = mean_in[r + 1];
+        rs2 = rstd_in[r + 1];
+      }
+      ln_bwd_row<NCH>(za, da, mu, rs, gam, r, H, lane, dz_out, dy_out, dres_add, dp, ag, ab, ad);
+      if (!more) break;
+      const bool more2 = r + 2 < r1;
+      if (more2) {
+        ln_bwd_load<NCH>(dout, z, r + 2, H, lane, za, da);
+        mu = mean_in[r + 2];
+        rs = rstd_in[r + 2];
+      }
+      ln_bwd_row<NCH>(zb, db, mu2, rs2, gam, r + 1, H, lane, dz_out, dy_out, dres_add, dp, ag, ab, ad);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < NCH; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const int col = 4 * (lane + 64 * i) + k;
+      red[wave][0][col] = ag[i][k];
+      red[wave][1][col] = ab[i][k];
+      red[wave][2][col] = ad[i][k];
+    }
+  __syncthreads();
+  for (int c = threadIdx.x; c < H; c += 256) {
+    atomicAdd(dgamma + c, red[0][0][c] + red[1][0][c] + red[2][0][c] + red[3][0][c]);
+    atomicAdd(dbeta + c, red[0][1][c] + red[1][1][c] + red[2][1][c] + red[3][1][c]);
+    if (dbias && dy_out) atomicAdd(dbias + c, red[0][2][c] + red[1][2][c] + red[2][2][c] + red[3][2][c]);
+  }
+}
+
 template <int NCH>
 static void ln_fwd_t(const bf16_t* y, const bf16_t* res, const bf16_t* gamma, const bf16_t* beta, bf16_t* z,
                      bf16_t* out, float* mean, float* rstd, int rows, int H, float eps, const DropoutParams& dp,
@@ -302,6 +375,17 @@ template <int NCH>
 static void ln_bwd_t(const bf16_t* dout, const bf16_t* z, const float* mean, const float* rstd, const bf16_t* gamma,
                      bf16_t* dz, bf16_t* dy, const bf16_t* dres_add, float* dgamma, float* dbeta, float* dbias,
                      int rows, int H, const DropoutParams& dp, hipStream_t st) {
+  if (!getenv("HSD_LN_SPLIT")) {
+    // ~16 rows per wave: 2048 waves = 8 per CU, a few thousand column atomics per block
+    const int rpw = std::max(4, (rows + 2047) / 2048);
+    const int waves = (rows + rpw - 1) / rpw;
+    const int blocks = (waves + kLnWaves - 1) / kLnWaves;
+    // dbias sums the gradient that enters the GEMM: dy (or dz, which equals dy when there is no dropout)
+    bf16_t* ysink = dy ? dy : nullptr;
+    hipLaunchKernelGGL((ln_bwd_fused_kernel<NCH>), dim3(blocks), dim3(256), 0, st, dout, z, mean, rstd, gamma, dz,
+                       ysink, dres_add, dgamma, dbeta, dbias, rows, H, rpw, dp);
+    return;
+  }
   hipLaunchKernelGGL((ln_bwd_rows_kernel<NCH>), dim3((rows + kLnWaves - 1) / kLnWaves), dim3(256), 0, st, dout, z,
                      mean, rstd, gamma, dz, dy, dres_add, rows, H, dp);
   const int gx = (H + 511) / 512;
