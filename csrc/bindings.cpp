@@ -5,6 +5,10 @@
 
 #include "kernels/launchers.h"
 
+namespace hsd {
+void register_comm(pybind11::module& m);
+}
+
 namespace {
 
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
@@ -287,6 +291,12 @@ void gemm2(torch::Tensor A, torch::Tensor B, torch::Tensor C, int64_t la, int64_
                     C2.has_value() ? BF(*C2) : nullptr, p, (uint64_t)seed, sp, wsp, dbp, cur_stream());
 }
 
+void transpose_many(torch::Tensor desc, int64_t total_tiles) {
+  TORCH_CHECK(desc.is_cuda() && desc.scalar_type() == torch::kInt64 && desc.dim() == 2 && desc.size(1) == 5 &&
+              desc.is_contiguous(), "transpose_many: int64 [n, 5] device descriptor table");
+  hsd::launch_transpose_many(desc.data_ptr<int64_t>(), (int)desc.size(0), (int)total_tiles, cur_stream());
+}
+
 int64_t gemm2_splits(int64_t M, int64_t N, int64_t K) { return hsd::gemm2_wgrad_splits((int)M, (int)N, (int)K); }
 bool gemm2_supported(int64_t la, int64_t lb, int64_t epi, int64_t M, int64_t N, int64_t K) {
   return la == lb && hsd::gemm2_supported((int)la, (int)lb, (int)epi, (int)M, (int)N, (int)K);
@@ -296,6 +306,7 @@ bool gemm2_supported(int64_t la, int64_t lb, int64_t epi, int64_t M, int64_t N, 
 
 PYBIND11_MODULE(_C, m) {
   m.doc() = "gfx950 HIP kernels for huggingface_sagemaker_tensorflow_distributed_amd";
+  hsd::register_comm(m);
   m.def("adam_step", &adam_step);
   m.def("ln_fwd", &ln_fwd);
   m.def("ln_bwd", &ln_bwd);
@@ -312,5 +323,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm2", &gemm2);
   m.def("gemm2_splits", &gemm2_splits);
   m.def("gemm2_supported", &gemm2_supported);
+  m.def("transpose_many", &transpose_many);
   m.def("gemm_wgrad_variant", &gemm_wgrad_variant);
 }

@@ -1,0 +1,261 @@
+// Native gradient-communication engine: the MI355X replacement for Horovod's C++ core + NCCL
+// (reference: hvd.DistributedOptimizer at scripts/train.py:114 and BroadcastGlobalVariablesCallback at
+// scripts/train.py:133).
+//
+// * One RCCL communicator per process (one process per GPU), bootstrapped from an ncclUniqueId that
+//   Python passes around through torch's TCPStore — no MPI, no per-step negotiation.
+// * A dedicated high-priority HIP stream for collectives. Every collective is ordered after the work
+//   already queued on the caller's (compute) stream by an event, so it overlaps with the backward
+//   kernels queued after it; `wait_all` makes the compute stream wait for the collectives' events
+//   (the host never blocks).
+// * Static gradient buckets over ONE flat gradient buffer (the FlatParamStore's main_grad): the
+//   backward kernels mark parameters ready in a deterministic order on every rank, so the engine
+//   launches bucket b's in-place ncclAllReduce as soon as its last parameter is ready — the role of
+//   Horovod's 64 MiB fusion buffer + coordinator, without the coordinator.
+#include <torch/extension.h>
+#include <c10/hip/HIPStream.h>
+#include <c10/hip/HIPCachingAllocator.h>
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <cstring>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+namespace hsd {
+namespace {
+
+#define HIP_OK(x)                                                                       \
+  do {                                                                                  \
+    hipError_t e__ = (x);                                                               \
+    if (e__ != hipSuccess) throw std::runtime_error(std::string("HIP: ") + hipGetErrorString(e__) + " at " #x); \
+  } while (0)
+#define NCCL_OK(x)                                                                      \
+  do {                                                                                  \
+    ncclResult_t r__ = (x);                                                             \
+    if (r__ != ncclSuccess) throw std::runtime_error(std::string("RCCL: ") + ncclGetErrorString(r__) + " at " #x); \
+  } while (0)
+
+ncclDataType_t to_nccl(at::ScalarType t) {
+  switch (t) {
+    case at::kFloat: return ncclFloat32;
+    case at::kDouble: return ncclFloat64;
+    case at::kHalf: return ncclFloat16;
+    case at::kBFloat16: return ncclBfloat16;
+    case at::kInt: return ncclInt32;
+    case at::kLong: return ncclInt64;
+    case at::kByte: return ncclUint8;
+    default: throw std::runtime_error("CommEngine: unsupported dtype");
+  }
+}
+
+struct Bucket {
+  int64_t start = 0, end = 0;  // element range in the flat buffer
+  int nparams = 0;
+  int pending = 0;
+  bool launched = false;
+  hipEvent_t done = nullptr;
+};
+
+class CommEngine {
+ public:
+  CommEngine(int64_t rank, int64_t world, const std::string& uid, int64_t device, bool high_priority)
+      : rank_((int)rank), world_((int)world), device_((int)device) {
+    if (uid.size() != sizeof(ncclUniqueId)) throw std::runtime_error("CommEngine: bad unique id size");
+    HIP_OK(hipSetDevice(device_));
+    int lo = 0, hi = 0;
+    HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
+    HIP_OK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, high_priority ? hi : lo));
+    ncclUniqueId id;
+    std::memcpy(&id, uid.data(), sizeof(id));
+    NCCL_OK(ncclCommInitRank(&comm_, world_, id, rank_));
+    HIP_OK(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
+  }
+
+  ~CommEngine() {
+    for (auto& b : buckets_)
+      if (b.done) (void)hipEventDestroy(b.done);
+    for (auto e : extra_) (void)hipEventDestroy(e);
+    if (ready_) (void)hipEventDestroy(ready_);
+    if (comm_) (void)ncclCommDestroy(comm_);
+    if (stream_) (void)hipStreamDestroy(stream_);
+  }
+
+  static std::string unique_id() {
+    ncclUniqueId id;
+    NCCL_OK(ncclGetUniqueId(&id));
+    return std::string(reinterpret_cast<const char*>(&id), sizeof(id));
+  }
+
+  int64_t rank() const { return rank_; }
+  int64_t world() const { return world_; }
+
+  // ---------------------------------------------------------------- one-shot collectives
+  // in-place all-reduce SUM of `t` ordered after the caller's stream; the caller's stream waits for it
+  // before any later work only if `wait` is set (otherwise call wait_all()).
+  void allreduce(torch::Tensor t, bool wait) {
+    check(t);
+    order_after_caller();
+    NCCL_OK(ncclAllReduce(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), to_nccl(t.scalar_type()), ncclSum, comm_,
+                          stream_));
+    record_stream(t);
+    hipEvent_t e = make_event();
+    HIP_OK(hipEventRecord(e, stream_));
+    if (wait) HIP_OK(hipStreamWaitEvent(caller(), e, 0));
+  }
+
+  void broadcast(torch::Tensor t, int64_t root) {
+    check(t);
+    order_after_caller();
+    NCCL_OK(ncclBroadcast(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), to_nccl(t.scalar_type()), (int)root, comm_,
+                          stream_));
+    record_stream(t);
+    hipEvent_t e = make_event();
+    HIP_OK(hipEventRecord(e, stream_));
+    HIP_OK(hipStreamWaitEvent(caller(), e, 0));
+  }
+
+  // ---------------------------------------------------------------- gradient buckets
+  // flat: the gradient buffer; ranges: [start, end) element ranges; counts: parameters per bucket;
+  // param_bucket[i] = bucket of parameter i.
+  void set_buckets(torch::Tensor flat, std::vector<int64_t> starts, std::vector<int64_t> ends,
+                   std::vector<int64_t> counts, std::vector<int64_t> param_bucket) {
+    check(flat);
+    if (starts.size() != ends.size() || starts.size() != counts.size())
+      throw std::runtime_error("set_buckets: size mismatch");
+    for (auto& b : buckets_)
+      if (b.done) (void)hipEventDestroy(b.done);
+    buckets_.clear();
+    flat_ = flat;
+    for (size_t i = 0; i < starts.size(); ++i) {
+      Bucket b;
+      b.start = starts[i];
+      b.end = ends[i];
+      b.nparams = (int)counts[i];
+      if (b.start < 0 || b.end > flat.numel() || b.start > b.end) throw std::runtime_error("set_buckets: bad range");
+      HIP_OK(hipEventCreateWithFlags(&b.done, hipEventDisableTiming));
+      buckets_.push_back(b);
+    }
+    param_bucket_.assign(param_bucket.begin(), param_bucket.end());
+    begin_step();
+  }
+
+  void begin_step() {
+    for (auto& b : buckets_) {
+      b.pending = b.nparams;
+      b.launched = false;
+    }
+  }
+
+  // a parameter's gradient is complete (its producing kernels are queued on the caller's stream)
+  // returns the bucket index launched, or -1
+  int64_t mark_ready(int64_t param) {
+    if (param < 0 || (size_t)param >= param_bucket_.size()) throw std::runtime_error("mark_ready: bad index");
+    Bucket& b = buckets_[param_bucket_[param]];
+    if (b.launched) throw std::runtime_error("mark_ready: gradient arrived after its bucket was reduced");
+    if (--b.pending == 0) {
+      launch(b);
+      return param_bucket_[param];
+    }
+    return -1;
+  }
+
+  // launch every bucket not launched yet (unused parameters), then order the caller's stream after
+  // all bucket reductions
+  void finish() {
+    for (auto& b : buckets_)
+      if (!b.launched) launch(b);
+    for (auto& b : buckets_) HIP_OK(hipStreamWaitEvent(caller(), b.done, 0));
+  }
+
+  void wait_all() {
+    HIP_OK(hipEventRecord(ready_, stream_));
+    HIP_OK(hipStreamWaitEvent(caller(), ready_, 0));
+  }
+
+  int64_t num_buckets() const { return (int64_t)buckets_.size(); }
+  int64_t launched_count() const {
+    int64_t n = 0;
+    for (auto& b : buckets_) n += b.launched ? 1 : 0;
+    return n;
+  }
+
+ private:
+  hipStream_t caller() const { return c10::hip::getCurrentHIPStream(device_).stream(); }
+
+  void check(const torch::Tensor& t) const {
+    if (!t.is_cuda() || t.get_device() != device_) throw std::runtime_error("CommEngine: tensor on the wrong device");
+    if (!t.is_contiguous()) throw std::runtime_error("CommEngine: tensor must be contiguous");
+  }
+
+  void order_after_caller() {
+    HIP_OK(hipEventRecord(ready_, caller()));
+    HIP_OK(hipStreamWaitEvent(stream_, ready_, 0));
+  }
+
+  void record_stream(const torch::Tensor& t) {
+    c10::hip::HIPCachingAllocator::recordStream(t.storage().data_ptr(),
+                                                c10::hip::getStreamFromExternal(stream_, device_));
+  }
+
+  hipEvent_t make_event() {
+    // small ring of reusable events for one-shot collectives
+    if (extra_.size() < 16) {
+      hipEvent_t e;
+      HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+      extra_.push_back(e);
+      return e;
+    }
+    hipEvent_t e = extra_[next_extra_];
+    next_extra_ = (next_extra_ + 1) % extra_.size();
+    return e;
+  }
+
+  void launch(Bucket& b) {
+    order_after_caller();
+    const int64_t n = b.end - b.start;
+    if (n > 0) {
+      char* base = static_cast<char*>(flat_.data_ptr()) + b.start * flat_.element_size();
+      NCCL_OK(ncclAllReduce(base, base, (size_t)n, to_nccl(flat_.scalar_type()), ncclSum, comm_, stream_));
+    }
+    HIP_OK(hipEventRecord(b.done, stream_));
+    b.launched = true;
+  }
+
+  int rank_, world_, device_;
+  hipStream_t stream_ = nullptr;
+  ncclComm_t comm_ = nullptr;
+  hipEvent_t ready_ = nullptr;
+  std::vector<hipEvent_t> extra_;
+  size_t next_extra_ = 0;
+  std::vector<Bucket> buckets_;
+  std::vector<int64_t> param_bucket_;
+  torch::Tensor flat_;
+};
+
+}  // namespace
+
+void register_comm(pybind11::module& m) {
+  namespace py = pybind11;
+  py::class_<CommEngine>(m, "CommEngine")
+      .def(py::init([](int64_t rank, int64_t world, py::bytes uid, int64_t device, bool high_priority) {
+             return new CommEngine(rank, world, std::string(uid), device, high_priority);
+           }),
+           py::arg("rank"), py::arg("world"), py::arg("uid"), py::arg("device"), py::arg("high_priority") = true)
+      .def_static("unique_id", []() { return py::bytes(CommEngine::unique_id()); })
+      .def("allreduce", &CommEngine::allreduce, py::arg("t"), py::arg("wait") = true)
+      .def("broadcast", &CommEngine::broadcast, py::arg("t"), py::arg("root") = 0)
+      .def("set_buckets", &CommEngine::set_buckets)
+      .def("begin_step", &CommEngine::begin_step)
+      .def("mark_ready", &CommEngine::mark_ready)
+      .def("finish", &CommEngine::finish)
+      .def("wait_all", &CommEngine::wait_all)
+      .def("num_buckets", &CommEngine::num_buckets)
+      .def("launched_count", &CommEngine::launched_count)
+      .def_property_readonly("rank", &CommEngine::rank)
+      .def_property_readonly("world", &CommEngine::world);
+}
+
+}  // namespace hsd

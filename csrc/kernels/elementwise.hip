@@ -141,3 +141,51 @@ void launch_dropout(const bf16_t* x, bf16_t* out, int64_t n, double p, uint64_t 
 }
 
 }  // namespace hsd
+
+namespace hsd {
+
+// Batched bf16 transpose for the dgrad weights: dst_i [cols][rows] = src_i [rows][cols]ᵀ for every matrix
+// of a descriptor table {src, dst, rows, cols, first_tile} (int64 x 5, device memory), one launch for
+// all of them after the optimizer step. Block = 256 threads = one 64x64 tile through a padded LDS tile.
+__global__ __launch_bounds__(256) void transpose_many_kernel(const int64_t* __restrict__ desc, int n) {
+  __shared__ bf16_t tile[64][64 + 2];
+  const int bid = blockIdx.x;
+  int mi = 0;
+  while (mi + 1 < n && desc[(mi + 1) * 5 + 4] <= bid) ++mi;
+  const bf16_t* src = reinterpret_cast<const bf16_t*>(desc[mi * 5 + 0]);
+  bf16_t* dst = reinterpret_cast<bf16_t*>(desc[mi * 5 + 1]);
+  const int rows = (int)desc[mi * 5 + 2], cols = (int)desc[mi * 5 + 3];
+  const int t = bid - (int)desc[mi * 5 + 4];
+  const int tcols = (cols + 63) / 64;
+  const int r0 = (t / tcols) * 64, c0 = (t % tcols) * 64;
+  const int tid = threadIdx.x;
+  // load 64 rows x 64 cols: thread -> (row tid>>2 (+0, 64/... ), 16 cols chunk (tid&3)*16)
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int r = (tid >> 4) + 16 * it, c = (tid & 15) * 4;
+    if (r0 + r < rows && c0 + c + 3 < cols) {
+      const u32x2 v = *reinterpret_cast<const u32x2*>(src + (int64_t)(r0 + r) * cols + c0 + c);
+      tile[r][c] = (bf16_t)(v.x & 0xFFFF); tile[r][c + 1] = (bf16_t)(v.x >> 16);
+      tile[r][c + 2] = (bf16_t)(v.y & 0xFFFF); tile[r][c + 3] = (bf16_t)(v.y >> 16);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < 4; ++it) {
+    const int c = (tid >> 4) + 16 * it, r = (tid & 15) * 4;  // output row c (= input col), 4 input rows
+    if (c0 + c < cols && r0 + r + 3 < rows) {
+      u32x2 o;
+      o.x = (uint32_t)tile[r][c] | ((uint32_t)tile[r + 1][c] << 16);
+      o.y = (uint32_t)tile[r + 2][c] | ((uint32_t)tile[r + 3][c] << 16);
+      *reinterpret_cast<u32x2*>(dst + (int64_t)(c0 + c) * rows + r0 + r) = o;
+    }
+  }
+}
+
+void launch_transpose_many(const int64_t* desc, int n, int total_tiles, hipStream_t st) {
+  if (n <= 0 || total_tiles <= 0) return;
+  hipLaunchKernelGGL(transpose_many_kernel, dim3(total_tiles), dim3(256), 0, st, desc, n);
+  HSD_CHECK_LAUNCH();
+}
+
+}  // namespace hsd

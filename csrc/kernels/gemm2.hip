@@ -122,7 +122,7 @@ __device__ __forceinline__ u32x2 pack4(const f32x4& v) {
   return o;
 }
 
-template <int LA, int LB, int EPI, int BN>
+template <int LA, int LB, int EPI, int BN, int SYNC>
 __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
   constexpr int WN = BN / 4;       // wave tile columns
   constexpr int NREP = WN / 16;    // 16-col MFMA blocks per wave
@@ -163,114 +163,254 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
 #pragma unroll
     for (int j = 0; j < NREP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  // prologue: tile 0 whole, first D0 slots of tile 1
-#pragma unroll
-  for (int q = 0; q < G; ++q) dma_slot(q, smem, kbeg);
-  if (nt > 1) {
-#pragma unroll
-    for (int q = 0; q < D0; ++q) dma_slot(q, smem + STAGE, kbeg + BK);
-    vmcnt<D0>();
-  } else {
-    vmcnt<0>();
-  }
-  G2_BARRIER();
-
   const int arow = wm * 128;
   const int bcol = wn * WN;
   bf16x8 fa[4][2], fb0[NB0][2], fb1[NB1][2];
+  if constexpr (SYNC == 0) {
+    // prologue: tile 0 whole, first D0 slots of tile 1
+  #pragma unroll
+    for (int q = 0; q < G; ++q) dma_slot(q, smem, kbeg);
+    if (nt > 1) {
+  #pragma unroll
+      for (int q = 0; q < D0; ++q) dma_slot(q, smem + STAGE, kbeg + BK);
+      vmcnt<D0>();
+    } else {
+      vmcnt<0>();
+    }
+    G2_BARRIER();
 
-  for (int t = 0; t < nt; ++t) {
-    const bf16_t* cA = smem + (t & 1) * STAGE;
-    const bf16_t* cB = cA + TA;
-    bf16_t* nS = smem + ((t + 1) & 1) * STAGE;
-    const bool n1 = t + 1 < nt, n2 = t + 2 < nt;
-    const int k1 = kbeg + (t + 1) * BK, k2 = kbeg + (t + 2) * BK;
 
-    // ---------------- P1: A-sub0, B-sub0
+    for (int t = 0; t < nt; ++t) {
+      const bf16_t* cA = smem + (t & 1) * STAGE;
+      const bf16_t* cB = cA + TA;
+      bf16_t* nS = smem + ((t + 1) & 1) * STAGE;
+      const bool n1 = t + 1 < nt, n2 = t + 2 < nt;
+      const int k1 = kbeg + (t + 1) * BK, k2 = kbeg + (t + 2) * BK;
+
+      // ---------------- P1: A-sub0, B-sub0
+  #pragma unroll
+      for (int j = 0; j < NB0; ++j)
+  #pragma unroll
+        for (int ks = 0; ks < 2; ++ks) fb0[j][ks] = frag<LB>(cB, bcol + 16 * j, ks, lane);
+  #pragma unroll
+      for (int i = 0; i < 4; ++i)
+  #pragma unroll
+        for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<LA>(cA, arow + 16 * i, ks, lane);
+      if (n1) {
+  #pragma unroll
+        for (int q = D0; q < D0 + 2; ++q) dma_slot(q, nS, k1);
+      }
+      G2_BARRIER();
+      __builtin_amdgcn_s_setprio(1);
+  #pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+  #pragma unroll
+        for (int i = 0; i < 4; ++i)
+  #pragma unroll
+          for (int j = 0; j < NB0; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][ks], fa[i][ks], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      G2_BARRIER();
+
+      // ---------------- P2: B-sub1
+  #pragma unroll
+      for (int j = 0; j < NB1; ++j)
+  #pragma unroll
+        for (int ks = 0; ks < 2; ++ks) fb1[j][ks] = frag<LB>(cB, bcol + 16 * (NB0 + j), ks, lane);
+      if (n1) {
+  #pragma unroll
+        for (int q = D0 + 2; q < D0 + 4; ++q) dma_slot(q, nS, k1);
+      }
+      G2_BARRIER();
+      __builtin_amdgcn_s_setprio(1);
+  #pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+  #pragma unroll
+        for (int i = 0; i < 4; ++i)
+  #pragma unroll
+          for (int j = 0; j < NB1; ++j)
+            acc[i][NB0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][ks], fa[i][ks], acc[i][NB0 + j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      G2_BARRIER();
+
+      // ---------------- P3: A-sub1
+  #pragma unroll
+      for (int i = 0; i < 4; ++i)
+  #pragma unroll
+        for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<LA>(cA, arow + 64 + 16 * i, ks, lane);
+      if (n1) {
+  #pragma unroll
+        for (int q = D0 + 4; q < G; ++q) dma_slot(q, nS, k1);
+      }
+      G2_BARRIER();
+      __builtin_amdgcn_s_setprio(1);
+  #pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+  #pragma unroll
+        for (int i = 0; i < 4; ++i)
+  #pragma unroll
+          for (int j = 0; j < NB1; ++j)
+            acc[4 + i][NB0 + j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][ks], fa[i][ks], acc[4 + i][NB0 + j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      G2_BARRIER();
+
+      // ---------------- P4: registers only; first D0 slots of tile t+2 into this (now free) stage
+      if (n2) {
+  #pragma unroll
+        for (int q = 0; q < D0; ++q) dma_slot(q, const_cast<bf16_t*>(cA), k2);
+      }
+      __builtin_amdgcn_s_setprio(1);
+  #pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+  #pragma unroll
+        for (int i = 0; i < 4; ++i)
+  #pragma unroll
+          for (int j = 0; j < NB0; ++j)
+            acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][ks], fa[i][ks], acc[4 + i][j], 0, 0, 0);
+      __builtin_amdgcn_s_setprio(0);
+      if (n2) vmcnt<D0>();
+      else vmcnt<0>();
+      G2_BARRIER();
+    }
+  } else if constexpr (SYNC == 2) {
+    // Software-pipelined LDS reads, one barrier per K-tile placed MID-tile: after the last reads of
+    // stage t (A-sub1) every wave meets, tile t+1 (DMA'd a full tile earlier) becomes visible, tile
+    // t+2's DMA goes into stage t, and A-sub0 of tile t+1 is read underneath the A-sub1 MFMAs.
+    // Separate registers for A-sub0 / A-sub1 let each read overlap the previous group's MFMAs.
+    bf16x8 fa1[4][2];
+#define G2_SB() __builtin_amdgcn_sched_barrier(0)
+#define G2_MMA(ACC_I0, FA, FB, NBX, J0)                                                                      \
+  _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) _Pragma("unroll") for (int i = 0; i < 4; ++i)               \
+      _Pragma("unroll") for (int j = 0; j < NBX; ++j) acc[ACC_I0 + i][J0 + j] =                                \
+          __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[j][ks], FA[i][ks], acc[ACC_I0 + i][J0 + j], 0, 0, 0);
 #pragma unroll
-    for (int j = 0; j < NB0; ++j)
+    for (int q = 0; q < G; ++q) dma_slot(q, smem, kbeg);
+    if (nt > 1) {
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) fb0[j][ks] = frag<LB>(cB, bcol + 16 * j, ks, lane);
+      for (int q = 0; q < G; ++q) dma_slot(q, smem + STAGE, kbeg + BK);
+      vmcnt<G>();
+    } else {
+      vmcnt<0>();
+    }
+    G2_BARRIER();
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<LA>(cA, arow + 16 * i, ks, lane);
-    if (n1) {
+      for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<LA>(smem, arow + 16 * i, ks, lane);
+    for (int t = 0; t < nt; ++t) {
+      const bf16_t* cA = smem + (t & 1) * STAGE;
+      const bf16_t* cB = cA + TA;
+      const bf16_t* nA = smem + ((t + 1) & 1) * STAGE;
 #pragma unroll
-      for (int q = D0; q < D0 + 2; ++q) dma_slot(q, nS, k1);
-    }
-    G2_BARRIER();
-    __builtin_amdgcn_s_setprio(1);
+      for (int j = 0; j < NB0; ++j)
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+        for (int ks = 0; ks < 2; ++ks) fb0[j][ks] = frag<LB>(cB, bcol + 16 * j, ks, lane);
+      G2_SB();
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int j = 0; j < NB1; ++j)
 #pragma unroll
-        for (int j = 0; j < NB0; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][ks], fa[i][ks], acc[i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    G2_BARRIER();
-
-    // ---------------- P2: B-sub1
-#pragma unroll
-    for (int j = 0; j < NB1; ++j)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) fb1[j][ks] = frag<LB>(cB, bcol + 16 * (NB0 + j), ks, lane);
-    if (n1) {
-#pragma unroll
-      for (int q = D0 + 2; q < D0 + 4; ++q) dma_slot(q, nS, k1);
-    }
-    G2_BARRIER();
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+        for (int ks = 0; ks < 2; ++ks) fb1[j][ks] = frag<LB>(cB, bcol + 16 * (NB0 + j), ks, lane);
+      G2_SB();
+      G2_MMA(0, fa, fb0, NB0, 0)
+      G2_SB();
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < NB1; ++j)
-          acc[i][NB0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][ks], fa[i][ks], acc[i][NB0 + j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    G2_BARRIER();
-
-    // ---------------- P3: A-sub1
+        for (int ks = 0; ks < 2; ++ks) fa1[i][ks] = frag<LA>(cA, arow + 64 + 16 * i, ks, lane);
+      G2_SB();
+      G2_MMA(0, fa, fb1, NB1, NB0)
+      G2_SB();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      vmcnt<0>();
+      G2_BARRIER();
+      if (t + 2 < nt) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+        for (int q = 0; q < G; ++q) dma_slot(q, const_cast<bf16_t*>(cA), kbeg + (t + 2) * BK);
+      }
+      if (t + 1 < nt) {
 #pragma unroll
-      for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<LA>(cA, arow + 64 + 16 * i, ks, lane);
-    if (n1) {
+        for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int q = D0 + 4; q < G; ++q) dma_slot(q, nS, k1);
+          for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<LA>(nA, arow + 16 * i, ks, lane);
+      }
+      G2_SB();
+      G2_MMA(4, fa1, fb1, NB1, NB0)
+      G2_MMA(4, fa1, fb0, NB0, 0)
+      G2_SB();
     }
+    vmcnt<0>();
     G2_BARRIER();
-    __builtin_amdgcn_s_setprio(1);
+#undef G2_MMA
+#undef G2_SB
+  } else {
+    // ONE barrier per K-tile: tile t+1's DMA (into the other stage, free since the previous barrier) is
+    // issued in two halves at the start of P1 / P2 and retired by vmcnt(0) before the end-of-tile
+    // barrier; the four phases run without barriers so the two waves of a SIMD drift and overlap
+    // each other's LDS reads with MFMAs.
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+    for (int q = 0; q < G; ++q) dma_slot(q, smem, kbeg);
+    vmcnt<0>();
+    G2_BARRIER();
+    for (int t = 0; t < nt; ++t) {
+      const bf16_t* cA = smem + (t & 1) * STAGE;
+      const bf16_t* cB = cA + TA;
+      bf16_t* nS = smem + ((t + 1) & 1) * STAGE;
+      const bool n1 = t + 1 < nt;
+      const int k1 = kbeg + (t + 1) * BK;
+      if (n1) {
+#pragma unroll
+        for (int q = 0; q < G / 2; ++q) dma_slot(q, nS, k1);
+      }
+#pragma unroll
+      for (int j = 0; j < NB0; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) fb0[j][ks] = frag<LB>(cB, bcol + 16 * j, ks, lane);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < NB1; ++j)
-          acc[4 + i][NB0 + j] =
-              __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][ks], fa[i][ks], acc[4 + i][NB0 + j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    G2_BARRIER();
-
-    // ---------------- P4: registers only; first D0 slots of tile t+2 into this (now free) stage
-    if (n2) {
+        for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<LA>(cA, arow + 16 * i, ks, lane);
 #pragma unroll
-      for (int q = 0; q < D0; ++q) dma_slot(q, const_cast<bf16_t*>(cA), k2);
-    }
-    __builtin_amdgcn_s_setprio(1);
+      for (int ks = 0; ks < 2; ++ks)
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks)
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < NB0; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][ks], fa[i][ks], acc[i][j], 0, 0, 0);
+      if (n1) {
+#pragma unroll
+        for (int q = G / 2; q < G; ++q) dma_slot(q, nS, k1);
+      }
+#pragma unroll
+      for (int j = 0; j < NB1; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) fb1[j][ks] = frag<LB>(cB, bcol + 16 * (NB0 + j), ks, lane);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < NB1; ++j)
+            acc[i][NB0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][ks], fa[i][ks], acc[i][NB0 + j], 0, 0, 0);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < NB0; ++j)
-          acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][ks], fa[i][ks], acc[4 + i][j], 0, 0, 0);
-    __builtin_amdgcn_s_setprio(0);
-    if (n2) vmcnt<D0>();
-    else vmcnt<0>();
-    G2_BARRIER();
+        for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<LA>(cA, arow + 64 + 16 * i, ks, lane);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+          for (int j = 0; j < NB1; ++j)
+            acc[4 + i][NB0 + j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][ks], fa[i][ks], acc[4 + i][NB0 + j], 0, 0, 0);
+#pragma unroll
+          for (int j = 0; j < NB0; ++j)
+            acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][ks], fa[i][ks], acc[4 + i][j], 0, 0, 0);
+        }
+      vmcnt<0>();
+      G2_BARRIER();
+    }
   }
 
   // ================================================================ epilogue
@@ -437,6 +577,16 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
 
 }  // namespace g2
 
+// Main-loop schedule (tools/ab_gemm2.py, interleaved in one process): NT with a short K (<= 1024: the
+// forward / dgrad GEMMs whose reduction is the hidden size) runs best with one barrier per K-tile
+// (SYNC 1: +5-10 %), NT with a long K (2304 / 3072) and the TT wgrad with the 8-phase form (SYNC 0).
+// HSD_G2_SYNC overrides for A/B runs.
+static int g2_sync_mode(int la, int K) {
+  const char* e = getenv("HSD_G2_SYNC");
+  if (e) return atoi(e);
+  return (la == 0 && K <= 1024) ? 1 : 0;
+}
+
 template <int LA, int LB, int EPI, int BN>
 static void g2_launch(const G2Params& p0, int splits, hipStream_t st) {
   G2Params p = p0;
@@ -448,7 +598,10 @@ static void g2_launch(const G2Params& p0, int splits, hipStream_t st) {
   splits = (p.K + kps - 1) / kps;
   p.kps = kps;
   dim3 grid(tiles_m * p.tiles_n, splits);
-  hipLaunchKernelGGL((g2::gemm2_kernel<LA, LB, EPI, BN>), grid, dim3(512), 0, st, p);
+  const int mode = g2_sync_mode(LA, p.K);
+  if (mode == 1) hipLaunchKernelGGL((g2::gemm2_kernel<LA, LB, EPI, BN, 1>), grid, dim3(512), 0, st, p);
+  else if (mode == 2) hipLaunchKernelGGL((g2::gemm2_kernel<LA, LB, EPI, BN, 2>), grid, dim3(512), 0, st, p);
+  else hipLaunchKernelGGL((g2::gemm2_kernel<LA, LB, EPI, BN, 0>), grid, dim3(512), 0, st, p);
   HSD_CHECK_LAUNCH();
 }
 

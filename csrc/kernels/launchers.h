@@ -37,6 +37,8 @@ void launch_gelu_bwd_colsum(const bf16_t* dg, const bf16_t* y, bf16_t* da, float
                             hipStream_t st);
 void launch_colsum(const bf16_t* x, float* dbias, int rows, int N, hipStream_t st);
 void launch_dropout(const bf16_t* x, bf16_t* out, int64_t n, double p, uint64_t seed, hipStream_t st);
+// desc: int64 [n][5] = {src, dst, rows, cols, first_tile}; rows, cols multiples of 4
+void launch_transpose_many(const int64_t* desc, int n, int total_tiles, hipStream_t st);
 // attention.hip
 void launch_attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse2, int B, int S, int heads,
                      double p, uint64_t seed, hipStream_t st);

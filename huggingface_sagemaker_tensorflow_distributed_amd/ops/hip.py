@@ -334,7 +334,9 @@ def gemm_dgrad(dy, w, epi=EPI_STORE, aux=None, dbias=None):
     the layer that produced ``aux``) from the epilogue; returns ``(dx, fused)``-style via attribute."""
     dx = torch.empty((dy.shape[0], w.shape[1]), dtype=dy.dtype, device=dy.device)
     if _nt_ok(dy.shape[0], w.shape[1], dy.shape[1], epi):
-        wt = w.t().contiguous()
+        wt = getattr(w, "_hsd_wt", None)  # FlatParamStore keeps Wᵀ fresh (one batched transpose per step)
+        if wt is None or wt.shape[0] != w.shape[1] or wt.shape[1] != w.shape[0]:
+            wt = w.t().contiguous()
         fuse = dbias is not None and epi == EPI_DGELU and w.shape[1] % 256 == 0
         _C.gemm2(dy, wt, dx, 0, 0, epi, None, aux, None, 0.0, 0, 1, None, dbias if fuse else None)
         if dbias is not None and not fuse:

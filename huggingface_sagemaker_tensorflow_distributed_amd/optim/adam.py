@@ -73,6 +73,7 @@ class FusedAdam:
             hip.adam_step(s.master, self.exp_avg, self.exp_avg_sq, s.grad, s.compute if write_compute else None,
                           self._decay_mask, step, eps_eff, self.beta1, self.beta2, float(grad_scale),
                           self.lr * self.weight_decay)
+            s.refresh_transposed()
             return
         # reference path (CPU): identical math on flat buffers
         g = s.grad.to(torch.float32) * grad_scale

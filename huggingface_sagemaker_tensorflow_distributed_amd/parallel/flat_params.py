@@ -12,6 +12,7 @@ complete front-to-back while backward is still running.
 """
 from __future__ import annotations
 
+import re
 from dataclasses import dataclass
 from typing import Dict, List, Optional
 
@@ -19,6 +20,9 @@ import torch
 import torch.nn as nn
 
 ALIGN = 64  # elements; keeps every view 128-B (bf16) / 256-B (fp32) aligned for 16-B vector IO
+
+# 2-D weights whose transposed bf16 copy the dgrad GEMMs read (B operand of dX = dY·W is Wᵀ, k-contiguous)
+TRANSPOSED_WEIGHTS = re.compile(r"(^|\.)layers\.\d+\.(qkv|attn_out|ffn1|ffn2)_weight$")
 
 
 def _round_up(x: int, a: int) -> int:
@@ -72,6 +76,7 @@ class FlatParamStore:
             p.main_grad = self.grad[seg.offset:seg.offset + seg.numel].view(seg.shape)
             p.grad = None
         self._index: Dict[int, int] = {id(p): i for i, p in enumerate(self.params)}
+        self._setup_transposed()
         # gradient-ready notification: HIP backward kernels write main_grad directly and call
         # p._hsd_ready(); torch-autograd gradients (CPU path, small torch-op heads) are folded into
         # main_grad by a post-accumulate hook first.
@@ -97,6 +102,40 @@ class FlatParamStore:
         return hook
 
     # ----------------------------------------------------------------------------------
+    def _setup_transposed(self) -> None:
+        """bf16 Wᵀ copies (one flat buffer) for the dgrad GEMMs, refreshed by ONE batched transpose launch
+        after every optimizer step instead of a transpose per GEMM per step."""
+        self.transposed = None
+        self._tdesc = None
+        if self.device.type != "cuda" or self.compute_dtype != torch.bfloat16:
+            return
+        idx = [i for i, n in enumerate(self.names) if TRANSPOSED_WEIGHTS.search(n) and len(self.segments[i].shape) == 2
+               and self.segments[i].shape[0] % 4 == 0 and self.segments[i].shape[1] % 4 == 0]
+        if not idx:
+            return
+        total = sum(self.segments[i].numel for i in idx)
+        self.transposed = torch.empty(total, dtype=self.compute_dtype, device=self.device)
+        desc, off, tiles = [], 0, 0
+        for i in idx:
+            rows, cols = self.segments[i].shape
+            p = self.params[i]
+            wt = self.transposed[off:off + rows * cols].view(cols, rows)
+            p._hsd_wt = wt
+            desc.append([p.data.data_ptr(), wt.data_ptr(), rows, cols, tiles])
+            tiles += ((rows + 63) // 64) * ((cols + 63) // 64)
+            off += rows * cols
+        self._tdesc = torch.tensor(desc, dtype=torch.int64, device=self.device)
+        self._ttiles = tiles
+        self.refresh_transposed()
+
+    @torch.no_grad()
+    def refresh_transposed(self) -> None:
+        if self._tdesc is None:
+            return
+        from ..ops import hip
+
+        hip._C.transpose_many(self._tdesc, self._ttiles)
+
     def index_of(self, p: torch.Tensor) -> int:
         return self._index[id(p)]
 
@@ -110,6 +149,7 @@ class FlatParamStore:
     def sync_compute_from_master(self) -> None:
         if self.compute is not self.master:
             self.compute.copy_(self.master)
+        self.refresh_transposed()
 
     def decay_block_mask(self, block: int) -> torch.Tensor:
         """uint8 per ``block`` elements: 1 = apply weight decay. Segments are ALIGN-aligned."""

@@ -64,3 +64,27 @@ def test_bert_base_train_steps_loss_decreases(gpu):
         losses.append(float(tr.train_step([batches[step % 4]])))
     assert all(l == l for l in losses), "NaN loss"
     assert sum(losses[-8:]) / 8 < sum(losses[:8]) / 8, losses
+
+
+def test_store_transposed_weights_track_optimizer(gpu):
+    """FlatParamStore keeps bf16 Wᵀ copies for the dgrad GEMMs in sync with the weights after each step."""
+    from huggingface_sagemaker_tensorflow_distributed_amd.optim import FusedAdam
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel import FlatParamStore
+
+    cfg = resolve_config("hsd-tiny-bert").replace(hidden_size=256, num_attention_heads=4, intermediate_size=512)
+    m = build_model(cfg, seed=0).to(gpu)
+    store = FlatParamStore(m, gpu, compute_dtype=torch.bfloat16)
+    opt = FusedAdam(store, lr=1e-3)
+    tracked = [(n, p) for n, p in m.named_parameters() if hasattr(p, "_hsd_wt")]
+    assert len(tracked) == 4 * cfg.num_hidden_layers
+    ids = torch.randint(5, cfg.vocab_size, (2, 128), device=gpu)
+    labels = torch.randint(0, 2, (2,), device=gpu)
+    for _ in range(2):
+        store.zero_grad()
+        m.rng.new_step(0)
+        loss, _ = m(ids, attention_mask=torch.ones_like(ids), labels=labels)
+        loss.backward()
+        opt.step()
+        torch.cuda.synchronize()
+        for n, p in tracked:
+            assert torch.equal(p._hsd_wt, p.detach().t()), n
