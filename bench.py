@@ -88,7 +88,9 @@ def main():
             "dtype": "bf16", "data": "synthetic (random-init weights, full-length seq, dropout on)",
             "config": {"model": a.model, "global_batch": a.batch_size * world, "per_gpu_batch": a.batch_size,
                        "seq_len": a.seq_len, "parallelism": f"dp{world}",
-                       "ops": "torch-reference" if os.environ.get("HSD_OPS") == "torch" else "hip"},
+                       "ops": "torch-reference" if os.environ.get("HSD_OPS") == "torch" else "hip",
+                       "comm": ("native-rccl" if getattr(trainer.bucketer, "engine", None) is not None
+                                else ("torch-" + backend.state().backend if world > 1 else "none"))},
         }), flush=True)
     backend.shutdown()
 

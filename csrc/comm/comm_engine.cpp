@@ -18,6 +18,8 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <memory>
 #include <stdexcept>
@@ -26,6 +28,12 @@
 
 namespace hsd {
 namespace {
+
+bool dbg() {
+  static bool d = getenv("HSD_COMM_DEBUG") != nullptr;
+  return d;
+}
+#define DBG(...) do { if (dbg()) { fprintf(stderr, "[comm] " __VA_ARGS__); fflush(stderr); } } while (0)
 
 #define HIP_OK(x)                                                                       \
   do {                                                                                  \
@@ -64,23 +72,24 @@ class CommEngine {
   CommEngine(int64_t rank, int64_t world, const std::string& uid, int64_t device, bool high_priority)
       : rank_((int)rank), world_((int)world), device_((int)device) {
     if (uid.size() != sizeof(ncclUniqueId)) throw std::runtime_error("CommEngine: bad unique id size");
+    DBG("ctor rank %d world %d dev %d\n", rank_, world_, device_);
     HIP_OK(hipSetDevice(device_));
     int lo = 0, hi = 0;
     HIP_OK(hipDeviceGetStreamPriorityRange(&lo, &hi));
     HIP_OK(hipStreamCreateWithPriority(&stream_, hipStreamNonBlocking, high_priority ? hi : lo));
     ncclUniqueId id;
     std::memcpy(&id, uid.data(), sizeof(id));
+    DBG("stream ok, init comm\n");
     NCCL_OK(ncclCommInitRank(&comm_, world_, id, rank_));
+    DBG("comm ok\n");
     HIP_OK(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
   }
 
   ~CommEngine() {
-    for (auto& b : buckets_)
-      if (b.done) (void)hipEventDestroy(b.done);
-    for (auto e : extra_) (void)hipEventDestroy(e);
-    if (ready_) (void)hipEventDestroy(ready_);
+    // drain, then release the communicator; the stream and events are left to process teardown (the
+    // caching allocator may still hold blocks whose last use was recorded on this stream)
+    if (stream_) (void)hipStreamSynchronize(stream_);
     if (comm_) (void)ncclCommDestroy(comm_);
-    if (stream_) (void)hipStreamDestroy(stream_);
   }
 
   static std::string unique_id() {
@@ -93,14 +102,17 @@ class CommEngine {
   int64_t world() const { return world_; }
 
   // ---------------------------------------------------------------- one-shot collectives
-  // in-place all-reduce SUM of `t` ordered after the caller's stream; the caller's stream waits for it
-  // before any later work only if `wait` is set (otherwise call wait_all()).
+  // in-place all-reduce SUM of `t` ordered after the caller's stream; with `wait` the caller's stream waits
+  // for it before any later work (otherwise call wait_all() before `t` is read or freed).
   void allreduce(torch::Tensor t, bool wait) {
     check(t);
+    DBG("allreduce n=%ld\n", (long)t.numel());
     order_after_caller();
+    DBG("ordered\n");
     NCCL_OK(ncclAllReduce(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), to_nccl(t.scalar_type()), ncclSum, comm_,
                           stream_));
-    record_stream(t);
+    DBG("launched\n");
+    if (!wait) record_stream(t);
     hipEvent_t e = make_event();
     HIP_OK(hipEventRecord(e, stream_));
     if (wait) HIP_OK(hipStreamWaitEvent(caller(), e, 0));
@@ -111,7 +123,6 @@ class CommEngine {
     order_after_caller();
     NCCL_OK(ncclBroadcast(t.data_ptr(), t.data_ptr(), (size_t)t.numel(), to_nccl(t.scalar_type()), (int)root, comm_,
                           stream_));
-    record_stream(t);
     hipEvent_t e = make_event();
     HIP_OK(hipEventRecord(e, stream_));
     HIP_OK(hipStreamWaitEvent(caller(), e, 0));

@@ -18,9 +18,10 @@ from . import backend
 
 
 def broadcast_tensor(t: torch.Tensor, src: int = 0) -> torch.Tensor:
-    if backend.is_distributed():
-        dist.broadcast(t, src=src)
-    return t
+    """Broadcast from ``src`` — native RCCL engine on GPUs, torch.distributed otherwise."""
+    from .comm import broadcast_
+
+    return broadcast_(t, src)
 
 
 def broadcast_parameters(store, optimizer=None, src: int = 0) -> None:

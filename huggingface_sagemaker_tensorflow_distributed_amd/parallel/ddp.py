@@ -12,6 +12,9 @@ MI355X design:
   is written — gradients are written by the backward kernels straight into ``main_grad`` — so RCCL
   traffic runs on RCCL's own HIP stream underneath the rest of backward;
 * the ``1/N`` average is folded into the optimizer kernel (no extra pass);
+* on GPUs the bucket bookkeeping and the ``ncclAllReduce`` launches live in the native C++
+  :class:`CommEngine` (``csrc/comm/comm_engine.cpp``: dedicated high-priority HIP stream, event
+  ordering, no host sync); CPU/gloo worlds (tests) use ``torch.distributed`` with the same buckets;
 * bucket size default is sized for xGMI: large enough that ring latency
   (≈tens of µs per collective) is amortised over 7 links, small enough that the tail bucket after
   the last backward kernel is short.
@@ -48,7 +51,7 @@ class GradBucketer:
     """Static buckets over a :class:`FlatParamStore`'s gradient buffer."""
 
     def __init__(self, store: FlatParamStore, bucket_mb: Optional[float] = None, group=None,
-                 overlap: bool = True):
+                 overlap: bool = True, native: Optional[bool] = None):
         self.store = store
         self.group = group
         self.world = backend.size()
@@ -69,10 +72,30 @@ class GradBucketer:
             for pi in b.params:
                 self._param_bucket[pi] = b
         self.sync_enabled = True
+        self.engine = None
+        if (native is None or native) and group is None:
+            from .comm import get_engine
+
+            try:
+                self.engine = get_engine()
+            except Exception as e:  # pragma: no cover - depends on the RCCL install
+                logger.warning("native CommEngine unavailable (%s); using torch.distributed buckets", e)
+                self.engine = None
+            if self.engine is not None:
+                param_bucket = [0] * len(store.segments)
+                for b in self.buckets:
+                    for pi in b.params:
+                        param_bucket[pi] = b.index
+                self.engine.set_buckets(store.grad, [b.start for b in self.buckets], [b.end for b in self.buckets],
+                                        [len(b.params) for b in self.buckets], param_bucket)
         store.ready_callback = self.mark_ready
 
     # ---------------------------------------------------------------- hooks
     def mark_ready(self, i: int) -> None:
+        if self.engine is not None:
+            if self.overlap and self.sync_enabled:
+                self.engine.mark_ready(i)
+            return
         b = self._param_bucket[i]
         if b.launched:
             raise RuntimeError(f"gradient for {self.store.names[i]} arrived after its bucket was reduced "
@@ -88,6 +111,9 @@ class GradBucketer:
 
     # ---------------------------------------------------------------- step API
     def begin(self) -> None:
+        if self.engine is not None:
+            self.engine.begin_step()
+            return
         for b in self.buckets:
             b.ready.clear()
             b.handle = None
@@ -96,6 +122,9 @@ class GradBucketer:
     def finish(self) -> None:
         """Launch any bucket not yet launched (unused params / no-overlap mode), then wait all."""
         if self.world <= 1 or not self.sync_enabled:
+            return
+        if self.engine is not None:
+            self.engine.finish()  # launches unlaunched buckets; compute stream waits (host does not)
             return
         for b in self.buckets:
             if not b.launched:
