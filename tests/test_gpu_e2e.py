@@ -88,3 +88,29 @@ def test_store_transposed_weights_track_optimizer(gpu):
         torch.cuda.synchronize()
         for n, p in tracked:
             assert torch.equal(p._hsd_wt, p.detach().t()), n
+
+
+@pytest.mark.parametrize("model,seq,bs", [("bert-base-uncased", 128, 32), ("bert-large-uncased-whole-word-masking", 512, 8)])
+def test_train_script_on_gpu_writes_reference_artifacts(gpu, tmp_path, model, seq, bs):
+    """scripts/train.py end to end on the GPU (the reference's job: fit -> evaluate -> save_pretrained),
+    including the reference's own bert-large-wwm S=512 configuration (launch.py:14-17)."""
+    import json
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, SM_OUTPUT_DATA_DIR=str(tmp_path / "data"), SM_MODEL_DIR=str(tmp_path / "model"),
+               SM_NUM_GPUS="1", SM_FRAMEWORK_PARAMS="{}")
+    cmd = [sys.executable, os.path.join(root, "scripts", "train.py"), "--epochs", "1", "--train_batch_size", str(bs),
+           "--eval_batch_size", "4", "--model_name_or_path", model, "--max_seq_length", str(seq),
+           "--num_train_examples", str(bs * 4), "--num_eval_examples", "16", "--log_every", "1"]
+    r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    train = (tmp_path / "data" / "train_results.txt").read_text()
+    assert train.startswith("loss = [") and "sparse_categorical_accuracy = [" in train and "train_runtime = {" in train
+    ev = (tmp_path / "data" / "eval_results.txt").read_text().splitlines()
+    assert ev[0].startswith("loss = ") and ev[1].startswith("sparse_categorical_accuracy = ")
+    cfg = json.loads((tmp_path / "model" / "config.json").read_text())
+    assert cfg["architectures"] == ["BertForSequenceClassification"]
+    assert (tmp_path / "model" / "model.safetensors").exists()
