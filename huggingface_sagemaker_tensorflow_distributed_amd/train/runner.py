@@ -118,6 +118,16 @@ def run(argv: Optional[Sequence[str]] = None, mode: str = "train") -> dict:
                                                            drop_last=True, batch_size=per_rank_eval), dev)
     out = {"args": args}
     callbacks = [FaultInjection()]
+    if args.benchmark or args.profile:
+        from ..obs import ProfilerCallback, ThroughputMeter
+
+        if args.benchmark:
+            callbacks.append(ThroughputMeter(args.output_data_dir, per_rank_train, max_len, warmup=args.warmup_steps,
+                                             log_every=args.log_every,
+                                             info={"model": args.model_name_or_path, "dtype": parts["dtype"],
+                                                   "script": mode, "data": args.dataset}))
+        if args.profile:
+            callbacks.append(ProfilerCallback(args.output_data_dir, start=args.warmup_steps, steps=3, rank=rank))
     if args.save_every_epoch:
         callbacks.append(ModelCheckpoint(os.path.join(args.model_dir, "checkpoint-{epoch}")))
 

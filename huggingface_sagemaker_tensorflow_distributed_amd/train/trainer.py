@@ -15,6 +15,7 @@ reported history is global.
 """
 from __future__ import annotations
 
+import contextlib
 import logging
 import math
 import time
@@ -24,6 +25,7 @@ from typing import Callable, Dict, Iterable, List, Optional
 import torch
 
 from .. import ops
+from ..obs.profiler import range as prange
 from ..parallel import backend
 from ..parallel.collectives import allreduce_sums, params_in_sync
 
@@ -101,18 +103,19 @@ class Trainer:
         loss = None
         for i, mb in enumerate(micro_batches):
             last = i == k - 1
-            if self.bucketer is not None and not last:
-                with self.bucketer.no_sync():
+            ctx = self.bucketer.no_sync() if (self.bucketer is not None and not last) else contextlib.nullcontext()
+            with ctx:
+                with prange("forward"):
                     loss, logits = self._forward_loss(mb)
+                with prange("backward+allreduce"):
                     loss.backward()
-            else:
-                loss, logits = self._forward_loss(mb)
-                loss.backward()
             if meter is not None:
                 meter.update(loss, logits, mb["labels"])
-        if self.bucketer is not None:
-            self.bucketer.finish()
-        self.optimizer.step(grad_scale=1.0 / (self.world * k))
+        with prange("allreduce-wait"):
+            if self.bucketer is not None:
+                self.bucketer.finish()
+        with prange("optimizer"):
+            self.optimizer.step(grad_scale=1.0 / (self.world * k))
         self.global_step += 1
         if self.check_sync and self.global_step % self.check_sync == 0:
             if not params_in_sync(self.store):
