@@ -254,17 +254,17 @@ void gemm2(torch::Tensor A, torch::Tensor B, torch::Tensor C, int64_t la, int64_
   TORCH_CHECK(C.size(0) == M && C.size(1) == N, "gemm2 C shape");
   TORCH_CHECK(hsd::gemm2_supported((int)la, (int)lb, (int)epi, (int)M, (int)N, (int)K), "gemm2: unsupported shape/epilogue");
   TORCH_CHECK(A.stride(0) % 8 == 0 && B.stride(0) % 8 == 0 && C.stride(0) % 8 == 0, "gemm2 leading dims alignment");
-  const bool f32out = epi >= 6;
+  const bool f32out = epi == 6 || epi == 7;
   TORCH_CHECK(C.scalar_type() == (f32out ? torch::kFloat32 : torch::kBFloat16), "gemm2 C dtype");
-  if (epi == 1 || epi == 2 || epi == 3) {
+  if (epi == 1 || epi == 2 || epi == 3 || epi == 8) {
     TORCH_CHECK(bias.has_value() && bias->numel() == N && bias->scalar_type() == torch::kBFloat16 &&
                 bias->is_contiguous(), "gemm2 bias");
   }
-  if (epi == 3 || epi == 4 || epi == 5) {
+  if (epi == 3 || epi == 4 || epi == 5 || epi == 9) {
     TORCH_CHECK(aux.has_value() && aux->dim() == 2 && aux->size(0) == M && aux->size(1) == N &&
                 aux->stride(1) == 1 && aux->stride(0) % 8 == 0 && aux->scalar_type() == torch::kBFloat16, "gemm2 aux");
   }
-  if (epi == 2) {
+  if (epi == 2 || epi == 8) {
     TORCH_CHECK(C2.has_value() && C2->sizes() == C.sizes() && C2->strides() == C.strides() &&
                 C2->scalar_type() == torch::kBFloat16, "gemm2 C2");
   }
@@ -280,7 +280,7 @@ void gemm2(torch::Tensor A, torch::Tensor B, torch::Tensor C, int64_t la, int64_
   if (!f32out) TORCH_CHECK(sp == 1, "split-K only with fp32 output");
   float* dbp = nullptr;
   if (dbias.has_value()) {
-    TORCH_CHECK(epi == 5 && N % 256 == 0, "gemm2 fused dbias: DGELU epilogue with N % 256 == 0");
+    TORCH_CHECK((epi == 5 || epi == 9) && N % 256 == 0, "gemm2 fused dbias: DGELU / MUL epilogue with N % 256 == 0");
     check_f32(*dbias, "dbias");
     TORCH_CHECK(dbias->numel() == N, "dbias size");
     dbp = dbias->data_ptr<float>();

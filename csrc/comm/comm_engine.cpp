@@ -186,6 +186,17 @@ class CommEngine {
     HIP_OK(hipStreamWaitEvent(caller(), ready_, 0));
   }
 
+  // every collective is also ordered after the work queued on this stream (e.g. the wgrad side stream)
+  void add_dependency_stream(int64_t stream_ptr) {
+    hipStream_t s = reinterpret_cast<hipStream_t>(stream_ptr);
+    for (auto d : deps_)
+      if (d == s) return;
+    hipEvent_t e;
+    HIP_OK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+    deps_.push_back(s);
+    dep_events_.push_back(e);
+  }
+
   int64_t num_buckets() const { return (int64_t)buckets_.size(); }
   int64_t launched_count() const {
     int64_t n = 0;
@@ -204,6 +215,11 @@ class CommEngine {
   void order_after_caller() {
     HIP_OK(hipEventRecord(ready_, caller()));
     HIP_OK(hipStreamWaitEvent(stream_, ready_, 0));
+    // gradients may also be produced on registered side streams (the wgrad stream): order after them too
+    for (size_t i = 0; i < deps_.size(); ++i) {
+      HIP_OK(hipEventRecord(dep_events_[i], deps_[i]));
+      HIP_OK(hipStreamWaitEvent(stream_, dep_events_[i], 0));
+    }
   }
 
   void record_stream(const torch::Tensor& t) {
@@ -243,6 +259,8 @@ class CommEngine {
   size_t next_extra_ = 0;
   std::vector<Bucket> buckets_;
   std::vector<int64_t> param_bucket_;
+  std::vector<hipStream_t> deps_;
+  std::vector<hipEvent_t> dep_events_;
   torch::Tensor flat_;
 };
 
@@ -263,6 +281,7 @@ void register_comm(pybind11::module& m) {
       .def("mark_ready", &CommEngine::mark_ready)
       .def("finish", &CommEngine::finish)
       .def("wait_all", &CommEngine::wait_all)
+      .def("add_dependency_stream", &CommEngine::add_dependency_stream)
       .def("num_buckets", &CommEngine::num_buckets)
       .def("launched_count", &CommEngine::launched_count)
       .def_property_readonly("rank", &CommEngine::rank)

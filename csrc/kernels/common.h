@@ -120,6 +120,14 @@ __device__ __forceinline__ float gelu_erf_grad(float x) {
   return fmaf(x * 0.3989422804014327f, g.e, half_1p_erf);
 }
 
+// gelu(x) and gelu'(x) from one set of erf parts (the FFN forward keeps gelu' for the backward)
+__device__ __forceinline__ void gelu_and_grad(float x, float& g, float& dg) {
+  const GeluParts q = gelu_parts(x);
+  const float half_1p_erf = x >= 0.0f ? fmaf(-0.5f, q.pe, 1.0f) : 0.5f * q.pe;
+  g = x * half_1p_erf;
+  dg = fmaf(x * 0.3989422804014327f, q.e, half_1p_erf);
+}
+
 }  // namespace hsd
 
 #define HSD_CHECK_LAUNCH()                                                                    \

@@ -27,8 +27,16 @@
 
 namespace hsd {
 
+// E2_BIAS_GELU_D: C = gelu'(y), C2 = gelu(y) (y = acc + bias) — the FFN1 forward keeps the GELU DERIVATIVE
+// for backward, so the FFN2 dgrad epilogue is a plain product (E2_MUL: C = bf16(acc) * aux) instead of
+// re-evaluating erf/exp per element.
 enum Epi2 : int { E2_STORE = 0, E2_BIAS = 1, E2_BIAS_GELU = 2, E2_BIAS_DROP_RES = 3, E2_RES = 4, E2_DGELU = 5,
-                  E2_F32_ATOMIC = 6, E2_F32_SLAB = 7 };
+                  E2_F32_ATOMIC = 6, E2_F32_SLAB = 7, E2_BIAS_GELU_D = 8, E2_MUL = 9 };
+
+__host__ __device__ constexpr bool epi_bias(int e) { return e == E2_BIAS || e == E2_BIAS_GELU || e == E2_BIAS_DROP_RES || e == E2_BIAS_GELU_D; }
+__host__ __device__ constexpr bool epi_aux(int e) { return e == E2_BIAS_DROP_RES || e == E2_RES || e == E2_DGELU || e == E2_MUL; }
+__host__ __device__ constexpr bool epi_two_out(int e) { return e == E2_BIAS_GELU || e == E2_BIAS_GELU_D; }
+__host__ __device__ constexpr bool epi_bf16_out(int e) { return e <= E2_DGELU || e == E2_BIAS_GELU_D || e == E2_MUL; }
 
 struct G2Params {
   const bf16_t* A;
@@ -45,6 +53,7 @@ struct G2Params {
   DropoutParams dp;
   int kps;  // K elements per split (multiple of 64)
   int tiles_n;
+  int ntiles;    // tiles_m * tiles_n
   float* dbias;  // E2_DGELU: optional fp32 column sums of the output (the bias gradient), BN 256 only
 };
 
@@ -122,6 +131,80 @@ __device__ __forceinline__ u32x2 pack4(const f32x4& v) {
   return o;
 }
 
+
+// Epilogue math for one 16-B chunk (8 consecutive n of row m) of the staged bf16(acc [+ bias]) tile `o`;
+// `x` is the aux chunk. Returns the primary output in `o` and (two-output epilogues) the second in `o2`.
+template <int EPI>
+__device__ __forceinline__ void epi_chunk(u32x4& o, u32x4& o2, const u32x4& x, int m, int n, const G2Params& p,
+                                          float (&csum)[8]) {
+  if constexpr (EPI == E2_BIAS_GELU) {
+    o2.x = pack_bf2(gelu_erf(lo_bf(o.x)), gelu_erf(hi_bf(o.x)));
+    o2.y = pack_bf2(gelu_erf(lo_bf(o.y)), gelu_erf(hi_bf(o.y)));
+    o2.z = pack_bf2(gelu_erf(lo_bf(o.z)), gelu_erf(hi_bf(o.z)));
+    o2.w = pack_bf2(gelu_erf(lo_bf(o.w)), gelu_erf(hi_bf(o.w)));
+  } else if constexpr (EPI == E2_BIAS_GELU_D) {
+    float v[8] = {lo_bf(o.x), hi_bf(o.x), lo_bf(o.y), hi_bf(o.y), lo_bf(o.z), hi_bf(o.z), lo_bf(o.w), hi_bf(o.w)};
+    float a[8], d[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) gelu_and_grad(v[e], a[e], d[e]);
+    o.x = pack_bf2(d[0], d[1]); o.y = pack_bf2(d[2], d[3]); o.z = pack_bf2(d[4], d[5]); o.w = pack_bf2(d[6], d[7]);
+    o2.x = pack_bf2(a[0], a[1]); o2.y = pack_bf2(a[2], a[3]); o2.z = pack_bf2(a[4], a[5]); o2.w = pack_bf2(a[6], a[7]);
+  } else if constexpr (EPI == E2_BIAS_DROP_RES) {
+    // z = bf16(bf16(y · keep · scale) + residual)
+    float v[8] = {lo_bf(o.x), hi_bf(o.x), lo_bf(o.y), hi_bf(o.y), lo_bf(o.z), hi_bf(o.z), lo_bf(o.w), hi_bf(o.w)};
+    if (p.dp.enabled) {
+      const uint32_t pair0 = (uint32_t)(((int64_t)m * p.N + n) >> 1);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t b = dropout_bits(pair0 + e, p.dp.seed_lo, p.dp.seed_hi);
+        v[2 * e] = bf2f(f2bf(v[2 * e] * keep_factor(b, 0, p.dp)));
+        v[2 * e + 1] = bf2f(f2bf(v[2 * e + 1] * keep_factor(b, 1, p.dp)));
+      }
+    }
+    o.x = pack_bf2(v[0] + lo_bf(x.x), v[1] + hi_bf(x.x));
+    o.y = pack_bf2(v[2] + lo_bf(x.y), v[3] + hi_bf(x.y));
+    o.z = pack_bf2(v[4] + lo_bf(x.z), v[5] + hi_bf(x.z));
+    o.w = pack_bf2(v[6] + lo_bf(x.w), v[7] + hi_bf(x.w));
+  } else if constexpr (EPI == E2_RES) {
+    o.x = pack_bf2(lo_bf(o.x) + lo_bf(x.x), hi_bf(o.x) + hi_bf(x.x));
+    o.y = pack_bf2(lo_bf(o.y) + lo_bf(x.y), hi_bf(o.y) + hi_bf(x.y));
+    o.z = pack_bf2(lo_bf(o.z) + lo_bf(x.z), hi_bf(o.z) + hi_bf(x.z));
+    o.w = pack_bf2(lo_bf(o.w) + lo_bf(x.w), hi_bf(o.w) + hi_bf(x.w));
+  } else if constexpr (EPI == E2_DGELU || EPI == E2_MUL) {
+    if constexpr (EPI == E2_DGELU) {
+      o.x = pack_bf2(lo_bf(o.x) * gelu_erf_grad(lo_bf(x.x)), hi_bf(o.x) * gelu_erf_grad(hi_bf(x.x)));
+      o.y = pack_bf2(lo_bf(o.y) * gelu_erf_grad(lo_bf(x.y)), hi_bf(o.y) * gelu_erf_grad(hi_bf(x.y)));
+      o.z = pack_bf2(lo_bf(o.z) * gelu_erf_grad(lo_bf(x.z)), hi_bf(o.z) * gelu_erf_grad(hi_bf(x.z)));
+      o.w = pack_bf2(lo_bf(o.w) * gelu_erf_grad(lo_bf(x.w)), hi_bf(o.w) * gelu_erf_grad(hi_bf(x.w)));
+    } else {
+      o.x = pack_bf2(lo_bf(o.x) * lo_bf(x.x), hi_bf(o.x) * hi_bf(x.x));
+      o.y = pack_bf2(lo_bf(o.y) * lo_bf(x.y), hi_bf(o.y) * hi_bf(x.y));
+      o.z = pack_bf2(lo_bf(o.z) * lo_bf(x.z), hi_bf(o.z) * hi_bf(x.z));
+      o.w = pack_bf2(lo_bf(o.w) * lo_bf(x.w), hi_bf(o.w) * hi_bf(x.w));
+    }
+    csum[0] += lo_bf(o.x); csum[1] += hi_bf(o.x); csum[2] += lo_bf(o.y); csum[3] += hi_bf(o.y);
+    csum[4] += lo_bf(o.z); csum[5] += hi_bf(o.z); csum[6] += lo_bf(o.w); csum[7] += hi_bf(o.w);
+  }
+}
+
+// column sums of 8 columns per lane, lanes with equal (lane & 7) hold the same columns: reduce + atomics
+__device__ __forceinline__ void colsum_flush(float (&csum)[8], float* dbias, int nw, int N, int lane) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float v = csum[e];
+    v += __shfl_xor(v, 8, 64);
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    csum[e] = v;
+  }
+  if (lane < 8 && nw + lane * 8 < N) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) atomicAdd(dbias + nw + lane * 8 + e, csum[e]);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) csum[e] = 0.f;
+}
+
 template <int LA, int LB, int EPI, int BN, int SYNC>
 __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
   constexpr int WN = BN / 4;       // wave tile columns
@@ -142,13 +225,16 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 2, wn = wave & 3;
 
-  // XCD-aware bijective remap: blocks sharing an XCD get consecutive tiles (same A row panel)
+  // 1-D grid over (split, tile), XCD-aware bijective remap: the blocks an XCD runs together get
+  // consecutive (split-major) indices, i.e. the same K-range (token window for the TT wgrad) and
+  // neighbouring tiles (shared A row panels / B column panels) -> L2 reuse inside the XCD.
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int split = v / p.ntiles, wg = v % p.ntiles;
   const int tm = wg / p.tiles_n, tn = wg % p.tiles_n;
   const int m0 = tm * BM, n0 = tn * BN;
-  const int kbeg = blockIdx.y * p.kps;
+  const int kbeg = split * p.kps;
   const int kend = min(p.K, kbeg + p.kps);
   const int nt = (kend - kbeg) / BK;
 
@@ -433,7 +519,7 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
           atomicAdd(c + 2, acc[i][j][2]);
           atomicAdd(c + 3, acc[i][j][3]);
         } else {
-          float* c = reinterpret_cast<float*>(p.C) + (int64_t)blockIdx.y * p.M * p.N + (int64_t)m * p.N + n;
+          float* c = reinterpret_cast<float*>(p.C) + (int64_t)split * p.M * p.N + (int64_t)m * p.N + n;
           *reinterpret_cast<f32x4*>(c) = acc[i][j];
         }
       }
@@ -443,8 +529,8 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
     // rows with 16-B lanes: each lane owns 8 consecutive n of one m.
     constexpr int SROW = WN + 8;
     constexpr int CPR = WN / 8;  // 16-B chunks per row
-    constexpr bool kBias = EPI == E2_BIAS || EPI == E2_BIAS_GELU || EPI == E2_BIAS_DROP_RES;
-    constexpr bool kAux = EPI == E2_BIAS_DROP_RES || EPI == E2_RES || EPI == E2_DGELU;
+    constexpr bool kBias = epi_bias(EPI);
+    constexpr bool kAux = epi_aux(EPI);
     bf16_t* stg = smem + wave * (64 * SROW);
     f32x4 bv[NREP];
     if constexpr (kBias) {
@@ -456,7 +542,7 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
       }
     }
     bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
-    constexpr bool kColsum = EPI == E2_DGELU && CPR == 8;
+    constexpr bool kColsum = (EPI == E2_DGELU || EPI == E2_MUL) && CPR == 8;
     float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int h = 0; h < 2; ++h) {
@@ -479,6 +565,8 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
         if constexpr (kAux) {
           const int m = min(mw + 64 * h + row, p.M - 1);
           xv[it] = *reinterpret_cast<const u32x4*>(p.aux + (int64_t)m * p.ldaux + nw + c8 * 8);
+        } else {
+          xv[it] = u32x4{0, 0, 0, 0};
         }
       }
 #pragma unroll
@@ -489,74 +577,195 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
         const int n = nw + c8 * 8;
         if (m >= p.M) continue;
         const int64_t co = (int64_t)m * p.ldc + n;
-        u32x4 o = sv[it];
-        if constexpr (EPI == E2_BIAS_GELU) {
-          *reinterpret_cast<u32x4*>(C + co) = o;  // pre-activation (kept for backward)
-          u32x4 g;
-          g.x = pack_bf2(gelu_erf(lo_bf(o.x)), gelu_erf(hi_bf(o.x)));
-          g.y = pack_bf2(gelu_erf(lo_bf(o.y)), gelu_erf(hi_bf(o.y)));
-          g.z = pack_bf2(gelu_erf(lo_bf(o.z)), gelu_erf(hi_bf(o.z)));
-          g.w = pack_bf2(gelu_erf(lo_bf(o.w)), gelu_erf(hi_bf(o.w)));
-          *reinterpret_cast<u32x4*>(p.C2 + co) = g;
-          continue;
-        } else if constexpr (EPI == E2_BIAS_DROP_RES) {
-          // z = bf16(bf16(y · keep · scale) + residual)
-          float v[8] = {lo_bf(o.x), hi_bf(o.x), lo_bf(o.y), hi_bf(o.y), lo_bf(o.z), hi_bf(o.z), lo_bf(o.w), hi_bf(o.w)};
-          if (p.dp.enabled) {
-            const uint32_t pair0 = (uint32_t)(((int64_t)m * p.N + n) >> 1);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              const uint32_t b = dropout_bits(pair0 + e, p.dp.seed_lo, p.dp.seed_hi);
-              v[2 * e] = bf2f(f2bf(v[2 * e] * keep_factor(b, 0, p.dp)));
-              v[2 * e + 1] = bf2f(f2bf(v[2 * e + 1] * keep_factor(b, 1, p.dp)));
-            }
-          }
-          const u32x4 x = xv[it];
-          o.x = pack_bf2(v[0] + lo_bf(x.x), v[1] + hi_bf(x.x));
-          o.y = pack_bf2(v[2] + lo_bf(x.y), v[3] + hi_bf(x.y));
-          o.z = pack_bf2(v[4] + lo_bf(x.z), v[5] + hi_bf(x.z));
-          o.w = pack_bf2(v[6] + lo_bf(x.w), v[7] + hi_bf(x.w));
-        } else if constexpr (EPI == E2_RES) {
-          const u32x4 x = xv[it];
-          o.x = pack_bf2(lo_bf(o.x) + lo_bf(x.x), hi_bf(o.x) + hi_bf(x.x));
-          o.y = pack_bf2(lo_bf(o.y) + lo_bf(x.y), hi_bf(o.y) + hi_bf(x.y));
-          o.z = pack_bf2(lo_bf(o.z) + lo_bf(x.z), hi_bf(o.z) + hi_bf(x.z));
-          o.w = pack_bf2(lo_bf(o.w) + lo_bf(x.w), hi_bf(o.w) + hi_bf(x.w));
-        } else if constexpr (EPI == E2_DGELU) {
-          const u32x4 x = xv[it];
-          o.x = pack_bf2(lo_bf(o.x) * gelu_erf_grad(lo_bf(x.x)), hi_bf(o.x) * gelu_erf_grad(hi_bf(x.x)));
-          o.y = pack_bf2(lo_bf(o.y) * gelu_erf_grad(lo_bf(x.y)), hi_bf(o.y) * gelu_erf_grad(hi_bf(x.y)));
-          o.z = pack_bf2(lo_bf(o.z) * gelu_erf_grad(lo_bf(x.z)), hi_bf(o.z) * gelu_erf_grad(hi_bf(x.z)));
-          o.w = pack_bf2(lo_bf(o.w) * gelu_erf_grad(lo_bf(x.w)), hi_bf(o.w) * gelu_erf_grad(hi_bf(x.w)));
-          if constexpr (kColsum) {
-            csum[0] += lo_bf(o.x); csum[1] += hi_bf(o.x); csum[2] += lo_bf(o.y); csum[3] += hi_bf(o.y);
-            csum[4] += lo_bf(o.z); csum[5] += hi_bf(o.z); csum[6] += lo_bf(o.w); csum[7] += hi_bf(o.w);
-          }
-        }
+        u32x4 o = sv[it], o2;
+        epi_chunk<EPI>(o, o2, xv[it], m, n, p, csum);
         *reinterpret_cast<u32x4*>(C + co) = o;
+        if constexpr (epi_two_out(EPI)) *reinterpret_cast<u32x4*>(p.C2 + co) = o2;
       }
       __builtin_amdgcn_wave_barrier();
     }
     if constexpr (kColsum) {
-      // lanes with equal (lane & 7) own the same 8 columns: reduce over lane bits 3..5, then 8 lanes add
-      if (p.dbias != nullptr) {
+      if (p.dbias != nullptr) colsum_flush(csum, p.dbias, nw, p.N, lane);
+    }
+  }
+}
+
+// Persistent NT variant: each workgroup walks tiles blockIdx.x, +gridDim.x, ... as ONE sequence of K-steps
+// (stage = step & 1), so the next tile's first K-step is DMA'd during the current tile's last K-step and
+// its epilogue, and the epilogue's stores drain while the next tile's MFMAs run. The epilogue stages one
+// 16-row MFMA block at a time through a wave-private LDS slice placed AFTER the two operand stages.
+template <int EPI, int BN>
+__global__ __launch_bounds__(512, 1) void gemm2p_kernel(G2Params p, int ntiles) {
+  constexpr int WN = BN / 4, NREP = WN / 16, NB0 = 2, NB1 = NREP - NB0;
+  constexpr int TA = BM * 64, TB = BN * 64, STAGE = TA + TB;
+  constexpr int GA = 4, GB = BN / 64, G = GA + GB;
+  constexpr int SROW = WN + 8, CPR = WN / 8;
+  constexpr int ITER = (16 * CPR + 63) / 64;
+  constexpr bool kBias = epi_bias(EPI);
+  constexpr bool kAux = epi_aux(EPI);
+  constexpr bool kColsum = (EPI == E2_DGELU || EPI == E2_MUL) && CPR == 8;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * STAGE + 8 * 16 * SROW];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int arow = wm * 128, bcol = wn * WN;
+  const int q4 = lane >> 4, lr = lane & 15;
+  const int nt = p.K / BK;
+  bf16_t* stg = smem + 2 * STAGE + wave * 16 * SROW;
+  bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
+
+  auto tile_origin = [&](int tile, int& m0, int& n0) {
+    const int xcd = tile & 7, q8 = ntiles >> 3, r8 = ntiles & 7;
+    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (tile >> 3);
+    m0 = (wg / p.tiles_n) * BM;
+    n0 = (wg % p.tiles_n) * BN;
+  };
+  auto dma_step = [&](int m0, int n0, int kt, bf16_t* stage) {
 #pragma unroll
-        for (int e = 0; e < 8; ++e) {
-          float v = csum[e];
-          v += __shfl_xor(v, 8, 64);
-          v += __shfl_xor(v, 16, 64);
-          v += __shfl_xor(v, 32, 64);
-          csum[e] = v;
-        }
-        if (lane < 8) {
-          const int n = nw + lane * 8;
-          if (n < p.N) {
+    for (int q = 0; q < G; ++q) {
+      if (q < GA) dma<0, BM>(stage, p.A, p.lda, m0, p.M, kt * BK, wave * GA + q, lane);
+      else dma<0, BN>(stage + TA, p.B, p.ldb, n0, p.N, kt * BK, wave * GB + (q - GA), lane);
+    }
+  };
+
+  f32x4 acc[8][NREP];
 #pragma unroll
-            for (int e = 0; e < 8; ++e) atomicAdd(p.dbias + n + e, csum[e]);
-          }
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < NREP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  bf16x8 fa[4][2], fb0[NB0][2], fb1[NB1][2];
+
+  int tile = blockIdx.x;
+  if (tile >= ntiles) return;
+  int m0, n0;
+  tile_origin(tile, m0, n0);
+  dma_step(m0, n0, 0, smem);
+  vmcnt<0>();
+  G2_BARRIER();
+  int step = 0;
+  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  while (true) {
+    const int next_tile = tile + gridDim.x;
+    int nm0 = 0, nn0 = 0;
+    if (next_tile < ntiles) tile_origin(next_tile, nm0, nn0);
+    for (int t = 0; t < nt; ++t, ++step) {
+      const bf16_t* cA = smem + (step & 1) * STAGE;
+      const bf16_t* cB = cA + TA;
+      bf16_t* nS = smem + ((step + 1) & 1) * STAGE;
+      if (t + 1 < nt) dma_step(m0, n0, t + 1, nS);
+      else if (next_tile < ntiles) dma_step(nm0, nn0, 0, nS);
+#pragma unroll
+      for (int j = 0; j < NB0; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) fb0[j][ks] = frag<0>(cB, bcol + 16 * j, ks, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<0>(cA, arow + 16 * i, ks, lane);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < NB0; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][ks], fa[i][ks], acc[i][j], 0, 0, 0);
+#pragma unroll
+      for (int j = 0; j < NB1; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) fb1[j][ks] = frag<0>(cB, bcol + 16 * (NB0 + j), ks, lane);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < NB1; ++j)
+            acc[i][NB0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][ks], fa[i][ks], acc[i][NB0 + j], 0, 0, 0);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<0>(cA, arow + 64 + 16 * i, ks, lane);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+#pragma unroll
+          for (int j = 0; j < NB1; ++j)
+            acc[4 + i][NB0 + j] =
+                __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][ks], fa[i][ks], acc[4 + i][NB0 + j], 0, 0, 0);
+#pragma unroll
+          for (int j = 0; j < NB0; ++j)
+            acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][ks], fa[i][ks], acc[4 + i][j], 0, 0, 0);
         }
+      if (t + 1 < nt) {
+        vmcnt<0>();
+        G2_BARRIER();
       }
     }
+    // the next tile's first K-step (DMA'd at the start of this tile's last K-step) has landed for every
+    // wave, and every wave is past its last LDS read of this tile: one barrier publishes / frees both.
+    // The epilogue's stores then stay in flight until the next K-step's vmcnt(0).
+    vmcnt<0>();
+    G2_BARRIER();
+
+    // ---------------------------------------------------------------- epilogue (16-row passes)
+    const int mw = m0 + arow, nw = n0 + bcol;
+    f32x4 bv[NREP];
+    if constexpr (kBias) {
+#pragma unroll
+      for (int j = 0; j < NREP; ++j) {
+        const int n = min(nw + 16 * j + 4 * q4, p.N - 4);
+        const u32x2 b = *reinterpret_cast<const u32x2*>(p.bias + n);
+        bv[j] = f32x4{lo_bf(b.x), hi_bf(b.x), lo_bf(b.y), hi_bf(b.y)};
+      }
+    }
+    u32x4 xv[8][ITER];
+    if constexpr (kAux) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int it = 0; it < ITER; ++it) {
+          const int idx = min(lane + 64 * it, 16 * CPR - 1);
+          const int row = idx / CPR, c8 = idx % CPR;
+          const int m = min(mw + 16 * i + row, p.M - 1);
+          xv[i][it] = *reinterpret_cast<const u32x4*>(p.aux + (int64_t)m * p.ldaux + nw + c8 * 8);
+        }
+    }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+#pragma unroll
+      for (int j = 0; j < NREP; ++j) {
+        f32x4 v = acc[i][j];
+        if constexpr (kBias) v += bv[j];
+        *reinterpret_cast<u32x2*>(stg + lr * SROW + 16 * j + 4 * q4) = pack4(v);
+        acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+      __builtin_amdgcn_wave_barrier();
+#pragma unroll
+      for (int it = 0; it < ITER; ++it) {
+        const int idx = lane + 64 * it;
+        if (idx >= 16 * CPR) continue;
+        const int row = idx / CPR, c8 = idx % CPR;
+        const int m = mw + 16 * i + row;
+        const int n = nw + c8 * 8;
+        u32x4 o = *reinterpret_cast<const u32x4*>(stg + row * SROW + c8 * 8);
+        if (m >= p.M) continue;
+        const int64_t co = (int64_t)m * p.ldc + n;
+        u32x4 o2;
+        u32x4 x = u32x4{0, 0, 0, 0};
+        if constexpr (kAux) x = xv[i][it];
+        epi_chunk<EPI>(o, o2, x, m, n, p, csum);
+        *reinterpret_cast<u32x4*>(C + co) = o;
+        if constexpr (epi_two_out(EPI)) *reinterpret_cast<u32x4*>(p.C2 + co) = o2;
+      }
+      __builtin_amdgcn_wave_barrier();
+    }
+    if constexpr (kColsum) {
+      if (p.dbias != nullptr) colsum_flush(csum, p.dbias, nw, p.N, lane);
+    }
+    if (next_tile >= ntiles) break;
+    tile = next_tile;
+    m0 = nm0;
+    n0 = nn0;
   }
 }
 
@@ -587,8 +796,33 @@ static int g2_sync_mode(int la, int K) {
   return (la == 0 && K <= 1024) ? 1 : 0;
 }
 
+template <int EPI, int BN>
+static void g2p_launch(const G2Params& p0, hipStream_t st) {
+  G2Params p = p0;
+  const int tiles_m = (p.M + g2::BM - 1) / g2::BM;
+  p.tiles_n = (p.N + BN - 1) / BN;
+  p.kps = p.K;
+  const int ntiles = tiles_m * p.tiles_n;
+  p.ntiles = ntiles;
+  static int cus = [] {
+    int dev = 0, n = 0;
+    hipGetDevice(&dev);
+    hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+    return n > 0 ? n : 256;
+  }();
+  const int grid = ntiles < cus ? ntiles : cus;
+  hipLaunchKernelGGL((g2::gemm2p_kernel<EPI, BN>), dim3(grid), dim3(512), 0, st, p, ntiles);
+  HSD_CHECK_LAUNCH();
+}
+
 template <int LA, int LB, int EPI, int BN>
 static void g2_launch(const G2Params& p0, int splits, hipStream_t st) {
+  if constexpr (LA == 0 && LB == 0 && epi_bf16_out(EPI)) {
+    if (g2_sync_mode(LA, p0.K) == 3) {
+      g2p_launch<EPI, BN>(p0, st);
+      return;
+    }
+  }
   G2Params p = p0;
   const int tiles_m = (p.M + g2::BM - 1) / g2::BM;
   p.tiles_n = (p.N + BN - 1) / BN;
@@ -597,7 +831,8 @@ static void g2_launch(const G2Params& p0, int splits, hipStream_t st) {
   kps = (kps + g2::BK - 1) / g2::BK * g2::BK;
   splits = (p.K + kps - 1) / kps;
   p.kps = kps;
-  dim3 grid(tiles_m * p.tiles_n, splits);
+  p.ntiles = tiles_m * p.tiles_n;
+  dim3 grid(p.ntiles * splits);
   const int mode = g2_sync_mode(LA, p.K);
   if (mode == 1) hipLaunchKernelGGL((g2::gemm2_kernel<LA, LB, EPI, BN, 1>), grid, dim3(512), 0, st, p);
   else if (mode == 2) hipLaunchKernelGGL((g2::gemm2_kernel<LA, LB, EPI, BN, 2>), grid, dim3(512), 0, st, p);
@@ -622,7 +857,7 @@ int gemm2_pick_bn(int M, int N) {
 
 bool gemm2_supported(int la, int lb, int epi, int M, int N, int K) {
   if (K % 64 || M < 1 || N % 8) return false;
-  if (la == 0 && lb == 0) return epi <= E2_DGELU && gemm2_pick_bn(M, N) != 0;
+  if (la == 0 && lb == 0) return epi_bf16_out(epi) && gemm2_pick_bn(M, N) != 0;
   if (la == 1 && lb == 1) return (epi == E2_F32_ATOMIC || epi == E2_F32_SLAB) && M % 8 == 0 && N % 256 == 0;
   return false;
 }
@@ -648,7 +883,7 @@ void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const b
   if (la == 0 && lb == 0) {
     int bn = gemm2_pick_bn(M, N);
     if (dbias != nullptr) {
-      if (epi != E2_DGELU || N % 256) abort();  // fused bias-grad column sums: 8 columns per lane (BN 256)
+      if ((epi != E2_DGELU && epi != E2_MUL) || N % 256) abort();  // fused column sums: 8 columns per lane (BN 256)
       bn = 256;
     }
 #define G2_NT(E)                                                     \
@@ -663,6 +898,8 @@ void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const b
       G2_NT(E2_BIAS_DROP_RES)
       G2_NT(E2_RES)
       G2_NT(E2_DGELU)
+      G2_NT(E2_BIAS_GELU_D)
+      G2_NT(E2_MUL)
       default: abort();
     }
 #undef G2_NT

@@ -100,6 +100,12 @@ def attention(qkv, mask_bias, batch, seq, heads, p, seed):
     return _ref.attention(qkv, mask_bias, batch, seq, heads, p, seed, p > 0)
 
 
+def join_side_streams() -> None:
+    """Order the current stream after the wgrad side stream (no-op on CPU / reference ops)."""
+    if torch.cuda.is_available() and not _FORCE_TORCH:
+        _hipmod().join_side_streams()
+
+
 def cross_entropy(logits, labels):
     return _ref.cross_entropy(logits, labels)
 

@@ -47,6 +47,53 @@ class _Grad:
         return None
 
 
+# ------------------------------------------------------------------------------------------ wgrad stream
+# Weight-gradient GEMMs are independent of the rest of the backward chain (dgrad -> previous layer), so
+# they run on a side stream: their compute overlaps the dgrad GEMMs' memory-bound epilogues and the
+# attention / LayerNorm kernels on other CUs. Gradient readiness (bucket all-reduce) is signalled from
+# the side stream; the comm engine also orders every collective after it, and the trainer joins it
+# before the optimizer (join_side_streams).
+import os as _os
+
+_WGRAD_STREAM = _os.environ.get("HSD_WGRAD_STREAM", "1") != "0"
+_SIDE = {}
+
+
+def side_stream(device) -> Optional[torch.cuda.Stream]:
+    if not _WGRAD_STREAM:
+        return None
+    key = device.index if device.index is not None else torch.cuda.current_device()
+    s = _SIDE.get(key)
+    if s is None:
+        s = torch.cuda.Stream(device=key)
+        _SIDE[key] = s
+    return s
+
+
+def join_side_streams() -> None:
+    """Make the current stream wait for every side stream (call before consuming gradients)."""
+    cur = torch.cuda.current_stream() if _SIDE else None
+    for s in _SIDE.values():
+        if s.device == cur.device:
+            cur.wait_stream(s)
+
+
+def wgrad_done(g: "_Grad", dy: torch.Tensor, x: torch.Tensor):
+    """``g += dyᵀ·x`` then ``g.done()`` — on the wgrad side stream when the gradient lands in the flat
+    fp32 main_grad buffer (training with a FlatParamStore), synchronously otherwise."""
+    s = side_stream(dy.device) if (g.mg is not None and g.buf is g.mg) else None
+    if s is None:
+        gemm_wgrad_(g, dy, x)
+        return g.done()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        gemm_wgrad_(g, dy, x)
+        r = g.done()
+    dy.record_stream(s)
+    x.record_stream(s)
+    return r
+
+
 def _wgrad_(g: _Grad, dy2d: torch.Tensor, x2d: torch.Tensor) -> None:
     """g += dyᵀ·x  (fp32 accumulate)."""
     g.buf.add_(torch.mm(dy2d.t(), x2d).to(torch.float32))
@@ -280,6 +327,7 @@ def attention(qkv, mask_bias, batch, seq, heads, p, seed):
 
 # ------------------------------------------------------------------------------------------ GEMM helpers
 EPI_STORE, EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_DROP_RES, EPI_RES, EPI_DGELU, EPI_F32_ATOMIC = range(7)
+EPI_F32_SLAB, EPI_BIAS_GELU_D, EPI_MUL = 7, 8, 9  # gemm2 only
 
 # split-K factors for the wgrad GEMM (fp32 atomic epilogue), measured with tools/bench_gemm.py at
 # T = 32768 tokens; key = (out_features, in_features)
@@ -337,7 +385,7 @@ def gemm_dgrad(dy, w, epi=EPI_STORE, aux=None, dbias=None):
         wt = getattr(w, "_hsd_wt", None)  # FlatParamStore keeps Wᵀ fresh (one batched transpose per step)
         if wt is None or wt.shape[0] != w.shape[1] or wt.shape[1] != w.shape[0]:
             wt = w.t().contiguous()
-        fuse = dbias is not None and epi == EPI_DGELU and w.shape[1] % 256 == 0
+        fuse = dbias is not None and epi in (EPI_DGELU, EPI_MUL) and w.shape[1] % 256 == 0
         _C.gemm2(dy, wt, dx, 0, 0, epi, None, aux, None, 0.0, 0, 1, None, dbias if fuse else None)
         if dbias is not None and not fuse:
             _C.colsum(dx, dbias)
@@ -406,8 +454,7 @@ class _AttnBlock(torch.autograd.Function):
             _C.ln_bwd(dout2, z, mean, rstd, ln_w, None, dy, None, g_lnw.buf, g_lnb.buf, g_ob.buf, 0.0, 0)
             dz = dy
         r_lnw, r_lnb, r_ob = g_lnw.done(), g_lnb.done(), g_ob.done()
-        gemm_wgrad_(g_ow, dy, actx)
-        r_ow = g_ow.done()
+        r_ow = wgrad_done(g_ow, dy, actx)
         dctx = gemm_dgrad(dy, out_w)
         dqkv = torch.empty_like(qkv)
         dq_acc = torch.zeros(actx.shape, dtype=torch.float32, device=actx.device) if S > 128 else None
@@ -415,8 +462,7 @@ class _AttnBlock(torch.autograd.Function):
         g_qw, g_qb = _Grad(qkv_w), _Grad(qkv_b)
         _C.colsum(dqkv, g_qb.buf)
         r_qb = g_qb.done()
-        gemm_wgrad_(g_qw, dqkv, h2d)
-        r_qw = g_qw.done()
+        r_qw = wgrad_done(g_qw, dqkv, h2d)
         dh = gemm_dgrad(dqkv, qkv_w, EPI_RES, aux=dz) if ctx.needs_input_grad[0] else None
         return (dh.view(dout.shape) if dh is not None else None, r_qw, r_qb, r_ow, r_ob, r_lnw, r_lnb,
                 None, None, None, None, None, None, None, None, None)
@@ -436,17 +482,21 @@ class _FFNBlock(torch.autograd.Function):
     def forward(ctx, h, w1, b1, w2, b2, ln_w, ln_b, eps, p, seed):
         h2d = h.reshape(-1, h.shape[-1])
         act = torch.empty((h2d.shape[0], w1.shape[0]), dtype=h.dtype, device=h.device)
-        pre = gemm_fwd(h2d, w1, EPI_BIAS_GELU, bias=b1, out2=act)
+        # keep gelu'(pre) instead of pre when the gemm2 path handles both FFN GEMMs: the FFN2 dgrad
+        # epilogue is then a product (no erf/exp per element in backward)
+        keep_grad = _nt_ok(h2d.shape[0], w1.shape[0], h2d.shape[1], EPI_BIAS_GELU_D) and \
+            _nt_ok(h2d.shape[0], w1.shape[0], w2.shape[0], EPI_MUL)
+        pre = gemm_fwd(h2d, w1, EPI_BIAS_GELU_D if keep_grad else EPI_BIAS_GELU, bias=b1, out2=act)
         z = gemm_fwd(act, w2, EPI_BIAS_DROP_RES, bias=b2, aux=h2d, p=p, seed=seed)
         out, mean, rstd = _ln_fwd(z, ln_w, ln_b, eps)
         ctx.save_for_backward(h2d, w1, b1, w2, b2, ln_w, ln_b, pre, act, z, mean, rstd)
-        ctx.cfg = (float(p), seed)
+        ctx.cfg = (float(p), seed, keep_grad)
         return out.view(h.shape)
 
     @staticmethod
     def backward(ctx, dout):
         h2d, w1, b1, w2, b2, ln_w, ln_b, pre, act, z, mean, rstd = ctx.saved_tensors
-        p, seed = ctx.cfg
+        p, seed, keep_grad = ctx.cfg
         dout2 = dout.reshape(z.shape).contiguous()
         g_lnw, g_lnb, g_w2, g_b2 = _Grad(ln_w), _Grad(ln_b), _Grad(w2), _Grad(b2)
         dy = torch.empty_like(z)
@@ -457,13 +507,11 @@ class _FFNBlock(torch.autograd.Function):
             _C.ln_bwd(dout2, z, mean, rstd, ln_w, None, dy, None, g_lnw.buf, g_lnb.buf, g_b2.buf, 0.0, 0)
             dz = dy
         r_lnw, r_lnb, r_b2 = g_lnw.done(), g_lnb.done(), g_b2.done()
-        gemm_wgrad_(g_w2, dy, act)
-        r_w2 = g_w2.done()
+        r_w2 = wgrad_done(g_w2, dy, act)
         g_w1, g_b1 = _Grad(w1), _Grad(b1)
-        da = gemm_dgrad(dy, w2, EPI_DGELU, aux=pre, dbias=g_b1.buf)
+        da = gemm_dgrad(dy, w2, EPI_MUL if keep_grad else EPI_DGELU, aux=pre, dbias=g_b1.buf)
         r_b1 = g_b1.done()
-        gemm_wgrad_(g_w1, da, h2d)
-        r_w1 = g_w1.done()
+        r_w1 = wgrad_done(g_w1, da, h2d)
         dh = gemm_dgrad(da, w1, EPI_RES, aux=dz) if ctx.needs_input_grad[0] else None
         return (dh.view(dout.shape) if dh is not None else None, r_w1, r_b1, r_w2, r_b2, r_lnw, r_lnb,
                 None, None, None)

@@ -70,6 +70,7 @@ class FusedAdam:
         if s.master.is_cuda:
             from ..ops import hip
 
+            hip.join_side_streams()  # weight gradients may still be in flight on the wgrad stream
             hip.adam_step(s.master, self.exp_avg, self.exp_avg_sq, s.grad, s.compute if write_compute else None,
                           self._decay_mask, step, eps_eff, self.beta1, self.beta2, float(grad_scale),
                           self.lr * self.weight_decay)

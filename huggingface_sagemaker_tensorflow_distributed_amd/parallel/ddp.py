@@ -82,6 +82,12 @@ class GradBucketer:
                 logger.warning("native CommEngine unavailable (%s); using torch.distributed buckets", e)
                 self.engine = None
             if self.engine is not None:
+                if store.device.type == "cuda":
+                    from ..ops import hip as _hip
+
+                    side = _hip.side_stream(store.device)
+                    if side is not None:
+                        self.engine.add_dependency_stream(side.cuda_stream)
                 param_bucket = [0] * len(store.segments)
                 for b in self.buckets:
                     for pi in b.params:
@@ -106,6 +112,10 @@ class GradBucketer:
 
     def _launch(self, b: _Bucket) -> None:
         view = self.store.grad[b.start:b.end]
+        if view.is_cuda:
+            from ..ops import hip as _hip
+
+            _hip.join_side_streams()  # gradients of this bucket may come from the wgrad stream
         b.handle = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         b.launched = True
 

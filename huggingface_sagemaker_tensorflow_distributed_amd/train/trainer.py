@@ -112,6 +112,8 @@ class Trainer:
             if meter is not None:
                 meter.update(loss, logits, mb["labels"])
         with prange("allreduce-wait"):
+            if self.device.type == "cuda":
+                ops.join_side_streams()
             if self.bucketer is not None:
                 self.bucketer.finish()
         with prange("optimizer"):

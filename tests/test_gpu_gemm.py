@@ -190,3 +190,23 @@ def test_gemm2_dgelu_fused_dbias(gpu):
     C_.gemm2(A, B, C, 0, 0, 5, None, pre, None, 0.0, 0, 1, None, db)
     _check(C, (A.float() @ B.float().t()).bfloat16().float() * _gelu_grad(pre.float()))
     _check(db, 0.5 + C.float().sum(0), 1e-3)
+
+
+def test_gemm2_gelu_derivative_and_mul_epilogues(gpu):
+    """E2_BIAS_GELU_D (C = gelu'(y), C2 = gelu(y)) and E2_MUL (C = bf16(acc) * aux, + fused column sums)."""
+    torch.manual_seed(14)
+    C_ = _C()
+    M, N, K = 512, 3072, 768
+    A, B, bias = _mk((M, K), gpu), _mk((N, K), gpu, 0.1), _mk((N,), gpu)
+    D = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    G = torch.empty_like(D)
+    C_.gemm2(A, B, D, 0, 0, 8, bias, None, G, 0.0, 0, 1, None, None)
+    y = (A.float() @ B.float().t() + bias.float()).bfloat16().float()
+    _check(G, torch.nn.functional.gelu(y))
+    _check(D, _gelu_grad(y))
+    dy, W = _mk((M, 768), gpu), _mk((N, 768), gpu, 0.1)
+    out = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    db = torch.zeros(N, device=gpu)
+    C_.gemm2(dy, W, out, 0, 0, 9, None, D, None, 0.0, 0, 1, None, db)
+    _check(out, (dy.float() @ W.float().t()).bfloat16().float() * D.float())
+    _check(db, out.float().sum(0), 1e-3)

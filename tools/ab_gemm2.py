@@ -43,6 +43,9 @@ for name, (N, K) in {"qkv": (2304, 768), "out": (768, 768), "ffn1": (3072, 768),
     bufs[f"{name}_gelu"] = [y, y2]
     bufs[f"{name}_dgrad"] = [dx]
     bufs[f"{name}_wgrad"] = [gw]
+    if os.environ.get("AB_ONLY_WGRAD"):
+        cases[f"{name}_wgrad"] = (fl, lambda dy=dy, x=x, gw=gw, sp=sp, ws=ws: C_.gemm2(dy, x, gw, 1, 1, 7, None, None, None, 0.0, 0, sp, ws, None))
+        continue
     cases[f"{name}_fwd"] = (fl, lambda x=x, w=w, y=y: C_.gemm2(x, w, y, 0, 0, 0, None, None, None, 0.0, 0, 1, None, None))
     res_in = torch.randn(T, N, device="cuda").bfloat16()
     resK = torch.randn(T, K, device="cuda").bfloat16()
