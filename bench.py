@@ -32,7 +32,7 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch_size", type=int, default=int(os.environ.get("HSD_BENCH_BATCH", "256")),
+    ap.add_argument("--batch_size", type=int, default=int(os.environ.get("HSD_BENCH_BATCH", "1024")),
                     help="per-GPU batch")
     ap.add_argument("--seq_len", type=int, default=128)
     ap.add_argument("--model", default="bert-base-uncased")

@@ -55,7 +55,8 @@ class _Grad:
 # before the optimizer (join_side_streams).
 import os as _os
 
-_WGRAD_STREAM = _os.environ.get("HSD_WGRAD_STREAM", "1") != "0"
+_WGRAD_STREAM = _os.environ.get("HSD_WGRAD_STREAM", "0") == "1"  # opt-in: +1% at B=256, but record_stream
+# keeps freed activations from being reused promptly and collapses large-batch throughput
 _SIDE = {}
 
 
