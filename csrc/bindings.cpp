@@ -168,7 +168,7 @@ void attn_fwd(torch::Tensor qkv, c10::optional<torch::Tensor> mask, torch::Tenso
 
 void attn_bwd(torch::Tensor qkv, c10::optional<torch::Tensor> mask, torch::Tensor o, torch::Tensor dout,
               torch::Tensor lse2, torch::Tensor dqkv, c10::optional<torch::Tensor> dq_acc, int64_t B, int64_t S,
-              int64_t heads, double p, int64_t seed) {
+              int64_t heads, double p, int64_t seed, c10::optional<torch::Tensor> dbias) {
   check_bf16(qkv, "qkv"); check_bf16(o, "o"); check_bf16(dout, "dout"); check_bf16(dqkv, "dqkv");
   check_f32(lse2, "lse2");
   TORCH_CHECK(qkv.size(-1) == 3 * heads * 64 && dqkv.numel() == qkv.numel(), "attn_bwd shapes");
@@ -176,8 +176,9 @@ void attn_bwd(torch::Tensor qkv, c10::optional<torch::Tensor> mask, torch::Tenso
   TORCH_CHECK(S <= 128 || dq_acc.has_value(), "S > 128 needs a zeroed fp32 dq accumulator");
   if (dq_acc.has_value()) { check_f32(*dq_acc, "dq_acc"); TORCH_CHECK(dq_acc->numel() == o.numel(), "dq_acc"); }
   if (mask.has_value()) { check_f32(*mask, "mask"); TORCH_CHECK(mask->numel() == B * S, "mask shape"); }
+  if (dbias.has_value()) { check_f32(*dbias, "dbias"); TORCH_CHECK(dbias->numel() == 3 * heads * 64, "dbias shape"); }
   hsd::launch_attn_bwd(CBF(qkv), OPT_F(mask), CBF(o), CBF(dout), lse2.data_ptr<float>(), BF(dqkv), OPT_F(dq_acc),
-                       (int)B, (int)S, (int)heads, p, (uint64_t)seed, cur_stream());
+                       OPT_F(dbias), (int)B, (int)S, (int)heads, p, (uint64_t)seed, cur_stream());
 }
 
 // C[M,N] (+)= A·B with fused epilogue. la=0: A [M,K]; la=1: A [K,M]. lb=0: B [N,K]; lb=1: B [K,N].
@@ -317,7 +318,9 @@ PYBIND11_MODULE(_C, m) {
   m.def("colsum", &colsum);
   m.def("dropout", &dropout);
   m.def("attn_fwd", &attn_fwd);
-  m.def("attn_bwd", &attn_bwd);
+  m.def("attn_bwd", &attn_bwd, py::arg("qkv"), py::arg("mask"), py::arg("o"), py::arg("dout"), py::arg("lse2"),
+        py::arg("dqkv"), py::arg("dq_acc"), py::arg("B"), py::arg("S"), py::arg("heads"), py::arg("p"), py::arg("seed"),
+        py::arg("dbias") = py::none());
   m.def("gemm", &gemm);
   m.def("gemm_variant", &gemm_variant);
   m.def("gemm2", &gemm2);

@@ -372,7 +372,8 @@ bool attn128_supported(int S, int head_dim);
 void launch_attn128_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse2, int B, int heads, double p,
                         uint64_t seed, hipStream_t st);
 void launch_attn128_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
-                        bf16_t* dqkv, int B, int heads, double p, uint64_t seed, hipStream_t st);
+                        bf16_t* dqkv, float* dbias, int B, int heads, double p, uint64_t seed, hipStream_t st);
+void launch_colsum(const bf16_t* x, float* dbias, int rows, int N, hipStream_t st);
 
 void launch_attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse2, int B, int S, int heads,
                      double p, uint64_t seed, hipStream_t st) {
@@ -388,9 +389,10 @@ void launch_attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* l
 }
 
 void launch_attn_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
-                     bf16_t* dqkv, float* dq_acc, int B, int S, int heads, double p, uint64_t seed, hipStream_t st) {
+                     bf16_t* dqkv, float* dq_acc, float* dbias, int B, int S, int heads, double p, uint64_t seed,
+                     hipStream_t st) {
   if (attn128_supported(S, kD) && !getenv("HSD_ATTN_GENERIC")) {
-    launch_attn128_bwd(qkv, mask, o, dout, lse2, dqkv, B, heads, p, seed, st);
+    launch_attn128_bwd(qkv, mask, o, dout, lse2, dqkv, dbias, B, heads, p, seed, st);
     return;
   }
   DropoutParams dp = make_dropout(p, seed);
@@ -407,6 +409,7 @@ void launch_attn_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, cons
     hipLaunchKernelGGL(dq_convert_kernel, dim3(blocks), dim3(256), 0, st, dq_acc, dqkv, T, H);
     HSD_CHECK_LAUNCH();
   }
+  if (dbias) launch_colsum(dqkv, dbias, B * S, 3 * heads * kD, st);
 }
 
 }  // namespace hsd

@@ -86,7 +86,8 @@ __device__ __forceinline__ void dma_img(bf16_t* img, const bf16_t* __restrict__ 
 // acc (32 rows on the lane x 64 d in regs: d = 32*blk + (reg&3) + 8(reg>>2) + 4h) * scale -> bf16 rows
 // of `dst` (row stride ld) through the wave-private staging slice `stg` ([32][64]).
 __device__ __forceinline__ void store_rows(bf16_t* stg, const f32x16& a0, const f32x16& a1, float scale,
-                                           bf16_t* __restrict__ dst, int64_t ld, int lane) {
+                                           bf16_t* __restrict__ dst, int64_t ld, int lane,
+                                           float* colsum_lds = nullptr) {
   const int r = lane & 31, h = lane >> 5;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -99,11 +100,34 @@ __device__ __forceinline__ void store_rows(bf16_t* stg, const f32x16& a0, const 
     *reinterpret_cast<u32x2*>(stg + stoff(r, 32 + 8 * i + 4 * h)) = w1;
   }
   __builtin_amdgcn_wave_barrier();
+  float cs[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int it = 0; it < 4; ++it) {
     const int row = (lane >> 3) + 8 * it, c = lane & 7;
     const u32x4 v = *reinterpret_cast<const u32x4*>(stg + stoff(row, c * 8));
     *reinterpret_cast<u32x4*>(dst + (int64_t)row * ld + c * 8) = v;
+    if (colsum_lds) {
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        cs[2 * k] += lo_bf(v[k]);
+        cs[2 * k + 1] += hi_bf(v[k]);
+      }
+    }
+  }
+  if (colsum_lds) {
+    // lanes with equal (lane & 7) hold the same 8 columns: reduce over lane bits 3..5
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float x = cs[e];
+      x += __shfl_xor(x, 8, 64);
+      x += __shfl_xor(x, 16, 64);
+      x += __shfl_xor(x, 32, 64);
+      cs[e] = x;
+    }
+    if (lane < 8) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) colsum_lds[lane * 8 + e] = cs[e];
+    }
   }
   __builtin_amdgcn_wave_barrier();
 }
@@ -204,15 +228,17 @@ __global__ __launch_bounds__(256, 2) void attn128_bwd_kernel(const bf16_t* __res
                                                              const bf16_t* __restrict__ o,
                                                              const bf16_t* __restrict__ dout,
                                                              const float* __restrict__ lse2,
-                                                             bf16_t* __restrict__ dqkv, int heads, float sl2,
-                                                             float scale, DropoutParams dp) {
-  // [Q | dO | dS | lse | delta]; after the main loop Q's slot holds K, dO's slot the output staging
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * S * D + S * S + 4 * S];
+                                                             bf16_t* __restrict__ dqkv, float* __restrict__ dbias,
+                                                             int heads, float sl2, float scale, DropoutParams dp) {
+  // [Q | dO | dS | lse | delta | bias-grad partials]; after the main loop Q's slot holds K, dO's slot the
+  // output staging
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * S * D + S * S + 4 * S + 2 * 3 * 4 * D];
   bf16_t* Qs = lds;
   bf16_t* dOs = lds + S * D;
   bf16_t* dSt = lds + 2 * S * D;
   float* lse_s = reinterpret_cast<float*>(lds + 2 * S * D + S * S);
   float* del_s = lse_s + S;
+  float* bsum = del_s + S;  // [3 (q,k,v)][4 waves][64]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hf = lane >> 5;
@@ -320,8 +346,9 @@ __global__ __launch_bounds__(256, 2) void attn128_bwd_kernel(const bf16_t* __res
   dma_img(Qs, base + H, ld, wave * 4, 4, lane);
   bf16_t* stg = dOs + wave * 32 * D;
   bf16_t* rowbase = dqkv + ((int64_t)b * S + wave * 32) * ld + hh * D;
-  store_rows(stg, dv0, dv1, 1.0f, rowbase + 2 * H, ld, lane);
-  store_rows(stg, dk0, dk1, scale, rowbase + H, ld, lane);
+  float* bs_w = dbias ? bsum + wave * D : nullptr;
+  store_rows(stg, dv0, dv1, 1.0f, rowbase + 2 * H, ld, lane, dbias ? bs_w + 2 * 4 * D : nullptr);
+  store_rows(stg, dk0, dk1, scale, rowbase + H, ld, lane, dbias ? bs_w + 4 * D : nullptr);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   // dQᵀ[d][q] = Σ_key Kᵀ[d][key] dSᵀ[key][q], wave w: queries 32w..32w+31
@@ -334,7 +361,16 @@ __global__ __launch_bounds__(256, 2) void attn128_bwd_kernel(const bf16_t* __res
       dq0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(Qs, kb * 32, s, 0, lane), bs, dq0, 0, 0, 0);
       dq1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(Qs, kb * 32, s, 1, lane), bs, dq1, 0, 0, 0);
     }
-  store_rows(stg, dq0, dq1, scale, rowbase, ld, lane);
+  store_rows(stg, dq0, dq1, scale, rowbase, ld, lane, bs_w);
+  if (dbias) {
+    // qkv bias gradient: column sums of this (batch, head)'s dQ | dK | dV, one atomic per column
+    __syncthreads();
+    if (tid < 3 * D) {
+      const int which = tid / D, c = tid % D;
+      const float* b = bsum + which * 4 * D + c;
+      atomicAdd(dbias + which * H + hh * D + c, b[0] + b[D] + b[2 * D] + b[3 * D]);
+    }
+  }
 }
 
 }  // namespace a128
@@ -350,12 +386,12 @@ void launch_attn128_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float
 }
 
 void launch_attn128_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
-                        bf16_t* dqkv, int B, int heads, double p, uint64_t seed, hipStream_t st) {
+                        bf16_t* dqkv, float* dbias, int B, int heads, double p, uint64_t seed, hipStream_t st) {
   DropoutParams dp = make_dropout(p, seed);
   const float sl2 = a128::kLog2e / sqrtf((float)a128::D);
   const float scale = 1.0f / sqrtf((float)a128::D);
   hipLaunchKernelGGL(a128::attn128_bwd_kernel, dim3(B * heads), dim3(256), 0, st, qkv, mask, o, dout, lse2, dqkv,
-                     heads, sl2, scale, dp);
+                     dbias, heads, sl2, scale, dp);
   HSD_CHECK_LAUNCH();
 }
 

@@ -42,8 +42,10 @@ void launch_transpose_many(const int64_t* desc, int n, int total_tiles, hipStrea
 // attention.hip
 void launch_attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse2, int B, int S, int heads,
                      double p, uint64_t seed, hipStream_t st);
+// dbias (optional): fp32 [3H] += column sums of dqkv (the fused QKV bias gradient)
 void launch_attn_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
-                     bf16_t* dqkv, float* dq_acc, int B, int S, int heads, double p, uint64_t seed, hipStream_t st);
+                     bf16_t* dqkv, float* dq_acc, float* dbias, int B, int S, int heads, double p, uint64_t seed,
+                     hipStream_t st);
 }  // namespace hsd
 
 namespace hsd {

@@ -459,9 +459,10 @@ class _AttnBlock(torch.autograd.Function):
         dctx = gemm_dgrad(dy, out_w)
         dqkv = torch.empty_like(qkv)
         dq_acc = torch.zeros(actx.shape, dtype=torch.float32, device=actx.device) if S > 128 else None
-        _C.attn_bwd(qkv, mb if has_mask else None, actx, dctx, lse, dqkv, dq_acc, B, S, heads, p_a, _s64(seed_a))
         g_qw, g_qb = _Grad(qkv_w), _Grad(qkv_b)
-        _C.colsum(dqkv, g_qb.buf)
+        # the QKV bias gradient (column sums of dqkv) comes out of the attention backward itself
+        _C.attn_bwd(qkv, mb if has_mask else None, actx, dctx, lse, dqkv, dq_acc, B, S, heads, p_a, _s64(seed_a),
+                    g_qb.buf)
         r_qb = g_qb.done()
         r_qw = wgrad_done(g_qw, dqkv, h2d)
         dh = gemm_dgrad(dqkv, qkv_w, EPI_RES, aux=dz) if ctx.needs_input_grad[0] else None
