@@ -55,7 +55,13 @@ struct G2Params {
   int tiles_n;
   int ntiles;    // tiles_m * tiles_n
   float* dbias;  // E2_DGELU: optional fp32 column sums of the output (the bias gradient), BN 256 only
+  int nt_store;  // non-temporal (streaming) epilogue stores
 };
+
+__device__ __forceinline__ void st16(bf16_t* dst, const u32x4& v, int nt) {
+  if (nt) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst));
+  else *reinterpret_cast<u32x4*>(dst) = v;
+}
 
 namespace g2 {
 
@@ -579,8 +585,8 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
         const int64_t co = (int64_t)m * p.ldc + n;
         u32x4 o = sv[it], o2;
         epi_chunk<EPI>(o, o2, xv[it], m, n, p, csum);
-        *reinterpret_cast<u32x4*>(C + co) = o;
-        if constexpr (epi_two_out(EPI)) *reinterpret_cast<u32x4*>(p.C2 + co) = o2;
+        st16(C + co, o, p.nt_store);
+        if constexpr (epi_two_out(EPI)) st16(p.C2 + co, o2, p.nt_store);
       }
       __builtin_amdgcn_wave_barrier();
     }
@@ -754,8 +760,8 @@ __global__ __launch_bounds__(512, 1) void gemm2p_kernel(G2Params p, int ntiles) 
         u32x4 x = u32x4{0, 0, 0, 0};
         if constexpr (kAux) x = xv[i][it];
         epi_chunk<EPI>(o, o2, x, m, n, p, csum);
-        *reinterpret_cast<u32x4*>(C + co) = o;
-        if constexpr (epi_two_out(EPI)) *reinterpret_cast<u32x4*>(p.C2 + co) = o2;
+        st16(C + co, o, p.nt_store);
+        if constexpr (epi_two_out(EPI)) st16(p.C2 + co, o2, p.nt_store);
       }
       __builtin_amdgcn_wave_barrier();
     }
@@ -786,14 +792,15 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
 
 }  // namespace g2
 
-// Main-loop schedule (tools/ab_gemm2.py, interleaved in one process): NT with a short K (<= 1024: the
-// forward / dgrad GEMMs whose reduction is the hidden size) runs best with one barrier per K-tile
-// (SYNC 1: +5-10 %), NT with a long K (2304 / 3072) and the TT wgrad with the 8-phase form (SYNC 0).
-// HSD_G2_SYNC overrides for A/B runs.
+// Main-loop schedule (tools/ab_gemm2.py, interleaved in one process): NT (forward / dgrad) runs best with
+// one barrier per K-tile (SYNC 1: +3-10 % at 131k tokens; at 32k tokens the 8-phase form still wins for
+// K >= 2304 by ~5 %), the TT wgrad with the 8-phase form (SYNC 0). The persistent NT kernel (3) and the
+// pipelined-read form (2) measured within noise / slower. HSD_G2_SYNC overrides for A/B runs;
+// HSD_G2_NT=1 makes the epilogue stores non-temporal (measured neutral).
 static int g2_sync_mode(int la, int K) {
   const char* e = getenv("HSD_G2_SYNC");
   if (e) return atoi(e);
-  return (la == 0 && K <= 1024) ? 1 : 0;
+  return la == 0 ? 1 : 0;
 }
 
 template <int EPI, int BN>
@@ -877,6 +884,10 @@ void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const b
                   double p_drop, uint64_t seed, int splits, float* ws, float* dbias, hipStream_t st) {
   G2Params p{};
   p.dbias = dbias;
+  {
+    const char* e = getenv("HSD_G2_NT");
+    p.nt_store = e ? atoi(e) : 0;
+  }
   p.A = A; p.lda = lda; p.B = B; p.ldb = ldb; p.M = M; p.N = N; p.K = K; p.C = C; p.ldc = ldc;
   p.bias = bias; p.aux = aux; p.ldaux = ldaux; p.C2 = C2;
   p.dp = make_dropout(p_drop, seed);

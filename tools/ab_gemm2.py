@@ -8,8 +8,9 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from huggingface_sagemaker_tensorflow_distributed_amd.ops import hip  # noqa: E402
 
 C_ = hip._C
-T = 32768
+T = int(os.environ.get("AB_T", "32768"))
 variants = [int(v) for v in (sys.argv[1] if len(sys.argv) > 1 else "0,1").split(",")]
+AB_VAR = os.environ.get("AB_VAR", "HSD_G2_SYNC")  # environment variable the variants set
 
 
 def timeit(fn, iters=20):
@@ -68,7 +69,7 @@ bad = []
 for k, (fl, fn) in cases.items():
     snaps = []
     for v in variants:
-        os.environ["HSD_G2_SYNC"] = str(v)
+        os.environ[AB_VAR] = str(v)
         for t in list(bufs[k]):
             t.zero_()
         fn()
@@ -84,7 +85,7 @@ res = {k: {v: [] for v in variants} for k in cases}
 for rnd in range(3):
     for k, (fl, fn) in cases.items():
         for v in variants:
-            os.environ["HSD_G2_SYNC"] = str(v)
+            os.environ[AB_VAR] = str(v)
             res[k][v].append(fl / timeit(fn) / 1e12)
 for k in cases:
     print(k, "  ".join(f"v{v}: {max(res[k][v]):7.1f} (med {sorted(res[k][v])[1]:7.1f})" for v in variants), flush=True)
