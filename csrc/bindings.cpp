@@ -292,6 +292,28 @@ void gemm2(torch::Tensor A, torch::Tensor B, torch::Tensor C, int64_t la, int64_
                     C2.has_value() ? BF(*C2) : nullptr, p, (uint64_t)seed, sp, wsp, dbp, cur_stream());
 }
 
+// logits [R, V] (bf16 | fp32), labels int64 [R] (-100 = ignore); stats fp32 [2] += {Σ loss, correct};
+// dlogits (optional, same dtype/shape) = (softmax - onehot) / n_valid
+void xent(torch::Tensor logits, torch::Tensor labels, c10::optional<torch::Tensor> dlogits, torch::Tensor stats,
+          torch::Tensor n_valid) {
+  TORCH_CHECK(logits.is_cuda() && logits.dim() == 2 && logits.is_contiguous(), "xent logits");
+  const bool bf = logits.scalar_type() == torch::kBFloat16;
+  TORCH_CHECK(bf || logits.scalar_type() == torch::kFloat32, "xent logits dtype");
+  TORCH_CHECK(labels.scalar_type() == torch::kInt64 && labels.is_contiguous() && labels.numel() == logits.size(0),
+              "xent labels");
+  check_f32(stats, "stats");
+  check_f32(n_valid, "n_valid");
+  TORCH_CHECK(stats.numel() >= 2 && n_valid.numel() == 1, "xent stats");
+  void* dl = nullptr;
+  if (dlogits.has_value()) {
+    TORCH_CHECK(dlogits->sizes() == logits.sizes() && dlogits->scalar_type() == logits.scalar_type() &&
+                dlogits->is_contiguous(), "xent dlogits");
+    dl = dlogits->data_ptr();
+  }
+  hsd::launch_xent(logits.data_ptr(), bf, labels.data_ptr<int64_t>(), dl, stats.data_ptr<float>(),
+                   n_valid.data_ptr<float>(), (int)logits.size(0), (int)logits.size(1), cur_stream());
+}
+
 void transpose_many(torch::Tensor desc, int64_t total_tiles) {
   TORCH_CHECK(desc.is_cuda() && desc.scalar_type() == torch::kInt64 && desc.dim() == 2 && desc.size(1) == 5 &&
               desc.is_contiguous(), "transpose_many: int64 [n, 5] device descriptor table");
@@ -327,5 +349,6 @@ PYBIND11_MODULE(_C, m) {
   m.def("gemm2_splits", &gemm2_splits);
   m.def("gemm2_supported", &gemm2_supported);
   m.def("transpose_many", &transpose_many);
+  m.def("xent", &xent);
   m.def("gemm_wgrad_variant", &gemm_wgrad_variant);
 }

@@ -37,6 +37,9 @@ void launch_gelu_bwd_colsum(const bf16_t* dg, const bf16_t* y, bf16_t* da, float
                             hipStream_t st);
 void launch_colsum(const bf16_t* x, float* dbias, int rows, int N, hipStream_t st);
 void launch_dropout(const bf16_t* x, bf16_t* out, int64_t n, double p, uint64_t seed, hipStream_t st);
+// xent.hip: fused softmax cross-entropy (+ gradient, + argmax-correct count); stats = {Σloss, correct}
+void launch_xent(const void* logits, bool bf16, const int64_t* labels, void* dlogits, float* stats,
+                 const float* n_valid, int rows, int V, hipStream_t st);
 // desc: int64 [n][5] = {src, dst, rows, cols, first_tile}; rows, cols multiples of 4
 void launch_transpose_many(const int64_t* desc, int n, int total_tiles, hipStream_t st);
 // attention.hip

@@ -107,6 +107,12 @@ def join_side_streams() -> None:
 
 
 def cross_entropy(logits, labels):
+    """Mean CE over non-ignored labels. On the HIP path the fused kernel also counts argmax hits; the count
+    rides on the loss tensor (``loss._hsd_correct``) so metrics need no second pass over the logits."""
+    if _hip(logits):
+        loss, correct = _hipmod().cross_entropy(logits, labels)
+        loss._hsd_correct = correct
+        return loss
     return _ref.cross_entropy(logits, labels)
 
 

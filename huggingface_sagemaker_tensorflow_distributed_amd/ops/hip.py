@@ -111,10 +111,16 @@ def adam_step(p, m, v, g, out, decay, step, eps, b1, b2, gscale, lr_wd):
 
 # ------------------------------------------------------------------------------------------ linear
 class _Linear(torch.autograd.Function):
+    """y = x Wᵀ + b for the task heads (pooler / classifier / MLM dense): gemm2 when the shape tiles,
+    otherwise the library GEMM (e.g. the 2-way classifier)."""
+
     @staticmethod
     def forward(ctx, x, w, b):
-        x2 = x.reshape(-1, x.shape[-1])
-        y = torch.addmm(b, x2, w.t())
+        x2 = x.reshape(-1, x.shape[-1]).contiguous()
+        if x2.dtype == torch.bfloat16 and _nt_ok(x2.shape[0], w.shape[0], x2.shape[1], EPI_BIAS):
+            y = gemm_fwd(x2, w, EPI_BIAS, bias=b)
+        else:
+            y = torch.addmm(b, x2, w.t())
         ctx.save_for_backward(x2, w, b)
         ctx.xshape = x.shape
         return y.view(*x.shape[:-1], w.shape[0])
@@ -123,9 +129,17 @@ class _Linear(torch.autograd.Function):
     def backward(ctx, dy):
         x2, w, b = ctx.saved_tensors
         dy2 = dy.reshape(-1, w.shape[0]).contiguous()
-        dx = torch.mm(dy2, w).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if dy2.dtype == torch.bfloat16 and _nt_ok(dy2.shape[0], w.shape[1], dy2.shape[1], EPI_STORE):
+                dx = gemm_dgrad(dy2, w).view(ctx.xshape)
+            else:
+                dx = torch.mm(dy2, w).view(ctx.xshape)
         gw, gb = _Grad(w), _Grad(b)
-        _wgrad_(gw, dy2, x2)
+        if dy2.dtype == torch.bfloat16 and _C.gemm2_supported(1, 1, 7, w.shape[0], w.shape[1], dy2.shape[0]):
+            gemm_wgrad_(gw, dy2, x2)
+        else:
+            _wgrad_(gw, dy2, x2)
         if dy2.shape[1] % 8 == 0:
             _C.colsum(dy2, gb.buf)
         else:
@@ -521,3 +535,36 @@ class _FFNBlock(torch.autograd.Function):
 
 def ffn_block(h, w1, b1, w2, b2, ln_w, ln_b, eps, p, seed):
     return _FFNBlock.apply(h, w1, b1, w2, b2, ln_w, ln_b, eps, p, seed)
+
+
+# ------------------------------------------------------------------------------------------ loss
+class _CrossEntropy(torch.autograd.Function):
+    """Mean softmax cross-entropy over non-ignored rows (-100) with the gradient produced by the same
+    kernel (xent.hip); also returns the argmax-correct count as a non-differentiable output."""
+
+    @staticmethod
+    def forward(ctx, logits, labels):
+        lg = logits.contiguous()
+        lab = labels.contiguous().long()
+        n_valid = lab.ne(-100).sum().to(torch.float32).reshape(1)
+        stats = torch.zeros(2, dtype=torch.float32, device=lg.device)
+        dl = torch.empty_like(lg) if ctx.needs_input_grad[0] else None
+        _C.xent(lg, lab, dl, stats, n_valid)
+        ctx.save_for_backward(dl if dl is not None else stats)
+        loss = stats[0:1] / n_valid.clamp(min=1.0)
+        ctx.mark_non_differentiable(stats)
+        return loss.reshape(()), stats[1]
+
+    @staticmethod
+    def backward(ctx, dloss, _dcorrect):
+        (dl,) = ctx.saved_tensors
+        return dl * dloss.to(dl.dtype), None
+
+
+def cross_entropy(logits, labels):
+    """(loss, correct_count) for [R, V] logits (bf16 / fp32) and int labels (-100 ignored)."""
+    if logits.dtype not in (torch.bfloat16, torch.float32) or logits.dim() != 2:
+        from .reference import accuracy_count, cross_entropy as ref
+
+        return ref(logits, labels), accuracy_count(logits, labels)
+    return _CrossEntropy.apply(logits, labels)

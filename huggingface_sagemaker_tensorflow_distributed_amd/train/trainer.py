@@ -54,7 +54,10 @@ class _Meter:
 
     def update(self, loss: torch.Tensor, logits: torch.Tensor, labels: torch.Tensor) -> None:
         n = labels.numel() if logits.dim() == 2 else labels.ne(-100).sum()
-        if logits.dim() == 2 and logits.shape[0] == labels.numel():
+        fused = getattr(loss, "_hsd_correct", None)
+        if fused is not None:
+            correct = fused
+        elif logits.dim() == 2 and logits.shape[0] == labels.numel():
             correct = ops.accuracy_count(logits, labels)
         else:
             correct = torch.zeros((), device=logits.device)

@@ -244,3 +244,23 @@ def test_attention128_matches_generic_kernel(gpu, p, monkeypatch):
         outs.append((o.float(), x.grad.float()))
     _close(outs[0][0], outs[1][0], 1e-2, 1e-2, "fwd")
     _close(outs[0][1], outs[1][1], 2e-2, 2e-2, "bwd")
+
+
+@pytest.mark.parametrize("R,V,dtype", [(64, 2, torch.float32), (300, 2, torch.bfloat16), (97, 50265, torch.bfloat16),
+                                       (33, 1003, torch.float32)])
+def test_fused_cross_entropy(gpu, R, V, dtype):
+    """xent.hip: loss, gradient and argmax-correct count vs torch (ignore_index -100)."""
+    hip = _hip()
+    torch.manual_seed(8)
+    logits = (torch.randn(R, V, device=gpu) * 3).to(dtype).requires_grad_()
+    labels = torch.randint(0, V, (R,), device=gpu)
+    labels[::5] = -100
+    loss, correct = hip.cross_entropy(logits, labels)
+    loss.backward()
+    l32 = logits.detach().float().requires_grad_()
+    ref = torch.nn.functional.cross_entropy(l32, labels, ignore_index=-100)
+    ref.backward()
+    assert abs(loss.item() - ref.item()) < 1e-3 * max(1.0, abs(ref.item()))
+    _close(logits.grad, l32.grad, 2e-2 if dtype == torch.bfloat16 else 1e-5, 1e-3, "dlogits")
+    keep = labels.ne(-100)
+    assert int(correct.item()) == int((l32.argmax(-1) == labels)[keep].sum().item())
