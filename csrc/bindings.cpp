@@ -173,8 +173,11 @@ void attn_bwd(torch::Tensor qkv, c10::optional<torch::Tensor> mask, torch::Tenso
   check_f32(lse2, "lse2");
   TORCH_CHECK(qkv.size(-1) == 3 * heads * 64 && dqkv.numel() == qkv.numel(), "attn_bwd shapes");
   TORCH_CHECK(o.numel() == B * S * heads * 64 && dout.numel() == o.numel(), "attn_bwd o shapes");
-  TORCH_CHECK(S <= 128 || dq_acc.has_value(), "S > 128 needs a zeroed fp32 dq accumulator");
-  if (dq_acc.has_value()) { check_f32(*dq_acc, "dq_acc"); TORCH_CHECK(dq_acc->numel() == o.numel(), "dq_acc"); }
+  TORCH_CHECK(S <= 128 || dq_acc.has_value(), "S > 128 needs an fp32 workspace (attn_bwd_ws_numel)");
+  if (dq_acc.has_value()) {
+    check_f32(*dq_acc, "dq_acc");
+    TORCH_CHECK(dq_acc->numel() == (hsd::attn_streaming((int)S) ? B * heads * S : o.numel()), "dq_acc workspace size");
+  }
   if (mask.has_value()) { check_f32(*mask, "mask"); TORCH_CHECK(mask->numel() == B * S, "mask shape"); }
   if (dbias.has_value()) { check_f32(*dbias, "dbias"); TORCH_CHECK(dbias->numel() == 3 * heads * 64, "dbias shape"); }
   hsd::launch_attn_bwd(CBF(qkv), OPT_F(mask), CBF(o), CBF(dout), lse2.data_ptr<float>(), BF(dqkv), OPT_F(dq_acc),
@@ -340,6 +343,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("colsum", &colsum);
   m.def("dropout", &dropout);
   m.def("attn_fwd", &attn_fwd);
+  // backward workspace for S > 128: (numel, must_be_zeroed)
+  m.def("attn_bwd_ws", [](int64_t B, int64_t S, int64_t heads) {
+    if (S <= 128) return std::make_pair<int64_t, bool>(0, false);
+    if (hsd::attn_streaming((int)S)) return std::make_pair<int64_t, bool>(B * heads * S, false);
+    return std::make_pair<int64_t, bool>(B * S * heads * 64, true);
+  });
   m.def("attn_bwd", &attn_bwd, py::arg("qkv"), py::arg("mask"), py::arg("o"), py::arg("dout"), py::arg("lse2"),
         py::arg("dqkv"), py::arg("dq_acc"), py::arg("B"), py::arg("S"), py::arg("heads"), py::arg("p"), py::arg("seed"),
         py::arg("dbias") = py::none());

@@ -374,11 +374,25 @@ void launch_attn128_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float
 void launch_attn128_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
                         bf16_t* dqkv, float* dbias, int B, int heads, double p, uint64_t seed, hipStream_t st);
 void launch_colsum(const bf16_t* x, float* dbias, int rows, int N, hipStream_t st);
+bool attnS_supported(int S, int head_dim);
+void launch_attnS_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse2, int B, int S, int heads,
+                      double p, uint64_t seed, hipStream_t st);
+void launch_attnS_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
+                      bf16_t* dqkv, float* delta_ws, float* dbias, int B, int S, int heads, double p, uint64_t seed,
+                      hipStream_t st);
+
+// S in 256..1024 (multiple of 128) runs the streaming kernels of attentionS.hip; its backward takes
+// an fp32 [B*heads*S] scratch (no zeroing) where the generic kernel takes a zeroed [B*S, H] dq accumulator.
+bool attn_streaming(int S) { return attnS_supported(S, kD) && !getenv("HSD_ATTN_GENERIC"); }
 
 void launch_attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse2, int B, int S, int heads,
                      double p, uint64_t seed, hipStream_t st) {
   if (attn128_supported(S, kD) && !getenv("HSD_ATTN_GENERIC")) {
     launch_attn128_fwd(qkv, mask, out, lse2, B, heads, p, seed, st);
+    return;
+  }
+  if (attn_streaming(S)) {
+    launch_attnS_fwd(qkv, mask, out, lse2, B, S, heads, p, seed, st);
     return;
   }
   DropoutParams dp = make_dropout(p, seed);
@@ -393,6 +407,10 @@ void launch_attn_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, cons
                      hipStream_t st) {
   if (attn128_supported(S, kD) && !getenv("HSD_ATTN_GENERIC")) {
     launch_attn128_bwd(qkv, mask, o, dout, lse2, dqkv, dbias, B, heads, p, seed, st);
+    return;
+  }
+  if (attn_streaming(S)) {
+    launch_attnS_bwd(qkv, mask, o, dout, lse2, dqkv, dq_acc, dbias, B, S, heads, p, seed, st);
     return;
   }
   DropoutParams dp = make_dropout(p, seed);

@@ -1,0 +1,416 @@
+// Flash attention for S = 256 .. 1024 (multiple of 128), head_dim 64 — the long-sequence configs of
+// SURVEY.md §2.10 (bert-large / roberta-large at max_seq_length 512; K4-K7 forward, K14 backward).
+// S == 128 keeps the single-workgroup kernels of attention128.hip.
+//
+// All three kernels use one workgroup = 4 waves = 128 rows of one (batch, head), the wave's 32 rows on
+// the MFMA lanes (v_mfma_f32_32x32x16_bf16), and stream the other operand pair through LDS in 64-row
+// tiles: global_load_lds DMA into a double-buffered [64][64] swizzled image (attn_common.h), one
+// barrier per tile, the DMA of tile t+1 in flight while tile t is multiplied.
+//
+// * forward (queries on lanes, K/V streamed): online softmax in the log2 domain; Oᵀ += Vᵀ·Pᵀ with the
+//   Sᵀ accumulator as the B operand; O staged to 128-B row stores; lse2 saved for the backward.
+// * backward dK/dV (keys on lanes, Q/dO streamed): P recomputed from lse2, dVᵀ += dOᵀ·P̃, dKᵀ += Qᵀ·dS,
+//   k/v bias gradients as column sums of the stored rows.
+// * backward dQ (queries on lanes, K/V streamed): Sᵀ and dPᵀ recomputed, dQᵀ += Kᵀ·dSᵀ, q bias gradient.
+//   Splitting dQ into its own pass (instead of fp32 atomics across key blocks) keeps every output
+//   written exactly once and deterministic, at the price of recomputing S and dP (7 instead of 5
+//   GEMM-equivalents) — the MFMA work is cheap next to the atomics traffic it replaces.
+// * delta[q] = Σ_d dO·O is a separate bandwidth kernel (every key block needs all of it).
+// Dropout / mask / lse conventions are identical to attention.hip / attention128.hip.
+#include "attn_common.h"
+
+namespace hsd {
+namespace aS {
+
+using namespace attn;
+constexpr int kMaxS = 1024;
+constexpr int TILE = 64 * D;  // one [64][64] bf16 image
+
+// 64 rows x 64 cols starting at src0 into a [64][64] image: 8 DMA instructions, 2 per wave
+__device__ __forceinline__ void dma_tile(bf16_t* img, const bf16_t* __restrict__ src0, int64_t ld, int wave, int lane) {
+  dma_img(img, src0, ld, wave * 2, 2, lane);
+}
+
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 2) void attnS_fwd_kernel(const bf16_t* __restrict__ qkv,
+                                                           const float* __restrict__ mask, bf16_t* __restrict__ out,
+                                                           float* __restrict__ lse2, int S, int heads, float sl2,
+                                                           DropoutParams dp) {
+  // [K0 K1 | V0 V1 | mask bias]; after the loop K0|K1 is the output staging
+  __shared__ __attribute__((aligned(16))) bf16_t lds[4 * TILE + 2 * kMaxS];
+  bf16_t* Kb = lds;
+  bf16_t* Vb = lds + 2 * TILE;
+  float* mb_s = reinterpret_cast<float*>(lds + 4 * TILE);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, hf = lane >> 5;
+  const int bh = blockIdx.y, b = bh / heads, hh = bh % heads;
+  const int H = heads * D, ld = 3 * H;
+  const bf16_t* base = qkv + (int64_t)b * S * ld + hh * D;
+  const int q0 = blockIdx.x * 128 + wave * 32;
+  const int q = q0 + r;
+
+  dma_tile(Kb, base + H, ld, wave, lane);
+  dma_tile(Vb, base + 2 * H, ld, wave, lane);
+  bf16x8 qf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(base + (int64_t)q * ld + 16 * s + 8 * hf);
+  for (int k = tid; k < S; k += 256) mb_s[k] = mask ? fmaxf(mask[(int64_t)b * S + k] * kLog2e, -1e30f) : 0.f;
+
+  f32x16 o0 = {}, o1 = {};
+  float m = -INFINITY, l = 0.f;
+  const uint32_t rowbase = (uint32_t)(((int64_t)bh * S + q) * S);
+  const int nt = S / 64;
+#pragma unroll 1
+  for (int kt = 0; kt < nt; ++kt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const bf16_t* Ks = Kb + (kt & 1) * TILE;
+    const bf16_t* Vs = Vb + (kt & 1) * TILE;
+    if (kt + 1 < nt) {
+      const int64_t off = (int64_t)(kt + 1) * 64 * ld;
+      dma_tile(Kb + ((kt + 1) & 1) * TILE, base + off + H, ld, wave, lane);
+      dma_tile(Vb + ((kt + 1) & 1) * TILE, base + off + 2 * H, ld, wave, lane);
+    }
+    // Sᵀ[key][q] for the tile's 2 key blocks of 32
+    f32x16 st[2];
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      st[kb] = f32x16{};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 a = *reinterpret_cast<const bf16x8*>(Ks + toff(kb * 32 + r, 16 * s + 8 * hf));
+        st[kb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, qf[s], st[kb], 0, 0, 0);
+      }
+    }
+    float mx = m;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const f32x4 mb = *reinterpret_cast<const f32x4*>(mb_s + kt * 64 + kb * 32 + 8 * g4 + 4 * hf);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float x = fmaf(st[kb][4 * g4 + e], sl2, mb[e]);
+          st[kb][4 * g4 + e] = x;
+          mx = fmaxf(mx, x);
+        }
+      }
+    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    const float alpha = __builtin_amdgcn_exp2f(m - mx);
+    m = mx;
+    float ls = 0.f;
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int reg = 0; reg < 16; ++reg) {
+        const float p = __builtin_amdgcn_exp2f(st[kb][reg] - mx);
+        ls += p;
+        st[kb][reg] = p;
+      }
+    l = fmaf(l, alpha, ls);
+#pragma unroll
+    for (int reg = 0; reg < 16; ++reg) {
+      o0[reg] *= alpha;
+      o1[reg] *= alpha;
+    }
+    if (dp.enabled) {
+#pragma unroll
+      for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+        for (int reg = 0; reg < 16; reg += 2) {
+          const int key = kt * 64 + kb * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * hf;
+          const uint32_t bits = dropout_bits((rowbase + key) >> 1, dp.seed_lo, dp.seed_hi);
+          st[kb][reg] *= keep_factor(bits, 0, dp);
+          st[kb][reg + 1] *= keep_factor(bits, 1, dp);
+        }
+    }
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb)
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pb = pack8(st[kb], s);
+        o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(Vs, kb * 32, s, 0, lane), pb, o0, 0, 0, 0);
+        o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(Vs, kb * 32, s, 1, lane), pb, o1, 0, 0, 0);
+      }
+  }
+  l += __shfl_xor(l, 32, 64);
+  if (hf == 0) lse2[(int64_t)bh * S + q] = m + __log2f(l);
+  __syncthreads();  // K images no longer read: reuse as staging
+  store_rows(Kb + wave * 32 * D, o0, o1, 1.0f / l, out + ((int64_t)b * S + q0) * H + hh * D, H, lane);
+}
+
+// ------------------------------------------------------------------------------------------------
+// delta[bh*S + s] = Σ_d dO[b*S+s][h*64+d] · O[b*S+s][h*64+d]; 8 threads per (token, head)
+__global__ __launch_bounds__(256) void attnS_delta_kernel(const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout,
+                                                          float* __restrict__ delta, int T, int S, int heads) {
+  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
+  const int64_t item = g >> 3;
+  const int c = (int)(g & 7);
+  const bool ok = item < (int64_t)T * heads;
+  const int64_t it = ok ? item : 0;
+  const int64_t t = it / heads;
+  const int hh = (int)(it % heads);
+  const int64_t off = t * heads * D + hh * D + c * 8;
+  const u32x4 ov = *reinterpret_cast<const u32x4*>(o + off);
+  const u32x4 dv = *reinterpret_cast<const u32x4*>(dout + off);
+  float acc = 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) acc += lo_bf(dv[k]) * lo_bf(ov[k]) + hi_bf(dv[k]) * hi_bf(ov[k]);
+  acc += __shfl_xor(acc, 1, 64);
+  acc += __shfl_xor(acc, 2, 64);
+  acc += __shfl_xor(acc, 4, 64);
+  if (ok && c == 0) {
+    const int64_t bb = t / S, s = t % S;
+    delta[(bb * heads + hh) * S + s] = acc;
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 2) void attnS_bwd_kv_kernel(const bf16_t* __restrict__ qkv,
+                                                              const float* __restrict__ mask,
+                                                              const bf16_t* __restrict__ dout,
+                                                              const float* __restrict__ lse2,
+                                                              const float* __restrict__ delta,
+                                                              bf16_t* __restrict__ dqkv, float* __restrict__ dbias,
+                                                              int S, int heads, float sl2, float scale,
+                                                              DropoutParams dp) {
+  // [Q0 Q1 | dO0 dO1 | lse | delta | k/v bias partials]; after the loop Q0|Q1 is the output staging
+  __shared__ __attribute__((aligned(16))) bf16_t lds[4 * TILE + 4 * kMaxS + 2 * 2 * 4 * D];
+  bf16_t* Qb = lds;
+  bf16_t* dOb = lds + 2 * TILE;
+  float* lse_s = reinterpret_cast<float*>(lds + 4 * TILE);
+  float* del_s = lse_s + kMaxS;
+  float* bsum = del_s + kMaxS;  // [2 (k,v)][4 waves][64]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, hf = lane >> 5;
+  const int bh = blockIdx.y, b = bh / heads, hh = bh % heads;
+  const int H = heads * D, ld = 3 * H;
+  const bf16_t* base = qkv + (int64_t)b * S * ld + hh * D;
+  const bf16_t* dobase = dout + (int64_t)b * S * H + hh * D;
+  const int k0 = blockIdx.x * 128 + wave * 32;
+  const int key = k0 + r;
+
+  dma_tile(Qb, base, ld, wave, lane);
+  dma_tile(dOb, dobase, H, wave, lane);
+  bf16x8 kf[4], vf[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    kf[s] = *reinterpret_cast<const bf16x8*>(base + (int64_t)key * ld + H + 16 * s + 8 * hf);
+    vf[s] = *reinterpret_cast<const bf16x8*>(base + (int64_t)key * ld + 2 * H + 16 * s + 8 * hf);
+  }
+  const float kb2 = mask ? fmaxf(mask[(int64_t)b * S + key] * kLog2e, -1e30f) : 0.f;
+  for (int i = tid; i < S; i += 256) {
+    lse_s[i] = lse2[(int64_t)bh * S + i];
+    del_s[i] = delta[(int64_t)bh * S + i];
+  }
+
+  f32x16 dk0 = {}, dk1 = {}, dv0 = {}, dv1 = {};
+  const bool odd = (lane & 1) != 0;
+  const int nt = S / 64;
+#pragma unroll 1
+  for (int qt = 0; qt < nt; ++qt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const bf16_t* Qs = Qb + (qt & 1) * TILE;
+    const bf16_t* dOs = dOb + (qt & 1) * TILE;
+    if (qt + 1 < nt) {
+      dma_tile(Qb + ((qt + 1) & 1) * TILE, base + (int64_t)(qt + 1) * 64 * ld, ld, wave, lane);
+      dma_tile(dOb + ((qt + 1) & 1) * TILE, dobase + (int64_t)(qt + 1) * 64 * H, H, wave, lane);
+    }
+#pragma unroll
+    for (int qs = 0; qs < 2; ++qs) {
+      f32x16 sacc = {}, dpacc = {};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 aq = *reinterpret_cast<const bf16x8*>(Qs + toff(qs * 32 + r, 16 * s + 8 * hf));
+        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aq, kf[s], sacc, 0, 0, 0);
+        const bf16x8 ad = *reinterpret_cast<const bf16x8*>(dOs + toff(qs * 32 + r, 16 * s + 8 * hf));
+        dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ad, vf[s], dpacc, 0, 0, 0);
+      }
+      // rows: query qi = (reg&3) + 8(reg>>2) + 4hf of the sub-block; col (lane): key
+      f32x16 pd, ds;
+#pragma unroll
+      for (int reg = 0; reg < 16; reg += 2) {
+        const int qi0 = qt * 64 + qs * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * hf;  // rows qi0, qi0 + 1
+        const f32x2 lse = *reinterpret_cast<const f32x2*>(lse_s + qi0);
+        const f32x2 del = *reinterpret_cast<const f32x2*>(del_s + qi0);
+        const float p0 = __builtin_amdgcn_exp2f(fmaf(sacc[reg], sl2, kb2) - lse[0]);
+        const float p1 = __builtin_amdgcn_exp2f(fmaf(sacc[reg + 1], sl2, kb2) - lse[1]);
+        float f0 = 1.f, f1 = 1.f;
+        if (dp.enabled) {
+          // keys 2j, 2j+1 (lanes l, l^1) share one hash per query row: the even lane hashes row qi0,
+          // the odd lane row qi0 + 1, then they swap
+          const int qmine = odd ? qi0 + 1 : qi0;
+          const uint32_t e = (uint32_t)(((int64_t)bh * S + qmine) * S + key);
+          const uint32_t bits = dropout_bits(e >> 1, dp.seed_lo, dp.seed_hi);
+          const uint32_t other = (uint32_t)__shfl_xor((int)bits, 1, 64);
+          f0 = keep_factor(odd ? other : bits, key & 1, dp);
+          f1 = keep_factor(odd ? bits : other, key & 1, dp);
+        }
+        pd[reg] = p0 * f0;
+        pd[reg + 1] = p1 * f1;
+        ds[reg] = p0 * fmaf(dpacc[reg], f0, -del[0]);
+        ds[reg + 1] = p1 * fmaf(dpacc[reg + 1], f1, -del[1]);
+      }
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 pb = pack8(pd, s);
+        const bf16x8 sb = pack8(ds, s);
+        dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(dOs, qs * 32, s, 0, lane), pb, dv0, 0, 0, 0);
+        dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(dOs, qs * 32, s, 1, lane), pb, dv1, 0, 0, 0);
+        dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(Qs, qs * 32, s, 0, lane), sb, dk0, 0, 0, 0);
+        dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(Qs, qs * 32, s, 1, lane), sb, dk1, 0, 0, 0);
+      }
+    }
+  }
+  __syncthreads();  // Q images no longer read: reuse as staging
+  bf16_t* stg = Qb + wave * 32 * D;
+  bf16_t* rowbase = dqkv + ((int64_t)b * S + k0) * ld + hh * D;
+  store_rows(stg, dv0, dv1, 1.0f, rowbase + 2 * H, ld, lane, dbias ? bsum + (4 + wave) * D : nullptr);
+  store_rows(stg, dk0, dk1, scale, rowbase + H, ld, lane, dbias ? bsum + wave * D : nullptr);
+  if (dbias) {
+    __syncthreads();
+    if (tid < 2 * D) {
+      const int which = tid / D, c = tid % D;
+      const float* p = bsum + which * 4 * D + c;
+      atomicAdd(dbias + (1 + which) * H + hh * D + c, p[0] + p[D] + p[2 * D] + p[3 * D]);
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------------
+__global__ __launch_bounds__(256, 2) void attnS_bwd_q_kernel(const bf16_t* __restrict__ qkv,
+                                                             const float* __restrict__ mask,
+                                                             const bf16_t* __restrict__ dout,
+                                                             const float* __restrict__ lse2,
+                                                             const float* __restrict__ delta,
+                                                             bf16_t* __restrict__ dqkv, float* __restrict__ dbias,
+                                                             int S, int heads, float sl2, float scale,
+                                                             DropoutParams dp) {
+  // [K0 K1 | V0 V1 | mask bias | q bias partials]; after the loop K0|K1 is the output staging
+  __shared__ __attribute__((aligned(16))) bf16_t lds[4 * TILE + 2 * kMaxS + 2 * 4 * D];
+  bf16_t* Kb = lds;
+  bf16_t* Vb = lds + 2 * TILE;
+  float* mb_s = reinterpret_cast<float*>(lds + 4 * TILE);
+  float* bsum = mb_s + kMaxS;  // [4 waves][64]
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 31, hf = lane >> 5;
+  const int bh = blockIdx.y, b = bh / heads, hh = bh % heads;
+  const int H = heads * D, ld = 3 * H;
+  const bf16_t* base = qkv + (int64_t)b * S * ld + hh * D;
+  const int q0 = blockIdx.x * 128 + wave * 32;
+  const int q = q0 + r;
+
+  dma_tile(Kb, base + H, ld, wave, lane);
+  dma_tile(Vb, base + 2 * H, ld, wave, lane);
+  bf16x8 qf[4], df[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    qf[s] = *reinterpret_cast<const bf16x8*>(base + (int64_t)q * ld + 16 * s + 8 * hf);
+    df[s] = *reinterpret_cast<const bf16x8*>(dout + ((int64_t)b * S + q) * H + hh * D + 16 * s + 8 * hf);
+  }
+  const float lse_q = lse2[(int64_t)bh * S + q];
+  const float del_q = delta[(int64_t)bh * S + q];
+  for (int k = tid; k < S; k += 256) mb_s[k] = mask ? fmaxf(mask[(int64_t)b * S + k] * kLog2e, -1e30f) : 0.f;
+
+  f32x16 dq0 = {}, dq1 = {};
+  const uint32_t rowbase = (uint32_t)(((int64_t)bh * S + q) * S);
+  const int nt = S / 64;
+#pragma unroll 1
+  for (int kt = 0; kt < nt; ++kt) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    const bf16_t* Ks = Kb + (kt & 1) * TILE;
+    const bf16_t* Vs = Vb + (kt & 1) * TILE;
+    if (kt + 1 < nt) {
+      const int64_t off = (int64_t)(kt + 1) * 64 * ld;
+      dma_tile(Kb + ((kt + 1) & 1) * TILE, base + off + H, ld, wave, lane);
+      dma_tile(Vb + ((kt + 1) & 1) * TILE, base + off + 2 * H, ld, wave, lane);
+    }
+#pragma unroll
+    for (int kb = 0; kb < 2; ++kb) {
+      // Sᵀ[key][q] = K·Qᵀ, dPᵀ[key][q] = V·dOᵀ (query on the lane, key in the registers)
+      f32x16 sacc = {}, dpacc = {};
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const bf16x8 ak = *reinterpret_cast<const bf16x8*>(Ks + toff(kb * 32 + r, 16 * s + 8 * hf));
+        sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ak, qf[s], sacc, 0, 0, 0);
+        const bf16x8 av = *reinterpret_cast<const bf16x8*>(Vs + toff(kb * 32 + r, 16 * s + 8 * hf));
+        dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, df[s], dpacc, 0, 0, 0);
+      }
+      f32x16 ds;
+#pragma unroll
+      for (int g4 = 0; g4 < 4; ++g4) {
+        const int kk = kt * 64 + kb * 32 + 8 * g4 + 4 * hf;  // keys kk .. kk+3 in regs 4g4 .. 4g4+3
+        const f32x4 mb = *reinterpret_cast<const f32x4*>(mb_s + kk);
+#pragma unroll
+        for (int e = 0; e < 4; e += 2) {
+          const int reg = 4 * g4 + e;
+          const float p0 = __builtin_amdgcn_exp2f(fmaf(sacc[reg], sl2, mb[e]) - lse_q);
+          const float p1 = __builtin_amdgcn_exp2f(fmaf(sacc[reg + 1], sl2, mb[e + 1]) - lse_q);
+          float f0 = 1.f, f1 = 1.f;
+          if (dp.enabled) {
+            const uint32_t bits = dropout_bits((rowbase + kk + e) >> 1, dp.seed_lo, dp.seed_hi);
+            f0 = keep_factor(bits, 0, dp);
+            f1 = keep_factor(bits, 1, dp);
+          }
+          ds[reg] = p0 * fmaf(dpacc[reg], f0, -del_q);
+          ds[reg + 1] = p1 * fmaf(dpacc[reg + 1], f1, -del_q);
+        }
+      }
+      // dQᵀ[d][q] += Σ_key Kᵀ[d][key] dSᵀ[key][q]
+#pragma unroll
+      for (int s = 0; s < 2; ++s) {
+        const bf16x8 sb = pack8(ds, s);
+        dq0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(Ks, kb * 32, s, 0, lane), sb, dq0, 0, 0, 0);
+        dq1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(Ks, kb * 32, s, 1, lane), sb, dq1, 0, 0, 0);
+      }
+    }
+  }
+  __syncthreads();  // K images no longer read: reuse as staging
+  store_rows(Kb + wave * 32 * D, dq0, dq1, scale, dqkv + ((int64_t)b * S + q0) * ld + hh * D, ld, lane,
+             dbias ? bsum + wave * D : nullptr);
+  if (dbias) {
+    __syncthreads();
+    if (tid < D) atomicAdd(dbias + hh * D + tid, bsum[tid] + bsum[D + tid] + bsum[2 * D + tid] + bsum[3 * D + tid]);
+  }
+}
+
+}  // namespace aS
+
+bool attnS_supported(int S, int head_dim) {
+  return head_dim == attn::D && S % 128 == 0 && S >= 256 && S <= aS::kMaxS;
+}
+
+void launch_attnS_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse2, int B, int S, int heads,
+                      double p, uint64_t seed, hipStream_t st) {
+  DropoutParams dp = make_dropout(p, seed);
+  const float sl2 = attn::kLog2e / sqrtf((float)attn::D);
+  hipLaunchKernelGGL(aS::attnS_fwd_kernel, dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, out, lse2, S, heads,
+                     sl2, dp);
+  HSD_CHECK_LAUNCH();
+}
+
+// delta_ws: fp32 [B*heads*S] scratch
+void launch_attnS_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
+                      bf16_t* dqkv, float* delta_ws, float* dbias, int B, int S, int heads, double p, uint64_t seed,
+                      hipStream_t st) {
+  DropoutParams dp = make_dropout(p, seed);
+  const float sl2 = attn::kLog2e / sqrtf((float)attn::D);
+  const float scale = 1.0f / sqrtf((float)attn::D);
+  const int64_t threads = (int64_t)B * S * heads * 8;
+  hipLaunchKernelGGL(aS::attnS_delta_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, o, dout,
+                     delta_ws, B * S, S, heads);
+  HSD_CHECK_LAUNCH();
+  hipLaunchKernelGGL(aS::attnS_bwd_kv_kernel, dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, dout, lse2,
+                     delta_ws, dqkv, dbias, S, heads, sl2, scale, dp);
+  HSD_CHECK_LAUNCH();
+  hipLaunchKernelGGL(aS::attnS_bwd_q_kernel, dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, dout, lse2,
+                     delta_ws, dqkv, dbias, S, heads, sl2, scale, dp);
+  HSD_CHECK_LAUNCH();
+}
+
+}  // namespace hsd

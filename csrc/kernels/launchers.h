@@ -43,6 +43,7 @@ void launch_xent(const void* logits, bool bf16, const int64_t* labels, void* dlo
 // desc: int64 [n][5] = {src, dst, rows, cols, first_tile}; rows, cols multiples of 4
 void launch_transpose_many(const int64_t* desc, int n, int total_tiles, hipStream_t st);
 // attention.hip
+bool attn_streaming(int S);
 void launch_attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse2, int B, int S, int heads,
                      double p, uint64_t seed, hipStream_t st);
 // dbias (optional): fp32 [3H] += column sums of dqkv (the fused QKV bias gradient)

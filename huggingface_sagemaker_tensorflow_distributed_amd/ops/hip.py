@@ -324,12 +324,19 @@ class _Attention(torch.autograd.Function):
     def backward(ctx, dout):
         qkv, out, lse, mb = ctx.saved_tensors
         dqkv = torch.empty_like(qkv)
-        dq_acc = None
-        if ctx.S > 128:
-            dq_acc = torch.zeros(out.shape, dtype=torch.float32, device=out.device)
+        dq_acc = _attn_ws(ctx.B, ctx.S, ctx.heads, out.device)
         _C.attn_bwd(qkv, mb if ctx.has_mask else None, out, dout.contiguous(), lse, dqkv, dq_acc, ctx.B, ctx.S,
                     ctx.heads, ctx.p, _s64(ctx.seed))
         return dqkv, None, None, None, None, None, None
+
+
+def _attn_ws(B, S, heads, device):
+    """fp32 scratch of the attention backward for S > 128 (delta rows of the streaming kernels, or the
+    zeroed dQ accumulator of the generic one)."""
+    n, zero = _C.attn_bwd_ws(B, S, heads)
+    if n == 0:
+        return None
+    return (torch.zeros if zero else torch.empty)(n, dtype=torch.float32, device=device)
 
 
 def attention(qkv, mask_bias, batch, seq, heads, p, seed):
@@ -472,7 +479,7 @@ class _AttnBlock(torch.autograd.Function):
         r_ow = wgrad_done(g_ow, dy, actx)
         dctx = gemm_dgrad(dy, out_w)
         dqkv = torch.empty_like(qkv)
-        dq_acc = torch.zeros(actx.shape, dtype=torch.float32, device=actx.device) if S > 128 else None
+        dq_acc = _attn_ws(B, S, heads, actx.device)
         g_qw, g_qb = _Grad(qkv_w), _Grad(qkv_b)
         # the QKV bias gradient (column sums of dqkv) comes out of the attention backward itself
         _C.attn_bwd(qkv, mb if has_mask else None, actx, dctx, lse, dqkv, dq_acc, B, S, heads, p_a, _s64(seed_a),

@@ -128,7 +128,7 @@ def test_embed_ln(gpu, p, type_vocab):
     _close(be.grad, be32.grad, 2e-1, 5e-2, "dbeta")
 
 
-@pytest.mark.parametrize("S", [32, 128, 256])
+@pytest.mark.parametrize("S", [32, 128, 256, 384, 512])
 @pytest.mark.parametrize("p", [0.0, 0.1])
 @pytest.mark.parametrize("masked", [False, True])
 def test_attention(gpu, S, p, masked):
@@ -174,14 +174,15 @@ def test_adam_kernel_matches_reference(gpu):
     torch.testing.assert_close(out.float(), pr.bfloat16().float())
 
 
+@pytest.mark.parametrize("S", [128, 256])
 @pytest.mark.parametrize("p", [0.0, 0.1])
-def test_fused_blocks_vs_reference(gpu, p):
-    """attn_block / ffn_block (GEMM epilogues + fused backward) vs composed fp32 reference ops."""
-    from huggingface_sagemaker_tensorflow_distributed_amd import ops
-
+def test_fused_blocks_vs_reference(gpu, p, S):
+    """attn_block / ffn_block (GEMM epilogues + fused backward) vs composed fp32 reference ops.
+    S = 128 runs attention128.hip, S = 256 the streaming kernels of attentionS.hip (incl. the fused
+    qkv bias gradient of both)."""
     hip = _hip()
     torch.manual_seed(5)
-    B, S, heads, H, I = 4, 128, 4, 256, 512
+    B, heads, H, I = 4, 4, 256, 512
     T = B * S
     mk = lambda *s, sc=0.05: (torch.randn(*s, device=gpu) * sc).bfloat16().requires_grad_()  # noqa: E731
     h = torch.randn(T, H, device=gpu).bfloat16().requires_grad_()
@@ -222,12 +223,14 @@ def test_fused_blocks_vs_reference(gpu, p):
         assert rel < 4e-2, f"{n}: rel err {rel:.3g}"
 
 
+@pytest.mark.parametrize("S", [128, 256, 512])
 @pytest.mark.parametrize("p", [0.0, 0.1])
-def test_attention128_matches_generic_kernel(gpu, p, monkeypatch):
-    """The S == 128 one-workgroup-per-head kernels (attention128.hip) vs the tiled generic kernels."""
+def test_attention_fast_paths_match_generic_kernel(gpu, p, S, monkeypatch):
+    """The S == 128 one-workgroup-per-head kernels (attention128.hip) and the S > 128 streaming kernels
+    (attentionS.hip) vs the tiled generic kernels (same dropout masks, so tight tolerances)."""
     hip = _hip()
     torch.manual_seed(7)
-    B, S, heads = 3, 128, 12
+    B, heads = 3, 12
     H = heads * 64
     qkv = torch.randn(B * S, 3 * H, device=gpu, dtype=torch.bfloat16)
     am = torch.ones(B, S, dtype=torch.long, device=gpu)
