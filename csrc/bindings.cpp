@@ -102,6 +102,15 @@ void embed_fwd(torch::Tensor ids, torch::Tensor pos_ids, c10::optional<torch::Te
   const int rows = (int)ids.numel();
   TORCH_CHECK(H % 4 == 0 && H <= 1024 && out.numel() == (int64_t)rows * H, "embed shapes");
   TORCH_CHECK(type.has_value() == type_ids.has_value(), "type table and ids go together");
+#ifdef HSD_DEBUG
+  // the kernels index the tables with these ids unchecked
+  auto in_range = [](const torch::Tensor& t, int64_t n) {
+    return t.numel() == 0 || (t.min().item<int64_t>() >= 0 && t.max().item<int64_t>() < n);
+  };
+  TORCH_CHECK(in_range(ids, word.size(0)), "HSD_DEBUG: input id out of vocabulary range");
+  TORCH_CHECK(in_range(pos_ids, pos.size(0)), "HSD_DEBUG: position id out of range");
+  if (type_ids.has_value()) TORCH_CHECK(in_range(*type_ids, type->size(0)), "HSD_DEBUG: token type id out of range");
+#endif
   hsd::launch_embed_fwd(ids.data_ptr<int64_t>(), pos_ids.data_ptr<int64_t>(), OPT_I64(type_ids), CBF(word),
                         CBF(pos), type.has_value() ? CBF(*type) : nullptr, CBF(gamma), CBF(beta), BF(out),
                         mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, H, (float)eps, p, (uint64_t)seed,
@@ -330,7 +339,7 @@ bool gemm2_supported(int64_t la, int64_t lb, int64_t epi, int64_t M, int64_t N, 
 
 }  // namespace
 
-PYBIND11_MODULE(_C, m) {
+PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 HIP kernels for huggingface_sagemaker_tensorflow_distributed_amd";
   hsd::register_comm(m);
   m.def("adam_step", &adam_step);

@@ -49,6 +49,7 @@ __global__ __launch_bounds__(256, 2) void attnS_fwd_kernel(const bf16_t* __restr
   const bf16_t* base = qkv + (int64_t)b * S * ld + hh * D;
   const int q0 = blockIdx.x * 128 + wave * 32;
   const int q = q0 + r;
+  HSD_DASSERT(S % 64 == 0 && S <= kMaxS && q < S);
 
   dma_tile(Kb, base + H, ld, wave, lane);
   dma_tile(Vb, base + 2 * H, ld, wave, lane);
@@ -191,6 +192,7 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_kv_kernel(const bf16_t* __re
   const bf16_t* dobase = dout + (int64_t)b * S * H + hh * D;
   const int k0 = blockIdx.x * 128 + wave * 32;
   const int key = k0 + r;
+  HSD_DASSERT(S % 64 == 0 && S <= kMaxS && key < S);
 
   dma_tile(Qb, base, ld, wave, lane);
   dma_tile(dOb, dobase, H, wave, lane);
@@ -303,6 +305,7 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_q_kernel(const bf16_t* __res
   const bf16_t* base = qkv + (int64_t)b * S * ld + hh * D;
   const int q0 = blockIdx.x * 128 + wave * 32;
   const int q = q0 + r;
+  HSD_DASSERT(S % 64 == 0 && S <= kMaxS && q < S);
 
   dma_tile(Kb, base + H, ld, wave, lane);
   dma_tile(Vb, base + 2 * H, ld, wave, lane);

@@ -130,6 +130,28 @@ __device__ __forceinline__ void gelu_and_grad(float x, float& g, float& dg) {
 
 }  // namespace hsd
 
+// Debug build (HSD_DEBUG=1 python -m ..._build, loaded as _C_debug when HSD_DEBUG=1 at run time;
+// SURVEY.md §5 'bounds-check debug builds'): every launch is followed by a device synchronisation so a
+// fault is reported at the kernel that caused it, and HSD_DASSERT device checks are compiled in.
+#ifdef HSD_DEBUG
+#define HSD_CHECK_LAUNCH()                                                                    \
+  do {                                                                                        \
+    hipError_t e__ = hipGetLastError();                                                       \
+    if (e__ == hipSuccess) e__ = hipDeviceSynchronize();                                      \
+    if (e__ != hipSuccess) {                                                                  \
+      fprintf(stderr, "HIP error %s after launch at %s:%d\n", hipGetErrorString(e__), __FILE__, __LINE__); \
+      abort();                                                                                \
+    }                                                                                         \
+  } while (0)
+#define HSD_DASSERT(c)                                                                        \
+  do {                                                                                        \
+    if (!(c)) {                                                                               \
+      printf("HSD_DASSERT(%s) failed at %s:%d block (%d,%d) thread %d\n", #c, __FILE__, __LINE__, \
+             (int)blockIdx.x, (int)blockIdx.y, (int)threadIdx.x);                             \
+      __builtin_trap();                                                                       \
+    }                                                                                         \
+  } while (0)
+#else
 #define HSD_CHECK_LAUNCH()                                                                    \
   do {                                                                                        \
     hipError_t e__ = hipGetLastError();                                                       \
@@ -138,3 +160,7 @@ __device__ __forceinline__ void gelu_and_grad(float x, float& g, float& dg) {
       abort();                                                                                \
     }                                                                                         \
   } while (0)
+#define HSD_DASSERT(c) \
+  do {                 \
+  } while (0)
+#endif

@@ -243,6 +243,7 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
   const int kbeg = split * p.kps;
   const int kend = min(p.K, kbeg + p.kps);
   const int nt = (kend - kbeg) / BK;
+  HSD_DASSERT(v < nwg && m0 < p.M && n0 < p.N && kbeg < p.K && (kend - kbeg) % BK == 0);
 
   auto dma_slot = [&](int q, bf16_t* stage, int k0) {
     if (q < GA) dma<LA, BM>(stage, p.A, p.lda, m0, p.M, k0, wave * GA + q, lane);
