@@ -38,13 +38,17 @@ def main():
     ap.add_argument("--model", default="bert-base-uncased")
     ap.add_argument("--bucket_mb", type=float, default=None)
     ap.add_argument("--grad_dtype", default=None)
+    ap.add_argument("--dtype", choices=["bf16", "fp8"], default="bf16",
+                    help="fp8: fp8 forward/dgrad GEMMs (secondary config; the headline is bf16)")
+    ap.add_argument("--task", choices=["sequence-classification", "masked-lm"], default="sequence-classification")
     a = ap.parse_args()
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     if a.gpus != world_env:
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world_env}; using WORLD_SIZE", file=sys.stderr)
     targs, _ = build_parser("train").parse_known_args(
-        ["--model_name_or_path", a.model, "--train_batch_size", str(a.batch_size), "--dtype", "bf16",
+        ["--model_name_or_path", a.model, "--train_batch_size", str(a.batch_size), "--dtype", a.dtype,
+         "--task", a.task,
          "--learning_rate", "5e-5", "--log_every", "0"]
         + (["--bucket_mb", str(a.bucket_mb)] if a.bucket_mb else [])
         + (["--grad_dtype", a.grad_dtype] if a.grad_dtype else []))
@@ -52,8 +56,11 @@ def main():
     trainer, dev, world, rank = parts["trainer"], parts["device"], parts["world"], parts["rank"]
     cfg = parts["model"].cfg
     n_batches = 4
-    ds = hdata.synthetic_classification(a.batch_size * n_batches, a.seq_len, cfg.vocab_size,
-                                        seed=1234 + rank, full_length=True)
+    if a.task == "masked-lm":
+        ds = hdata.synthetic_mlm(a.batch_size * n_batches, a.seq_len, cfg.vocab_size, seed=1234 + rank)
+    else:
+        ds = hdata.synthetic_classification(a.batch_size * n_batches, a.seq_len, cfg.vocab_size,
+                                            seed=1234 + rank, full_length=True)
     batches = []
     for i in range(n_batches):
         sl = slice(i * a.batch_size, (i + 1) * a.batch_size)
@@ -85,8 +92,9 @@ def main():
             "metric": METRIC, "value": round(value, 2), "unit": "sequences/sec", "n_gpus": world,
             "steps": a.steps, "warmup": a.warmup, "ms_per_step": round(ms, 4), "higher_is_better": True,
             "scaling": "weak", "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
-            "dtype": "bf16", "data": "synthetic (random-init weights, full-length seq, dropout on)",
-            "config": {"model": a.model, "global_batch": a.batch_size * world, "per_gpu_batch": a.batch_size,
+            "dtype": a.dtype, "data": "synthetic (random-init weights, full-length seq, dropout on)",
+            "config": {"model": a.model, "task": a.task, "global_batch": a.batch_size * world,
+                       "per_gpu_batch": a.batch_size,
                        "seq_len": a.seq_len, "parallelism": f"dp{world}",
                        "ops": "torch-reference" if os.environ.get("HSD_OPS") == "torch" else "hip",
                        "comm": ("native-rccl" if getattr(trainer.bucketer, "engine", None) is not None

@@ -250,6 +250,74 @@ void gemm_wgrad_variant(torch::Tensor dy, torch::Tensor x, torch::Tensor C, int6
 
 // gemm2: la=lb=0 -> NT (A [M,K], B [N,K]) bf16 C with epilogue 0..5;
 //        la=lb=1 -> TT (A [K,M], B [K,N]) fp32 C += A^T B, epi 6 atomics / 7 slabs in ws.
+// fp8 per-tensor quantisation: q = sat(x · FMT_MAX / amax), sinv = amax / FMT_MAX (device scalars)
+void fp8_quant(torch::Tensor x, torch::Tensor amax, torch::Tensor q, torch::Tensor sinv, int64_t fmt,
+               bool compute_amax) {
+  check_bf16(x, "x");
+  check_f32(amax, "amax"); check_f32(sinv, "sinv");
+  TORCH_CHECK(q.is_cuda() && q.scalar_type() == torch::kUInt8 && q.is_contiguous() && q.numel() == x.numel(),
+              "fp8_quant q: contiguous uint8 of x's size");
+  TORCH_CHECK(fmt == 0 || fmt == 1, "fmt: 0 = e4m3, 1 = e5m2");
+  TORCH_CHECK(amax.numel() >= 1 && sinv.numel() >= 1, "fp8_quant scalars");
+  hsd::launch_fp8_quant(CBF(x), x.numel(), amax.data_ptr<float>(), q.data_ptr<uint8_t>(), sinv.data_ptr<float>(),
+                        (int)fmt, compute_amax, cur_stream());
+}
+
+void fp8_quant_many(torch::Tensor amax_desc, int64_t amax_blocks, torch::Tensor quant_desc, int64_t quant_blocks,
+                    torch::Tensor amax, torch::Tensor sinv, int64_t fmt) {
+  TORCH_CHECK(amax_desc.is_cuda() && amax_desc.scalar_type() == torch::kInt64 && amax_desc.dim() == 2 &&
+              amax_desc.size(1) == 5 && amax_desc.is_contiguous(), "amax_desc int64 [n][5]");
+  TORCH_CHECK(quant_desc.is_cuda() && quant_desc.scalar_type() == torch::kInt64 && quant_desc.dim() == 2 &&
+              quant_desc.size(1) == 5 && quant_desc.is_contiguous(), "quant_desc int64 [n][5]");
+  check_f32(amax, "amax"); check_f32(sinv, "sinv");
+  TORCH_CHECK(fmt == 0 || fmt == 1, "fmt");
+  hsd::launch_fp8_quant_many(amax_desc.data_ptr<int64_t>(), (int)amax_desc.size(0), (int)amax_blocks,
+                             quant_desc.data_ptr<int64_t>(), (int)quant_desc.size(0), (int)quant_blocks,
+                             amax.data_ptr<float>(), sinv.data_ptr<float>(), (int)fmt, cur_stream());
+}
+
+// C = epilogue(sa·sb · A8 · B8ᵀ): A8 [M][K], B8 [N][K] uint8 (fp8 bits), same epilogue codes as gemm2 (bf16 out)
+void gemm8(torch::Tensor A, int64_t fa, torch::Tensor sa, torch::Tensor B, int64_t fb, torch::Tensor sb,
+           torch::Tensor C, int64_t epi, c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> aux,
+           c10::optional<torch::Tensor> C2, double p, int64_t seed, c10::optional<torch::Tensor> dbias) {
+  TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda(), "gemm8 operands must be GPU tensors");
+  TORCH_CHECK(A.scalar_type() == torch::kUInt8 && B.scalar_type() == torch::kUInt8, "gemm8 inputs: uint8 fp8 bits");
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "gemm8 operands must be 2-D");
+  TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && C.stride(1) == 1, "gemm8 unit inner stride");
+  const int64_t M = A.size(0), K = A.size(1), N = B.size(0);
+  TORCH_CHECK(B.size(1) == K, "gemm8 K mismatch");
+  TORCH_CHECK(C.size(0) == M && C.size(1) == N && C.scalar_type() == torch::kBFloat16, "gemm8 C");
+  TORCH_CHECK(hsd::gemm8_supported((int)epi, (int)M, (int)N, (int)K), "gemm8: unsupported shape/epilogue");
+  TORCH_CHECK(A.stride(0) % 16 == 0 && B.stride(0) % 16 == 0 && C.stride(0) % 8 == 0, "gemm8 leading dims alignment");
+  TORCH_CHECK(fa == 0 || fa == 1, "gemm8 fa");
+  TORCH_CHECK(fb == 0, "gemm8: weights (B) are e4m3");
+  check_f32(sa, "sa"); check_f32(sb, "sb");
+  if (epi == 1 || epi == 2 || epi == 3 || epi == 8) {
+    TORCH_CHECK(bias.has_value() && bias->numel() == N && bias->scalar_type() == torch::kBFloat16 &&
+                bias->is_contiguous(), "gemm8 bias");
+  }
+  if (epi == 3 || epi == 4 || epi == 5 || epi == 9) {
+    TORCH_CHECK(aux.has_value() && aux->dim() == 2 && aux->size(0) == M && aux->size(1) == N &&
+                aux->stride(1) == 1 && aux->stride(0) % 8 == 0 && aux->scalar_type() == torch::kBFloat16, "gemm8 aux");
+  }
+  if (epi == 2 || epi == 8) {
+    TORCH_CHECK(C2.has_value() && C2->sizes() == C.sizes() && C2->strides() == C.strides() &&
+                C2->scalar_type() == torch::kBFloat16, "gemm8 C2");
+  }
+  float* dbp = nullptr;
+  if (dbias.has_value()) {
+    TORCH_CHECK((epi == 5 || epi == 9) && N % 256 == 0, "gemm8 fused dbias: DGELU / MUL epilogue with N % 256 == 0");
+    check_f32(*dbias, "dbias");
+    TORCH_CHECK(dbias->numel() == N, "dbias size");
+    dbp = dbias->data_ptr<float>();
+  }
+  hsd::launch_gemm8((int)epi, A.data_ptr<uint8_t>(), A.stride(0), (int)fa, sa.data_ptr<float>(), B.data_ptr<uint8_t>(),
+                    B.stride(0), (int)fb, sb.data_ptr<float>(), (int)M, (int)N, (int)K, BF(C), C.stride(0),
+                    bias.has_value() ? CBF(*bias) : nullptr, aux.has_value() ? CBF(*aux) : nullptr,
+                    aux.has_value() ? aux->stride(0) : 0, C2.has_value() ? BF(*C2) : nullptr, p, (uint64_t)seed, dbp,
+                    cur_stream());
+}
+
 void gemm2(torch::Tensor A, torch::Tensor B, torch::Tensor C, int64_t la, int64_t lb, int64_t epi,
            c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> aux, c10::optional<torch::Tensor> C2,
            double p, int64_t seed, int64_t splits, c10::optional<torch::Tensor> ws,
@@ -351,6 +419,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gelu_bwd_colsum", &gelu_bwd_colsum);
   m.def("colsum", &colsum);
   m.def("dropout", &dropout);
+  m.def("fp8_quant", &fp8_quant);
+  m.def("fp8_quant_many", &fp8_quant_many);
+  m.def("fp8_elems_per_block", &hsd::fp8_elems_per_block);
+  m.def("gemm8", &gemm8, py::arg("A"), py::arg("fa"), py::arg("sa"), py::arg("B"), py::arg("fb"), py::arg("sb"),
+        py::arg("C"), py::arg("epi"), py::arg("bias") = py::none(), py::arg("aux") = py::none(),
+        py::arg("C2") = py::none(), py::arg("p") = 0.0, py::arg("seed") = 0, py::arg("dbias") = py::none());
+  m.def("gemm8_supported", &hsd::gemm8_supported);
   m.def("attn_fwd", &attn_fwd);
   // backward workspace for S > 128: (numel, must_be_zeroed)
   m.def("attn_bwd_ws", [](int64_t B, int64_t S, int64_t heads) {

@@ -1,0 +1,218 @@
+// Shared pieces of the MFMA GEMMs (gemm2.hip bf16, gemm8.hip fp8): epilogue kinds, launch parameters,
+// the barrier / counted-wait helpers and the bf16-output epilogue (wave-private LDS staging, 16-B row
+// stores, fused bias / GELU / dropout+residual / derivative products / bias-gradient column sums).
+#pragma once
+#include "common.h"
+
+namespace hsd {
+
+// E2_BIAS_GELU_D: C = gelu'(y), C2 = gelu(y) (y = acc + bias) — the FFN1 forward keeps the GELU DERIVATIVE
+// for backward, so the FFN2 dgrad epilogue is a plain product (E2_MUL: C = bf16(acc) * aux) instead of
+// re-evaluating erf/exp per element.
+enum Epi2 : int { E2_STORE = 0, E2_BIAS = 1, E2_BIAS_GELU = 2, E2_BIAS_DROP_RES = 3, E2_RES = 4, E2_DGELU = 5,
+                  E2_F32_ATOMIC = 6, E2_F32_SLAB = 7, E2_BIAS_GELU_D = 8, E2_MUL = 9 };
+
+__host__ __device__ constexpr bool epi_bias(int e) { return e == E2_BIAS || e == E2_BIAS_GELU || e == E2_BIAS_DROP_RES || e == E2_BIAS_GELU_D; }
+__host__ __device__ constexpr bool epi_aux(int e) { return e == E2_BIAS_DROP_RES || e == E2_RES || e == E2_DGELU || e == E2_MUL; }
+__host__ __device__ constexpr bool epi_two_out(int e) { return e == E2_BIAS_GELU || e == E2_BIAS_GELU_D; }
+__host__ __device__ constexpr bool epi_bf16_out(int e) { return e <= E2_DGELU || e == E2_BIAS_GELU_D || e == E2_MUL; }
+
+struct G2Params {
+  const bf16_t* A;
+  int64_t lda;
+  const bf16_t* B;
+  int64_t ldb;
+  int M, N, K;
+  void* C;  // bf16 [M][ldc], or fp32 (atomic: [M][ldc]; slab: [splits][M][N])
+  int64_t ldc;
+  const bf16_t* bias;
+  const bf16_t* aux;
+  int64_t ldaux;
+  bf16_t* C2;
+  DropoutParams dp;
+  int kps;  // K elements per split (multiple of 64)
+  int tiles_n;
+  int ntiles;    // tiles_m * tiles_n
+  float* dbias;  // E2_DGELU: optional fp32 column sums of the output (the bias gradient), BN 256 only
+  int nt_store;  // non-temporal (streaming) epilogue stores
+};
+
+__device__ __forceinline__ void st16(bf16_t* dst, const u32x4& v, int nt) {
+  if (nt) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst));
+  else *reinterpret_cast<u32x4*>(dst) = v;
+}
+
+namespace g2 {
+
+constexpr int BM = 256;
+
+__device__ __forceinline__ int f1(int row) { return (row >> 1) & 7; }
+
+#define G2_BARRIER()                       \
+  do {                                     \
+    asm volatile("" ::: "memory");         \
+    __builtin_amdgcn_sched_barrier(0);     \
+    __builtin_amdgcn_s_barrier();          \
+    __builtin_amdgcn_sched_barrier(0);     \
+    asm volatile("" ::: "memory");         \
+  } while (0)
+
+template <int N>
+__device__ __forceinline__ void vmcnt() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+__device__ __forceinline__ u32x2 pack4(const f32x4& v) {
+  u32x2 o;
+  o.x = pack_bf2(v[0], v[1]);
+  o.y = pack_bf2(v[2], v[3]);
+  return o;
+}
+
+
+// Epilogue math for one 16-B chunk (8 consecutive n of row m) of the staged bf16(acc [+ bias]) tile `o`;
+// `x` is the aux chunk. Returns the primary output in `o` and (two-output epilogues) the second in `o2`.
+template <int EPI>
+__device__ __forceinline__ void epi_chunk(u32x4& o, u32x4& o2, const u32x4& x, int m, int n, const G2Params& p,
+                                          float (&csum)[8]) {
+  if constexpr (EPI == E2_BIAS_GELU) {
+    o2.x = pack_bf2(gelu_erf(lo_bf(o.x)), gelu_erf(hi_bf(o.x)));
+    o2.y = pack_bf2(gelu_erf(lo_bf(o.y)), gelu_erf(hi_bf(o.y)));
+    o2.z = pack_bf2(gelu_erf(lo_bf(o.z)), gelu_erf(hi_bf(o.z)));
+    o2.w = pack_bf2(gelu_erf(lo_bf(o.w)), gelu_erf(hi_bf(o.w)));
+  } else if constexpr (EPI == E2_BIAS_GELU_D) {
+    float v[8] = {lo_bf(o.x), hi_bf(o.x), lo_bf(o.y), hi_bf(o.y), lo_bf(o.z), hi_bf(o.z), lo_bf(o.w), hi_bf(o.w)};
+    float a[8], d[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) gelu_and_grad(v[e], a[e], d[e]);
+    o.x = pack_bf2(d[0], d[1]); o.y = pack_bf2(d[2], d[3]); o.z = pack_bf2(d[4], d[5]); o.w = pack_bf2(d[6], d[7]);
+    o2.x = pack_bf2(a[0], a[1]); o2.y = pack_bf2(a[2], a[3]); o2.z = pack_bf2(a[4], a[5]); o2.w = pack_bf2(a[6], a[7]);
+  } else if constexpr (EPI == E2_BIAS_DROP_RES) {
+    // z = bf16(bf16(y · keep · scale) + residual)
+    float v[8] = {lo_bf(o.x), hi_bf(o.x), lo_bf(o.y), hi_bf(o.y), lo_bf(o.z), hi_bf(o.z), lo_bf(o.w), hi_bf(o.w)};
+    if (p.dp.enabled) {
+      const uint32_t pair0 = (uint32_t)(((int64_t)m * p.N + n) >> 1);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const uint32_t b = dropout_bits(pair0 + e, p.dp.seed_lo, p.dp.seed_hi);
+        v[2 * e] = bf2f(f2bf(v[2 * e] * keep_factor(b, 0, p.dp)));
+        v[2 * e + 1] = bf2f(f2bf(v[2 * e + 1] * keep_factor(b, 1, p.dp)));
+      }
+    }
+    o.x = pack_bf2(v[0] + lo_bf(x.x), v[1] + hi_bf(x.x));
+    o.y = pack_bf2(v[2] + lo_bf(x.y), v[3] + hi_bf(x.y));
+    o.z = pack_bf2(v[4] + lo_bf(x.z), v[5] + hi_bf(x.z));
+    o.w = pack_bf2(v[6] + lo_bf(x.w), v[7] + hi_bf(x.w));
+  } else if constexpr (EPI == E2_RES) {
+    o.x = pack_bf2(lo_bf(o.x) + lo_bf(x.x), hi_bf(o.x) + hi_bf(x.x));
+    o.y = pack_bf2(lo_bf(o.y) + lo_bf(x.y), hi_bf(o.y) + hi_bf(x.y));
+    o.z = pack_bf2(lo_bf(o.z) + lo_bf(x.z), hi_bf(o.z) + hi_bf(x.z));
+    o.w = pack_bf2(lo_bf(o.w) + lo_bf(x.w), hi_bf(o.w) + hi_bf(x.w));
+  } else if constexpr (EPI == E2_DGELU || EPI == E2_MUL) {
+    if constexpr (EPI == E2_DGELU) {
+      o.x = pack_bf2(lo_bf(o.x) * gelu_erf_grad(lo_bf(x.x)), hi_bf(o.x) * gelu_erf_grad(hi_bf(x.x)));
+      o.y = pack_bf2(lo_bf(o.y) * gelu_erf_grad(lo_bf(x.y)), hi_bf(o.y) * gelu_erf_grad(hi_bf(x.y)));
+      o.z = pack_bf2(lo_bf(o.z) * gelu_erf_grad(lo_bf(x.z)), hi_bf(o.z) * gelu_erf_grad(hi_bf(x.z)));
+      o.w = pack_bf2(lo_bf(o.w) * gelu_erf_grad(lo_bf(x.w)), hi_bf(o.w) * gelu_erf_grad(hi_bf(x.w)));
+    } else {
+      o.x = pack_bf2(lo_bf(o.x) * lo_bf(x.x), hi_bf(o.x) * hi_bf(x.x));
+      o.y = pack_bf2(lo_bf(o.y) * lo_bf(x.y), hi_bf(o.y) * hi_bf(x.y));
+      o.z = pack_bf2(lo_bf(o.z) * lo_bf(x.z), hi_bf(o.z) * hi_bf(x.z));
+      o.w = pack_bf2(lo_bf(o.w) * lo_bf(x.w), hi_bf(o.w) * hi_bf(x.w));
+    }
+    csum[0] += lo_bf(o.x); csum[1] += hi_bf(o.x); csum[2] += lo_bf(o.y); csum[3] += hi_bf(o.y);
+    csum[4] += lo_bf(o.z); csum[5] += hi_bf(o.z); csum[6] += lo_bf(o.w); csum[7] += hi_bf(o.w);
+  }
+}
+
+// column sums of 8 columns per lane, lanes with equal (lane & 7) hold the same columns: reduce + atomics
+__device__ __forceinline__ void colsum_flush(float (&csum)[8], float* dbias, int nw, int N, int lane) {
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float v = csum[e];
+    v += __shfl_xor(v, 8, 64);
+    v += __shfl_xor(v, 16, 64);
+    v += __shfl_xor(v, 32, 64);
+    csum[e] = v;
+  }
+  if (lane < 8 && nw + lane * 8 < N) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) atomicAdd(dbias + nw + lane * 8 + e, csum[e]);
+  }
+#pragma unroll
+  for (int e = 0; e < 8; ++e) csum[e] = 0.f;
+}
+
+// bf16-output epilogue of a 256 x BN tile held as acc[8][BN/64] (acc[i][j] = D[n][m] block: lane l holds
+// m = 16i + (l&15), n = 16j + 4(l>>4) + r), staged through the wave's [64][BN/4 + 8] slice of `smem`.
+template <int EPI, int BN>
+__device__ __forceinline__ void epilogue_bf16(f32x4 (&acc)[8][BN / 64], const G2Params& p, bf16_t* smem, int wave,
+                                              int lane, int mw, int nw) {
+  constexpr int WN = BN / 4, NREP = WN / 16;
+  const int q4 = lane >> 4, lr = lane & 15;
+  // stage bf16(acc [+ bias]) through a wave-private LDS slice ([64 rows][WN + 8]), then write whole
+  // rows with 16-B lanes: each lane owns 8 consecutive n of one m.
+  constexpr int SROW = WN + 8;
+  constexpr int CPR = WN / 8;  // 16-B chunks per row
+  constexpr bool kBias = epi_bias(EPI);
+  constexpr bool kAux = epi_aux(EPI);
+  bf16_t* stg = smem + wave * (64 * SROW);
+  f32x4 bv[NREP];
+  if constexpr (kBias) {
+#pragma unroll
+    for (int j = 0; j < NREP; ++j) {
+      const int n = min(nw + 16 * j + 4 * q4, p.N - 4);
+      const u32x2 b = *reinterpret_cast<const u32x2*>(p.bias + n);
+      bv[j] = f32x4{lo_bf(b.x), hi_bf(b.x), lo_bf(b.y), hi_bf(b.y)};
+    }
+  }
+  bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
+  constexpr bool kColsum = (EPI == E2_DGELU || EPI == E2_MUL) && CPR == 8;
+  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NREP; ++j) {
+        f32x4 v = acc[4 * h + i][j];
+        if constexpr (kBias) v += bv[j];
+        *reinterpret_cast<u32x2*>(stg + (16 * i + lr) * SROW + 16 * j + 4 * q4) = pack4(v);
+      }
+    __builtin_amdgcn_wave_barrier();
+    constexpr int ITER = 64 * CPR / 64;
+    u32x4 sv[ITER], xv[ITER];
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int idx = lane + 64 * it;
+      const int row = idx / CPR, c8 = idx % CPR;
+      sv[it] = *reinterpret_cast<const u32x4*>(stg + row * SROW + c8 * 8);
+      if constexpr (kAux) {
+        const int m = min(mw + 64 * h + row, p.M - 1);
+        xv[it] = *reinterpret_cast<const u32x4*>(p.aux + (int64_t)m * p.ldaux + nw + c8 * 8);
+      } else {
+        xv[it] = u32x4{0, 0, 0, 0};
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int idx = lane + 64 * it;
+      const int row = idx / CPR, c8 = idx % CPR;
+      const int m = mw + 64 * h + row;
+      const int n = nw + c8 * 8;
+      if (m >= p.M) continue;
+      const int64_t co = (int64_t)m * p.ldc + n;
+      u32x4 o = sv[it], o2;
+      epi_chunk<EPI>(o, o2, xv[it], m, n, p, csum);
+      st16(C + co, o, p.nt_store);
+      if constexpr (epi_two_out(EPI)) st16(p.C2 + co, o2, p.nt_store);
+    }
+    __builtin_amdgcn_wave_barrier();
+  }
+  if constexpr (kColsum) {
+    if (p.dbias != nullptr) colsum_flush(csum, p.dbias, nw, p.N, lane);
+  }
+}
+
+}  // namespace g2
+}  // namespace hsd

@@ -61,6 +61,17 @@ void launch_gemm_variant(int la, int lb, int variant, const bf16_t* A, int64_t l
                          int M, int N, int K, bf16_t* C, int64_t ldc, hipStream_t st);
 // gemm2.hip — 256-row-tile 8-phase MFMA GEMM: (0,0) NT bf16 out with epilogues 0..5; (1,1) TT fp32 out
 // (epi 6 = atomics, 7 = split-K slabs in `ws` [splits][M][N] + reduce into C)
+// fp8 (gemm8.hip / fp8.hip)
+bool gemm8_supported(int epi, int M, int N, int K);
+void launch_gemm8(int epi, const uint8_t* A, int64_t lda, int fa, const float* sa, const uint8_t* B, int64_t ldb,
+                  int fb, const float* sb, int M, int N, int K, bf16_t* C, int64_t ldc, const bf16_t* bias,
+                  const bf16_t* aux, int64_t ldaux, bf16_t* C2, double p_drop, uint64_t seed, float* dbias,
+                  hipStream_t st);
+void launch_fp8_quant(const bf16_t* x, int64_t n, float* amax, uint8_t* q, float* sinv, int fmt, bool compute_amax,
+                      hipStream_t st);
+void launch_fp8_quant_many(const int64_t* amax_desc, int n_amax, int amax_blocks, const int64_t* quant_desc,
+                           int n_quant, int quant_blocks_total, float* amax, float* sinv, int fmt, hipStream_t st);
+int fp8_elems_per_block();
 void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, int M, int N,
                   int K, void* C, int64_t ldc, const bf16_t* bias, const bf16_t* aux, int64_t ldaux, bf16_t* C2,
                   double p_drop, uint64_t seed, int splits, float* ws, float* dbias, hipStream_t st);

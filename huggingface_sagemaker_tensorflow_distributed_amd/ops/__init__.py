@@ -100,6 +100,17 @@ def attention(qkv, mask_bias, batch, seq, heads, p, seed):
     return _ref.attention(qkv, mask_bias, batch, seq, heads, p, seed, p > 0)
 
 
+def hip_active(device) -> bool:
+    """True when tensors on ``device`` run the HIP kernels (not the reference ops)."""
+    return torch.device(device).type == "cuda" and not _FORCE_TORCH
+
+
+def set_fp8(on: bool, grad_fmt: str = "e4m3") -> None:
+    """Route the encoder's forward / dgrad GEMMs through the fp8 kernel (weights need fp8 copies:
+    ``FlatParamStore(..., fp8=True)``)."""
+    _hipmod().set_fp8(on, grad_fmt)
+
+
 def join_side_streams() -> None:
     """Order the current stream after the wgrad side stream (no-op on CPU / reference ops)."""
     if torch.cuda.is_available() and not _FORCE_TORCH:

@@ -387,9 +387,48 @@ def _nt_ok(M, N, K, epi):
     return _C.gemm2_supported(0, 0, epi, M, N, K)
 
 
+# ---- fp8 GEMM path (gemm8.hip / fp8.hip) -------------------------------------------
+# With fp8 on, the forward and dgrad GEMMs of every weight the FlatParamStore keeps an fp8 copy of (the
+# encoder's qkv / attn_out / ffn1 / ffn2) run on the fp8 MFMA kernel: the activation (forward) or the
+# incoming gradient (dgrad) is quantised per tensor on the device, the weight copies are re-quantised
+# once per optimizer step. Weight gradients stay bf16 x bf16 -> fp32 (gemm2 TT), as do the task heads.
+FP8_E4M3, FP8_E5M2 = 0, 1
+_FP8 = {"on": False, "grad_fmt": FP8_E4M3}
+
+
+def set_fp8(on: bool, grad_fmt: str = "e4m3") -> None:
+    _FP8["on"] = bool(on)
+    _FP8["grad_fmt"] = FP8_E5M2 if grad_fmt == "e5m2" else FP8_E4M3
+
+
+def fp8_enabled() -> bool:
+    return _FP8["on"]
+
+
+def quant_fp8(x: torch.Tensor, fmt: int = FP8_E4M3):
+    """(q uint8 [same shape], sinv fp32 [1]) with q = sat(x · FMT_MAX / amax(x)), sinv = amax / FMT_MAX."""
+    x = x.contiguous()
+    q = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
+    sc = torch.zeros(2, dtype=torch.float32, device=x.device)  # [amax, sinv]
+    _C.fp8_quant(x, sc[0:1], q, sc[1:2], fmt, True)
+    return q, sc[1:2]
+
+
+def _fp8_w(w, attr):
+    if not _FP8["on"]:
+        return None
+    return getattr(w, attr, None)
+
+
 def gemm_fwd(x, w, epi, bias=None, aux=None, out2=None, p=0.0, seed=0):
-    """y[T, N] = x[T, K] · w[N, K]ᵀ with epilogue (gemm2 8-phase kernel; 128-tile kernel for odd shapes)."""
+    """y[T, N] = x[T, K] · w[N, K]ᵀ with epilogue (gemm2 8-phase kernel; 128-tile kernel for odd shapes;
+    gemm8 fp8 kernel when fp8 is on and the weight has an fp8 copy)."""
     y = torch.empty((x.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)
+    wq = _fp8_w(w, "_hsd_q")
+    if wq is not None and _C.gemm8_supported(epi, x.shape[0], w.shape[0], x.shape[1]):
+        qx, sx = quant_fp8(x)
+        _C.gemm8(qx, FP8_E4M3, sx, wq, FP8_E4M3, w._hsd_qs, y, epi, bias, aux, out2, float(p), _s64(seed), None)
+        return y
     if _nt_ok(x.shape[0], w.shape[0], x.shape[1], epi):
         _C.gemm2(x, w, y, 0, 0, epi, bias, aux, out2, float(p), _s64(seed), 1, None, None)
     else:
@@ -403,6 +442,15 @@ def gemm_dgrad(dy, w, epi=EPI_STORE, aux=None, dbias=None):
     ``dbias`` (DGELU only): fp32 [K] buffer that receives the column sums of dx (the bias gradient of
     the layer that produced ``aux``) from the epilogue; returns ``(dx, fused)``-style via attribute."""
     dx = torch.empty((dy.shape[0], w.shape[1]), dtype=dy.dtype, device=dy.device)
+    wqt = _fp8_w(w, "_hsd_qt")
+    if wqt is not None and _C.gemm8_supported(epi, dy.shape[0], w.shape[1], dy.shape[1]):
+        fuse = dbias is not None and epi in (EPI_DGELU, EPI_MUL) and w.shape[1] % 256 == 0
+        fmt = _FP8["grad_fmt"]
+        qdy, sdy = quant_fp8(dy, fmt)
+        _C.gemm8(qdy, fmt, sdy, wqt, FP8_E4M3, w._hsd_qs, dx, epi, None, aux, None, 0.0, 0, dbias if fuse else None)
+        if dbias is not None and not fuse:
+            _C.colsum(dx, dbias)
+        return dx
     if _nt_ok(dy.shape[0], w.shape[1], dy.shape[1], epi):
         wt = getattr(w, "_hsd_wt", None)  # FlatParamStore keeps Wᵀ fresh (one batched transpose per step)
         if wt is None or wt.shape[0] != w.shape[1] or wt.shape[1] != w.shape[0]:

@@ -46,8 +46,9 @@ def _no_decay(name: str) -> bool:
 
 class FlatParamStore:
     def __init__(self, model: nn.Module, device: torch.device, compute_dtype: torch.dtype = torch.float32,
-                 grad_dtype: torch.dtype = torch.float32):
+                 grad_dtype: torch.dtype = torch.float32, fp8: bool = False):
         self.device = torch.device(device)
+        self.fp8 = fp8
         self.compute_dtype = compute_dtype
         self.grad_dtype = grad_dtype
         named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
@@ -107,6 +108,7 @@ class FlatParamStore:
         after every optimizer step instead of a transpose per GEMM per step."""
         self.transposed = None
         self._tdesc = None
+        self._fp8_desc = None
         if self.device.type != "cuda" or self.compute_dtype != torch.bfloat16:
             return
         idx = [i for i, n in enumerate(self.names) if TRANSPOSED_WEIGHTS.search(n) and len(self.segments[i].shape) == 2
@@ -126,7 +128,51 @@ class FlatParamStore:
             off += rows * cols
         self._tdesc = torch.tensor(desc, dtype=torch.int64, device=self.device)
         self._ttiles = tiles
+        self._fp8_desc = None
+        if self.fp8:
+            self._setup_fp8(idx)
         self.refresh_transposed()
+
+    def _setup_fp8(self, idx) -> None:
+        """fp8 (e4m3) copies of every encoder weight W and of its stored transpose Wᵀ, with one per-tensor
+        scale shared by both: the forward GEMM reads W8, the dgrad GEMM W8ᵀ. All
+        of them are re-quantised by two batched launches (amax, quantise) after every optimizer step."""
+        from ..ops import hip
+
+        per_block = hip._C.fp8_elems_per_block()
+        total = sum(self.segments[i].numel for i in idx)
+        self.fp8_w = torch.empty(total, dtype=torch.uint8, device=self.device)
+        self.fp8_wt = torch.empty(total, dtype=torch.uint8, device=self.device)
+        self.fp8_amax = torch.zeros(len(idx), dtype=torch.float32, device=self.device)
+        self.fp8_sinv = torch.ones(len(idx), dtype=torch.float32, device=self.device)
+        amax_rows, quant_rows, ab, qb, off = [], [], 0, 0, 0
+        for t, i in enumerate(idx):
+            rows, cols = self.segments[i].shape
+            n = rows * cols
+            p = self.params[i]
+            q = self.fp8_w[off:off + n].view(rows, cols)
+            qt = self.fp8_wt[off:off + n].view(cols, rows)
+            p._hsd_q, p._hsd_qt, p._hsd_qs = q, qt, self.fp8_sinv[t:t + 1]
+            nb = (n + per_block - 1) // per_block
+            amax_rows.append([p.data.data_ptr(), 0, n, t, ab])
+            ab += nb
+            quant_rows.append([p.data.data_ptr(), q.data_ptr(), n, t, qb])
+            qb += nb
+            quant_rows.append([p._hsd_wt.data_ptr(), qt.data_ptr(), n, t, qb])
+            qb += nb
+            off += n
+        self._fp8_desc = (torch.tensor(amax_rows, dtype=torch.int64, device=self.device), ab,
+                          torch.tensor(quant_rows, dtype=torch.int64, device=self.device), qb)
+
+    @torch.no_grad()
+    def refresh_fp8(self) -> None:
+        if self._fp8_desc is None:
+            return
+        from ..ops import hip
+
+        ad, ab, qd, qb = self._fp8_desc
+        self.fp8_amax.zero_()
+        hip._C.fp8_quant_many(ad, ab, qd, qb, self.fp8_amax, self.fp8_sinv, 0)
 
     @torch.no_grad()
     def refresh_transposed(self) -> None:
@@ -135,6 +181,7 @@ class FlatParamStore:
         from ..ops import hip
 
         hip._C.transpose_many(self._tdesc, self._ttiles)
+        self.refresh_fp8()
 
     def index_of(self, p: torch.Tensor) -> int:
         return self._index[id(p)]

@@ -21,6 +21,7 @@ from typing import List, Optional, Sequence
 import torch
 
 from .. import data as hdata
+from .. import ops
 from ..models import from_pretrained, save_pretrained
 from ..optim import FusedAdam
 from ..parallel import FlatParamStore, GradBucketer, ShardSampler, backend, broadcast_parameters
@@ -39,6 +40,12 @@ _DTYPES = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp8": torch.bfloat16}
 def _datasets(args, cfg, tokenizer, max_len: int):
     n_train = args.num_train_examples
     n_eval = args.num_eval_examples
+    if getattr(args, "task", "sequence-classification") == "masked-lm":
+        if args.dataset != "synthetic":
+            raise ValueError("--task masked-lm trains on --dataset synthetic (no text corpus offline)")
+        tr = hdata.synthetic_mlm(n_train or 2048, max_len, cfg.vocab_size, seed=args.seed)
+        te = hdata.synthetic_mlm(n_eval or 512, max_len, cfg.vocab_size, seed=args.seed + 1)
+        return tr, te
     if args.dataset == "synthetic":
         tr = hdata.synthetic_classification(n_train or 2048, max_len, cfg.vocab_size, seed=args.seed,
                                             num_labels=cfg.num_labels)
@@ -67,12 +74,20 @@ def build(args, mode: str):
     grad_dtype = {"fp32": torch.float32, "bf16": torch.bfloat16}[args.grad_dtype or "fp32"]
     torch.manual_seed(args.seed)
 
-    model = from_pretrained(args.model_name_or_path or "bert-base-uncased", num_labels=args.num_labels,
+    task = getattr(args, "task", "sequence-classification")
+    model = from_pretrained(args.model_name_or_path or "bert-base-uncased", task=task, num_labels=args.num_labels,
                             seed=args.seed)
     model.to(dev)
     model.rng.base_seed = args.seed
     model.rng.rank = rank
-    store = FlatParamStore(model, dev, compute_dtype=compute_dtype, grad_dtype=grad_dtype)
+    # --dtype fp8: bf16 activations / master-weight copies plus fp8 (e4m3) weight copies and per-tensor
+    # quantised fp8 forward + dgrad GEMMs on the HIP path (ops/hip.py set_fp8); CPU runs stay bf16.
+    fp8 = dtype_name == "fp8" and on_gpu and ops.hip_active(dev)
+    if dtype_name == "fp8" and not fp8:
+        logger.warning("--dtype fp8 needs the HIP path on a GPU; computing in bf16")
+    if fp8:
+        ops.set_fp8(True, getattr(args, "fp8_grad_format", "e4m3"))
+    store = FlatParamStore(model, dev, compute_dtype=compute_dtype, grad_dtype=grad_dtype, fp8=fp8)
     base_lr = float(args.learning_rate)
     lr = base_lr * world if mode == "train" else base_lr  # scripts/train.py:112 vs singe_node_train.py:78
     opt = FusedAdam(store, lr=lr, eps=args.adam_epsilon, eps_mode=args.adam_eps_mode,

@@ -53,7 +53,8 @@ class _Meter:
         self.t = torch.zeros(3, dtype=torch.float64, device=device)
 
     def update(self, loss: torch.Tensor, logits: torch.Tensor, labels: torch.Tensor) -> None:
-        n = labels.numel() if logits.dim() == 2 else labels.ne(-100).sum()
+        # classification: one label per logits row; MLM: logits only for the non-ignored (masked) tokens
+        n = labels.numel() if (logits.dim() == 2 and logits.shape[0] == labels.numel()) else labels.ne(-100).sum()
         fused = getattr(loss, "_hsd_correct", None)
         if fused is not None:
             correct = fused

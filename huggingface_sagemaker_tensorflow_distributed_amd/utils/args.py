@@ -81,6 +81,10 @@ def _add_framework_flags(p: argparse.ArgumentParser) -> None:
     g.add_argument("--log_every", type=int, default=50)
     g.add_argument("--device", type=str, default=None, help="cuda | cpu (default: cuda if available)")
     g.add_argument("--num_labels", type=int, default=2)
+    g.add_argument("--task", choices=["sequence-classification", "masked-lm"], default="sequence-classification",
+                   help="masked-lm: RoBERTa MLM pretraining (BASELINE.json config 5)")
+    g.add_argument("--fp8_grad_format", choices=["e4m3", "e5m2"], default="e4m3",
+                   help="--dtype fp8: format of the quantised gradients in the dgrad GEMMs")
 
 
 def build_parser(script: str = "train") -> argparse.ArgumentParser:

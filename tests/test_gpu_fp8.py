@@ -1,0 +1,137 @@
+"""fp8 path (csrc/kernels/fp8.hip, gemm8.hip) vs plain-PyTorch fp32 references.
+
+The quantised operands are dequantised with torch's own OCP float8 dtypes (float8_e4m3fn / float8_e5m2),
+which also pins the encoding the gfx950 conversion instructions produce (OCP, not the MI300 fnuz one).
+"""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _hip():
+    from huggingface_sagemaker_tensorflow_distributed_amd.ops import hip
+
+    return hip
+
+
+def _deq(q, sinv, fmt):
+    dt = torch.float8_e4m3fn if fmt == 0 else torch.float8_e5m2
+    return q.view(dt).float() * sinv.float()
+
+
+@pytest.mark.parametrize("fmt", [0, 1])
+@pytest.mark.parametrize("n", [4096 * 33, 1000 * 7 + 3])
+def test_fp8_quant_roundtrip(gpu, fmt, n):
+    hip = _hip()
+    torch.manual_seed(0)
+    x = (torch.randn(n, device=gpu) * 3).bfloat16()
+    q, sinv = hip.quant_fp8(x, fmt)
+    amax = x.float().abs().max()
+    fmax = 448.0 if fmt == 0 else 57344.0
+    torch.testing.assert_close(sinv, (amax / fmax).reshape(1), rtol=1e-6, atol=0)
+    d = _deq(q, sinv, fmt)
+    rel = 2.0 ** -4 if fmt == 0 else 2.0 ** -3  # half an ulp of a 3 / 2-bit mantissa
+    err = (d - x.float()).abs()
+    tol = rel * x.float().abs() + 2.0 ** -9 * amax / fmax * 64  # subnormal floor
+    assert (err <= tol).all(), float(err.max())
+    # the largest magnitude maps to the format maximum
+    assert float(_deq(q, torch.ones(1, device=gpu), fmt).abs().max()) == fmax
+
+
+@pytest.mark.parametrize("M,N,K,epi", [(512, 768, 768, 1), (300, 1024, 1024, 0), (1024, 3072, 768, 8),
+                                       (512, 768, 3072, 3), (768, 1024, 4096, 4), (512, 768, 3072, 9)])
+@pytest.mark.parametrize("fa", [0, 1])
+def test_gemm8_matches_fp32_reference(gpu, M, N, K, epi, fa):
+    hip = _hip()
+    C = hip._C
+    torch.manual_seed(1)
+    x = torch.randn(M, K, device=gpu).bfloat16()
+    w = (torch.randn(N, K, device=gpu) * 0.05).bfloat16()
+    qx, sx = hip.quant_fp8(x, fa)
+    qw, sw = hip.quant_fp8(w, 0)
+    acc = _deq(qx, sx, fa) @ _deq(qw, sw, 0).t()
+    bias = (torch.randn(N, device=gpu) * 0.1).bfloat16()
+    aux = torch.randn(M, N, device=gpu).bfloat16()
+    y = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    y2 = torch.empty_like(y)
+    dbias = torch.zeros(N, device=gpu) if epi == 9 else None
+    C.gemm8(qx, fa, sx, qw, 0, sw, y, epi, bias if epi in (1, 2, 3, 8) else None,
+            aux if epi in (3, 4, 5, 9) else None, y2 if epi in (2, 8) else None, 0.0, 0, dbias)
+    if epi == 0:
+        ref = acc
+    elif epi == 1:
+        ref = acc + bias.float()
+    elif epi == 8:  # C = gelu'(y), C2 = gelu(y)
+        z = (acc + bias.float()).bfloat16().float().requires_grad_()
+        g = torch.nn.functional.gelu(z)
+        (dg,) = torch.autograd.grad(g.sum(), z)
+        torch.testing.assert_close(y2.float(), g.detach(), atol=3e-2, rtol=3e-2)
+        ref = dg
+    elif epi == 3:  # dropout p=0: y + bias + residual
+        ref = (acc + bias.float()).bfloat16().float() + aux.float()
+    elif epi == 4:
+        ref = acc.bfloat16().float() + aux.float()
+    else:  # 9: C = acc * aux, dbias = column sums
+        ref = acc.bfloat16().float() * aux.float()
+        torch.testing.assert_close(dbias, y.float().sum(0), atol=1e-1, rtol=2e-2)
+    err = (y.float() - ref).abs()
+    tol = 2e-2 * ref.abs().max() + 1e-2 * ref.abs()
+    assert (err <= tol).float().mean() > 0.999, float(err.max())
+
+
+def test_store_fp8_weight_copies(gpu):
+    """FlatParamStore(fp8=True) keeps W8 / W8ᵀ in step with the bf16 weights (shared scale)."""
+    from huggingface_sagemaker_tensorflow_distributed_amd.models import build_model, resolve_config
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel import FlatParamStore
+
+    cfg = resolve_config("roberta-large").replace(num_hidden_layers=1)
+    m = build_model(cfg, task="masked-lm", seed=0).to(gpu)
+    store = FlatParamStore(m, gpu, compute_dtype=torch.bfloat16, fp8=True)
+    for name in ("qkv_weight", "attn_out_weight", "ffn1_weight", "ffn2_weight"):
+        w = dict(m.named_parameters())[f"encoder.layers.0.{name}"]
+        d = _deq(w._hsd_q, w._hsd_qs, 0)
+        dt = _deq(w._hsd_qt, w._hsd_qs, 0)
+        torch.testing.assert_close(dt, d.t(), atol=0, rtol=0)
+        err = (d - w.float()).abs()
+        assert (err <= 2.0 ** -4 * w.float().abs() + 1e-6).float().mean() > 0.999, name
+    # after an update the copies follow
+    with torch.no_grad():
+        store.master.mul_(1.5)
+    store.sync_compute_from_master()
+    w = dict(m.named_parameters())["encoder.layers.0.ffn1_weight"]
+    d = _deq(w._hsd_q, w._hsd_qs, 0)
+    assert ((d - w.float()).abs() <= 2.0 ** -4 * w.float().abs() + 1e-6).float().mean() > 0.999
+
+
+def test_fp8_mlm_step_tracks_bf16(gpu):
+    """roberta-large (2 layers) MLM train step with fp8 GEMMs vs the same step in bf16."""
+    from huggingface_sagemaker_tensorflow_distributed_amd import data as hdata
+    from huggingface_sagemaker_tensorflow_distributed_amd.models import build_model, resolve_config
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel import FlatParamStore
+
+    hip = _hip()
+    cfg = resolve_config("roberta-large").replace(num_hidden_layers=2)
+    ds = hdata.synthetic_mlm(4, 256, cfg.vocab_size, seed=3)
+    ids = torch.from_numpy(ds.input_ids).long().to(gpu)
+    am = torch.from_numpy(ds.attention_mask).long().to(gpu)
+    labels = torch.from_numpy(ds.labels).long().to(gpu)
+    out = {}
+    for fp8 in (False, True):
+        m = build_model(cfg, task="masked-lm", seed=0).to(gpu)
+        store = FlatParamStore(m, gpu, compute_dtype=torch.bfloat16, fp8=fp8)
+        hip.set_fp8(fp8)
+        try:
+            m.train()
+            m.rng.new_step(0)
+            store.zero_grad()
+            loss, _ = m(ids, attention_mask=am, labels=labels)
+            loss.backward()
+            torch.cuda.synchronize()
+        finally:
+            hip.set_fp8(False)
+        out[fp8] = (float(loss), store.grad.float().clone())
+    (l0, g0), (l1, g1) = out[False], out[True]
+    assert abs(l1 - l0) / abs(l0) < 2e-2, (l0, l1)
+    cos = torch.nn.functional.cosine_similarity(g0, g1, dim=0)
+    assert torch.isfinite(g1).all() and cos > 0.97, float(cos)
