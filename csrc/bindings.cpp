@@ -252,15 +252,20 @@ void gemm_wgrad_variant(torch::Tensor dy, torch::Tensor x, torch::Tensor C, int6
 //        la=lb=1 -> TT (A [K,M], B [K,N]) fp32 C += A^T B, epi 6 atomics / 7 slabs in ws.
 // fp8 per-tensor quantisation: q = sat(x · FMT_MAX / amax), sinv = amax / FMT_MAX (device scalars)
 void fp8_quant(torch::Tensor x, torch::Tensor amax, torch::Tensor q, torch::Tensor sinv, int64_t fmt,
-               bool compute_amax) {
+               bool compute_amax, c10::optional<torch::Tensor> amax_track) {
   check_bf16(x, "x");
   check_f32(amax, "amax"); check_f32(sinv, "sinv");
   TORCH_CHECK(q.is_cuda() && q.scalar_type() == torch::kUInt8 && q.is_contiguous() && q.numel() == x.numel(),
               "fp8_quant q: contiguous uint8 of x's size");
   TORCH_CHECK(fmt == 0 || fmt == 1, "fmt: 0 = e4m3, 1 = e5m2");
   TORCH_CHECK(amax.numel() >= 1 && sinv.numel() >= 1, "fp8_quant scalars");
+  float* trk = nullptr;
+  if (amax_track.has_value()) {
+    check_f32(*amax_track, "amax_track");
+    trk = amax_track->data_ptr<float>();
+  }
   hsd::launch_fp8_quant(CBF(x), x.numel(), amax.data_ptr<float>(), q.data_ptr<uint8_t>(), sinv.data_ptr<float>(),
-                        (int)fmt, compute_amax, cur_stream());
+                        (int)fmt, compute_amax, trk, cur_stream());
 }
 
 void fp8_quant_many(torch::Tensor amax_desc, int64_t amax_blocks, torch::Tensor quant_desc, int64_t quant_blocks,
@@ -419,7 +424,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gelu_bwd_colsum", &gelu_bwd_colsum);
   m.def("colsum", &colsum);
   m.def("dropout", &dropout);
-  m.def("fp8_quant", &fp8_quant);
+  m.def("fp8_quant", &fp8_quant, py::arg("x"), py::arg("amax"), py::arg("q"), py::arg("sinv"), py::arg("fmt"),
+        py::arg("compute_amax"), py::arg("amax_track") = py::none());
   m.def("fp8_quant_many", &fp8_quant_many);
   m.def("fp8_elems_per_block", &hsd::fp8_elems_per_block);
   m.def("gemm8", &gemm8, py::arg("A"), py::arg("fa"), py::arg("sa"), py::arg("B"), py::arg("fb"), py::arg("sb"),

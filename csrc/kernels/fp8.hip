@@ -5,9 +5,12 @@
 //   q     = sat_fmt(x · s),  s = FMT_MAX / amax       (16-B loads, 8 values -> 8 bytes per lane)
 //   sinv  = 1 / s                                      (the GEMM epilogue multiplies acc by sinv_a·sinv_b)
 //
-// Everything stays on the device (amax / sinv are device scalars), so quantising an activation costs two
-// launches and no host synchronisation. The *_many variants batch all weight matrices of the model
-// (W and its stored transpose share one amax) into one launch each after every optimizer step.
+// Everything stays on the device (amax / sinv are device scalars): no host synchronisation. Activations
+// and gradients use DELAYED scaling — the scale comes from the amax the same site saw in the previous
+// step and the quantising pass records this step's amax on the fly — so a tensor is read once; only a
+// site's first use (no history yet) runs the separate amax pass ("current" scaling). The *_many
+// variants batch all weight matrices of the model (W and its stored transpose share one amax) into one
+// launch each after every optimizer step.
 #include "common.h"
 
 namespace hsd {
@@ -15,8 +18,10 @@ namespace hsd {
 constexpr float kE4M3Max = 448.0f, kE5M2Max = 57344.0f;
 
 __device__ __forceinline__ void atomic_max_pos(float* addr, float v) {
-  // non-negative floats order like their bit patterns
-  atomicMax(reinterpret_cast<unsigned int*>(addr), __float_as_uint(v));
+  // non-negative floats order like their bit patterns; skip the (same-address, serialising) atomic when a
+  // larger value is already there — after the first few blocks almost every block skips it
+  if (v > __hip_atomic_load(addr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
+    atomicMax(reinterpret_cast<unsigned int*>(addr), __float_as_uint(v));
 }
 
 __device__ __forceinline__ float block_max(float v) {
@@ -66,19 +71,26 @@ __device__ __forceinline__ uint32_t cvt4(float a, float b, float c, float d) {
 }
 
 template <int FMT>
-__device__ __forceinline__ void quant_range(const bf16_t* __restrict__ x, uint8_t* __restrict__ q, int64_t beg,
-                                            int64_t end, int64_t stride, float s) {
+__device__ __forceinline__ float quant_range(const bf16_t* __restrict__ x, uint8_t* __restrict__ q, int64_t beg,
+                                             int64_t end, int64_t stride, float s) {
+  float m = 0.f;
   for (int64_t i = beg; i < end; i += stride) {
     if (i + 8 <= end) {
       const u32x4 v = *reinterpret_cast<const u32x4*>(x + i);
+#pragma unroll
+      for (int k = 0; k < 4; ++k) m = fmaxf(m, fmaxf(fabsf(lo_bf(v[k])), fabsf(hi_bf(v[k]))));
       u32x2 o;
       o.x = cvt4<FMT>(lo_bf(v[0]) * s, hi_bf(v[0]) * s, lo_bf(v[1]) * s, hi_bf(v[1]) * s);
       o.y = cvt4<FMT>(lo_bf(v[2]) * s, hi_bf(v[2]) * s, lo_bf(v[3]) * s, hi_bf(v[3]) * s);
       *reinterpret_cast<u32x2*>(q + i) = o;
     } else {
-      for (int64_t j = i; j < end; ++j) q[j] = (uint8_t)(cvt4<FMT>(bf2f(x[j]) * s, 0.f, 0.f, 0.f) & 0xFF);
+      for (int64_t j = i; j < end; ++j) {
+        m = fmaxf(m, fabsf(bf2f(x[j])));
+        q[j] = (uint8_t)(cvt4<FMT>(bf2f(x[j]) * s, 0.f, 0.f, 0.f) & 0xFF);
+      }
     }
   }
+  return m;
 }
 
 __device__ __forceinline__ float fmt_scale(int fmt, float amax) {
@@ -92,14 +104,19 @@ __global__ __launch_bounds__(256) void amax_kernel(const bf16_t* __restrict__ x,
   if (threadIdx.x == 0) atomic_max_pos(amax, m);
 }
 
+// scale from amax_in; amax_track (optional) accumulates this tensor's amax for the next step's scale
 template <int FMT>
 __global__ __launch_bounds__(256) void quant_kernel(const bf16_t* __restrict__ x, int64_t n,
-                                                    const float* __restrict__ amax, uint8_t* __restrict__ q,
-                                                    float* __restrict__ sinv) {
-  const float s = fmt_scale(FMT, *amax);
+                                                    const float* __restrict__ amax_in, uint8_t* __restrict__ q,
+                                                    float* __restrict__ sinv, float* __restrict__ amax_track) {
+  const float s = fmt_scale(FMT, *amax_in);
   if (blockIdx.x == 0 && threadIdx.x == 0) *sinv = 1.0f / s;
   const int64_t stride = (int64_t)gridDim.x * 256 * 8;
-  quant_range<FMT>(x, q, ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8, n, stride, s);
+  const float m = quant_range<FMT>(x, q, ((int64_t)blockIdx.x * 256 + threadIdx.x) * 8, n, stride, s);
+  if (amax_track != nullptr) {
+    const float bm = block_max(m);
+    if (threadIdx.x == 0) atomic_max_pos(amax_track, bm);
+  }
 }
 
 // ---- batched (weights) -------------------------------------------------------------------------
@@ -140,7 +157,7 @@ __global__ __launch_bounds__(256) void quant_many_kernel(const int64_t* __restri
   if (blockIdx.x == d[4] && threadIdx.x == 0) sinv[d[3]] = 1.0f / s;
   const int64_t b0 = ((int64_t)blockIdx.x - d[4]) * kElemsPerBlock;
   const int64_t end = b0 + kElemsPerBlock < n ? b0 + kElemsPerBlock : n;
-  quant_range<FMT>(x, q, b0 + threadIdx.x * 8, end, 256 * 8, s);
+  (void)quant_range<FMT>(x, q, b0 + threadIdx.x * 8, end, 256 * 8, s);
 }
 
 // ---- host --------------------------------------------------------------------------------------
@@ -149,17 +166,18 @@ static int quant_blocks(int64_t n) {
   return (int)(b < 1 ? 1 : (b > 4096 ? 4096 : b));
 }
 
-// amax must be zeroed by the caller (it accumulates with atomicMax)
+// compute_amax: first run the amax pass into `amax` (which must then be zeroed by the caller); the
+// scale is taken from `amax`; amax_track (optional, atomicMax) records this tensor's amax.
 void launch_fp8_quant(const bf16_t* x, int64_t n, float* amax, uint8_t* q, float* sinv, int fmt, bool compute_amax,
-                      hipStream_t st) {
+                      float* amax_track, hipStream_t st) {
   if (n <= 0) return;
   const int blocks = quant_blocks(n);
   if (compute_amax) {
     hipLaunchKernelGGL(amax_kernel, dim3(blocks), dim3(256), 0, st, x, n, amax);
     HSD_CHECK_LAUNCH();
   }
-  if (fmt == 0) hipLaunchKernelGGL(quant_kernel<0>, dim3(blocks), dim3(256), 0, st, x, n, amax, q, sinv);
-  else hipLaunchKernelGGL(quant_kernel<1>, dim3(blocks), dim3(256), 0, st, x, n, amax, q, sinv);
+  if (fmt == 0) hipLaunchKernelGGL(quant_kernel<0>, dim3(blocks), dim3(256), 0, st, x, n, amax, q, sinv, amax_track);
+  else hipLaunchKernelGGL(quant_kernel<1>, dim3(blocks), dim3(256), 0, st, x, n, amax, q, sinv, amax_track);
   HSD_CHECK_LAUNCH();
 }
 

@@ -68,7 +68,7 @@ void launch_gemm8(int epi, const uint8_t* A, int64_t lda, int fa, const float* s
                   const bf16_t* aux, int64_t ldaux, bf16_t* C2, double p_drop, uint64_t seed, float* dbias,
                   hipStream_t st);
 void launch_fp8_quant(const bf16_t* x, int64_t n, float* amax, uint8_t* q, float* sinv, int fmt, bool compute_amax,
-                      hipStream_t st);
+                      float* amax_track, hipStream_t st);
 void launch_fp8_quant_many(const int64_t* amax_desc, int n_amax, int amax_blocks, const int64_t* quant_desc,
                            int n_quant, int quant_blocks_total, float* amax, float* sinv, int fmt, hipStream_t st);
 int fp8_elems_per_block();

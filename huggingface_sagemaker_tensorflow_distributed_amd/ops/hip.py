@@ -405,13 +405,23 @@ def fp8_enabled() -> bool:
     return _FP8["on"]
 
 
-def quant_fp8(x: torch.Tensor, fmt: int = FP8_E4M3):
-    """(q uint8 [same shape], sinv fp32 [1]) with q = sat(x · FMT_MAX / amax(x)), sinv = amax / FMT_MAX."""
+def quant_fp8(x: torch.Tensor, fmt: int = FP8_E4M3, state: Optional[torch.Tensor] = None):
+    """(q uint8 [same shape], sinv fp32 [1]) with q = sat(x · FMT_MAX / amax), sinv = amax / FMT_MAX.
+
+    ``state`` None: current scaling (amax of x, two passes). Otherwise a delayed-scaling site, fp32 [2] =
+    (amax scaling this step, running amax of this step — rolled by FlatParamStore.refresh_fp8): one pass;
+    the site's first use calibrates with the amax pass."""
     x = x.contiguous()
     q = torch.empty(x.shape, dtype=torch.uint8, device=x.device)
-    sc = torch.zeros(2, dtype=torch.float32, device=x.device)  # [amax, sinv]
-    _C.fp8_quant(x, sc[0:1], q, sc[1:2], fmt, True)
-    return q, sc[1:2]
+    if state is None:
+        sc = torch.zeros(2, dtype=torch.float32, device=x.device)  # [amax, sinv]
+        _C.fp8_quant(x, sc[0:1], q, sc[1:2], fmt, True)
+        return q, sc[1:2]
+    sinv = torch.empty(1, dtype=torch.float32, device=x.device)
+    calibrated = getattr(state, "_hsd_cal", False)
+    _C.fp8_quant(x, state[0:1], q, sinv, fmt, not calibrated, state[1:2])
+    state._hsd_cal = True
+    return q, sinv
 
 
 def _fp8_w(w, attr):
@@ -426,7 +436,7 @@ def gemm_fwd(x, w, epi, bias=None, aux=None, out2=None, p=0.0, seed=0):
     y = torch.empty((x.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)
     wq = _fp8_w(w, "_hsd_q")
     if wq is not None and _C.gemm8_supported(epi, x.shape[0], w.shape[0], x.shape[1]):
-        qx, sx = quant_fp8(x)
+        qx, sx = quant_fp8(x, FP8_E4M3, getattr(w, "_hsd_fp8_x", None))
         _C.gemm8(qx, FP8_E4M3, sx, wq, FP8_E4M3, w._hsd_qs, y, epi, bias, aux, out2, float(p), _s64(seed), None)
         return y
     if _nt_ok(x.shape[0], w.shape[0], x.shape[1], epi):
@@ -446,7 +456,7 @@ def gemm_dgrad(dy, w, epi=EPI_STORE, aux=None, dbias=None):
     if wqt is not None and _C.gemm8_supported(epi, dy.shape[0], w.shape[1], dy.shape[1]):
         fuse = dbias is not None and epi in (EPI_DGELU, EPI_MUL) and w.shape[1] % 256 == 0
         fmt = _FP8["grad_fmt"]
-        qdy, sdy = quant_fp8(dy, fmt)
+        qdy, sdy = quant_fp8(dy, fmt, getattr(w, "_hsd_fp8_g", None))
         _C.gemm8(qdy, fmt, sdy, wqt, FP8_E4M3, w._hsd_qs, dx, epi, None, aux, None, 0.0, 0, dbias if fuse else None)
         if dbias is not None and not fuse:
             _C.colsum(dx, dbias)

@@ -145,6 +145,9 @@ class FlatParamStore:
         self.fp8_wt = torch.empty(total, dtype=torch.uint8, device=self.device)
         self.fp8_amax = torch.zeros(len(idx), dtype=torch.float32, device=self.device)
         self.fp8_sinv = torch.ones(len(idx), dtype=torch.float32, device=self.device)
+        # delayed-scaling history of the two activation-side quantisation sites of each weight:
+        # [weight][0 = forward input x, 1 = dgrad input dy][0 = amax used for this step's scale, 1 = running]
+        self.fp8_act = torch.zeros(len(idx), 2, 2, dtype=torch.float32, device=self.device)
         amax_rows, quant_rows, ab, qb, off = [], [], 0, 0, 0
         for t, i in enumerate(idx):
             rows, cols = self.segments[i].shape
@@ -153,6 +156,7 @@ class FlatParamStore:
             q = self.fp8_w[off:off + n].view(rows, cols)
             qt = self.fp8_wt[off:off + n].view(cols, rows)
             p._hsd_q, p._hsd_qt, p._hsd_qs = q, qt, self.fp8_sinv[t:t + 1]
+            p._hsd_fp8_x, p._hsd_fp8_g = self.fp8_act[t, 0], self.fp8_act[t, 1]
             nb = (n + per_block - 1) // per_block
             amax_rows.append([p.data.data_ptr(), 0, n, t, ab])
             ab += nb
@@ -171,6 +175,11 @@ class FlatParamStore:
         from ..ops import hip
 
         ad, ab, qd, qb = self._fp8_desc
+        # roll the activation amax history: next step scales with this step's amax (sites not used this
+        # step keep their previous value)
+        prev, cur = self.fp8_act[..., 0], self.fp8_act[..., 1]
+        prev.copy_(torch.where(cur > 0, cur, prev))
+        cur.zero_()
         self.fp8_amax.zero_()
         hip._C.fp8_quant_many(ad, ab, qd, qb, self.fp8_amax, self.fp8_sinv, 0)
 

@@ -135,3 +135,24 @@ def test_fp8_mlm_step_tracks_bf16(gpu):
     assert abs(l1 - l0) / abs(l0) < 2e-2, (l0, l1)
     cos = torch.nn.functional.cosine_similarity(g0, g1, dim=0)
     assert torch.isfinite(g1).all() and cos > 0.97, float(cos)
+
+
+def test_fp8_delayed_scaling_site(gpu):
+    """A delayed-scaling site: the first use calibrates (amax pass), later uses scale with the previous
+    step's amax (values beyond it saturate) and record the running amax for the next roll."""
+    hip = _hip()
+    torch.manual_seed(2)
+    x = torch.randn(8192, device=gpu).bfloat16()
+    a = float(x.float().abs().max())
+    st = torch.zeros(2, device=gpu)
+    q, sinv = hip.quant_fp8(x, 0, st)
+    torch.testing.assert_close(st.cpu(), torch.tensor([a, a]), rtol=0, atol=0)
+    torch.testing.assert_close(sinv.cpu(), torch.tensor([a / 448.0]), rtol=1e-6, atol=0)
+    # roll (what FlatParamStore.refresh_fp8 does), then a tensor twice as large
+    st[0] = st[1]
+    st[1] = 0
+    q2, sinv2 = hip.quant_fp8(x * 2, 0, st)
+    torch.testing.assert_close(sinv2.cpu(), torch.tensor([a / 448.0]), rtol=1e-6, atol=0)
+    assert abs(float(st[1]) - 2 * a) <= 1e-6 * a
+    d = _deq(q2, sinv2, 0)
+    assert float(d.abs().max()) <= a * (1 + 1e-6)  # saturated at the old amax
