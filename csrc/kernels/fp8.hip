@@ -37,14 +37,25 @@ __device__ __forceinline__ float block_max(float v) {
   return r;  // valid in thread 0
 }
 
-// |x| max over [beg, end) of x, elements in 16-B vectors where possible
+// |x| max over [beg, end) of x (same access pattern as quant_range)
+__device__ __forceinline__ float absmax8(const u32x4& v, float m) {
+#pragma unroll
+  for (int k = 0; k < 4; ++k) m = fmaxf(m, fmaxf(fabsf(lo_bf(v[k])), fabsf(hi_bf(v[k]))));
+  return m;
+}
 __device__ __forceinline__ float absmax_range(const bf16_t* __restrict__ x, int64_t beg, int64_t end, int64_t stride) {
   float m = 0.f;
-  for (int64_t i = beg; i < end; i += stride) {
-    if (i + 8 <= end) {
-      const u32x4 v = *reinterpret_cast<const u32x4*>(x + i);
+  int64_t i = beg;
+  for (; i + 3 * stride + 8 <= end; i += 4 * stride) {
+    u32x4 v[4];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) m = fmaxf(m, fmaxf(fabsf(lo_bf(v[k])), fabsf(hi_bf(v[k]))));
+    for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const u32x4*>(x + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) m = absmax8(v[u], m);
+  }
+  for (; i < end; i += stride) {
+    if (i + 8 <= end) {
+      m = absmax8(*reinterpret_cast<const u32x4*>(x + i), m);
     } else {
       for (int64_t j = i; j < end; ++j) m = fmaxf(m, fabsf(bf2f(x[j])));
     }
@@ -71,18 +82,35 @@ __device__ __forceinline__ uint32_t cvt4(float a, float b, float c, float d) {
 }
 
 template <int FMT>
+__device__ __forceinline__ u32x2 quant8(const u32x4& v, float s) {
+  u32x2 o;
+  o.x = cvt4<FMT>(lo_bf(v[0]) * s, hi_bf(v[0]) * s, lo_bf(v[1]) * s, hi_bf(v[1]) * s);
+  o.y = cvt4<FMT>(lo_bf(v[2]) * s, hi_bf(v[2]) * s, lo_bf(v[3]) * s, hi_bf(v[3]) * s);
+  return o;
+}
+
+// quantise [beg, end) (thread's first element `beg`, `stride` between a thread's vectors); four 16-B
+// loads are issued before any is used so each thread keeps 64 B in flight. Returns max |x| seen.
+template <int FMT>
 __device__ __forceinline__ float quant_range(const bf16_t* __restrict__ x, uint8_t* __restrict__ q, int64_t beg,
                                              int64_t end, int64_t stride, float s) {
   float m = 0.f;
-  for (int64_t i = beg; i < end; i += stride) {
+  int64_t i = beg;
+  for (; i + 3 * stride + 8 <= end; i += 4 * stride) {
+    u32x4 v[4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u) v[u] = *reinterpret_cast<const u32x4*>(x + i + u * stride);
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      m = absmax8(v[u], m);
+      *reinterpret_cast<u32x2*>(q + i + u * stride) = quant8<FMT>(v[u], s);
+    }
+  }
+  for (; i < end; i += stride) {
     if (i + 8 <= end) {
       const u32x4 v = *reinterpret_cast<const u32x4*>(x + i);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) m = fmaxf(m, fmaxf(fabsf(lo_bf(v[k])), fabsf(hi_bf(v[k]))));
-      u32x2 o;
-      o.x = cvt4<FMT>(lo_bf(v[0]) * s, hi_bf(v[0]) * s, lo_bf(v[1]) * s, hi_bf(v[1]) * s);
-      o.y = cvt4<FMT>(lo_bf(v[2]) * s, hi_bf(v[2]) * s, lo_bf(v[3]) * s, hi_bf(v[3]) * s);
-      *reinterpret_cast<u32x2*>(q + i) = o;
+      m = absmax8(v, m);
+      *reinterpret_cast<u32x2*>(q + i) = quant8<FMT>(v, s);
     } else {
       for (int64_t j = i; j < end; ++j) {
         m = fmaxf(m, fabsf(bf2f(x[j])));
@@ -161,9 +189,10 @@ __global__ __launch_bounds__(256) void quant_many_kernel(const int64_t* __restri
 }
 
 // ---- host --------------------------------------------------------------------------------------
+// ~2 resident blocks per SIMD-set of 256 CUs, each thread >= 4 vectors
 static int quant_blocks(int64_t n) {
   const int64_t b = (n + 256 * 8 * 4 - 1) / (256 * 8 * 4);
-  return (int)(b < 1 ? 1 : (b > 4096 ? 4096 : b));
+  return (int)(b < 1 ? 1 : (b > 2048 ? 2048 : b));
 }
 
 // compute_amax: first run the amax pass into `amax` (which must then be zeroed by the caller); the
