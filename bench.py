@@ -41,6 +41,7 @@ def main():
     ap.add_argument("--dtype", choices=["bf16", "fp8"], default="bf16",
                     help="fp8: fp8 forward/dgrad GEMMs (secondary config; the headline is bf16)")
     ap.add_argument("--task", choices=["sequence-classification", "masked-lm"], default="sequence-classification")
+    ap.add_argument("--hip_graph", action="store_true", help="replay fwd+bwd from a captured HIP graph (N=1)")
     a = ap.parse_args()
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
@@ -48,7 +49,7 @@ def main():
         print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world_env}; using WORLD_SIZE", file=sys.stderr)
     targs, _ = build_parser("train").parse_known_args(
         ["--model_name_or_path", a.model, "--train_batch_size", str(a.batch_size), "--dtype", a.dtype,
-         "--task", a.task,
+         "--task", a.task, "--hip_graph", str(a.hip_graph),
          "--learning_rate", "5e-5", "--log_every", "0"]
         + (["--bucket_mb", str(a.bucket_mb)] if a.bucket_mb else [])
         + (["--grad_dtype", a.grad_dtype] if a.grad_dtype else []))
@@ -97,6 +98,7 @@ def main():
                        "per_gpu_batch": a.batch_size,
                        "seq_len": a.seq_len, "parallelism": f"dp{world}",
                        "ops": "torch-reference" if os.environ.get("HSD_OPS") == "torch" else "hip",
+                       "hip_graph": trainer._seed is not None,
                        "comm": ("native-rccl" if getattr(trainer.bucketer, "engine", None) is not None
                                 else ("torch-" + backend.state().backend if world > 1 else "none"))},
         }), flush=True)

@@ -323,6 +323,17 @@ void gemm8(torch::Tensor A, int64_t fa, torch::Tensor sa, torch::Tensor B, int64
                     cur_stream());
 }
 
+// device step seed for dropout (uint32/int32 [2] GPU tensor, kept alive by the caller), None = off
+void set_dropout_device_seed(c10::optional<torch::Tensor> t) {
+  if (!t.has_value()) {
+    hsd::set_dropout_dev_seed(nullptr);
+    return;
+  }
+  TORCH_CHECK(t->is_cuda() && t->numel() >= 2 && t->element_size() == 4 && t->is_contiguous(),
+              "device seed: contiguous 32-bit GPU tensor of >= 2 elements");
+  hsd::set_dropout_dev_seed(reinterpret_cast<const uint32_t*>(t->data_ptr()));
+}
+
 void gemm2(torch::Tensor A, torch::Tensor B, torch::Tensor C, int64_t la, int64_t lb, int64_t epi,
            c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> aux, c10::optional<torch::Tensor> C2,
            double p, int64_t seed, int64_t splits, c10::optional<torch::Tensor> ws,
@@ -424,6 +435,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gelu_bwd_colsum", &gelu_bwd_colsum);
   m.def("colsum", &colsum);
   m.def("dropout", &dropout);
+  m.def("set_dropout_device_seed", &set_dropout_device_seed);
   m.def("fp8_quant", &fp8_quant, py::arg("x"), py::arg("amax"), py::arg("q"), py::arg("sinv"), py::arg("fmt"),
         py::arg("compute_amax"), py::arg("amax_track") = py::none());
   m.def("fp8_quant_many", &fp8_quant_many);

@@ -150,7 +150,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
 #pragma unroll
         for (int reg = 0; reg < 16; reg += 2) {
           const int key = kt * 64 + kb * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * hf;
-          const uint32_t bits = dropout_bits((rowbase + key) >> 1, dp.seed_lo, dp.seed_hi);
+          const uint32_t bits = dropout_bits((rowbase + key) >> 1, dp);
           st[kb][reg] *= keep_factor(bits, 0, dp);
           st[kb][reg + 1] *= keep_factor(bits, 1, dp);
         }
@@ -270,7 +270,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const bf16_t* __restrict_
       float kf_ = 1.0f;
       if (dp.enabled) {
         const uint32_t e = (uint32_t)(((size_t)bh * S + min(qq, S - 1)) * S + kc);
-        kf_ = keep_factor(dropout_bits(e >> 1, dp.seed_lo, dp.seed_hi), (int)(e & 1), dp);
+        kf_ = keep_factor(dropout_bits(e >> 1, dp), (int)(e & 1), dp);
       }
       pd[reg] = p * kf_;
       ds[reg] = p * (dpacc[reg] * kf_ - del_s[qi]);

@@ -96,7 +96,7 @@ __global__ __launch_bounds__(256, 2) void attn128_fwd_kernel(const bf16_t* __res
 #pragma unroll
       for (int reg = 0; reg < 16; reg += 2) {
         const int key = kb * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * hf;
-        const uint32_t bits = dropout_bits((rowbase + key) >> 1, dp.seed_lo, dp.seed_hi);
+        const uint32_t bits = dropout_bits((rowbase + key) >> 1, dp);
         st[kb][reg] *= keep_factor(bits, 0, dp);
         st[kb][reg + 1] *= keep_factor(bits, 1, dp);
       }
@@ -203,7 +203,7 @@ __global__ __launch_bounds__(256, 2) void attn128_bwd_kernel(const bf16_t* __res
         // even lane hashes row qi0, odd lane row qi0+1, then they swap.
         const int qmine = odd ? qi0 + 1 : qi0;
         const uint32_t e = (uint32_t)(((int64_t)bh * S + qmine) * S + key);
-        const uint32_t bits = dropout_bits(e >> 1, dp.seed_lo, dp.seed_hi);
+        const uint32_t bits = dropout_bits(e >> 1, dp);
         const uint32_t other = (uint32_t)__shfl_xor((int)bits, 1, 64);
         const uint32_t b0 = odd ? other : bits;   // hash of row qi0
         const uint32_t b1 = odd ? bits : other;   // hash of row qi0 + 1

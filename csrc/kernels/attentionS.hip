@@ -121,7 +121,7 @@ __global__ __launch_bounds__(256, 2) void attnS_fwd_kernel(const bf16_t* __restr
 #pragma unroll
         for (int reg = 0; reg < 16; reg += 2) {
           const int key = kt * 64 + kb * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * hf;
-          const uint32_t bits = dropout_bits((rowbase + key) >> 1, dp.seed_lo, dp.seed_hi);
+          const uint32_t bits = dropout_bits((rowbase + key) >> 1, dp);
           st[kb][reg] *= keep_factor(bits, 0, dp);
           st[kb][reg + 1] *= keep_factor(bits, 1, dp);
         }
@@ -246,7 +246,7 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_kv_kernel(const bf16_t* __re
           // the odd lane row qi0 + 1, then they swap
           const int qmine = odd ? qi0 + 1 : qi0;
           const uint32_t e = (uint32_t)(((int64_t)bh * S + qmine) * S + key);
-          const uint32_t bits = dropout_bits(e >> 1, dp.seed_lo, dp.seed_hi);
+          const uint32_t bits = dropout_bits(e >> 1, dp);
           const uint32_t other = (uint32_t)__shfl_xor((int)bits, 1, 64);
           f0 = keep_factor(odd ? other : bits, key & 1, dp);
           f1 = keep_factor(odd ? bits : other, key & 1, dp);
@@ -356,7 +356,7 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_q_kernel(const bf16_t* __res
           const float p1 = __builtin_amdgcn_exp2f(fmaf(sacc[reg + 1], sl2, mb[e + 1]) - lse_q);
           float f0 = 1.f, f1 = 1.f;
           if (dp.enabled) {
-            const uint32_t bits = dropout_bits((rowbase + kk + e) >> 1, dp.seed_lo, dp.seed_hi);
+            const uint32_t bits = dropout_bits((rowbase + kk + e) >> 1, dp);
             f0 = keep_factor(bits, 0, dp);
             f1 = keep_factor(bits, 1, dp);
           }

@@ -70,7 +70,13 @@ struct DropoutParams {
   uint32_t thr;     // keep iff bits16 >= thr
   float scale;      // 1/(1-p)
   int enabled;
+  // optional device-side step seed XORed into (seed_lo, seed_hi): lets a captured HIP graph replay with
+  // fresh dropout masks every step (the per-site host seeds are baked into the graph)
+  const uint32_t* dev_seed;
 };
+
+// process-wide device step seed (uint32 [2]) picked up by every make_dropout (null = off)
+inline const uint32_t* g_dropout_dev_seed = nullptr;
 
 __host__ inline DropoutParams make_dropout(double p, uint64_t seed) {
   DropoutParams d;
@@ -80,7 +86,17 @@ __host__ inline DropoutParams make_dropout(double p, uint64_t seed) {
   d.thr = (uint32_t)(t + 0.5);
   d.scale = p > 0.0 ? (float)(1.0 / (1.0 - p)) : 1.0f;
   d.enabled = p > 0.0 ? 1 : 0;
+  d.dev_seed = g_dropout_dev_seed;
   return d;
+}
+
+__device__ __forceinline__ uint32_t dropout_bits(uint32_t pair, const DropoutParams& d) {
+  uint32_t lo = d.seed_lo, hi = d.seed_hi;
+  if (d.dev_seed != nullptr) {
+    lo ^= d.dev_seed[0];
+    hi ^= d.dev_seed[1];
+  }
+  return dropout_bits(pair, lo, hi);
 }
 
 // keep factor (0 or scale) for element `e` given its pair's bits

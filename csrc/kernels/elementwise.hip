@@ -87,8 +87,8 @@ __global__ __launch_bounds__(256) void dropout_kernel(const bf16_t* __restrict__
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     u32x2 w = reinterpret_cast<const u32x2*>(x)[i];
     uint32_t pair0 = (uint32_t)(i * 2);
-    uint32_t b0 = dropout_bits(pair0, dp.seed_lo, dp.seed_hi);
-    uint32_t b1 = dropout_bits(pair0 + 1, dp.seed_lo, dp.seed_hi);
+    uint32_t b0 = dropout_bits(pair0, dp);
+    uint32_t b1 = dropout_bits(pair0 + 1, dp);
     u32x2 o;
     o.x = pack_bf2(lo_bf(w.x) * keep_factor(b0, 0, dp), hi_bf(w.x) * keep_factor(b0, 1, dp));
     o.y = pack_bf2(lo_bf(w.y) * keep_factor(b1, 0, dp), hi_bf(w.y) * keep_factor(b1, 1, dp));
@@ -187,5 +187,7 @@ void launch_transpose_many(const int64_t* desc, int n, int total_tiles, hipStrea
   hipLaunchKernelGGL(transpose_many_kernel, dim3(total_tiles), dim3(256), 0, st, desc, n);
   HSD_CHECK_LAUNCH();
 }
+
+void set_dropout_dev_seed(const uint32_t* p) { g_dropout_dev_seed = p; }
 
 }  // namespace hsd

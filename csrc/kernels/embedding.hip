@@ -75,8 +75,8 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
       if (dp.enabled) {
         // dropout is applied to the bf16-rounded LN output (matches the reference op order)
         uint32_t pair0 = (uint32_t)(off >> 1);
-        uint32_t b0 = dropout_bits(pair0, dp.seed_lo, dp.seed_hi);
-        uint32_t b1 = dropout_bits(pair0 + 1, dp.seed_lo, dp.seed_hi);
+        uint32_t b0 = dropout_bits(pair0, dp);
+        uint32_t b1 = dropout_bits(pair0 + 1, dp);
         o[0] = bf2f(f2bf(o[0])) * keep_factor(b0, 0, dp);
         o[1] = bf2f(f2bf(o[1])) * keep_factor(b0, 1, dp);
         o[2] = bf2f(f2bf(o[2])) * keep_factor(b1, 0, dp);
@@ -136,7 +136,7 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const bf16_t* __restrict
         if (type) ev += bf2f(type[tid * H + e]);
         const size_t off = (size_t)row * H + e;
         float dv = bf2f(dout[off]);
-        if (dp.enabled) dv *= keep_factor(dropout_bits((uint32_t)(off >> 1), dp.seed_lo, dp.seed_hi), (int)(off & 1), dp);
+        if (dp.enabled) dv *= keep_factor(dropout_bits((uint32_t)(off >> 1), dp), (int)(off & 1), dp);
         d[i] = dv;
         xh[i] = (ev - mean) * rstd;
         g[i] = dv * gam[i];

@@ -94,7 +94,7 @@ __device__ __forceinline__ void epi_chunk(u32x4& o, u32x4& o2, const u32x4& x, i
       const uint32_t pair0 = (uint32_t)(((int64_t)m * p.N + n) >> 1);
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const uint32_t b = dropout_bits(pair0 + e, p.dp.seed_lo, p.dp.seed_hi);
+        const uint32_t b = dropout_bits(pair0 + e, p.dp);
         v[2 * e] = bf2f(f2bf(v[2 * e] * keep_factor(b, 0, p.dp)));
         v[2 * e + 1] = bf2f(f2bf(v[2 * e + 1] * keep_factor(b, 1, p.dp)));
       }

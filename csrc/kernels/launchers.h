@@ -61,6 +61,9 @@ void launch_gemm_variant(int la, int lb, int variant, const bf16_t* A, int64_t l
                          int M, int N, int K, bf16_t* C, int64_t ldc, hipStream_t st);
 // gemm2.hip — 256-row-tile 8-phase MFMA GEMM: (0,0) NT bf16 out with epilogues 0..5; (1,1) TT fp32 out
 // (epi 6 = atomics, 7 = split-K slabs in `ws` [splits][M][N] + reduce into C)
+// device step seed for dropout (common.h g_dropout_dev_seed); nullptr = off
+void set_dropout_dev_seed(const uint32_t* p);
+
 // fp8 (gemm8.hip / fp8.hip)
 bool gemm8_supported(int epi, int M, int N, int K);
 void launch_gemm8(int epi, const uint8_t* A, int64_t lda, int fa, const float* sa, const uint8_t* B, int64_t ldb,

@@ -41,8 +41,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
       if (dp.enabled) {
         // element index within the site tensor = off + k ; pairs (off+0,off+1), (off+2,off+3)
         uint32_t pair0 = (uint32_t)(off >> 1);
-        uint32_t b0 = dropout_bits(pair0, dp.seed_lo, dp.seed_hi);
-        uint32_t b1 = dropout_bits(pair0 + 1, dp.seed_lo, dp.seed_hi);
+        uint32_t b0 = dropout_bits(pair0, dp);
+        uint32_t b1 = dropout_bits(pair0 + 1, dp);
         a[0] *= keep_factor(b0, 0, dp);
         a[1] *= keep_factor(b0, 1, dp);
         a[2] *= keep_factor(b1, 0, dp);
@@ -161,8 +161,8 @@ __device__ __forceinline__ void ln_bwd_row(const u32x2 (&zw)[NCH], const u32x2 (
       float dy[4] = {dz[0], dz[1], dz[2], dz[3]};
       if (dp.enabled) {
         const uint32_t pair0 = (uint32_t)(off >> 1);
-        const uint32_t b0 = dropout_bits(pair0, dp.seed_lo, dp.seed_hi);
-        const uint32_t b1 = dropout_bits(pair0 + 1, dp.seed_lo, dp.seed_hi);
+        const uint32_t b0 = dropout_bits(pair0, dp);
+        const uint32_t b1 = dropout_bits(pair0 + 1, dp);
         dy[0] *= keep_factor(b0, 0, dp);
         dy[1] *= keep_factor(b0, 1, dp);
         dy[2] *= keep_factor(b1, 0, dp);

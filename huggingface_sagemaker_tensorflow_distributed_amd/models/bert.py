@@ -198,6 +198,7 @@ class RobertaForMaskedLM(_Base):
     """RoBERTa MLM (decoder tied to the word embeddings), for the roberta-large pretraining config."""
 
     base_prefix = "roberta"
+    graph_safe = False  # the masked-token gather has a data-dependent size (no HIP-graph capture)
 
     def __init__(self, cfg: ModelConfig):
         super().__init__(cfg)

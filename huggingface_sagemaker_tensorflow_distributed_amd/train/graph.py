@@ -1,0 +1,99 @@
+"""HIP-graph capture of the training step's forward + backward (SURVEY.md §2.4 'XLA / graph compilation
+-> HIP graphs for the step', §7.4 hard part 4 'host launch overhead').
+
+A BERT step is ~25 kernels per layer (several hundred launches per step); at small per-GPU batches the
+host cannot issue them as fast as the GPU retires them. :class:`CapturedStep` records forward + loss +
+backward ONCE into a ``torch.cuda.CUDAGraph`` (a hipGraph on ROCm) over static input buffers and then
+replays it: one launch per micro-step. The optimizer (one fused Adam + one batched Wᵀ refresh) stays
+eager — it is two launches and its step-dependent scalars live on the host.
+
+What makes a replay a *fresh* step:
+
+* inputs are copied into the static buffers (``copy_`` on the stream, no host sync);
+* dropout: every kernel's per-call-site seed is baked into the graph, and each step XORs a device-side
+  step seed into it (``_C.set_dropout_device_seed``; common.h ``DropoutParams::dev_seed``), so the masks
+  change every step without re-capture. Eager steps of a graph-enabled trainer use the same device
+  seed, so eager and replayed steps draw identical masks for the same step index;
+* gradients: the flat ``main_grad`` buffer is zeroed before the replay (kernels accumulate into it).
+
+Limits: one process (world 1; data-parallel steps keep the eager path so the bucketed all-reduce stays
+overlapped with backward), fixed batch shape per captured graph (a new shape captures a new graph),
+models without data-dependent shapes (the MLM head's masked-token gather syncs the host: eager only).
+"""
+from __future__ import annotations
+
+import logging
+from typing import Dict
+
+import torch
+
+from ..ops.rng import mix32_int
+
+logger = logging.getLogger(__name__)
+
+
+def step_seed(base_seed: int, rank: int, step: int):
+    """Two 32-bit words of the device step seed for ``step``."""
+    a = mix32_int((base_seed ^ 0x2545F491) & 0xFFFFFFFF)
+    b = mix32_int(a ^ ((step * 0x9E3779B9 + rank * 0x7F4A7C15) & 0xFFFFFFFF))
+    c = mix32_int(b ^ 0x68E31DA4)
+    return b, c
+
+
+class DeviceStepSeed:
+    """The process-wide device step seed (int32 [2]) read by every dropout kernel."""
+
+    def __init__(self, device, base_seed: int, rank: int):
+        from ..ops import hip
+
+        self.t = torch.zeros(2, dtype=torch.int32, device=device)
+        self.base_seed, self.rank = int(base_seed), int(rank)
+        hip._C.set_dropout_device_seed(self.t)
+
+    def set_step(self, step: int) -> None:
+        lo, hi = step_seed(self.base_seed, self.rank, step)
+        # stream-ordered fills (the value travels as a kernel argument: no host buffer the GPU could
+        # read after the host moved on to the next step); int32 view of the uint32 words
+        self.t[0].fill_(lo - (1 << 32) if lo >= 1 << 31 else lo)
+        self.t[1].fill_(hi - (1 << 32) if hi >= 1 << 31 else hi)
+
+    def close(self) -> None:
+        from ..ops import hip
+
+        hip._C.set_dropout_device_seed(None)
+
+
+class CapturedStep:
+    """forward + loss + backward of ``trainer`` for batches shaped like ``example``, as one graph."""
+
+    def __init__(self, trainer, example: Dict[str, torch.Tensor], warmup: int = 2):
+        self.trainer = trainer
+        self.static = {k: v.clone() for k, v in example.items()}
+        model, store = trainer.model, trainer.store
+        model.train()
+        # warm up on a side stream (kernel/workspace first-use allocations, lazy caches) — not captured
+        s = torch.cuda.Stream(device=trainer.device)
+        s.wait_stream(torch.cuda.current_stream(trainer.device))
+        with torch.cuda.stream(s):
+            for _ in range(warmup):
+                model.rng.new_step(0)
+                store.zero_grad()
+                loss, _ = trainer._forward_loss(self.static)
+                loss.backward()
+        torch.cuda.current_stream(trainer.device).wait_stream(s)
+        torch.cuda.synchronize(trainer.device)
+        store.zero_grad()
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.graph):
+            model.rng.new_step(0)  # per-site seeds fixed; the device step seed varies per replay
+            self.loss, self.logits = trainer._forward_loss(self.static)
+            self.loss.backward()
+        torch.cuda.synchronize(trainer.device)
+        logger.info("captured training step graph for batch shape %s", tuple(example["input_ids"].shape))
+
+    def run(self, batch: Dict[str, torch.Tensor]):
+        """Copy ``batch`` into the static inputs and replay (gradients ACCUMULATE into main_grad)."""
+        for k, v in batch.items():
+            self.static[k].copy_(v, non_blocking=True)
+        self.graph.replay()
+        return self.loss, self.logits

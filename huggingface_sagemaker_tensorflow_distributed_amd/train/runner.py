@@ -94,7 +94,8 @@ def build(args, mode: str):
                     weight_decay=args.weight_decay if args.optimizer == "adamw" else 0.0)
     bucketer = GradBucketer(store, bucket_mb=args.bucket_mb) if world > 1 else None
     trainer = Trainer(model, store, opt, bucketer, dev, grad_accum=args.gradient_accumulation_steps,
-                      check_sync=args.check_sync, log_every=args.log_every, step_watchdog=args.step_watchdog)
+                      check_sync=args.check_sync, log_every=args.log_every, step_watchdog=args.step_watchdog,
+                      hip_graph=bool(getattr(args, "hip_graph", False)))
     if args.resume_from:
         load_checkpoint(args.resume_from, trainer)
     broadcast_parameters(store, opt if args.resume_from else None)

@@ -76,7 +76,7 @@ class _Meter:
 
 class Trainer:
     def __init__(self, model, store, optimizer, bucketer=None, device=None, grad_accum: int = 1,
-                 check_sync: int = 0, log_every: int = 50, step_watchdog: float = 0.0):
+                 check_sync: int = 0, log_every: int = 50, step_watchdog: float = 0.0, hip_graph: bool = False):
         self.model = model
         self.store = store
         self.optimizer = optimizer
@@ -89,6 +89,34 @@ class Trainer:
         self.global_step = 0
         self.world = backend.size()
         self.rank = backend.rank()
+        self._graphs = {}
+        self._seed = None
+        self._graph_replay = True  # tests: False = graph-mode seeding with eager kernels
+        if hip_graph:
+            self.enable_hip_graph()
+
+    def enable_hip_graph(self) -> bool:
+        """Replay forward + backward from captured HIP graphs (train/graph.py). Single-process GPU runs of
+        models without data-dependent shapes; otherwise stays eager (returns False)."""
+        if self.device.type != "cuda" or self.bucketer is not None or self.world > 1:
+            logger.warning("--hip_graph: needs one GPU process (data-parallel steps stay eager)")
+            return False
+        if not getattr(self.model, "graph_safe", True):
+            logger.warning("--hip_graph: %s has data-dependent shapes; staying eager", type(self.model).__name__)
+            return False
+        from .graph import DeviceStepSeed
+
+        self._seed = DeviceStepSeed(self.device, self.model.rng.base_seed, self.rank)
+        return True
+
+    def _graph_for(self, mb):
+        key = tuple((k, tuple(v.shape), v.dtype) for k, v in sorted(mb.items()))
+        g = self._graphs.get(key)
+        if g is None:
+            from .graph import CapturedStep
+
+            g = self._graphs[key] = CapturedStep(self, mb)
+        return g
 
     # -------------------------------------------------------------------------- step
     def _forward_loss(self, batch):
@@ -99,7 +127,12 @@ class Trainer:
     def train_step(self, micro_batches: List[Dict[str, torch.Tensor]], meter: Optional[_Meter] = None) -> torch.Tensor:
         """One optimizer step over ``len(micro_batches)`` accumulation micro-steps."""
         self.model.train()
-        self.model.rng.new_step(self.global_step)
+        if self._seed is not None:
+            # graph mode: per-site seeds fixed (step 0), the device step seed carries the step
+            self._seed.set_step(self.global_step)
+            self.model.rng.new_step(0)
+        else:
+            self.model.rng.new_step(self.global_step)
         self.store.zero_grad()
         if self.bucketer is not None:
             self.bucketer.begin()
@@ -107,6 +140,12 @@ class Trainer:
         loss = None
         for i, mb in enumerate(micro_batches):
             last = i == k - 1
+            if self._seed is not None and self._graph_replay:
+                with prange("graph-replay"):
+                    loss, logits = self._graph_for(mb).run(mb)
+                if meter is not None:
+                    meter.update(loss, logits, mb["labels"])
+                continue
             ctx = self.bucketer.no_sync() if (self.bucketer is not None and not last) else contextlib.nullcontext()
             with ctx:
                 with prange("forward"):

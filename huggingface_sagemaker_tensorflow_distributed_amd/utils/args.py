@@ -73,6 +73,8 @@ def _add_framework_flags(p: argparse.ArgumentParser) -> None:
     g.add_argument("--benchmark", type=str2bool, default=False)
     g.add_argument("--warmup_steps", type=int, default=3, help="benchmark warmup steps")
     g.add_argument("--profile", type=str2bool, default=False)
+    g.add_argument("--hip_graph", type=str2bool, default=False,
+                   help="replay forward+backward from a captured HIP graph (single-process GPU runs)")
     g.add_argument("--save_every_epoch", type=str2bool, default=False)
     g.add_argument("--resume_from", type=str, default=None)
     g.add_argument("--check_sync", type=int, default=0, help="verify cross-rank param hash every N steps")
