@@ -73,6 +73,7 @@ __device__ __forceinline__ float mask_bias2(const float* mask, int b, int S, int
 __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict__ qkv, const float* __restrict__ mask,
                                                        bf16_t* __restrict__ out, float* __restrict__ lse2,
                                                        int S, int heads, float sl2, DropoutParams dp) {
+  dp = resolve_seed(dp);
   __shared__ __attribute__((aligned(16))) bf16_t Ks[64 * kD];
   __shared__ __attribute__((aligned(16))) bf16_t Vs[64 * kD];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -191,6 +192,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const bf16_t* __restrict_
                                                        const float* __restrict__ lse2, bf16_t* __restrict__ dqkv,
                                                        float* __restrict__ dq_acc, int S, int heads, float sl2,
                                                        float scale, DropoutParams dp) {
+  dp = resolve_seed(dp);
   __shared__ __attribute__((aligned(16))) bf16_t Qs[32 * kD];
   __shared__ __attribute__((aligned(16))) bf16_t dOs[32 * kD];
   __shared__ __attribute__((aligned(16))) bf16_t Kall[128 * kD];

@@ -30,6 +30,7 @@ __global__ __launch_bounds__(256, 2) void attn128_fwd_kernel(const bf16_t* __res
                                                              const float* __restrict__ mask, bf16_t* __restrict__ out,
                                                              float* __restrict__ lse2, int heads, float sl2,
                                                              DropoutParams dp) {
+  dp = resolve_seed(dp);
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * S * D + 4 * 32 * D + 2 * S];
   bf16_t* Ks = lds;
   bf16_t* Vs = lds + S * D;
@@ -123,6 +124,7 @@ __global__ __launch_bounds__(256, 2) void attn128_bwd_kernel(const bf16_t* __res
                                                              const float* __restrict__ lse2,
                                                              bf16_t* __restrict__ dqkv, float* __restrict__ dbias,
                                                              int heads, float sl2, float scale, DropoutParams dp) {
+  dp = resolve_seed(dp);
   // [Q | dO | dS | lse | delta | bias-grad partials]; after the main loop Q's slot holds K, dO's slot the
   // output staging
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * S * D + S * S + 4 * S + 2 * 3 * 4 * D];

@@ -36,6 +36,7 @@ __global__ __launch_bounds__(256, 2) void attnS_fwd_kernel(const bf16_t* __restr
                                                            const float* __restrict__ mask, bf16_t* __restrict__ out,
                                                            float* __restrict__ lse2, int S, int heads, float sl2,
                                                            DropoutParams dp) {
+  dp = resolve_seed(dp);
   // [K0 K1 | V0 V1 | mask bias]; after the loop K0|K1 is the output staging
   __shared__ __attribute__((aligned(16))) bf16_t lds[4 * TILE + 2 * kMaxS];
   bf16_t* Kb = lds;
@@ -176,6 +177,7 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_kv_kernel(const bf16_t* __re
                                                               bf16_t* __restrict__ dqkv, float* __restrict__ dbias,
                                                               int S, int heads, float sl2, float scale,
                                                               DropoutParams dp) {
+  dp = resolve_seed(dp);
   // [Q0 Q1 | dO0 dO1 | lse | delta | k/v bias partials]; after the loop Q0|Q1 is the output staging
   __shared__ __attribute__((aligned(16))) bf16_t lds[4 * TILE + 4 * kMaxS + 2 * 2 * 4 * D];
   bf16_t* Qb = lds;
@@ -291,6 +293,7 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_q_kernel(const bf16_t* __res
                                                              bf16_t* __restrict__ dqkv, float* __restrict__ dbias,
                                                              int S, int heads, float sl2, float scale,
                                                              DropoutParams dp) {
+  dp = resolve_seed(dp);
   // [K0 K1 | V0 V1 | mask bias | q bias partials]; after the loop K0|K1 is the output staging
   __shared__ __attribute__((aligned(16))) bf16_t lds[4 * TILE + 2 * kMaxS + 2 * 4 * D];
   bf16_t* Kb = lds;

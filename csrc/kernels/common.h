@@ -90,6 +90,17 @@ __host__ inline DropoutParams make_dropout(double p, uint64_t seed) {
   return d;
 }
 
+// fold the device step seed into the params ONCE per kernel (kernels call this on entry), so the per-element
+// hash below reads no memory
+__device__ __forceinline__ DropoutParams resolve_seed(DropoutParams d) {
+  if (d.dev_seed != nullptr) {
+    d.seed_lo ^= d.dev_seed[0];
+    d.seed_hi ^= d.dev_seed[1];
+    d.dev_seed = nullptr;
+  }
+  return d;
+}
+
 __device__ __forceinline__ uint32_t dropout_bits(uint32_t pair, const DropoutParams& d) {
   uint32_t lo = d.seed_lo, hi = d.seed_hi;
   if (d.dev_seed != nullptr) {

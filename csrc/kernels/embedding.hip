@@ -46,6 +46,7 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
                                                         bf16_t* __restrict__ out, float* __restrict__ mean_out,
                                                         float* __restrict__ rstd_out, int rows, int H, float eps,
                                                         DropoutParams dp) {
+  dp = resolve_seed(dp);
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -108,6 +109,7 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const bf16_t* __restrict
                                                         float* __restrict__ gtype, float* __restrict__ ggamma,
                                                         float* __restrict__ gbeta, int B, int S, int H, int bpc,
                                                         int pos_is_arange, DropoutParams dp) {
+  dp = resolve_seed(dp);
   __shared__ float red[4][4][NE * 64];
   const int lane = threadIdx.x & 63;
   const int wid = threadIdx.x >> 6;

@@ -256,6 +256,7 @@ __device__ __forceinline__ void wait_vmcnt() {
 
 template <int LA, int LB, int EPI, int BM_, int BN_, int WM, int WN, int NS>
 __global__ __launch_bounds__(512, 1) void gemm_dma_kernel(GemmParams p) {
+  p.dp = resolve_seed(p.dp);
   constexpr bool SWAP = EPI != EPI_F32_ATOMIC;
   constexpr int TA = BM_ * 64, TB = BN_ * 64, STAGE = TA + TB;
   constexpr int MB = BM_ / WM / 32, NB = BN_ / WN / 32;
@@ -364,6 +365,7 @@ static void gemm_dma_launch(const GemmParams& p0, int splits, hipStream_t st) {
 
 template <int LA, int LB, int EPI>
 __global__ __launch_bounds__(256, 2) void gemm_kernel(GemmParams p) {
+  p.dp = resolve_seed(p.dp);
   constexpr bool SWAP = EPI != EPI_F32_ATOMIC;
   __shared__ __attribute__((aligned(16))) bf16_t smem[2 * 2 * TILE_ELEMS];  // [stage][A|B][tile]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -462,6 +464,7 @@ static void gemm_launch(const GemmParams& p0, int splits, hipStream_t st) {
 // spread between the MFMA groups of stage t; one barrier per K-tile.
 template <int LA, int LB, int EPI, int BM_, int BN_>
 __global__ __launch_bounds__(256, 1) void gemm_big_kernel(GemmParams p) {
+  p.dp = resolve_seed(p.dp);
   constexpr bool SWAP = EPI != EPI_F32_ATOMIC;
   constexpr int NS = 2;
   constexpr int TA = BM_ * 64, TB = BN_ * 64, STAGE = TA + TB;

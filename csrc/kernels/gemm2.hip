@@ -81,6 +81,7 @@ __device__ __forceinline__ bf16x8 frag(const bf16_t* img, int rbase, int ks, int
 
 template <int LA, int LB, int EPI, int BN, int SYNC>
 __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
+  p.dp = resolve_seed(p.dp);
   constexpr int WN = BN / 4;       // wave tile columns
   constexpr int NREP = WN / 16;    // 16-col MFMA blocks per wave
   constexpr int NB0 = 2;           // B-sub0 blocks (cols 0..31 of the wave)
@@ -410,6 +411,7 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
 // 16-row MFMA block at a time through a wave-private LDS slice placed AFTER the two operand stages.
 template <int EPI, int BN>
 __global__ __launch_bounds__(512, 1) void gemm2p_kernel(G2Params p, int ntiles) {
+  p.dp = resolve_seed(p.dp);
   constexpr int WN = BN / 4, NREP = WN / 16, NB0 = 2, NB1 = NREP - NB0;
   constexpr int TA = BM * 64, TB = BN * 64, STAGE = TA + TB;
   constexpr int GA = 4, GB = BN / 64, G = GA + GB;

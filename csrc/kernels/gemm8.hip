@@ -56,6 +56,7 @@ __device__ __forceinline__ f32x4 mma8(const i32x8& b, const i32x8& a, const f32x
 template <int EPI, int BN, int FA, int FB>
 __global__ __launch_bounds__(512, 1) void gemm8_kernel(G2Params p, const float* __restrict__ sa,
                                                        const float* __restrict__ sb) {
+  p.dp = resolve_seed(p.dp);
   constexpr int WN = BN / 4;
   constexpr int NREP = WN / 16;
   constexpr int NB0 = 2;

@@ -25,6 +25,7 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
                                                      bf16_t* __restrict__ z_out, bf16_t* __restrict__ out,
                                                      float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                      int rows, int H, float eps, DropoutParams dp) {
+  dp = resolve_seed(dp);
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * kLnWaves + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -188,6 +189,7 @@ __global__ __launch_bounds__(256) void ln_bwd_rows_kernel(const bf16_t* __restri
                                                           bf16_t* __restrict__ dy_out,
                                                           const bf16_t* __restrict__ dres_add, int rows, int H,
                                                           DropoutParams dp) {
+  dp = resolve_seed(dp);
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * kLnWaves + (threadIdx.x >> 6);
   if (row >= rows) return;
@@ -292,6 +294,7 @@ __global__ __launch_bounds__(256) void ln_bwd_fused_kernel(const bf16_t* __restr
                                                            float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                            float* __restrict__ dbias, int rows, int H, int rpw,
                                                            DropoutParams dp) {
+  dp = resolve_seed(dp);
   __shared__ float red[kLnWaves][3][NCH * 256];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nq = H >> 2;
