@@ -1,0 +1,125 @@
+"""Trainer-level behaviour on CPU (SURVEY.md §4 'unit / CPU', §5 checkpoint/resume): resume equals
+uninterrupted training, gradient accumulation equals the full batch, the MLM task end to end, and the
+GPU-only switches (--dtype fp8, --hip_graph) degrading cleanly on CPU."""
+import json
+import os
+
+import pytest
+import torch
+
+from huggingface_sagemaker_tensorflow_distributed_amd.models import build_model, resolve_config
+from huggingface_sagemaker_tensorflow_distributed_amd.optim import FusedAdam
+from huggingface_sagemaker_tensorflow_distributed_amd.parallel import FlatParamStore
+from huggingface_sagemaker_tensorflow_distributed_amd.train.callbacks import load_checkpoint, save_checkpoint
+from huggingface_sagemaker_tensorflow_distributed_amd.train.trainer import Trainer
+
+CPU = torch.device("cpu")
+
+
+def _trainer(dropout=0.1, seed=0, **kw):
+    cfg = resolve_config("hsd-tiny-bert").replace(hidden_dropout_prob=dropout, attention_probs_dropout_prob=dropout)
+    model = build_model(cfg, seed=seed)
+    model.rng.base_seed = 7
+    store = FlatParamStore(model, CPU)
+    opt = FusedAdam(store, lr=1e-3)
+    return Trainer(model, store, opt, None, CPU, **kw)
+
+
+def _batches(n, B=8, S=16, seed=0):
+    g = torch.Generator().manual_seed(seed)
+    out = []
+    for _ in range(n):
+        am = torch.ones(B, S, dtype=torch.long)
+        am[::3, S // 2:] = 0
+        out.append({"input_ids": torch.randint(5, 1024, (B, S), generator=g), "attention_mask": am,
+                    "labels": torch.randint(0, 2, (B,), generator=g)})
+    return out
+
+
+def test_checkpoint_resume_equals_uninterrupted(tmp_path):
+    data = _batches(4)
+    ref = _trainer()
+    for b in data:
+        ref.train_step([b])
+    a = _trainer()
+    for b in data[:2]:
+        a.train_step([b])
+    ck = str(tmp_path / "checkpoint-1")
+    save_checkpoint(ck, a, epoch=1)
+    assert sorted(os.listdir(ck)) == ["config.json", "model.safetensors", "optimizer.pt", "trainer_state.json"]
+    assert json.load(open(os.path.join(ck, "trainer_state.json")))["global_step"] == 2
+    b = _trainer(seed=123)  # different init: everything must come from the checkpoint
+    st = load_checkpoint(ck, b)
+    assert st["epoch"] == 1 and b.global_step == 2
+    for x in data[2:]:
+        b.train_step([x])
+    torch.testing.assert_close(b.store.master, ref.store.master, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(b.optimizer.exp_avg_sq, ref.optimizer.exp_avg_sq, rtol=1e-5, atol=1e-9)
+
+
+def test_gradient_accumulation_equals_full_batch():
+    """k micro-steps of B/k == one step of B (dropout off: the masks of the two runs differ per call)."""
+    full = _batches(1, B=8)[0]
+    halves = [{k: v[:4] for k, v in full.items()}, {k: v[4:] for k, v in full.items()}]
+    a = _trainer(dropout=0.0)
+    a.train_step([full])
+    b = _trainer(dropout=0.0, grad_accum=2)
+    b.train_step(halves)
+    torch.testing.assert_close(b.store.master, a.store.master, rtol=1e-5, atol=1e-6)
+
+
+def test_dropout_masks_change_per_step_but_replay_within_step():
+    tr = _trainer()
+    b = _batches(1)[0]
+    m = tr.model
+    m.train()
+    m.rng.new_step(3)
+    l1 = m(b["input_ids"], attention_mask=b["attention_mask"], labels=b["labels"])[0]
+    m.rng.new_step(3)
+    l2 = m(b["input_ids"], attention_mask=b["attention_mask"], labels=b["labels"])[0]
+    m.rng.new_step(4)
+    l3 = m(b["input_ids"], attention_mask=b["attention_mask"], labels=b["labels"])[0]
+    assert float(l1.detach()) == float(l2.detach()) and float(l1.detach()) != float(l3.detach())
+
+
+def test_graph_step_seed_is_deterministic_and_varies():
+    from huggingface_sagemaker_tensorflow_distributed_amd.train.graph import step_seed
+
+    assert step_seed(7, 0, 5) == step_seed(7, 0, 5)
+    seeds = {step_seed(7, r, s) for r in range(4) for s in range(64)}
+    assert len(seeds) == 4 * 64
+    assert all(0 <= w < 2 ** 32 for s in seeds for w in s)
+
+
+def test_hip_graph_flag_stays_eager_on_cpu():
+    tr = _trainer(hip_graph=True)
+    assert tr._seed is None
+    tr.train_step(_batches(1))
+
+
+def _run_script(tmp_path, extra, monkeypatch):
+    from huggingface_sagemaker_tensorflow_distributed_amd.train.runner import run
+
+    d, m = tmp_path / "data", tmp_path / "model"
+    monkeypatch.setenv("SM_OUTPUT_DATA_DIR", str(d))
+    monkeypatch.setenv("SM_MODEL_DIR", str(m))
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        monkeypatch.delenv(k, raising=False)
+    return run(["--epochs", "1", "--train_batch_size", "4", "--eval_batch_size", "4", "--max_steps", "2",
+                "--num_train_examples", "16", "--num_eval_examples", "8", "--log_every", "0"] + extra), d, m
+
+
+def test_masked_lm_task_end_to_end_cpu(tmp_path, monkeypatch):
+    out, d, m = _run_script(tmp_path, ["--model_name_or_path", "hsd-tiny-roberta", "--task", "masked-lm",
+                                       "--max_seq_length", "32"], monkeypatch)
+    tr = open(d / "train_results.txt").read()
+    assert tr.startswith("loss = [") and "sparse_categorical_accuracy = [" in tr
+    cfg = json.load(open(m / "config.json"))
+    assert cfg["architectures"] == ["RobertaForMaskedLM"]
+
+
+def test_fp8_dtype_falls_back_to_bf16_on_cpu(tmp_path, monkeypatch):
+    """--dtype fp8 is a GPU (HIP) feature; on CPU the run completes in bf16 with a warning."""
+    out, d, m = _run_script(tmp_path, ["--model_name_or_path", "hsd-tiny-bert", "--dtype", "fp8",
+                                       "--max_seq_length", "16"], monkeypatch)
+    assert os.path.isfile(d / "eval_results.txt") and os.path.isfile(m / "model.safetensors")
