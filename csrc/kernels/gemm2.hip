@@ -305,6 +305,101 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
     G2_BARRIER();
 #undef G2_MMA
 #undef G2_SB
+  } else if constexpr (SYNC == 4 || SYNC == 5) {
+    // Staggered 4-phase schedule (cdna_hip_programming.md §5 "256² 8-phase template"; MI355X_MICROARCH.md
+    // "Two waves per SIMD" item 9): the wave groups wm = 0 / 1 — one wave of each on every SIMD — run ONE
+    // barrier apart, so on every SIMD one wave's MFMA cluster overlaps the other wave's LDS reads and DMA
+    // issue. Each phase is   reads (+ DMA issue) -> lgkmcnt(0) -> barrier -> MFMA cluster -> barrier.
+    // * lgkmcnt(0) before the barrier: a group one barrier behind has COMPLETED (not just issued) the reads
+    //   of the phase it is in, so the P4 DMA into the current stage (tile t+2) cannot overwrite live data.
+    // * the counted vmcnt sits before P4's FIRST barrier (one barrier earlier than the unstaggered form), so
+    //   the lagging group's DMAs of tile t+1 have landed before the leading group reads them in P1(t+1).
+    // Tile t+1's DMA: SYNC 4 issues it in P1 / P2 (two MFMA phases to land), SYNC 5 spreads it over
+    // P1 / P2 / P3 (2 pieces per phase, fewer issue stalls per phase); D0 slots of tile t+2 go out in P4.
+    constexpr int E1 = SYNC == 4 ? D0 + (G - D0 + 1) / 2 : D0 + 2;
+    constexpr int E2 = SYNC == 4 ? G : (D0 + 4 < G ? D0 + 4 : G);
+#define G2_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+#define G2_CLUSTER(ACC_I0, FA, FB, NBX, J0)                                                                  \
+  __builtin_amdgcn_s_setprio(1);                                                                             \
+  _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) _Pragma("unroll") for (int i = 0; i < 4; ++i)               \
+      _Pragma("unroll") for (int j = 0; j < NBX; ++j) acc[ACC_I0 + i][J0 + j] =                                \
+          __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[j][ks], FA[i][ks], acc[ACC_I0 + i][J0 + j], 0, 0, 0);     \
+  __builtin_amdgcn_s_setprio(0);
+#pragma unroll
+    for (int q = 0; q < G; ++q) dma_slot(q, smem, kbeg);
+    if (nt > 1) {
+#pragma unroll
+      for (int q = 0; q < D0; ++q) dma_slot(q, smem + STAGE, kbeg + BK);
+      vmcnt<D0>();
+    } else {
+      vmcnt<0>();
+    }
+    G2_BARRIER();
+    if (wm == 1) G2_BARRIER();
+    for (int t = 0; t < nt; ++t) {
+      const bf16_t* cA = smem + (t & 1) * STAGE;
+      const bf16_t* cB = cA + TA;
+      bf16_t* nS = smem + ((t + 1) & 1) * STAGE;
+      const bool n1 = t + 1 < nt, n2 = t + 2 < nt;
+      const int k1 = kbeg + (t + 1) * BK, k2 = kbeg + (t + 2) * BK;
+      // P1: A-sub0 + B-sub0 reads, first part of tile t+1's DMA
+#pragma unroll
+      for (int j = 0; j < NB0; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) fb0[j][ks] = frag<LB>(cB, bcol + 16 * j, ks, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<LA>(cA, arow + 16 * i, ks, lane);
+      if (n1) {
+#pragma unroll
+        for (int q = D0; q < E1; ++q) dma_slot(q, nS, k1);
+      }
+      G2_LGKM0();
+      G2_BARRIER();
+      G2_CLUSTER(0, fa, fb0, NB0, 0)
+      G2_BARRIER();
+      // P2: B-sub1 reads, more of tile t+1's DMA
+#pragma unroll
+      for (int j = 0; j < NB1; ++j)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) fb1[j][ks] = frag<LB>(cB, bcol + 16 * (NB0 + j), ks, lane);
+      if (n1) {
+#pragma unroll
+        for (int q = E1; q < E2; ++q) dma_slot(q, nS, k1);
+      }
+      G2_LGKM0();
+      G2_BARRIER();
+      G2_CLUSTER(0, fa, fb1, NB1, NB0)
+      G2_BARRIER();
+      // P3: A-sub1 reads (+ the rest of tile t+1's DMA, SYNC 5)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<LA>(cA, arow + 64 + 16 * i, ks, lane);
+      if (n1) {
+#pragma unroll
+        for (int q = E2; q < G; ++q) dma_slot(q, nS, k1);
+      }
+      G2_LGKM0();
+      G2_BARRIER();
+      G2_CLUSTER(4, fa, fb1, NB1, NB0)
+      G2_BARRIER();
+      // P4: no reads; D0 slots of tile t+2 into this stage; retire tile t+1
+      if (n2) {
+#pragma unroll
+        for (int q = 0; q < D0; ++q) dma_slot(q, const_cast<bf16_t*>(cA), k2);
+        vmcnt<D0>();
+      } else {
+        vmcnt<0>();
+      }
+      G2_BARRIER();
+      G2_CLUSTER(4, fa, fb0, NB0, 0)
+      G2_BARRIER();
+    }
+    if (wm == 0) G2_BARRIER();
+#undef G2_CLUSTER
+#undef G2_LGKM0
   } else {
     // ONE barrier per K-tile: tile t+1's DMA (into the other stage, free since the previous barrier) is
     // issued in two halves at the start of P1 / P2 and retired by vmcnt(0) before the end-of-tile
@@ -602,15 +697,16 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
 
 }  // namespace g2
 
-// Main-loop schedule (tools/ab_gemm2.py, interleaved in one process): NT (forward / dgrad) runs best with
-// one barrier per K-tile (SYNC 1: +3-10 % at 131k tokens; at 32k tokens the 8-phase form still wins for
-// K >= 2304 by ~5 %), the TT wgrad with the 8-phase form (SYNC 0). The persistent NT kernel (3) and the
-// pipelined-read form (2) measured within noise / slower. HSD_G2_SYNC overrides for A/B runs;
+// Main-loop schedule (tools/gemm_probe.py, interleaved rounds in one process, random operands, T = 131072
+// tokens; profiles/gemm_probe_r1_sync.json): NT (forward / dgrad) runs best with the staggered 4-phase
+// form (SYNC 4: +5-10 % over one-barrier-per-K-tile SYNC 1 on every BERT shape, +15 % at 8192^3); the TT
+// wgrad with the unstaggered 8-phase form (SYNC 0; the stagger is neutral there). The persistent NT kernel
+// (3) and the pipelined-read form (2) measured within noise / slower. HSD_G2_SYNC overrides for A/B runs;
 // HSD_G2_NT=1 makes the epilogue stores non-temporal (measured neutral).
 static int g2_sync_mode(int la, int K) {
   const char* e = getenv("HSD_G2_SYNC");
   if (e) return atoi(e);
-  return la == 0 ? 1 : 0;
+  return la == 0 ? 4 : 0;
 }
 
 template <int EPI, int BN>
@@ -653,6 +749,8 @@ static void g2_launch(const G2Params& p0, int splits, hipStream_t st) {
   const int mode = g2_sync_mode(LA, p.K);
   if (mode == 1) hipLaunchKernelGGL((g2::gemm2_kernel<LA, LB, EPI, BN, 1>), grid, dim3(512), 0, st, p);
   else if (mode == 2) hipLaunchKernelGGL((g2::gemm2_kernel<LA, LB, EPI, BN, 2>), grid, dim3(512), 0, st, p);
+  else if (mode == 4) hipLaunchKernelGGL((g2::gemm2_kernel<LA, LB, EPI, BN, 4>), grid, dim3(512), 0, st, p);
+  else if (mode == 5) hipLaunchKernelGGL((g2::gemm2_kernel<LA, LB, EPI, BN, 5>), grid, dim3(512), 0, st, p);
   else hipLaunchKernelGGL((g2::gemm2_kernel<LA, LB, EPI, BN, 0>), grid, dim3(512), 0, st, p);
   HSD_CHECK_LAUNCH();
 }

@@ -180,6 +180,28 @@ def test_gemm2_tt_wgrad(gpu, M, N, K, epi):
     _check(C, C0 + A.float().t() @ B.float(), 1e-3)
 
 
+@pytest.mark.parametrize("sync", [0, 1, 4, 5])
+@pytest.mark.parametrize("M,N,K", [(1000, 960, 192), (768, 3072, 512), (2048, 768, 3072)])
+def test_gemm2_schedules(gpu, monkeypatch, sync, M, N, K):
+    """Every main-loop schedule (HSD_G2_SYNC: 8-phase, one-barrier, staggered 4 / 5) gives the fp32-reference
+    NT product (bias epilogue) and, where the shape tiles, the TT weight gradient (tokens = M)."""
+    monkeypatch.setenv("HSD_G2_SYNC", str(sync))
+    torch.manual_seed(21)
+    C_ = _C()
+    A, B, bias = _mk((M, K), gpu), _mk((N, K), gpu, 0.1), _mk((N,), gpu)
+    C = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    C_.gemm2(A, B, C, 0, 0, 1, bias, None, None, 0.0, 0, 1, None, None)
+    _check(C, A.float() @ B.float().t() + bias.float())
+    if K % 256 == 0 and M % 64 == 0:
+        dy = _mk((M, N), gpu)
+        G0 = torch.randn(N, K, device=gpu)
+        G = G0.clone()
+        sp = C_.gemm2_splits(N, K, M)
+        ws = torch.empty(sp * N * K, device=gpu)
+        C_.gemm2(dy, A, G, 1, 1, 7, None, None, None, 0.0, 0, sp, ws, None)
+        _check(G, G0 + dy.float().t() @ A.float(), 1e-3)
+
+
 def test_gemm2_dgelu_fused_dbias(gpu):
     torch.manual_seed(13)
     C_ = _C()
