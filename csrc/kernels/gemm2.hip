@@ -92,7 +92,9 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
   constexpr int GA = 4;                              // DMA instructions per wave per stage for A
   constexpr int GB = (LB == 0) ? BN / 64 : 4;        // ... for B
   constexpr int G = GA + GB;                         // 8 (BN 256) or 7 (BN 192)
-  constexpr int D0 = 2;                              // issued in P4 of the previous tile
+  // slots of tile t+2 issued in P4 of tile t (the rest in P1-P3 of t+1); SYNC 6 / 7 = SYNC 0 / 4 with the
+  // WHOLE next-next tile issued in P4, so every DMA has a full K-tile of MFMAs to land
+  constexpr int D0 = (SYNC == 6 || SYNC == 7) ? G : 2;
   constexpr bool F32OUT = EPI == E2_F32_ATOMIC || EPI == E2_F32_SLAB;
 
   __shared__ __attribute__((aligned(16))) bf16_t smem[2 * STAGE];
@@ -128,7 +130,7 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
   const int arow = wm * 128;
   const int bcol = wn * WN;
   bf16x8 fa[4][2], fb0[NB0][2], fb1[NB1][2];
-  if constexpr (SYNC == 0) {
+  if constexpr (SYNC == 0 || SYNC == 6) {
     // prologue: tile 0 whole, first D0 slots of tile 1
   #pragma unroll
     for (int q = 0; q < G; ++q) dma_slot(q, smem, kbeg);
@@ -160,7 +162,7 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
         for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<LA>(cA, arow + 16 * i, ks, lane);
       if (n1) {
   #pragma unroll
-        for (int q = D0; q < D0 + 2; ++q) dma_slot(q, nS, k1);
+        for (int q = D0; q < (D0 + 2 < G ? D0 + 2 : G); ++q) dma_slot(q, nS, k1);
       }
       G2_BARRIER();
       __builtin_amdgcn_s_setprio(1);
@@ -181,7 +183,7 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
         for (int ks = 0; ks < 2; ++ks) fb1[j][ks] = frag<LB>(cB, bcol + 16 * (NB0 + j), ks, lane);
       if (n1) {
   #pragma unroll
-        for (int q = D0 + 2; q < D0 + 4; ++q) dma_slot(q, nS, k1);
+        for (int q = D0 + 2; q < (D0 + 4 < G ? D0 + 4 : G); ++q) dma_slot(q, nS, k1);
       }
       G2_BARRIER();
       __builtin_amdgcn_s_setprio(1);
@@ -305,7 +307,7 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
     G2_BARRIER();
 #undef G2_MMA
 #undef G2_SB
-  } else if constexpr (SYNC == 4 || SYNC == 5) {
+  } else if constexpr (SYNC == 4 || SYNC == 5 || SYNC == 7) {
     // Staggered 4-phase schedule (cdna_hip_programming.md §5 "256² 8-phase template"; MI355X_MICROARCH.md
     // "Two waves per SIMD" item 9): the wave groups wm = 0 / 1 — one wave of each on every SIMD — run ONE
     // barrier apart, so on every SIMD one wave's MFMA cluster overlaps the other wave's LDS reads and DMA
@@ -316,8 +318,8 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
     //   the lagging group's DMAs of tile t+1 have landed before the leading group reads them in P1(t+1).
     // Tile t+1's DMA: SYNC 4 issues it in P1 / P2 (two MFMA phases to land), SYNC 5 spreads it over
     // P1 / P2 / P3 (2 pieces per phase, fewer issue stalls per phase); D0 slots of tile t+2 go out in P4.
-    constexpr int E1 = SYNC == 4 ? D0 + (G - D0 + 1) / 2 : D0 + 2;
-    constexpr int E2 = SYNC == 4 ? G : (D0 + 4 < G ? D0 + 4 : G);
+    constexpr int E1 = SYNC != 5 ? D0 + (G - D0 + 1) / 2 : D0 + 2;
+    constexpr int E2 = SYNC != 5 ? G : (D0 + 4 < G ? D0 + 4 : G);
 #define G2_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
 #define G2_CLUSTER(ACC_I0, FA, FB, NBX, J0)                                                                  \
   __builtin_amdgcn_s_setprio(1);                                                                             \
@@ -706,7 +708,7 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
 static int g2_sync_mode(int la, int K) {
   const char* e = getenv("HSD_G2_SYNC");
   if (e) return atoi(e);
-  return la == 0 ? 4 : 0;
+  return la == 0 ? 4 : 7;
 }
 
 template <int EPI, int BN>
@@ -751,6 +753,8 @@ static void g2_launch(const G2Params& p0, int splits, hipStream_t st) {
   else if (mode == 2) hipLaunchKernelGGL((g2::gemm2_kernel<LA, LB, EPI, BN, 2>), grid, dim3(512), 0, st, p);
   else if (mode == 4) hipLaunchKernelGGL((g2::gemm2_kernel<LA, LB, EPI, BN, 4>), grid, dim3(512), 0, st, p);
   else if (mode == 5) hipLaunchKernelGGL((g2::gemm2_kernel<LA, LB, EPI, BN, 5>), grid, dim3(512), 0, st, p);
+  else if (mode == 6) hipLaunchKernelGGL((g2::gemm2_kernel<LA, LB, EPI, BN, 6>), grid, dim3(512), 0, st, p);
+  else if (mode == 7) hipLaunchKernelGGL((g2::gemm2_kernel<LA, LB, EPI, BN, 7>), grid, dim3(512), 0, st, p);
   else hipLaunchKernelGGL((g2::gemm2_kernel<LA, LB, EPI, BN, 0>), grid, dim3(512), 0, st, p);
   HSD_CHECK_LAUNCH();
 }

@@ -180,7 +180,7 @@ def test_gemm2_tt_wgrad(gpu, M, N, K, epi):
     _check(C, C0 + A.float().t() @ B.float(), 1e-3)
 
 
-@pytest.mark.parametrize("sync", [0, 1, 4, 5])
+@pytest.mark.parametrize("sync", [0, 1, 4, 5, 6, 7])
 @pytest.mark.parametrize("M,N,K", [(1000, 960, 192), (768, 3072, 512), (2048, 768, 3072)])
 def test_gemm2_schedules(gpu, monkeypatch, sync, M, N, K):
     """Every main-loop schedule (HSD_G2_SYNC: 8-phase, one-barrier, staggered 4 / 5) gives the fp32-reference

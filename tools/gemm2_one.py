@@ -8,7 +8,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 from huggingface_sagemaker_tensorflow_distributed_amd.ops import hip  # noqa: E402
 
 C_ = hip._C
-T = 32768
+T = int(os.environ.get("G1_T", "32768"))
 which = sys.argv[1] if len(sys.argv) > 1 else "fwd"
 N, K = (3072, 768) if which in ("fwd", "gelu", "dgelu", "wgrad") else (768, 768)
 x = torch.randn(T, K, device="cuda").bfloat16()
