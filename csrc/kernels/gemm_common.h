@@ -150,9 +150,14 @@ __device__ __forceinline__ void epilogue_bf16(f32x4 (&acc)[8][BN / 64], const G2
                                               int lane, int mw, int nw) {
   constexpr int WN = BN / 4, NREP = WN / 16;
   const int q4 = lane >> 4, lr = lane & 15;
-  // stage bf16(acc [+ bias]) through a wave-private LDS slice ([64 rows][WN + 8]), then write whole
+  // stage bf16(acc [+ bias]) through a wave-private LDS slice ([64 rows][SROW]), then write whole
   // rows with 16-B lanes: each lane owns 8 consecutive n of one m.
-  constexpr int SROW = WN + 8;
+  // WN = 64 (BN 256): unpadded 128-B rows whose 8-B slots are XOR-swizzled by (row & 15) -- the 16 lanes of a
+  // ds_write_b64 group (16 rows, one slot) then cover all 32 banks, and a ds_read_b128 of chunk c8 finds its
+  // two halves in chunk c8 ^ ((row & 15) >> 1), swapped when row is odd (both conflict-free; the padded
+  // [64][72] image measured 12 % LDS bank-conflict cycles, tools/pmc_gemm2.sh). Other widths keep the pad.
+  constexpr bool kSwz = WN == 64;
+  constexpr int SROW = kSwz ? WN : WN + 8;
   constexpr int CPR = WN / 8;  // 16-B chunks per row
   constexpr bool kBias = epi_bias(EPI);
   constexpr bool kAux = epi_aux(EPI);
@@ -177,7 +182,9 @@ __device__ __forceinline__ void epilogue_bf16(f32x4 (&acc)[8][BN / 64], const G2
       for (int j = 0; j < NREP; ++j) {
         f32x4 v = acc[4 * h + i][j];
         if constexpr (kBias) v += bv[j];
-        *reinterpret_cast<u32x2*>(stg + (16 * i + lr) * SROW + 16 * j + 4 * q4) = pack4(v);
+        const int row = 16 * i + lr;
+        const int col = kSwz ? (((4 * j + q4) ^ (row & 15)) << 2) : 16 * j + 4 * q4;
+        *reinterpret_cast<u32x2*>(stg + row * SROW + col) = pack4(v);
       }
     __builtin_amdgcn_wave_barrier();
     constexpr int ITER = 64 * CPR / 64;
@@ -186,7 +193,13 @@ __device__ __forceinline__ void epilogue_bf16(f32x4 (&acc)[8][BN / 64], const G2
     for (int it = 0; it < ITER; ++it) {
       const int idx = lane + 64 * it;
       const int row = idx / CPR, c8 = idx % CPR;
-      sv[it] = *reinterpret_cast<const u32x4*>(stg + row * SROW + c8 * 8);
+      if constexpr (kSwz) {
+        const int hs = row & 15;
+        const u32x4 t = *reinterpret_cast<const u32x4*>(stg + row * SROW + ((c8 ^ (hs >> 1)) << 3));
+        sv[it] = (hs & 1) ? u32x4{t.z, t.w, t.x, t.y} : t;
+      } else {
+        sv[it] = *reinterpret_cast<const u32x4*>(stg + row * SROW + c8 * 8);
+      }
       if constexpr (kAux) {
         const int m = min(mw + 64 * h + row, p.M - 1);
         xv[it] = *reinterpret_cast<const u32x4*>(p.aux + (int64_t)m * p.ldaux + nw + c8 * 8);
