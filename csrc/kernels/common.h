@@ -155,6 +155,28 @@ __device__ __forceinline__ void gelu_and_grad(float x, float& g, float& dg) {
   dg = fmaf(x * 0.3989422804014327f, q.e, half_1p_erf);
 }
 
+// Two elements per call on packed f32 math (v_pk_fma_f32 / v_pk_mul_f32: two lanes' worth of FMA per issue;
+// only v_rcp / v_exp stay scalar) for the VALU-bound GELU epilogue of the FFN1 GEMM; same FMAs, same results
+// as gelu_and_grad.
+__device__ __forceinline__ void gelu_and_grad2(f32x2 x, f32x2& g, f32x2& dg) {
+  const f32x2 a = {fabsf(x.x), fabsf(x.y)};
+  const f32x2 den = __builtin_elementwise_fma(a, f32x2{0.23164189784f, 0.23164189784f}, f32x2{1.0f, 1.0f});
+  const f32x2 t = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
+  f32x2 P = __builtin_elementwise_fma(t, f32x2{1.061405429f, 1.061405429f}, f32x2{-1.453152027f, -1.453152027f});
+  P = __builtin_elementwise_fma(t, P, f32x2{1.421413741f, 1.421413741f});
+  P = __builtin_elementwise_fma(t, P, f32x2{-0.284496736f, -0.284496736f});
+  P = __builtin_elementwise_fma(t, P, f32x2{0.254829592f, 0.254829592f});
+  P = P * t;
+  const f32x2 q = x * x * f32x2{-0.72134752044f, -0.72134752044f};
+  const f32x2 e = {__builtin_amdgcn_exp2f(q.x), __builtin_amdgcn_exp2f(q.y)};
+  const f32x2 pe = P * e;
+  const f32x2 pos = __builtin_elementwise_fma(f32x2{-0.5f, -0.5f}, pe, f32x2{1.0f, 1.0f});
+  const f32x2 neg = f32x2{0.5f, 0.5f} * pe;
+  const f32x2 h = {x.x >= 0.0f ? pos.x : neg.x, x.y >= 0.0f ? pos.y : neg.y};
+  g = x * h;
+  dg = __builtin_elementwise_fma(x * f32x2{0.3989422804014327f, 0.3989422804014327f}, e, h);
+}
+
 }  // namespace hsd
 
 // Debug build (HSD_DEBUG=1 python -m ..._build, loaded as _C_debug when HSD_DEBUG=1 at run time;

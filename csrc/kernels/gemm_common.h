@@ -84,7 +84,11 @@ __device__ __forceinline__ void epi_chunk(u32x4& o, u32x4& o2, const u32x4& x, i
     float v[8] = {lo_bf(o.x), hi_bf(o.x), lo_bf(o.y), hi_bf(o.y), lo_bf(o.z), hi_bf(o.z), lo_bf(o.w), hi_bf(o.w)};
     float a[8], d[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) gelu_and_grad(v[e], a[e], d[e]);
+    for (int e = 0; e < 8; e += 2) {
+      f32x2 ga, gd;
+      gelu_and_grad2(f32x2{v[e], v[e + 1]}, ga, gd);
+      a[e] = ga.x; a[e + 1] = ga.y; d[e] = gd.x; d[e + 1] = gd.y;
+    }
     o.x = pack_bf2(d[0], d[1]); o.y = pack_bf2(d[2], d[3]); o.z = pack_bf2(d[4], d[5]); o.w = pack_bf2(d[6], d[7]);
     o2.x = pack_bf2(a[0], a[1]); o2.y = pack_bf2(a[2], a[3]); o2.z = pack_bf2(a[4], a[5]); o2.w = pack_bf2(a[6], a[7]);
   } else if constexpr (EPI == E2_BIAS_DROP_RES) {
