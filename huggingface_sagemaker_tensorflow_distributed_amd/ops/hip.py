@@ -2,9 +2,11 @@
 
 Parameter gradients never go through autograd's ``AccumulateGrad``: the backward kernels add them
 (fp32) straight into the parameter's slice of the flat ``main_grad`` buffer
-(:class:`parallel.FlatParamStore`) and then call ``p._hsd_ready()`` so the gradient bucket holding
-it can start its RCCL all-reduce while the rest of backward runs. Without a store (unit tests) the
-gradient is returned normally.
+(:class:`parallel.FlatParamStore`) and return ``None`` for it. Readiness for the gradient bucket's RCCL
+all-reduce is signalled once per parameter by the store's post-accumulate hook, which autograd runs
+right after the last node that used the parameter (so a tied weight — MLM decoder = word embeddings —
+is signalled only after both of its contributions). Without a store (unit tests) the gradient is
+returned normally.
 """
 from __future__ import annotations
 
@@ -41,10 +43,7 @@ class _Grad:
             return self.buf.to(self.p.dtype)
         if self.buf is not self.mg:
             self.mg.add_(self.buf.to(self.mg.dtype))
-        ready = getattr(self.p, "_hsd_ready", None)
-        if ready is not None:
-            ready()
-        return None
+        return None  # bucket readiness: FlatParamStore's post-accumulate hook (fires once, after all uses)
 
 
 # ------------------------------------------------------------------------------------------ wgrad stream

@@ -51,7 +51,8 @@ def init(device: Optional[str] = None, timeout_s: float = 1800.0, backend: Optio
         dev = torch.device("cuda", torch.cuda.current_device())
     else:
         dev = torch.device("cpu")
-    be = backend or ("nccl" if use_cuda else "gloo")
+    # HSD_DIST_BACKEND=gloo: force the CPU-transport backend (e.g. several ranks sharing one GPU in a test)
+    be = backend or os.environ.get("HSD_DIST_BACKEND") or ("nccl" if use_cuda else "gloo")
     here = False
     if env["world_size"] > 1 and not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")

@@ -78,9 +78,10 @@ class FlatParamStore:
             p.grad = None
         self._index: Dict[int, int] = {id(p): i for i, p in enumerate(self.params)}
         self._setup_transposed()
-        # gradient-ready notification: HIP backward kernels write main_grad directly and call
-        # p._hsd_ready(); torch-autograd gradients (CPU path, small torch-op heads) are folded into
-        # main_grad by a post-accumulate hook first.
+        # gradient-ready notification: HIP backward kernels write main_grad directly and return None;
+        # torch-autograd gradients (CPU path, small torch-op heads) are folded into main_grad here. Either
+        # way autograd runs the post-accumulate hook exactly once per parameter per backward, after every
+        # node that used it (tied weights included), and that hook is the ONE readiness signal.
         self.ready_callback = None
         self._hooks = []
         for i, p in enumerate(self.params):

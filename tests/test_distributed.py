@@ -157,3 +157,60 @@ def test_train_script_two_ranks_end_to_end(tmp_path):
     assert (tmp_path / "data" / "eval_results.txt").read_text().count(" = ") == 2
     assert (tmp_path / "model" / "model.safetensors").exists()
     assert (tmp_path / "model" / "tokenizer.json").exists()
+
+
+class _KernelLinear(torch.autograd.Function):
+    """Models the HIP-op contract: the weight gradient is added straight into ``main_grad`` and the
+    Function returns None for it (no AccumulateGrad payload)."""
+
+    @staticmethod
+    def forward(ctx, x, w):
+        ctx.save_for_backward(x, w)
+        return x @ w.t()
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, w = ctx.saved_tensors
+        w.main_grad.add_(dy.t() @ x)
+        return dy @ w, None
+
+
+def _worker_none_grad_tied(rank, world, port):
+    _setenv(rank, world, port)
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel import FlatParamStore, GradBucketer, backend
+
+    backend.init(device="cpu")
+    torch.manual_seed(0)
+    m = torch.nn.Module()
+    m.emb = torch.nn.Parameter(torch.randn(16, 8))   # tied: used by a kernel op AND by torch autograd
+    m.w1 = torch.nn.Parameter(torch.randn(8, 8))
+    m.w2 = torch.nn.Parameter(torch.randn(8, 8))
+    store = FlatParamStore(m, torch.device("cpu"))
+    buck = GradBucketer(store, bucket_mb=1e-4)  # ~one parameter per bucket
+    for step in range(2):
+        store.zero_grad()
+        buck.begin()
+        x = torch.randn(4, 16, generator=torch.Generator().manual_seed(rank + 10 * step))
+        h = x @ m.emb                                   # torch-autograd use of emb
+        h = _KernelLinear.apply(h, m.w1)
+        h = _KernelLinear.apply(torch.tanh(h), m.w2)
+        logits = _KernelLinear.apply(h, m.emb)          # kernel use of the tied weight
+        logits.square().mean().backward()
+        buck.finish()
+        ref = torch.zeros_like(store.grad)
+        for r in range(world):
+            mr = {n: p.detach().clone().requires_grad_(True) for n, p in (("emb", m.emb), ("w1", m.w1), ("w2", m.w2))}
+            xr = torch.randn(4, 16, generator=torch.Generator().manual_seed(r + 10 * step))
+            hr = torch.tanh((xr @ mr["emb"]) @ mr["w1"].t()) @ mr["w2"].t()
+            (hr @ mr["emb"].t()).square().mean().backward()
+            for i, n in enumerate(store.names):
+                s = store.segments[i]
+                ref[s.offset:s.offset + s.numel] += mr[n].grad.reshape(-1)
+        torch.testing.assert_close(store.grad, ref, atol=1e-5, rtol=1e-5)
+    backend.shutdown()
+
+
+def test_kernel_none_grads_and_tied_weight_signal_once():
+    """Ops that write main_grad and return None (the HIP path) plus a tied weight: every bucket is reduced
+    exactly once, after all contributions (regression: the readiness signal used to fire twice)."""
+    mp.spawn(_worker_none_grad_tied, args=(2, _port()), nprocs=2, join=True)
