@@ -51,11 +51,13 @@ class GradBucketer:
     """Static buckets over a :class:`FlatParamStore`'s gradient buffer."""
 
     def __init__(self, store: FlatParamStore, bucket_mb: Optional[float] = None, group=None,
-                 overlap: bool = True, native: Optional[bool] = None):
+                 overlap: bool = True, native: Optional[bool] = None, engine=None):
+        """``engine``: an explicit native CommEngine (tests drive a world-of-one RCCL communicator through
+        the full HIP backward with it; overlap is then on regardless of the world size)."""
         self.store = store
         self.group = group
-        self.world = backend.size()
-        self.overlap = overlap and self.world > 1
+        self.world = engine.world if engine is not None else backend.size()
+        self.overlap = overlap and (self.world > 1 or engine is not None)
         self.bucket_bytes = int((bucket_mb or DEFAULT_BUCKET_MB) * (1 << 20))
         esize = store.grad.element_size()
         self.buckets: List[_Bucket] = []
@@ -72,8 +74,8 @@ class GradBucketer:
             for pi in b.params:
                 self._param_bucket[pi] = b
         self.sync_enabled = True
-        self.engine = None
-        if (native is None or native) and group is None:
+        self.engine = engine
+        if engine is None and (native is None or native) and group is None:
             from .comm import get_engine
 
             try:
@@ -81,19 +83,19 @@ class GradBucketer:
             except Exception as e:  # pragma: no cover - depends on the RCCL install
                 logger.warning("native CommEngine unavailable (%s); using torch.distributed buckets", e)
                 self.engine = None
-            if self.engine is not None:
-                if store.device.type == "cuda":
-                    from ..ops import hip as _hip
+        if self.engine is not None:
+            if store.device.type == "cuda":
+                from ..ops import hip as _hip
 
-                    side = _hip.side_stream(store.device)
-                    if side is not None:
-                        self.engine.add_dependency_stream(side.cuda_stream)
-                param_bucket = [0] * len(store.segments)
-                for b in self.buckets:
-                    for pi in b.params:
-                        param_bucket[pi] = b.index
-                self.engine.set_buckets(store.grad, [b.start for b in self.buckets], [b.end for b in self.buckets],
-                                        [len(b.params) for b in self.buckets], param_bucket)
+                side = _hip.side_stream(store.device)
+                if side is not None:
+                    self.engine.add_dependency_stream(side.cuda_stream)
+            param_bucket = [0] * len(store.segments)
+            for b in self.buckets:
+                for pi in b.params:
+                    param_bucket[pi] = b.index
+            self.engine.set_buckets(store.grad, [b.start for b in self.buckets], [b.end for b in self.buckets],
+                                    [len(b.params) for b in self.buckets], param_bucket)
         store.ready_callback = self.mark_ready
 
     # ---------------------------------------------------------------- hooks
@@ -131,10 +133,12 @@ class GradBucketer:
 
     def finish(self) -> None:
         """Launch any bucket not yet launched (unused params / no-overlap mode), then wait all."""
-        if self.world <= 1 or not self.sync_enabled:
+        if not self.sync_enabled:
             return
         if self.engine is not None:
             self.engine.finish()  # launches unlaunched buckets; compute stream waits (host does not)
+            return
+        if self.world <= 1:
             return
         for b in self.buckets:
             if not b.launched:
