@@ -87,6 +87,15 @@ def main():
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
     dt = float(t.item())
     ms = dt * 1e3 / a.steps
+    # comm/compute overlap of one extra, untimed step (native RCCL engine only): per-bucket HIP events
+    overlap = None
+    buck = trainer.bucketer
+    if buck is not None and buck.set_timing(True):
+        trainer.train_step([batches[0]])
+        overlap = buck.overlap_report()
+        buck.set_timing(False)
+        if overlap is not None:
+            overlap.pop("buckets", None)
     value = a.batch_size * world * a.steps / dt
     if rank == 0:
         print(json.dumps({
@@ -101,6 +110,7 @@ def main():
                        "hip_graph": trainer._seed is not None,
                        "comm": ("native-rccl" if getattr(trainer.bucketer, "engine", None) is not None
                                 else ("torch-" + backend.state().backend if world > 1 else "none"))},
+            **({"comm_overlap": overlap} if overlap is not None else {}),
         }), flush=True)
     backend.shutdown()
 

@@ -65,6 +65,7 @@ struct Bucket {
   int pending = 0;
   bool launched = false;
   hipEvent_t done = nullptr;
+  hipEvent_t t_start = nullptr, t_end = nullptr;  // timing events (only with set_timing(true))
 };
 
 class CommEngine {
@@ -136,8 +137,11 @@ class CommEngine {
     check(flat);
     if (starts.size() != ends.size() || starts.size() != counts.size())
       throw std::runtime_error("set_buckets: size mismatch");
-    for (auto& b : buckets_)
+    for (auto& b : buckets_) {
       if (b.done) (void)hipEventDestroy(b.done);
+      if (b.t_start) (void)hipEventDestroy(b.t_start);
+      if (b.t_end) (void)hipEventDestroy(b.t_end);
+    }
     buckets_.clear();
     flat_ = flat;
     for (size_t i = 0; i < starts.size(); ++i) {
@@ -147,6 +151,8 @@ class CommEngine {
       b.nparams = (int)counts[i];
       if (b.start < 0 || b.end > flat.numel() || b.start > b.end) throw std::runtime_error("set_buckets: bad range");
       HIP_OK(hipEventCreateWithFlags(&b.done, hipEventDisableTiming));
+      HIP_OK(hipEventCreate(&b.t_start));
+      HIP_OK(hipEventCreate(&b.t_end));
       buckets_.push_back(b);
     }
     param_bucket_.assign(param_bucket.begin(), param_bucket.end());
@@ -158,6 +164,42 @@ class CommEngine {
       b.pending = b.nparams;
       b.launched = false;
     }
+    if (timing_) HIP_OK(hipEventRecord(t_begin_, caller()));
+  }
+
+  // ---------------------------------------------------------------- overlap timeline
+  // With timing on, a step records: t_begin on the compute stream at begin_step, per-bucket start/end
+  // around each ncclAllReduce on the comm stream, and t_bwd_end on the compute stream when finish() is
+  // called (= every backward kernel queued). Off by default: timing events cost a little per record.
+  void set_timing(bool on) {
+    if (on && !t_begin_) {
+      HIP_OK(hipEventCreate(&t_begin_));
+      HIP_OK(hipEventCreate(&t_bwd_end_));
+    }
+    timing_ = on;
+  }
+
+  // {backward_end_ms, [bucket start_ms, end_ms, bytes]...} relative to begin_step of the last timed step
+  // (blocks the host until the last bucket has finished; call after the step).
+  std::vector<double> timings() {
+    if (!timing_ || buckets_.empty()) return {};
+    for (auto& b : buckets_)
+      if (!b.launched) throw std::runtime_error("timings: step not finished");
+    HIP_OK(hipStreamSynchronize(stream_));
+    HIP_OK(hipEventSynchronize(t_bwd_end_));
+    std::vector<double> out;
+    float ms = 0.f;
+    HIP_OK(hipEventElapsedTime(&ms, t_begin_, t_bwd_end_));
+    out.push_back(ms);
+    for (auto& b : buckets_) {
+      float a = 0.f, e = 0.f;
+      HIP_OK(hipEventElapsedTime(&a, t_begin_, b.t_start));
+      HIP_OK(hipEventElapsedTime(&e, t_begin_, b.t_end));
+      out.push_back(a);
+      out.push_back(e);
+      out.push_back((double)(b.end - b.start) * flat_.element_size());
+    }
+    return out;
   }
 
   // a parameter's gradient is complete (its producing kernels are queued on the caller's stream)
@@ -176,6 +218,7 @@ class CommEngine {
   // launch every bucket not launched yet (unused parameters), then order the caller's stream after
   // all bucket reductions
   void finish() {
+    if (timing_) HIP_OK(hipEventRecord(t_bwd_end_, caller()));
     for (auto& b : buckets_)
       if (!b.launched) launch(b);
     for (auto& b : buckets_) HIP_OK(hipStreamWaitEvent(caller(), b.done, 0));
@@ -243,10 +286,12 @@ class CommEngine {
   void launch(Bucket& b) {
     order_after_caller();
     const int64_t n = b.end - b.start;
+    if (timing_) HIP_OK(hipEventRecord(b.t_start, stream_));
     if (n > 0) {
       char* base = static_cast<char*>(flat_.data_ptr()) + b.start * flat_.element_size();
       NCCL_OK(ncclAllReduce(base, base, (size_t)n, to_nccl(flat_.scalar_type()), ncclSum, comm_, stream_));
     }
+    if (timing_) HIP_OK(hipEventRecord(b.t_end, stream_));
     HIP_OK(hipEventRecord(b.done, stream_));
     b.launched = true;
   }
@@ -255,6 +300,8 @@ class CommEngine {
   hipStream_t stream_ = nullptr;
   ncclComm_t comm_ = nullptr;
   hipEvent_t ready_ = nullptr;
+  bool timing_ = false;
+  hipEvent_t t_begin_ = nullptr, t_bwd_end_ = nullptr;
   std::vector<hipEvent_t> extra_;
   size_t next_extra_ = 0;
   std::vector<Bucket> buckets_;
@@ -278,6 +325,8 @@ void register_comm(pybind11::module& m) {
       .def("broadcast", &CommEngine::broadcast, py::arg("t"), py::arg("root") = 0)
       .def("set_buckets", &CommEngine::set_buckets)
       .def("begin_step", &CommEngine::begin_step)
+      .def("set_timing", &CommEngine::set_timing)
+      .def("timings", &CommEngine::timings)
       .def("mark_ready", &CommEngine::mark_ready)
       .def("finish", &CommEngine::finish)
       .def("wait_all", &CommEngine::wait_all)

@@ -49,6 +49,8 @@ class ThroughputMeter:
 
     def on_train_begin(self, trainer):
         self._events = []
+        buck = getattr(trainer, "bucketer", None)
+        self._timing = buck is not None and buck.set_timing(True)
 
     def on_batch_end(self, trainer, step):
         self._events.append(self._stamp())
@@ -81,6 +83,10 @@ class ThroughputMeter:
             torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         ms = float(t.item())
         world = backend.size()
+        comm = None
+        if getattr(self, "_timing", False):
+            comm = trainer.bucketer.overlap_report()  # last step's bucket timeline (this rank)
+            trainer.bucketer.set_timing(False)
         seqs = self.per_rank_batch * world * 1e3 / ms
         self.result = {
             "metric": "sequences/sec (whole node)", "value": seqs, "seq_per_s_per_gpu": seqs / world,
@@ -88,6 +94,8 @@ class ThroughputMeter:
             "warmup_steps": self.warmup, "per_gpu_batch": self.per_rank_batch, "global_batch": self.per_rank_batch * world,
             "seq_len": self.seq_len, **self.info,
         }
+        if comm is not None:
+            self.result["comm_overlap"] = comm
         if backend.rank() == 0:
             os.makedirs(self.out_dir, exist_ok=True)
             with open(os.path.join(self.out_dir, "benchmark.json"), "w") as f:

@@ -37,6 +37,19 @@ logger = logging.getLogger(__name__)
 DEFAULT_BUCKET_MB = float(os.environ.get("HSD_BUCKET_MB", "64"))
 
 
+def overlap_from_timeline(backward_ms: float, buckets) -> dict:
+    """``buckets``: (start_ms, end_ms, bytes) per bucket, all relative to the step's begin."""
+    comm = sum(max(0.0, e - s) for s, e, _ in buckets)
+    exposed = sum(max(0.0, e - max(s, backward_ms)) for s, e, _ in buckets)
+    last = max((e for _, e, _ in buckets), default=backward_ms)
+    nbytes = sum(b for _, _, b in buckets)
+    return {"backward_ms": round(backward_ms, 4), "comm_ms": round(comm, 4), "exposed_ms": round(exposed, 4),
+            "overlap_pct": round(100.0 * (1.0 - exposed / comm), 2) if comm > 0 else 100.0,
+            "tail_ms": round(max(0.0, last - backward_ms), 4), "bytes": int(nbytes),
+            "algbw_GBps": round(nbytes / (comm * 1e6), 2) if comm > 0 else None,
+            "buckets": [[round(s, 4), round(e, 4), int(b)] for s, e, b in buckets]}
+
+
 class _Bucket:
     __slots__ = ("index", "start", "end", "params", "ready", "handle", "launched")
 
@@ -157,6 +170,27 @@ class GradBucketer:
             yield
         finally:
             self.sync_enabled = prev
+
+    # ---------------------------------------------------------------- overlap timeline
+    def set_timing(self, on: bool) -> bool:
+        """Record per-bucket HIP timing events from the next step on (native engine only)."""
+        if self.engine is None:
+            return False
+        self.engine.set_timing(bool(on))
+        return True
+
+    def overlap_report(self) -> Optional[dict]:
+        """Comm/compute overlap of the last step run with timing on (SURVEY.md §5 'comm-engine timestamps').
+
+        ``backward_ms``: begin_step -> all backward kernels done (compute stream). Per bucket: start/end of its
+        all-reduce on the comm stream. ``exposed_ms``: collective time after backward finished, i.e. what the
+        step pays on top of compute; ``overlap_pct`` = 100 * (1 - exposed / total collective time)."""
+        if self.engine is None:
+            return None
+        t = list(self.engine.timings())
+        if not t:
+            return None
+        return overlap_from_timeline(t[0], [tuple(t[i:i + 3]) for i in range(1, len(t), 3)])
 
     def detach(self) -> None:
         self.store.ready_callback = None

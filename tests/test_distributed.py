@@ -214,3 +214,13 @@ def test_kernel_none_grads_and_tied_weight_signal_once():
     """Ops that write main_grad and return None (the HIP path) plus a tied weight: every bucket is reduced
     exactly once, after all contributions (regression: the readiness signal used to fire twice)."""
     mp.spawn(_worker_none_grad_tied, args=(2, _port()), nprocs=2, join=True)
+
+
+def test_overlap_from_timeline():
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel.ddp import overlap_from_timeline
+
+    # backward ends at 10 ms; bucket 0 fully hidden, bucket 1 straddles (2 ms exposed), bucket 2 after (3 ms)
+    r = overlap_from_timeline(10.0, [(2.0, 4.0, 100), (9.0, 12.0, 200), (12.0, 15.0, 300)])
+    assert r["comm_ms"] == 8.0 and r["exposed_ms"] == 5.0 and r["tail_ms"] == 5.0
+    assert r["overlap_pct"] == 37.5 and r["bytes"] == 600
+    assert overlap_from_timeline(5.0, [])["overlap_pct"] == 100.0

@@ -94,4 +94,13 @@ def test_hip_backward_through_native_engine(gpu):
         assert launched == eng.num_buckets()
         rel = (g - ref).norm() / ref.norm()
         assert rel < 1e-2, rel
+    # overlap timeline: every bucket but the tail ones starts before backward ends
+    assert buck.set_timing(True)
+    grads(buck)
+    rep = buck.overlap_report()
+    buck.set_timing(False)
+    assert rep is not None and len(rep["buckets"]) == eng.num_buckets()
+    assert rep["backward_ms"] > 0 and rep["bytes"] == store.grad.numel() * 4
+    assert all(0 <= s <= e for s, e, _ in rep["buckets"])
+    assert sum(s < rep["backward_ms"] for s, _, _ in rep["buckets"]) >= eng.num_buckets() - 2
     buck.detach()
