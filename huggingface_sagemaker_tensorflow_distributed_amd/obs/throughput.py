@@ -49,8 +49,10 @@ class ThroughputMeter:
 
     def on_train_begin(self, trainer):
         self._events = []
+        # per-bucket comm timeline (native RCCL engine only; other bucketers report False)
         buck = getattr(trainer, "bucketer", None)
-        self._timing = buck is not None and buck.set_timing(True)
+        set_timing = getattr(buck, "set_timing", None)
+        self._timing = bool(set_timing(True)) if set_timing is not None else False
 
     def on_batch_end(self, trainer, step):
         self._events.append(self._stamp())
