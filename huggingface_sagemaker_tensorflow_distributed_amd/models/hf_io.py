@@ -105,10 +105,12 @@ def from_pretrained(name_or_path: str, task: str = "sequence-classification", nu
                     seed: Optional[int] = 0) -> _Base:
     cfg = resolve_config(name_or_path, num_labels=num_labels)
     model = build_model(cfg, task=task, seed=seed)
+    model.weights_source = "random-init"  # what the run's provenance record reports
     if os.path.isdir(name_or_path):
         sd = read_checkpoint(name_or_path)
         if sd is not None:
             info = load_hf_state_dict(model, sd)
+            model.weights_source = os.path.abspath(name_or_path)
             if info["missing"]:
                 logger.info("Some weights were newly initialized: %s", info["missing"])
         else:

@@ -113,8 +113,12 @@ class GradBucketer:
 
     # ---------------------------------------------------------------- hooks
     def mark_ready(self, i: int) -> None:
+        # no_sync micro-steps only accumulate: readiness is counted on the synced (last) micro-step alone,
+        # on both paths, so a bucket fires once, after its gradients hold every micro-step's contribution
+        if not self.sync_enabled:
+            return
         if self.engine is not None:
-            if self.overlap and self.sync_enabled:
+            if self.overlap:
                 self.engine.mark_ready(i)
             return
         b = self._param_bucket[i]
@@ -122,7 +126,7 @@ class GradBucketer:
             raise RuntimeError(f"gradient for {self.store.names[i]} arrived after its bucket was reduced "
                                "(tied parameter used after its bucket completed?)")
         b.ready.add(i)
-        if self.overlap and self.sync_enabled and len(b.ready) == len(b.params):
+        if self.overlap and len(b.ready) == len(b.params):
             self._launch(b)
 
     def _launch(self, b: _Bucket) -> None:

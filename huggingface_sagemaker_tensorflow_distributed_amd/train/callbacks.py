@@ -62,6 +62,8 @@ def save_checkpoint(path: str, trainer, epoch: int) -> None:
 
 
 def load_checkpoint(path: str, trainer) -> dict:
+    """Restore weights, optimizer and step; returns the trainer state (``epoch`` = epochs completed, the
+    ``initial_epoch`` a resumed ``fit`` starts from)."""
     sd = read_checkpoint(path)
     if sd is None:
         raise FileNotFoundError(path)
@@ -86,6 +88,7 @@ def load_checkpoint(path: str, trainer) -> dict:
         with open(sf) as f:
             st = json.load(f)
         trainer.global_step = int(st.get("global_step", 0))
+    st.setdefault("epoch", 0)
     return st
 
 

@@ -13,6 +13,7 @@ step 1, Q5 rank-0-only save + barrier, Q6 global metrics.
 """
 from __future__ import annotations
 
+import json
 import logging
 import os
 import time
@@ -63,6 +64,28 @@ def _datasets(args, cfg, tokenizer, max_len: int):
     return tr, te
 
 
+def _provenance(args, model, rank: int, n_train: int, n_eval: int) -> dict:
+    """Say loudly when the run is not the reference's imdb fine-tune of pretrained weights: results files keep
+    the reference's exact format, so the data / weights they came from go to ``run_provenance.json`` beside
+    them and to a WARNING in the log."""
+    weights = getattr(model, "weights_source", "random-init")
+    synthetic = args.dataset == "synthetic"
+    info = {"dataset": args.dataset, "synthetic_data": synthetic, "weights": weights,
+            "model_name_or_path": args.model_name_or_path, "num_train_examples": n_train,
+            "num_eval_examples": n_eval}
+    if synthetic or weights == "random-init":
+        what = " and ".join(x for x in (("synthetic random data" if synthetic else ""),
+                                         ("random-init weights" if weights == "random-init" else "")) if x)
+        logger.warning("training on %s: train_results.txt / eval_results.txt are NOT comparable with the "
+                       "reference's imdb fine-tune of pretrained %s (see run_provenance.json)", what,
+                       args.model_name_or_path)
+    if rank == 0:
+        os.makedirs(args.output_data_dir, exist_ok=True)
+        with open(os.path.join(args.output_data_dir, "run_provenance.json"), "w") as f:
+            json.dump(info, f, indent=1)
+    return info
+
+
 def build(args, mode: str):
     """Construct model/store/optimizer/bucketer/trainer for ``args``. Returns a dict of parts."""
     st = backend.init(device=args.device, timeout_s=args.dist_timeout)
@@ -96,10 +119,11 @@ def build(args, mode: str):
     trainer = Trainer(model, store, opt, bucketer, dev, grad_accum=args.gradient_accumulation_steps,
                       check_sync=args.check_sync, log_every=args.log_every, step_watchdog=args.step_watchdog,
                       hip_graph=bool(getattr(args, "hip_graph", False)))
+    initial_epoch = 0
     if args.resume_from:
-        load_checkpoint(args.resume_from, trainer)
+        initial_epoch = int(load_checkpoint(args.resume_from, trainer).get("epoch", 0))
     broadcast_parameters(store, opt if args.resume_from else None)
-    return {"model": model, "store": store, "optimizer": opt, "bucketer": bucketer, "trainer": trainer,
+    return {"initial_epoch": initial_epoch, "model": model, "store": store, "optimizer": opt, "bucketer": bucketer, "trainer": trainer,
             "device": dev, "world": world, "rank": rank, "lr": lr, "dtype": dtype_name}
 
 
@@ -130,8 +154,12 @@ def run(argv: Optional[Sequence[str]] = None, mode: str = "train") -> dict:
 
     train_loader = hdata.BatchLoader(train_ds, ShardSampler(len(train_ds), rank, world, shuffle=False, seed=args.seed,
                                                              batch_size=per_rank_train), dev)
+    # eval scores every test example once (reference model.evaluate, scripts/train.py:170): shards padded with
+    # ignored rows, the last partial batch kept
     test_loader = hdata.BatchLoader(test_ds, ShardSampler(len(test_ds), rank, world, shuffle=False, seed=args.seed,
-                                                           drop_last=True, batch_size=per_rank_eval), dev)
+                                                           drop_last=False, mark_padding=True,
+                                                           batch_size=per_rank_eval), dev)
+    _provenance(args, model, rank, len(train_ds), len(test_ds))
     out = {"args": args}
     callbacks = [FaultInjection()]
     if args.benchmark or args.profile:
@@ -152,7 +180,7 @@ def run(argv: Optional[Sequence[str]] = None, mode: str = "train") -> dict:
             logger.info("*** Train ***")
         start = time.time()
         hist = trainer.fit(train_loader, args.epochs, callbacks=callbacks, verbose=(rank == 0),
-                           max_steps=args.max_steps)
+                           max_steps=args.max_steps, initial_epoch=parts["initial_epoch"])
         train_runtime = {"train_runtime": round(time.time() - start, 4)}
         if mode == "train":
             logger.info(f"train_runtime = {train_runtime}\n")
@@ -175,4 +203,5 @@ def run(argv: Optional[Sequence[str]] = None, mode: str = "train") -> dict:
         save_pretrained(model, args.model_dir, state_dict=master_state_dict(model, parts["store"]))
         tokenizer.save_pretrained(args.model_dir)
     backend.barrier()
+    out["global_step"] = trainer.global_step
     return out

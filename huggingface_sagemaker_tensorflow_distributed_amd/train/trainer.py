@@ -53,8 +53,9 @@ class _Meter:
         self.t = torch.zeros(3, dtype=torch.float64, device=device)
 
     def update(self, loss: torch.Tensor, logits: torch.Tensor, labels: torch.Tensor) -> None:
-        # classification: one label per logits row; MLM: logits only for the non-ignored (masked) tokens
-        n = labels.numel() if (logits.dim() == 2 and logits.shape[0] == labels.numel()) else labels.ne(-100).sum()
+        # classification: one label per logits row, -100 on the rows that only pad the eval shards;
+        # MLM: logits only for the non-ignored (masked) tokens. Either way n counts the scored rows.
+        n = labels.ne(-100).sum()
         fused = getattr(loss, "_hsd_correct", None)
         if fused is not None:
             correct = fused
@@ -62,7 +63,10 @@ class _Meter:
             correct = ops.accuracy_count(logits, labels)
         else:
             correct = torch.zeros((), device=logits.device)
-        upd = torch.stack([loss.detach().double() * n, correct.double(), torch.as_tensor(n, device=self.t.device).double()])
+        nd = n.to(self.t.device).double()
+        # an all-padding batch has a NaN mean loss on the torch path: it contributes nothing
+        lsum = torch.where(nd > 0, loss.detach().double() * nd, torch.zeros_like(nd))
+        upd = torch.stack([lsum, correct.to(self.t.device).double(), nd])
         self.t += upd
 
     def result(self, global_: bool = True) -> Dict[str, float]:
@@ -169,12 +173,14 @@ class Trainer:
 
     # -------------------------------------------------------------------------- fit
     def fit(self, loader, epochs: int, callbacks: Iterable = (), verbose: bool = True,
-            max_steps: Optional[int] = None) -> History:
+            max_steps: Optional[int] = None, initial_epoch: int = 0) -> History:
+        """Keras ``fit(epochs=..., initial_epoch=...)``: runs epochs ``initial_epoch .. epochs-1`` (a resumed
+        run continues the epoch count of its checkpoint instead of training ``epochs`` more)."""
         hist = History()
         callbacks = list(callbacks)
         for cb in callbacks:
             cb.on_train_begin(self)
-        for epoch in range(epochs):
+        for epoch in range(int(initial_epoch), epochs):
             if hasattr(loader, "sampler"):
                 loader.sampler.set_epoch(epoch)
             meter = _Meter(self.device)
@@ -217,6 +223,8 @@ class Trainer:
         for i, b in enumerate(loader):
             if max_steps and i >= max_steps:
                 continue  # drain
+            if b.get("num_valid", 1) == 0:
+                continue  # a shard's tail made only of padding rows
             loss, logits = self._forward_loss(b)
             meter.update(loss, logits, b["labels"])
         return meter.result(global_=True)

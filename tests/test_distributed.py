@@ -88,6 +88,82 @@ def test_dp_equals_single_process_global_batch(tmp_path, world):
     torch.testing.assert_close(store.master, dp_master, atol=2e-6, rtol=1e-5)
 
 
+def _worker_accum(rank, world, port, out_path):
+    _setenv(rank, world, port)
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel import backend, broadcast_parameters
+
+    backend.init(device="cpu")
+    model, store, opt, tr = _make(seed_init=100 + rank)
+    tr.grad_accum = 2
+    broadcast_parameters(store)
+    ids, am, lab = _data(8 * world)
+    for step in range(3):
+        base = rank * 8
+        mbs = [{"input_ids": ids[s:s + 4], "attention_mask": am[s:s + 4], "labels": lab[s:s + 4]}
+               for s in (base, base + 4)]
+        tr.train_step(mbs)
+    if rank == 0:
+        torch.save(store.master.clone(), out_path)
+    backend.shutdown()
+
+
+def test_dp_grad_accumulation_equals_single_process_global_batch(tmp_path):
+    """2 ranks x 2 no_sync micro-steps of 4 == 1 process on the global batch of 16 (the torch-bucket
+    path used to count readiness during no_sync micro-steps and reduce half-accumulated gradients)."""
+    world = 2
+    out = str(tmp_path / "accum.pt")
+    mp.spawn(_worker_accum, args=(world, _port(), out), nprocs=world, join=True)
+    dp_master = torch.load(out)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE"):
+        os.environ.pop(k, None)
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel import backend
+
+    backend.init(device="cpu")
+    model, store, opt, tr = _make(seed_init=100)
+    ids, am, lab = _data(8 * world)
+    for step in range(3):
+        tr.train_step([{"input_ids": ids, "attention_mask": am, "labels": lab}])
+    torch.testing.assert_close(store.master, dp_master, atol=2e-6, rtol=1e-5)
+
+
+def _worker_eval(rank, world, port, out_path):
+    _setenv(rank, world, port)
+    from huggingface_sagemaker_tensorflow_distributed_amd import data as hdata
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel import backend
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel.sampler import ShardSampler
+
+    backend.init(device="cpu")
+    model, store, opt, tr = _make(seed_init=7)
+    ds = hdata.synthetic_classification(37, 16, 1024, seed=5)
+    loader = hdata.BatchLoader(ds, ShardSampler(37, rank, world, drop_last=False, mark_padding=True, batch_size=4),
+                               torch.device("cpu"))
+    res = tr.evaluate(loader)
+    if rank == 0:
+        torch.save(torch.tensor([res["loss"], res["sparse_categorical_accuracy"]], dtype=torch.float64), out_path)
+    backend.shutdown()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_sharded_eval_equals_single_process_full_test_set(tmp_path, world):
+    """Eval over N ranks (padded shards, partial last batches) == one process scoring all 37 examples."""
+    out = str(tmp_path / "eval.pt")
+    mp.spawn(_worker_eval, args=(world, _port(), out), nprocs=world, join=True)
+    got = torch.load(out)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE"):
+        os.environ.pop(k, None)
+    from huggingface_sagemaker_tensorflow_distributed_amd import data as hdata
+
+    model, store, opt, tr = _make(seed_init=7)
+    ds = hdata.synthetic_classification(37, 16, 1024, seed=5)
+    model.eval()
+    with torch.no_grad():
+        lab = torch.from_numpy(ds.labels).long()
+        loss, logits = model(torch.from_numpy(ds.input_ids).long(),
+                             attention_mask=torch.from_numpy(ds.attention_mask).long(), labels=lab)
+    acc = float((logits.argmax(-1) == lab).double().mean())
+    torch.testing.assert_close(got, torch.tensor([float(loss), acc], dtype=torch.float64), rtol=1e-5, atol=1e-6)
+
+
 def _worker_buckets(rank, world, port):
     _setenv(rank, world, port)
     from huggingface_sagemaker_tensorflow_distributed_amd.parallel import backend
