@@ -781,8 +781,27 @@ bool gemm2_supported(int la, int lb, int epi, int M, int N, int K) {
   return false;
 }
 
+// gemm3.hip: the two-workgroups-per-CU 256 x 128 body. HSD_GEMM3 selects it per layout: bit 0 = NT (forward /
+// dgrad, bf16 epilogues), bit 1 = TT (weight gradients); shapes it does not tile stay on gemm2.
+bool gemm3_supported(int la, int lb, int epi, int M, int N, int K);
+int gemm3_wgrad_splits(int M, int N, int K);
+void launch_gemm3(int la, int lb, int epi, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, int M, int N,
+                  int K, void* C, int64_t ldc, const bf16_t* bias, const bf16_t* aux, int64_t ldaux, bf16_t* C2,
+                  double p_drop, uint64_t seed, int splits, float* ws, float* dbias, hipStream_t st);
+
+static int gemm3_mask() {
+  const char* e = getenv("HSD_GEMM3");
+  return e ? atoi(e) : 0;
+}
+
+static bool use_gemm3(int la, int lb, int epi, int M, int N, int K) {
+  const int bit = la == 0 ? 1 : 2;
+  return (gemm3_mask() & bit) && gemm3_supported(la, lb, epi, M, N, K);
+}
+
 // splits for the TT wgrad: fill ~one wave of 256 CUs with >= 4 K-tiles per block
 int gemm2_wgrad_splits(int M, int N, int K) {
+  if (use_gemm3(1, 1, E2_F32_SLAB, M, N, K)) return gemm3_wgrad_splits(M, N, K);
   const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
   int s = 256 / tiles;
   if (s < 1) s = 1;
@@ -794,6 +813,11 @@ int gemm2_wgrad_splits(int M, int N, int K) {
 void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, int M, int N,
                   int K, void* C, int64_t ldc, const bf16_t* bias, const bf16_t* aux, int64_t ldaux, bf16_t* C2,
                   double p_drop, uint64_t seed, int splits, float* ws, float* dbias, hipStream_t st) {
+  if (use_gemm3(la, lb, epi, M, N, K)) {
+    launch_gemm3(la, lb, epi, A, lda, B, ldb, M, N, K, C, ldc, bias, aux, ldaux, C2, p_drop, seed, splits, ws, dbias,
+                 st);
+    return;
+  }
   G2Params p{};
   p.dbias = dbias;
   {
