@@ -11,6 +11,8 @@
 //           dgamma / dbeta           (register partials, one atomic per column per block)
 #include "common.h"
 
+#include <stdlib.h>
+
 namespace hsd {
 
 template <int NCH>
@@ -184,6 +186,168 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const bf16_t* __restrict
   }
 }
 
+// 16-B backward (H % 8 == 0): each lane owns 8 consecutive columns per chunk for the row loads (dout and the
+// re-gathered word / position / type rows), the LN backward runs in that
+// layout, and the embedding gradient de goes through a wave-private LDS row so the fp32 atomics into the
+// word-gradient row are issued in the lane + 64 i layout (256 contiguous bytes per wave instruction — the full
+// atomic rate). The scalar kernel above loads 2 B per lane per element.
+template <int NC8, int NE>  // NE: atomic-layout elements per lane, H <= 64 * NE
+__global__ __launch_bounds__(256, 2) void embed_bwd16_kernel(const bf16_t* __restrict__ dout, const int64_t* __restrict__ ids,
+                                                          const int64_t* __restrict__ pos_ids,
+                                                          const int64_t* __restrict__ type_ids,
+                                                          const bf16_t* __restrict__ word, const bf16_t* __restrict__ pos,
+                                                          const bf16_t* __restrict__ type, const bf16_t* __restrict__ gamma,
+                                                          const float* __restrict__ mean_in,
+                                                          const float* __restrict__ rstd_in, float* __restrict__ gword,
+                                                          float* __restrict__ gpos, float* __restrict__ gtype,
+                                                          float* __restrict__ ggamma, float* __restrict__ gbeta, int B,
+                                                          int S, int H, int bpc, int pos_is_arange, DropoutParams dp) {
+  dp = resolve_seed(dp);
+  __shared__ __attribute__((aligned(16))) float lds[4][NC8 * 512];
+  const int lane = threadIdx.x & 63;
+  const int wid = threadIdx.x >> 6;
+  const int n8 = H >> 3;
+  const int s = blockIdx.x;
+  const int b0 = blockIdx.y * bpc;
+  const int b1 = min(B, b0 + bpc);
+  float* wl = lds[wid];
+  float gam[NC8][8], acc_g[NC8][8], acc_b[NC8][8], acc_p[NE], acc_t0[NE];
+#pragma unroll
+  for (int i = 0; i < NC8; ++i) {
+    const int c = lane + 64 * i;
+    u32x4 gw = u32x4{0, 0, 0, 0};
+    if (c < n8) gw = *reinterpret_cast<const u32x4*>(gamma + 8 * c);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      gam[i][2 * k] = lo_bf(gw[k]);
+      gam[i][2 * k + 1] = hi_bf(gw[k]);
+    }
+#pragma unroll
+    for (int k = 0; k < 8; ++k) acc_g[i][k] = acc_b[i][k] = 0.f;
+  }
+#pragma unroll
+  for (int i = 0; i < NE; ++i) acc_p[i] = acc_t0[i] = 0.f;
+
+  struct Row {
+    u32x4 d[NC8], w[NC8], p[NC8], t[NC8];
+    int64_t id, pid, tid;
+    float mean, rstd;
+  };
+  auto load = [&](int b, Row& r) {
+    const int row = b * S + s;
+    r.id = ids[row];
+    r.pid = pos_ids[row];
+    r.tid = type ? type_ids[row] : 0;
+    r.mean = mean_in[row];
+    r.rstd = rstd_in[row];
+#pragma unroll
+    for (int i = 0; i < NC8; ++i) {
+      const int c = lane + 64 * i;
+      r.d[i] = r.w[i] = r.p[i] = r.t[i] = u32x4{0, 0, 0, 0};
+      if (c < n8) {
+        r.d[i] = *reinterpret_cast<const u32x4*>(dout + (size_t)row * H + 8 * c);
+        r.w[i] = *reinterpret_cast<const u32x4*>(word + r.id * H + 8 * c);
+        r.p[i] = *reinterpret_cast<const u32x4*>(pos + r.pid * H + 8 * c);
+        if (type) r.t[i] = *reinterpret_cast<const u32x4*>(type + r.tid * H + 8 * c);
+      }
+    }
+  };
+  auto process = [&](int b, const Row& r) {
+    const int row = b * S + s;
+    float xh[NC8][8], g[NC8][8];
+    float s1 = 0.f, s2 = 0.f;
+#pragma unroll
+    for (int i = 0; i < NC8; ++i) {
+      const int c = lane + 64 * i;
+      const bool ok = c < n8;
+      const size_t off0 = (size_t)row * H + 8 * c;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        uint32_t bits = 0;
+        if (dp.enabled) bits = dropout_bits((uint32_t)(off0 >> 1) + k, dp);
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int e = 2 * k + h;
+          const float ev = (h ? hi_bf(r.w[i][k]) + hi_bf(r.p[i][k]) + hi_bf(r.t[i][k])
+                              : lo_bf(r.w[i][k]) + lo_bf(r.p[i][k]) + lo_bf(r.t[i][k]));
+          float dv = h ? hi_bf(r.d[i][k]) : lo_bf(r.d[i][k]);
+          if (dp.enabled) dv *= keep_factor(bits, h, dp);
+          xh[i][e] = ok ? (ev - r.mean) * r.rstd : 0.f;
+          g[i][e] = dv * gam[i][e];
+          s1 += g[i][e];
+          s2 += g[i][e] * xh[i][e];
+          acc_g[i][e] += dv * xh[i][e];
+          acc_b[i][e] += dv;
+        }
+      }
+    }
+    s1 = wave_sum(s1) / (float)H;
+    s2 = wave_sum(s2) / (float)H;
+#pragma unroll
+    for (int i = 0; i < NC8; ++i) {
+      const int c = lane + 64 * i;
+      if (c < n8) {
+        f32x4 lo, hi;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          lo[e] = r.rstd * (g[i][e] - s1 - xh[i][e] * s2);
+          hi[e] = r.rstd * (g[i][4 + e] - s1 - xh[i][4 + e] * s2);
+        }
+        *reinterpret_cast<f32x4*>(wl + 8 * c) = lo;
+        *reinterpret_cast<f32x4*>(wl + 8 * c + 4) = hi;
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+    for (int i = 0; i < NE; ++i) {
+      const int e = lane + 64 * i;
+      if (e < H) {
+        const float de = wl[e];
+        atomicAdd(gword + r.id * H + e, de);
+        if (pos_is_arange) acc_p[i] += de;
+        else atomicAdd(gpos + r.pid * H + e, de);
+        if (gtype) {
+          if (r.tid == 0) acc_t0[i] += de;
+          else atomicAdd(gtype + r.tid * H + e, de);
+        }
+      }
+    }
+    __builtin_amdgcn_wave_barrier();
+  };
+  for (int b = b0 + wid; b < b1; b += 4) {
+    Row r;
+    load(b, r);
+    process(b, r);
+  }
+  // block reduction of the four column partials through the (now free) LDS rows; one atomic per column
+#pragma unroll
+  for (int which = 0; which < 4; ++which) {
+    __syncthreads();
+    if (which < 2) {
+#pragma unroll
+      for (int i = 0; i < NC8; ++i) {
+        const int c = lane + 64 * i;
+        if (c < n8) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) wl[8 * c + e] = which == 0 ? acc_g[i][e] : acc_b[i][e];
+        }
+      }
+    } else {
+#pragma unroll
+      for (int i = 0; i < NE; ++i) {
+        const int e = lane + 64 * i;
+        if (e < H) wl[e] = which == 2 ? acc_p[i] : acc_t0[i];
+      }
+    }
+    __syncthreads();
+    float* dst = which == 0 ? ggamma : which == 1 ? gbeta : which == 2 ? (pos_is_arange ? gpos + (size_t)s * H : nullptr)
+                                                                          : gtype;
+    if (dst) {
+      for (int c = threadIdx.x; c < H; c += 256) atomicAdd(dst + c, lds[0][c] + lds[1][c] + lds[2][c] + lds[3][c]);
+    }
+  }
+}
+
 template <int NCH>
 static void embed_fwd_t(const int64_t* ids, const int64_t* pos_ids, const int64_t* type_ids, const bf16_t* word,
                         const bf16_t* pos, const bf16_t* type, const bf16_t* gamma, const bf16_t* beta, bf16_t* out,
@@ -223,6 +387,21 @@ void launch_embed_bwd(const bf16_t* dout, const int64_t* ids, const int64_t* pos
                       const float* mean, const float* rstd, float* gword, float* gpos, float* gtype, float* ggamma,
                       float* gbeta, int B, int S, int H, int pos_is_arange, double p, uint64_t seed, hipStream_t st) {
   DropoutParams dp = make_dropout(p, seed);
+  if (H % 8 == 0 && H <= 1024 && !getenv("HSD_EMBED_BWD_SCALAR")) {
+    int chunks = max(1, min(B, (2048 + S - 1) / S));
+    int bpc = (B + chunks - 1) / chunks;
+    chunks = (B + bpc - 1) / bpc;
+#define HSD_EB16(NC8, NE)                                                                                      \
+  hipLaunchKernelGGL((embed_bwd16_kernel<NC8, NE>), dim3(S, chunks), dim3(256), 0, st, dout, ids, pos_ids, type_ids, \
+                     word, pos, type, gamma, mean, rstd, gword, gpos, gtype, ggamma, gbeta, B, S, H, bpc,             \
+                     pos_is_arange, dp)
+    if (H <= 512) HSD_EB16(1, 8);
+    else if (H <= 768) HSD_EB16(2, 12);
+    else HSD_EB16(2, 16);
+#undef HSD_EB16
+    HSD_CHECK_LAUNCH();
+    return;
+  }
   const int ne = (H + 63) / 64;
   if (ne <= 1) embed_bwd_t<1>(dout, ids, pos_ids, type_ids, word, pos, type, gamma, mean, rstd, gword, gpos, gtype, ggamma, gbeta, B, S, H, pos_is_arange, dp, st);
   else if (ne <= 2) embed_bwd_t<2>(dout, ids, pos_ids, type_ids, word, pos, type, gamma, mean, rstd, gword, gpos, gtype, ggamma, gbeta, B, S, H, pos_is_arange, dp, st);

@@ -96,6 +96,89 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
   }
 }
 
+// Plain LayerNorm forward for the encoder's LN tails (z = dropout(y) + residual already comes out of the GEMM
+// epilogue, so no residual / dropout / z here): every wave walks `rpw` consecutive rows with the NEXT row's
+// 16-B loads in flight while the current row reduces. 5.1 TB/s at T = 131072, H = 768 against 3.6 TB/s for the
+// one-row-per-wave kernel above with its 8-B lanes (tools/bench_ln.py, profiles/bench_ln_r2.json). Needs
+// H % 8 == 0.
+template <int NC8>
+__global__ __launch_bounds__(256) void ln_fwd_plain16_kernel(const bf16_t* __restrict__ y,
+                                                             const bf16_t* __restrict__ gamma,
+                                                             const bf16_t* __restrict__ beta, bf16_t* __restrict__ out,
+                                                             float* __restrict__ mean_out, float* __restrict__ rstd_out,
+                                                             int rows, int H, int rpw, float eps) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int n8 = H >> 3;
+  const int r0 = (blockIdx.x * kLnWaves + wave) * rpw;
+  const int r1 = min(rows, r0 + rpw);
+  if (r0 >= r1) return;
+  u32x4 gw[NC8], bw[NC8];
+#pragma unroll
+  for (int i = 0; i < NC8; ++i) {
+    const int c = lane + 64 * i;
+    gw[i] = bw[i] = u32x4{0, 0, 0, 0};
+    if (c < n8) {
+      gw[i] = *reinterpret_cast<const u32x4*>(gamma + 8 * c);
+      bw[i] = *reinterpret_cast<const u32x4*>(beta + 8 * c);
+    }
+  }
+  auto load = [&](int row, u32x4(&yw)[NC8]) {
+#pragma unroll
+    for (int i = 0; i < NC8; ++i) {
+      const int c = lane + 64 * i;
+      yw[i] = u32x4{0, 0, 0, 0};
+      if (c < n8) yw[i] = *reinterpret_cast<const u32x4*>(y + (size_t)row * H + 8 * c);
+    }
+  };
+  auto process = [&](int row, const u32x4(&yw)[NC8]) {
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < NC8; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) s += lo_bf(yw[i][k]) + hi_bf(yw[i][k]);
+    const float mean = wave_sum(s) / (float)H;
+    float ss = 0.f;
+#pragma unroll
+    for (int i = 0; i < NC8; ++i) {
+      if (lane + 64 * i < n8) {
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const float d0 = lo_bf(yw[i][k]) - mean, d1 = hi_bf(yw[i][k]) - mean;
+          ss += d0 * d0;
+          ss += d1 * d1;
+        }
+      }
+    }
+    const float rstd = rsqrtf(wave_sum(ss) / (float)H + eps);
+#pragma unroll
+    for (int i = 0; i < NC8; ++i) {
+      const int c = lane + 64 * i;
+      if (c < n8) {
+        u32x4 o;
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+          o[k] = pack_bf2((lo_bf(yw[i][k]) - mean) * rstd * lo_bf(gw[i][k]) + lo_bf(bw[i][k]),
+                          (hi_bf(yw[i][k]) - mean) * rstd * hi_bf(gw[i][k]) + hi_bf(bw[i][k]));
+        *reinterpret_cast<u32x4*>(out + (size_t)row * H + 8 * c) = o;
+      }
+    }
+    if (lane == 0) {
+      mean_out[row] = mean;
+      rstd_out[row] = rstd;
+    }
+  };
+  u32x4 ya[NC8], yb[NC8];
+  load(r0, ya);
+  for (int r = r0; r < r1; r += 2) {
+    const bool more = r + 1 < r1;
+    if (more) load(r + 1, yb);
+    process(r, ya);
+    if (!more) break;
+    if (r + 2 < r1) load(r + 2, ya);
+    process(r + 1, yb);
+  }
+}
+
 // Block = 4 waves; block walks `rows_per_block` rows (wave-strided, TWO rows in flight per wave so the
 // second row's loads overlap the first row's reductions) accumulating column partials in registers.
 template <int NCH>
@@ -355,6 +438,20 @@ template <int NCH>
 static void ln_fwd_t(const bf16_t* y, const bf16_t* res, const bf16_t* gamma, const bf16_t* beta, bf16_t* z,
                      bf16_t* out, float* mean, float* rstd, int rows, int H, float eps, const DropoutParams& dp,
                      hipStream_t st) {
+  const char* env = getenv("HSD_LN_FWD_RPW");  // A/B: 1 = the one-row kernel; > 1 = rows per wave
+  const int mode = env ? atoi(env) : 0;
+  if (mode != 1 && res == nullptr && z == nullptr && !dp.enabled && H % 8 == 0 && H <= 1024) {
+    const int rpw = mode > 1 ? mode : std::max(2, std::min(16, rows / 8192));
+    const int waves = (rows + rpw - 1) / rpw;
+    const int blocks = (waves + kLnWaves - 1) / kLnWaves;
+    if (H <= 512)
+      hipLaunchKernelGGL((ln_fwd_plain16_kernel<1>), dim3(blocks), dim3(256), 0, st, y, gamma, beta, out, mean, rstd,
+                         rows, H, rpw, eps);
+    else
+      hipLaunchKernelGGL((ln_fwd_plain16_kernel<2>), dim3(blocks), dim3(256), 0, st, y, gamma, beta, out, mean, rstd,
+                         rows, H, rpw, eps);
+    return;
+  }
   dim3 grid((rows + kLnWaves - 1) / kLnWaves);
   hipLaunchKernelGGL((ln_fwd_kernel<NCH>), grid, dim3(256), 0, st, y, res, gamma, beta, z, out, mean, rstd, rows,
                      H, eps, dp);

@@ -95,21 +95,44 @@ def test_linear_gelu(gpu):
     _close(b.grad, b32.grad, 2e-1, 2e-2, "db")
 
 
+@pytest.mark.parametrize("H", [64, 256, 768, 1024])
+def test_layer_norm_plain(gpu, H):
+    """LN without residual / dropout (the encoder tails' LN, 16-B multi-row forward kernel) vs fp32 torch."""
+    hip = _hip()
+    torch.manual_seed(5)
+    T = 4099  # not a multiple of the rows-per-wave / waves-per-block tiling
+    x = torch.randn(T, H, device=gpu).bfloat16().requires_grad_()
+    g = (1 + 0.1 * torch.randn(H, device=gpu)).bfloat16().requires_grad_()
+    b = (0.1 * torch.randn(H, device=gpu)).bfloat16().requires_grad_()
+    out = hip.layer_norm(x, g, b, 1e-12)
+    x32, g32, b32 = [t.detach().float().requires_grad_() for t in (x, g, b)]
+    r = torch.nn.functional.layer_norm(x32, (H,), g32, b32, 1e-12)
+    _close(out, r, 3e-2, 2e-2, "fwd")
+    d = torch.randn_like(out)
+    out.backward(d)
+    r.backward(d.float())
+    _close(x.grad, x32.grad, 5e-2, 5e-2, "dx")
+    _close(g.grad, g32.grad, 2e-1, 2e-2, "dgamma")
+    _close(b.grad, b32.grad, 2e-1, 2e-2, "dbeta")
+
+
 @pytest.mark.parametrize("p", [0.0, 0.1])
 @pytest.mark.parametrize("type_vocab", [2, 0])
-def test_embed_ln(gpu, p, type_vocab):
+@pytest.mark.parametrize("arange", [True, False])
+def test_embed_ln(gpu, p, type_vocab, arange):
     hip = _hip()
     torch.manual_seed(2)
     B, S, H, V = 8, 64, 768, 1000
     ids = torch.randint(0, V, (B, S), device=gpu)
-    pos = torch.arange(S, device=gpu).unsqueeze(0).expand(B, S)
+    # RoBERTa-style position ids (padding_idx + 1 + arange, per-token gradient atomics) when not arange
+    pos = torch.arange(S, device=gpu).unsqueeze(0).expand(B, S) + (0 if arange else 2)
     tt = torch.randint(0, 2, (B, S), device=gpu) if type_vocab else None
     word = (torch.randn(V, H, device=gpu) * 0.02).bfloat16().requires_grad_()
-    pw = (torch.randn(S, H, device=gpu) * 0.02).bfloat16().requires_grad_()
+    pw = (torch.randn(S + 2, H, device=gpu) * 0.02).bfloat16().requires_grad_()
     tw = (torch.randn(2, H, device=gpu) * 0.02).bfloat16().requires_grad_() if type_vocab else None
     g = (1 + 0.1 * torch.randn(H, device=gpu)).bfloat16().requires_grad_()
     be = (0.1 * torch.randn(H, device=gpu)).bfloat16().requires_grad_()
-    out = hip.embed_ln(ids, pos, tt, word, pw, tw, g, be, 1e-12, p, 99, True)
+    out = hip.embed_ln(ids, pos, tt, word, pw, tw, g, be, 1e-12, p, 99, arange)
     f = lambda t: t.detach().float().requires_grad_() if t is not None else None  # noqa: E731
     word32, pw32, tw32, g32, be32 = f(word), f(pw), f(tw), f(g), f(be)
     r = ref.embed_ln(ids, pos, tt, word32, pw32, tw32, g32, be32, 1e-12, 0.0, 0, False)
