@@ -52,7 +52,7 @@ __device__ __forceinline__ float wave_max(float v) {
 }
 
 // ---- dropout hash (ops/rng.py) -------------------------------------------------------
-__device__ __forceinline__ uint32_t mix32(uint32_t x) {
+__host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
   x ^= x >> 16;
   x *= 0x7FEB352Du;
   x ^= x >> 15;
@@ -60,13 +60,18 @@ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
   x ^= x >> 16;
   return x;
 }
-// 32 random bits for element pair j: lo16 -> element 2j, hi16 -> element 2j+1
-__device__ __forceinline__ uint32_t dropout_bits(uint32_t pair, uint32_t seed_lo, uint32_t seed_hi) {
-  return mix32(mix32(pair ^ seed_lo) ^ seed_hi);
+// 32-bit key of a dropout site's 64-bit seed (mixed ONCE per site / kernel, not per element)
+__host__ __device__ __forceinline__ uint32_t dropout_key(uint32_t seed_lo, uint32_t seed_hi) {
+  return mix32(seed_lo ^ mix32(seed_hi));
 }
+// 32 random bits for element pair j: lo16 -> element 2j, hi16 -> element 2j+1. ONE lowbias32 round per pair
+// (a bijection of j ^ key, so no two pairs of a site collide): the attention kernels hash every (query, key)
+// pair, and a second per-pair round cost ~15 % of their time at p = 0.1 (tools/attn_one.py).
+__device__ __forceinline__ uint32_t dropout_bits_k(uint32_t pair, uint32_t key) { return mix32(pair ^ key); }
 
 struct DropoutParams {
   uint32_t seed_lo, seed_hi;
+  uint32_t key;     // dropout_key(seed_lo, seed_hi), device step seed folded in by resolve_seed
   uint32_t thr;     // keep iff bits16 >= thr
   float scale;      // 1/(1-p)
   int enabled;
@@ -82,6 +87,7 @@ __host__ inline DropoutParams make_dropout(double p, uint64_t seed) {
   DropoutParams d;
   d.seed_lo = (uint32_t)(seed & 0xFFFFFFFFull);
   d.seed_hi = (uint32_t)(seed >> 32);
+  d.key = dropout_key(d.seed_lo, d.seed_hi);
   double t = p * 65536.0;
   d.thr = (uint32_t)(t + 0.5);
   d.scale = p > 0.0 ? (float)(1.0 / (1.0 - p)) : 1.0f;
@@ -96,18 +102,16 @@ __device__ __forceinline__ DropoutParams resolve_seed(DropoutParams d) {
   if (d.dev_seed != nullptr) {
     d.seed_lo ^= d.dev_seed[0];
     d.seed_hi ^= d.dev_seed[1];
+    d.key = dropout_key(d.seed_lo, d.seed_hi);
     d.dev_seed = nullptr;
   }
   return d;
 }
 
 __device__ __forceinline__ uint32_t dropout_bits(uint32_t pair, const DropoutParams& d) {
-  uint32_t lo = d.seed_lo, hi = d.seed_hi;
-  if (d.dev_seed != nullptr) {
-    lo ^= d.dev_seed[0];
-    hi ^= d.dev_seed[1];
-  }
-  return dropout_bits(pair, lo, hi);
+  uint32_t key = d.key;
+  if (d.dev_seed != nullptr) key = dropout_key(d.seed_lo ^ d.dev_seed[0], d.seed_hi ^ d.dev_seed[1]);
+  return dropout_bits_k(pair, key);
 }
 
 // keep factor (0 or scale) for element `e` given its pair's bits

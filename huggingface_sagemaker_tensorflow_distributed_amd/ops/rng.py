@@ -7,8 +7,10 @@ stateful Philox stream; we need the same *distribution* (Bernoulli keep with pro
 
 Definition (mirrored in ``csrc/kernels/common.h::dropout_bits``):
 
+* the site's 64-bit seed is mixed once into a 32-bit key ``k = mix32(seed_lo ^ mix32(seed_hi))``
+  (``mix32`` = lowbias32, Wellons);
 * element pair ``j`` (elements ``2j`` and ``2j+1`` of the flattened site tensor) draws
-  ``h = mix32(mix32(j ^ seed_lo) ^ seed_hi)`` with ``mix32`` = lowbias32 (Wellons);
+  ``h = mix32(j ^ k)`` — one round per pair: the attention kernels hash every (query, key) pair;
 * element ``2j`` keeps iff ``(h & 0xFFFF) >= thr``; element ``2j+1`` keeps iff ``(h >> 16) >= thr``;
 * ``thr = round(p * 65536)``.
 """
@@ -47,6 +49,11 @@ def mix32_int(x: int) -> int:
     return x
 
 
+def site_key(seed_lo: int, seed_hi: int) -> int:
+    """32-bit key of a dropout site (``common.h::dropout_key``)."""
+    return mix32_int((seed_lo & M32) ^ mix32_int(seed_hi & M32))
+
+
 def threshold(p: float) -> int:
     return int(round(p * 65536.0))
 
@@ -55,9 +62,10 @@ def keep_mask(seed: int, numel: int, p: float, device=None) -> torch.Tensor:
     """Boolean keep mask of ``numel`` elements for a dropout site with 64-bit ``seed``."""
     seed_lo = seed & M32
     seed_hi = (seed >> 32) & M32
+    key = site_key(seed_lo, seed_hi)
     npairs = (numel + 1) // 2
     j = torch.arange(npairs, dtype=torch.int64, device=device)
-    h = mix32(mix32(j ^ seed_lo) ^ seed_hi)
+    h = mix32(j ^ key)
     lo = h & 0xFFFF
     hi = h >> 16
     bits = torch.stack([lo, hi], dim=1).reshape(-1)[:numel]

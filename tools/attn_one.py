@@ -1,0 +1,41 @@
+"""Runs the S=128 attention forward once and the backward `iters` times at the BERT-base B=1024 shape (for
+rocprofv3 --pmc passes); prints the mean times of both directions at p = 0 and p = 0.1."""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from huggingface_sagemaker_tensorflow_distributed_amd.ops import hip  # noqa: E402
+
+C_ = hip._C
+dev = "cuda"
+B, S, heads, H = 1024, 128, 12, 768
+T = B * S
+p = float(sys.argv[1]) if len(sys.argv) > 1 else 0.1
+iters = int(sys.argv[2]) if len(sys.argv) > 2 else 5
+torch.manual_seed(0)
+qkv = torch.randn(T, 3 * H, device=dev).bfloat16()
+out = torch.empty(T, H, device=dev, dtype=torch.bfloat16)
+lse = torch.empty(B * heads * S, device=dev)
+dqkv = torch.empty_like(qkv)
+dout = torch.randn(T, H, device=dev).bfloat16()
+mask = torch.zeros(B, S, device=dev)
+dbias = torch.zeros(3 * H, device=dev)
+st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+for pp in sorted({0.0, p}):
+    C_.attn_fwd(qkv, mask, out, lse, B, S, heads, pp, 123)
+    torch.cuda.synchronize()
+    st.record()
+    for _ in range(iters):
+        C_.attn_fwd(qkv, mask, out, lse, B, S, heads, pp, 123)
+    en.record()
+    torch.cuda.synchronize()
+    f = st.elapsed_time(en) / iters * 1e3
+    st.record()
+    for _ in range(iters):
+        C_.attn_bwd(qkv, mask, out, dout, lse, dqkv, None, B, S, heads, pp, 123, dbias)
+    en.record()
+    torch.cuda.synchronize()
+    b = st.elapsed_time(en) / iters * 1e3
+    print(f"p={pp}: fwd {f:.1f} us  bwd {b:.1f} us", flush=True)
