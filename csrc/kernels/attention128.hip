@@ -117,6 +117,7 @@ __global__ __launch_bounds__(256, 2) void attn128_fwd_kernel(const bf16_t* __res
 }
 
 // ------------------------------------------------------------------------------------------------
+template <bool DROP>
 __global__ __launch_bounds__(256, 2) void attn128_bwd_kernel(const bf16_t* __restrict__ qkv,
                                                              const float* __restrict__ mask,
                                                              const bf16_t* __restrict__ o,
@@ -180,18 +181,39 @@ __global__ __launch_bounds__(256, 2) void attn128_bwd_kernel(const bf16_t* __res
 
   f32x16 dk0 = {}, dk1 = {}, dv0 = {}, dv1 = {};
   const bool odd = (lane & 1) != 0;
+  // per-lane LDS offsets of the query-block-0 fragments; block qb adds qb * 32 rows (the images' swizzles
+  // depend on row bits 1..3 only, so they are the same for every block)
+  int off_row[4], off_tr[2][2][2];
+#pragma unroll
+  for (int s4 = 0; s4 < 4; ++s4) off_row[s4] = toff(r, 16 * s4 + 8 * hf);
+  {
+    const int g = lane >> 4, i = lane & 15, h = g >> 1, q = i >> 2, pp = i & 3;
+#pragma unroll
+    for (int s2 = 0; s2 < 2; ++s2)
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const int col = cb * 32 + 16 * (g & 1) + 4 * pp;
+        const int r0 = 16 * s2 + 4 * h + q;
+        off_tr[s2][cb][0] = toff(r0, col);
+        off_tr[s2][cb][1] = toff(r0 + 8, col);
+      }
+  }
+  // dropout pair index of (query qi0 (+1 on odd lanes), this lane's key): ((bh S + q) S + key) >> 1
+  const uint32_t pair_lane = (uint32_t)bh * (S * S / 2) + (uint32_t)(key >> 1) + (odd ? S / 2 : 0);
 #pragma unroll 1
   for (int qb = 0; qb < 4; ++qb) {
+    const int qoff = qb * 32 * 64;  // element offset of the block's first row in a [rows][64] image
     f32x16 sacc = {}, dpacc = {};
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      const bf16x8 aq = *reinterpret_cast<const bf16x8*>(Qs + toff(qb * 32 + r, 16 * s + 8 * hf));
-      sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aq, kf[s], sacc, 0, 0, 0);
-      const bf16x8 ad = *reinterpret_cast<const bf16x8*>(dOs + toff(qb * 32 + r, 16 * s + 8 * hf));
-      dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ad, vf[s], dpacc, 0, 0, 0);
+    for (int s4 = 0; s4 < 4; ++s4) {
+      const bf16x8 aq = *reinterpret_cast<const bf16x8*>(Qs + qoff + off_row[s4]);
+      sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aq, kf[s4], sacc, 0, 0, 0);
+      const bf16x8 ad = *reinterpret_cast<const bf16x8*>(dOs + qoff + off_row[s4]);
+      dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ad, vf[s4], dpacc, 0, 0, 0);
     }
     // rows: query qi = (reg&3) + 8(reg>>2) + 4hf of the block; col (lane): key
     f32x16 pd, ds;
+    const uint32_t pair_qb = pair_lane + (uint32_t)(qb * 32 + 4 * hf) * (S / 2);
 #pragma unroll
     for (int reg = 0; reg < 16; reg += 2) {
       const int qi0 = qb * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * hf;  // rows qi0, qi0 + 1
@@ -200,12 +222,10 @@ __global__ __launch_bounds__(256, 2) void attn128_bwd_kernel(const bf16_t* __res
       const float p0 = __builtin_amdgcn_exp2f(fmaf(sacc[reg], sl2, kb2) - lse[0]);
       const float p1 = __builtin_amdgcn_exp2f(fmaf(sacc[reg + 1], sl2, kb2) - lse[1]);
       float k0 = 1.f, k1 = 1.f;
-      if (dp.enabled) {
+      if constexpr (DROP) {
         // element ((bh*S + q)*S + key): keys 2j, 2j+1 (lanes l, l^1) share one hash per query row.
         // even lane hashes row qi0, odd lane row qi0+1, then they swap.
-        const int qmine = odd ? qi0 + 1 : qi0;
-        const uint32_t e = (uint32_t)(((int64_t)bh * S + qmine) * S + key);
-        const uint32_t bits = dropout_bits(e >> 1, dp);
+        const uint32_t bits = dropout_bits(pair_qb + (uint32_t)((reg & 3) + 8 * (reg >> 2)) * (S / 2), dp);
         const uint32_t other = (uint32_t)__shfl_xor((int)bits, 1, 64);
         const uint32_t b0 = odd ? other : bits;   // hash of row qi0
         const uint32_t b1 = odd ? bits : other;   // hash of row qi0 + 1
@@ -219,13 +239,16 @@ __global__ __launch_bounds__(256, 2) void attn128_bwd_kernel(const bf16_t* __res
     }
     // dVᵀ += dOᵀ·Pd, dKᵀ += Qᵀ·dS  (accumulators as B operands, rows of the images in the same order)
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const bf16x8 pb = pack8(pd, s);
-      const bf16x8 sb = pack8(ds, s);
-      dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(dOs, qb * 32, s, 0, lane), pb, dv0, 0, 0, 0);
-      dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(dOs, qb * 32, s, 1, lane), pb, dv1, 0, 0, 0);
-      dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(Qs, qb * 32, s, 0, lane), sb, dk0, 0, 0, 0);
-      dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(Qs, qb * 32, s, 1, lane), sb, dk1, 0, 0, 0);
+    for (int s2 = 0; s2 < 2; ++s2) {
+      const bf16x8 pb = pack8(pd, s2);
+      const bf16x8 sb = pack8(ds, s2);
+      auto tr = [&](const bf16_t* img, int cb) {
+        return cat8(tr_read(img, qoff + off_tr[s2][cb][0]), tr_read(img, qoff + off_tr[s2][cb][1]));
+      };
+      dv0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr(dOs, 0), pb, dv0, 0, 0, 0);
+      dv1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr(dOs, 1), pb, dv1, 0, 0, 0);
+      dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr(Qs, 0), sb, dk0, 0, 0, 0);
+      dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr(Qs, 1), sb, dk1, 0, 0, 0);
     }
     // dS -> [key][q] image
 #pragma unroll
@@ -237,15 +260,20 @@ __global__ __launch_bounds__(256, 2) void attn128_bwd_kernel(const bf16_t* __res
     }
   }
   __syncthreads();  // every dS written; Q / dO no longer read
-  // K -> Q's slot for dQ; dK, dV out through this wave's staging slice (dO's slot)
-  dma_img(Qs, base + H, ld, wave * 4, 4, lane);
+  // K -> Q's slot for dQ, from the K fragments this wave already holds (keys 32w..32w+31, 8 consecutive d
+  // per lane and s): LDS writes instead of a second HBM/L2 read, and no s_waitcnt vmcnt before the dQ phase
+  // (a vmcnt would also wait for the dK / dV stores below, which count on the same counter).
+#pragma unroll
+  for (int s = 0; s < 4; ++s) *reinterpret_cast<bf16x8*>(Qs + toff(key, 16 * s + 8 * hf)) = kf[s];
+  // dK, dV out through this wave's staging slice (dO's slot)
   bf16_t* stg = dOs + wave * 32 * D;
   bf16_t* rowbase = dqkv + ((int64_t)b * S + wave * 32) * ld + hh * D;
   float* bs_w = dbias ? bsum + wave * D : nullptr;
   store_rows(stg, dv0, dv1, 1.0f, rowbase + 2 * H, ld, lane, dbias ? bs_w + 2 * 4 * D : nullptr);
   store_rows(stg, dk0, dk1, scale, rowbase + H, ld, lane, dbias ? bs_w + 4 * D : nullptr);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
   // dQᵀ[d][q] = Σ_key Kᵀ[d][key] dSᵀ[key][q], wave w: queries 32w..32w+31
   f32x16 dq0 = {}, dq1 = {};
 #pragma unroll
@@ -285,8 +313,12 @@ void launch_attn128_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, c
   DropoutParams dp = make_dropout(p, seed);
   const float sl2 = a128::kLog2e / sqrtf((float)a128::D);
   const float scale = 1.0f / sqrtf((float)a128::D);
-  hipLaunchKernelGGL(a128::attn128_bwd_kernel, dim3(B * heads), dim3(256), 0, st, qkv, mask, o, dout, lse2, dqkv,
-                     dbias, heads, sl2, scale, dp);
+  if (dp.enabled)
+    hipLaunchKernelGGL(a128::attn128_bwd_kernel<true>, dim3(B * heads), dim3(256), 0, st, qkv, mask, o, dout, lse2,
+                       dqkv, dbias, heads, sl2, scale, dp);
+  else
+    hipLaunchKernelGGL(a128::attn128_bwd_kernel<false>, dim3(B * heads), dim3(256), 0, st, qkv, mask, o, dout, lse2,
+                       dqkv, dbias, heads, sl2, scale, dp);
   HSD_CHECK_LAUNCH();
 }
 
