@@ -3,7 +3,7 @@
 // (cdna_hip_programming.md §5.4 rule 24), every variant checked against an fp32 reference on sampled rows.
 //
 //   hipcc -O3 --offload-arch=gfx950 -Icsrc/kernels tools/gemm4_probe.cpp csrc/kernels/gemm2.hip \
-//         csrc/kernels/gemm3.hip csrc/kernels/gemm4.hip -o build/gemm4_probe      (tools/build_gemm4_probe.sh)
+//         csrc/kernels/gemm3.hip tools/experiments/gemm4.hip -o tools/bin/gemm4_probe
 //   build/gemm4_probe [epi] [shape,...]  -> one JSON line per shape
 #include <hip/hip_runtime.h>
 #include <stdio.h>
