@@ -69,7 +69,7 @@ def _worker_dp(rank, world, port, out_path):
     backend.shutdown()
 
 
-@pytest.mark.parametrize("world", [2, 4])
+@pytest.mark.parametrize("world", [2, 4, 8])
 def test_dp_equals_single_process_global_batch(tmp_path, world):
     """N ranks x per-rank batch 8 with grad averaging == 1 process on the 8N global batch."""
     out = str(tmp_path / "dp.pt")
@@ -184,8 +184,10 @@ def _worker_buckets(rank, world, port):
     backend.shutdown()
 
 
-def test_bucketed_allreduce_sums_and_overlaps():
-    mp.spawn(_worker_buckets, args=(2, _port()), nprocs=2, join=True)
+@pytest.mark.parametrize("world", [2, 8])
+def test_bucketed_allreduce_sums_and_overlaps(world):
+    # world 8 rehearses the driver's 8-GPU node on gloo: every rank's buckets launch once, sums exact
+    mp.spawn(_worker_buckets, args=(world, _port()), nprocs=world, join=True)
 
 
 def test_shard_sampler_disjoint_complete():
