@@ -3,7 +3,7 @@
 // (cdna_hip_programming.md §5.4 rule 24), every variant checked against an fp32 reference on sampled rows.
 //
 //   hipcc -O3 --offload-arch=gfx950 -Icsrc/kernels tools/gemm4_probe.cpp csrc/kernels/gemm2.hip \
-//         csrc/kernels/gemm3.hip tools/experiments/gemm4.hip tools/experiments/gemm5.hip -o tools/bin/gemm4_probe
+//         csrc/kernels/gemm3.hip tools/experiments/gemm4.hip -o tools/bin/gemm4_probe
 //   build/gemm4_probe [epi] [shape,...]  -> one JSON line per shape
 #include <hip/hip_runtime.h>
 #include <stdio.h>
@@ -23,9 +23,7 @@ void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const b
 void launch_gemm4(int epi, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, int M, int N, int K, bf16_t* C,
                   int64_t ldc, const bf16_t* bias, const bf16_t* aux, int64_t ldaux, bf16_t* C2, double p_drop,
                   uint64_t seed, hipStream_t st);
-void launch_gemm5(int epi, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, int M, int N, int K, bf16_t* C,
-                  int64_t ldc, const bf16_t* bias, const bf16_t* aux, int64_t ldaux, bf16_t* C2, double p_drop,
-                  uint64_t seed, hipStream_t st);
+
 }  // namespace hsd
 
 using hsd::bf16_t;
@@ -71,8 +69,8 @@ int main(int argc, char** argv) {
   std::vector<Shape> shapes = {{"sq7680", 7680, 7680, 7680}, {"qkv_fwd", T, 2304, 768}, {"out_fwd", T, 768, 768},
                                {"ffn1_fwd", T, 3072, 768},    {"ffn2_fwd", T, 768, 3072}, {"qkv_dgrad", T, 768, 2304},
                                {"ffn2_dgrad", T, 3072, 768}};
-  const char* variants[] = {"g2", "g4s3", "g5w96s0", "g5w96s1", "g5w128s1"};
-  const int NV = 5;
+  const char* variants[] = {"g2", "g4s0", "g4s1", "g4s3"};
+  const int NV = 4;
   hipStream_t st;
   CK(hipStreamCreate(&st));
   for (const Shape& s : shapes) {
@@ -109,13 +107,9 @@ int main(int argc, char** argv) {
     auto run = [&](int v) {
       if (v == 0) {
         hsd::launch_gemm2(0, 0, epi, A, K, B, K, M, N, K, C, N, bias, aux, N, C2, 0.0, 0, 1, nullptr, nullptr, st);
-      } else if (v == 1) {
-        setenv("HSD_G4_SCHED", "3", 1);
-        hsd::launch_gemm4(epi, A, K, B, K, M, N, K, C, N, bias, aux, N, C2, 0.0, 0, st);
       } else {
-        setenv("HSD_G5_WN", v == 4 ? "128" : "96", 1);
-        setenv("HSD_G5_SCHED", v == 2 ? "0" : "1", 1);
-        hsd::launch_gemm5(epi, A, K, B, K, M, N, K, C, N, bias, aux, N, C2, 0.0, 0, st);
+        setenv("HSD_G4_SCHED", v == 1 ? "0" : v == 2 ? "1" : "3", 1);
+        hsd::launch_gemm4(epi, A, K, B, K, M, N, K, C, N, bias, aux, N, C2, 0.0, 0, st);
       }
     };
     double err[NV];
