@@ -4,8 +4,8 @@
 //
 // All three kernels use one workgroup = 4 waves = 128 rows of one (batch, head), the wave's 32 rows on
 // the MFMA lanes (v_mfma_f32_32x32x16_bf16), and stream the other operand pair through LDS in 64-row
-// tiles: global_load_lds DMA into a double-buffered [64][64] swizzled image (attn_common.h), one
-// barrier per tile, the DMA of tile t+1 in flight while tile t is multiplied.
+// tiles: global_load_lds DMA into a 3-stage ring of [64][64] swizzled images (attn_common.h), one raw
+// barrier per tile, the DMAs of tiles t+1 and t+2 in flight while tile t is multiplied.
 //
 // * forward (queries on lanes, K/V streamed): online softmax in the log2 domain; Oᵀ += Vᵀ·Pᵀ with the
 //   Sᵀ accumulator as the B operand; O staged to 128-B row stores; lse2 saved for the backward.
@@ -19,6 +19,7 @@
 // Dropout / mask / lse conventions are identical to attention.hip / attention128.hip.
 #include "attn_common.h"
 
+
 namespace hsd {
 namespace aS {
 
@@ -26,22 +27,62 @@ using namespace attn;
 constexpr int kMaxS = 1024;
 constexpr int TILE = 64 * D;  // one [64][64] bf16 image
 
-// 64 rows x 64 cols starting at src0 into a [64][64] image: 8 DMA instructions, 2 per wave
+constexpr int NSTG = 3;       // LDS stages per streamed operand: tiles t+1 and t+2 in flight while t is used
+
+// 64 rows x 64 cols starting at src0 into a [64][64] image: 8 DMA instructions, 2 per wave.
+// Issued as inline asm (cdna_hip_programming.md "Operands and clobbers" LDS-DMA recipe) so that hipcc does not
+// track it: with the builtin, hipcc cannot prove that the stage being written (a runtime ring index) differs
+// from the stage being read, and waits vmcnt(0) before the first ds_read_b64_tr_b16 after every DMA, which
+// drains the prefetch. Completion is counted by hand in tile_barrier (4 wave-instructions per tile).
 __device__ __forceinline__ void dma_tile(bf16_t* img, const bf16_t* __restrict__ src0, int64_t ld, int wave, int lane) {
-  dma_img(img, src0, ld, wave * 2, 2, lane);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int g = wave * 2 + i;
+    const int row = g * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ swz(row);
+    const bf16_t* src = src0 + (int64_t)row * ld + lc * 8;
+    const uint32_t dst = (uint32_t)__builtin_amdgcn_readfirstlane(
+        (int)(uint32_t)(size_t)(__attribute__((address_space(3))) bf16_t*)(img + g * 512));
+    unsigned keep;
+    asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+                 : "=&s"(keep)
+                 : "v"(src), "s"(dst)
+                 : "memory");
+  }
+}
+
+// Wait until this wave's DMA of the tile about to be used has landed (the newer `inflight` tiles of two operands,
+// 4 DMA wave-instructions per tile, may stay in flight), then a raw barrier: every wave's part is visible and
+// every wave is done with the stage the next DMA overwrites. Never __syncthreads() here: its fence would wait
+// for vmcnt(0) and drain the prefetch (cdna_hip_programming.md §5 "Pipelining across barriers").
+// Register operands loaded by plain global loads before the loop must be COMPLETE before the loop: while an
+// LDS-DMA is in flight, hipcc waits vmcnt(0) at the first use of any pending plain load, and for a use inside
+// the loop that wait would run every iteration and drain the prefetch. A fake use right after the loads moves
+// that one wait to the prologue.
+template <typename T>
+__device__ __forceinline__ void settle(const T& v) {
+  asm volatile("" ::"v"(v));
+}
+
+template <int INFLIGHT>
+__device__ __forceinline__ void tile_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(4 * INFLIGHT) : "memory");
+  __builtin_amdgcn_s_barrier();
+  asm volatile("" ::: "memory");
 }
 
 // ------------------------------------------------------------------------------------------------
+template <bool DROP>
 __global__ __launch_bounds__(256, 2) void attnS_fwd_kernel(const bf16_t* __restrict__ qkv,
                                                            const float* __restrict__ mask, bf16_t* __restrict__ out,
                                                            float* __restrict__ lse2, int S, int heads, float sl2,
                                                            DropoutParams dp) {
   dp = resolve_seed(dp);
-  // [K0 K1 | V0 V1 | mask bias]; after the loop K0|K1 is the output staging
-  __shared__ __attribute__((aligned(16))) bf16_t lds[4 * TILE + 2 * kMaxS];
+  // [K0 K1 K2 | V0 V1 V2 | mask bias]; after the loop K0|K1 is the output staging
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * NSTG * TILE + 2 * kMaxS];
   bf16_t* Kb = lds;
-  bf16_t* Vb = lds + 2 * TILE;
-  float* mb_s = reinterpret_cast<float*>(lds + 4 * TILE);
+  bf16_t* Vb = lds + NSTG * TILE;
+  float* mb_s = reinterpret_cast<float*>(lds + 2 * NSTG * TILE);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hf = lane >> 5;
@@ -50,6 +91,7 @@ __global__ __launch_bounds__(256, 2) void attnS_fwd_kernel(const bf16_t* __restr
   const bf16_t* base = qkv + (int64_t)b * S * ld + hh * D;
   const int q0 = blockIdx.x * 128 + wave * 32;
   const int q = q0 + r;
+  const int nt = S / 64;
   HSD_DASSERT(S % 64 == 0 && S <= kMaxS && q < S);
 
   dma_tile(Kb, base + H, ld, wave, lane);
@@ -58,21 +100,28 @@ __global__ __launch_bounds__(256, 2) void attnS_fwd_kernel(const bf16_t* __restr
 #pragma unroll
   for (int s = 0; s < 4; ++s) qf[s] = *reinterpret_cast<const bf16x8*>(base + (int64_t)q * ld + 16 * s + 8 * hf);
   for (int k = tid; k < S; k += 256) mb_s[k] = mask ? fmaxf(mask[(int64_t)b * S + k] * kLog2e, -1e30f) : 0.f;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) settle(qf[s]);
+  if (nt > 1) {
+    dma_tile(Kb + TILE, base + 64 * ld + H, ld, wave, lane);
+    dma_tile(Vb + TILE, base + 64 * ld + 2 * H, ld, wave, lane);
+  }
 
   f32x16 o0 = {}, o1 = {};
   float m = -INFINITY, l = 0.f;
-  const uint32_t rowbase = (uint32_t)(((int64_t)bh * S + q) * S);
-  const int nt = S / 64;
-#pragma unroll 1
-  for (int kt = 0; kt < nt; ++kt) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const bf16_t* Ks = Kb + (kt & 1) * TILE;
-    const bf16_t* Vs = Vb + (kt & 1) * TILE;
-    if (kt + 1 < nt) {
-      const int64_t off = (int64_t)(kt + 1) * 64 * ld;
-      dma_tile(Kb + ((kt + 1) & 1) * TILE, base + off + H, ld, wave, lane);
-      dma_tile(Vb + ((kt + 1) & 1) * TILE, base + off + 2 * H, ld, wave, lane);
+  // dropout pair of (q, key): ((bh S + q) S + key) >> 1 = pair_q + key / 2 (key even in every hashed pair)
+  const uint32_t pair_q = (uint32_t)(((int64_t)bh * S + q) * (S / 2)) + 2 * hf;
+  auto tile = [&](const int stg, const int kt) {
+
+    if (kt + 1 < nt) tile_barrier<1>();
+    else tile_barrier<0>();
+    const bf16_t* Ks = Kb + stg * TILE;
+    const bf16_t* Vs = Vb + stg * TILE;
+    if (kt + 2 < nt) {
+      const int s2 = stg == 0 ? 2 : stg - 1;
+      const int64_t off = (int64_t)(kt + 2) * 64 * ld;
+      dma_tile(Kb + s2 * TILE, base + off + H, ld, wave, lane);
+      dma_tile(Vb + s2 * TILE, base + off + 2 * H, ld, wave, lane);
     }
     // Sᵀ[key][q] for the tile's 2 key blocks of 32
     f32x16 st[2];
@@ -116,13 +165,14 @@ __global__ __launch_bounds__(256, 2) void attnS_fwd_kernel(const bf16_t* __restr
       o0[reg] *= alpha;
       o1[reg] *= alpha;
     }
-    if (dp.enabled) {
+    if constexpr (DROP) {
+      const uint32_t pair_t = pair_q + (uint32_t)kt * 32;
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int reg = 0; reg < 16; reg += 2) {
-          const int key = kt * 64 + kb * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * hf;
-          const uint32_t bits = dropout_bits((rowbase + key) >> 1, dp);
+          // key = kt*64 + kb*32 + (reg & 3) + 8 (reg >> 2) + 4 hf
+          const uint32_t bits = dropout_bits(pair_t + (uint32_t)(kb * 16 + ((reg & 3) >> 1) + 4 * (reg >> 2)), dp);
           st[kb][reg] *= keep_factor(bits, 0, dp);
           st[kb][reg + 1] *= keep_factor(bits, 1, dp);
         }
@@ -135,7 +185,9 @@ __global__ __launch_bounds__(256, 2) void attnS_fwd_kernel(const bf16_t* __restr
         o0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(Vs, kb * 32, s, 0, lane), pb, o0, 0, 0, 0);
         o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(Vs, kb * 32, s, 1, lane), pb, o1, 0, 0, 0);
       }
-  }
+  };
+#pragma unroll 1
+  for (int t = 0, stg = 0; t < nt; ++t, stg = stg == NSTG - 1 ? 0 : stg + 1) tile(stg, t);
   l += __shfl_xor(l, 32, 64);
   if (hf == 0) lse2[(int64_t)bh * S + q] = m + __log2f(l);
   __syncthreads();  // K images no longer read: reuse as staging
@@ -169,6 +221,7 @@ __global__ __launch_bounds__(256) void attnS_delta_kernel(const bf16_t* __restri
 }
 
 // ------------------------------------------------------------------------------------------------
+template <bool DROP>
 __global__ __launch_bounds__(256, 2) void attnS_bwd_kv_kernel(const bf16_t* __restrict__ qkv,
                                                               const float* __restrict__ mask,
                                                               const bf16_t* __restrict__ dout,
@@ -178,11 +231,11 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_kv_kernel(const bf16_t* __re
                                                               int S, int heads, float sl2, float scale,
                                                               DropoutParams dp) {
   dp = resolve_seed(dp);
-  // [Q0 Q1 | dO0 dO1 | lse | delta | k/v bias partials]; after the loop Q0|Q1 is the output staging
-  __shared__ __attribute__((aligned(16))) bf16_t lds[4 * TILE + 4 * kMaxS + 2 * 2 * 4 * D];
+  // [Q0 Q1 Q2 | dO0 dO1 dO2 | lse | delta | k/v bias partials]; after the loop Q0|Q1 is the output staging
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * NSTG * TILE + 4 * kMaxS + 2 * 2 * 4 * D];
   bf16_t* Qb = lds;
-  bf16_t* dOb = lds + 2 * TILE;
-  float* lse_s = reinterpret_cast<float*>(lds + 4 * TILE);
+  bf16_t* dOb = lds + NSTG * TILE;
+  float* lse_s = reinterpret_cast<float*>(lds + 2 * NSTG * TILE);
   float* del_s = lse_s + kMaxS;
   float* bsum = del_s + kMaxS;  // [2 (k,v)][4 waves][64]
   const int tid = threadIdx.x, lane = tid & 63;
@@ -194,6 +247,7 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_kv_kernel(const bf16_t* __re
   const bf16_t* dobase = dout + (int64_t)b * S * H + hh * D;
   const int k0 = blockIdx.x * 128 + wave * 32;
   const int key = k0 + r;
+  const int nt = S / 64;
   HSD_DASSERT(S % 64 == 0 && S <= kMaxS && key < S);
 
   dma_tile(Qb, base, ld, wave, lane);
@@ -209,19 +263,32 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_kv_kernel(const bf16_t* __re
     lse_s[i] = lse2[(int64_t)bh * S + i];
     del_s[i] = delta[(int64_t)bh * S + i];
   }
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    settle(kf[s]);
+    settle(vf[s]);
+  }
+  settle(kb2);
+  if (nt > 1) {
+    dma_tile(Qb + TILE, base + 64 * ld, ld, wave, lane);
+    dma_tile(dOb + TILE, dobase + 64 * H, H, wave, lane);
+  }
 
   f32x16 dk0 = {}, dk1 = {}, dv0 = {}, dv1 = {};
   const bool odd = (lane & 1) != 0;
-  const int nt = S / 64;
-#pragma unroll 1
-  for (int qt = 0; qt < nt; ++qt) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const bf16_t* Qs = Qb + (qt & 1) * TILE;
-    const bf16_t* dOs = dOb + (qt & 1) * TILE;
-    if (qt + 1 < nt) {
-      dma_tile(Qb + ((qt + 1) & 1) * TILE, base + (int64_t)(qt + 1) * 64 * ld, ld, wave, lane);
-      dma_tile(dOb + ((qt + 1) & 1) * TILE, dobase + (int64_t)(qt + 1) * 64 * H, H, wave, lane);
+  // dropout pair of (query qi0 (+1 on odd lanes), this lane's key): ((bh S + q) S + key) >> 1
+  const uint32_t pair_lane = (uint32_t)((int64_t)bh * S * (S / 2)) + (uint32_t)(key >> 1) +
+                             (uint32_t)(4 * hf + (odd ? 1 : 0)) * (S / 2);
+  auto tile = [&](const int stg, const int qt) {
+
+    if (qt + 1 < nt) tile_barrier<1>();
+    else tile_barrier<0>();
+    const bf16_t* Qs = Qb + stg * TILE;
+    const bf16_t* dOs = dOb + stg * TILE;
+    if (qt + 2 < nt) {
+      const int s2 = stg == 0 ? 2 : stg - 1;
+      dma_tile(Qb + s2 * TILE, base + (int64_t)(qt + 2) * 64 * ld, ld, wave, lane);
+      dma_tile(dOb + s2 * TILE, dobase + (int64_t)(qt + 2) * 64 * H, H, wave, lane);
     }
 #pragma unroll
     for (int qs = 0; qs < 2; ++qs) {
@@ -235,6 +302,7 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_kv_kernel(const bf16_t* __re
       }
       // rows: query qi = (reg&3) + 8(reg>>2) + 4hf of the sub-block; col (lane): key
       f32x16 pd, ds;
+      const uint32_t pair_qs = pair_lane + (uint32_t)(qt * 64 + qs * 32) * (S / 2);
 #pragma unroll
       for (int reg = 0; reg < 16; reg += 2) {
         const int qi0 = qt * 64 + qs * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * hf;  // rows qi0, qi0 + 1
@@ -243,12 +311,10 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_kv_kernel(const bf16_t* __re
         const float p0 = __builtin_amdgcn_exp2f(fmaf(sacc[reg], sl2, kb2) - lse[0]);
         const float p1 = __builtin_amdgcn_exp2f(fmaf(sacc[reg + 1], sl2, kb2) - lse[1]);
         float f0 = 1.f, f1 = 1.f;
-        if (dp.enabled) {
+        if constexpr (DROP) {
           // keys 2j, 2j+1 (lanes l, l^1) share one hash per query row: the even lane hashes row qi0,
           // the odd lane row qi0 + 1, then they swap
-          const int qmine = odd ? qi0 + 1 : qi0;
-          const uint32_t e = (uint32_t)(((int64_t)bh * S + qmine) * S + key);
-          const uint32_t bits = dropout_bits(e >> 1, dp);
+          const uint32_t bits = dropout_bits(pair_qs + (uint32_t)((reg & 3) + 8 * (reg >> 2)) * (S / 2), dp);
           const uint32_t other = (uint32_t)__shfl_xor((int)bits, 1, 64);
           f0 = keep_factor(odd ? other : bits, key & 1, dp);
           f1 = keep_factor(odd ? bits : other, key & 1, dp);
@@ -268,12 +334,14 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_kv_kernel(const bf16_t* __re
         dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(Qs, qs * 32, s, 1, lane), sb, dk1, 0, 0, 0);
       }
     }
-  }
+  };
+#pragma unroll 1
+  for (int t = 0, stg = 0; t < nt; ++t, stg = stg == NSTG - 1 ? 0 : stg + 1) tile(stg, t);
   __syncthreads();  // Q images no longer read: reuse as staging
-  bf16_t* stg = Qb + wave * 32 * D;
+  bf16_t* stg_w = Qb + wave * 32 * D;
   bf16_t* rowbase = dqkv + ((int64_t)b * S + k0) * ld + hh * D;
-  store_rows(stg, dv0, dv1, 1.0f, rowbase + 2 * H, ld, lane, dbias ? bsum + (4 + wave) * D : nullptr);
-  store_rows(stg, dk0, dk1, scale, rowbase + H, ld, lane, dbias ? bsum + wave * D : nullptr);
+  store_rows(stg_w, dv0, dv1, 1.0f, rowbase + 2 * H, ld, lane, dbias ? bsum + (4 + wave) * D : nullptr);
+  store_rows(stg_w, dk0, dk1, scale, rowbase + H, ld, lane, dbias ? bsum + wave * D : nullptr);
   if (dbias) {
     __syncthreads();
     if (tid < 2 * D) {
@@ -285,6 +353,7 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_kv_kernel(const bf16_t* __re
 }
 
 // ------------------------------------------------------------------------------------------------
+template <bool DROP>
 __global__ __launch_bounds__(256, 2) void attnS_bwd_q_kernel(const bf16_t* __restrict__ qkv,
                                                              const float* __restrict__ mask,
                                                              const bf16_t* __restrict__ dout,
@@ -294,11 +363,11 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_q_kernel(const bf16_t* __res
                                                              int S, int heads, float sl2, float scale,
                                                              DropoutParams dp) {
   dp = resolve_seed(dp);
-  // [K0 K1 | V0 V1 | mask bias | q bias partials]; after the loop K0|K1 is the output staging
-  __shared__ __attribute__((aligned(16))) bf16_t lds[4 * TILE + 2 * kMaxS + 2 * 4 * D];
+  // [K0 K1 K2 | V0 V1 V2 | mask bias | q bias partials]; after the loop K0|K1 is the output staging
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * NSTG * TILE + 2 * kMaxS + 2 * 4 * D];
   bf16_t* Kb = lds;
-  bf16_t* Vb = lds + 2 * TILE;
-  float* mb_s = reinterpret_cast<float*>(lds + 4 * TILE);
+  bf16_t* Vb = lds + NSTG * TILE;
+  float* mb_s = reinterpret_cast<float*>(lds + 2 * NSTG * TILE);
   float* bsum = mb_s + kMaxS;  // [4 waves][64]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -308,6 +377,7 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_q_kernel(const bf16_t* __res
   const bf16_t* base = qkv + (int64_t)b * S * ld + hh * D;
   const int q0 = blockIdx.x * 128 + wave * 32;
   const int q = q0 + r;
+  const int nt = S / 64;
   HSD_DASSERT(S % 64 == 0 && S <= kMaxS && q < S);
 
   dma_tile(Kb, base + H, ld, wave, lane);
@@ -321,20 +391,32 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_q_kernel(const bf16_t* __res
   const float lse_q = lse2[(int64_t)bh * S + q];
   const float del_q = delta[(int64_t)bh * S + q];
   for (int k = tid; k < S; k += 256) mb_s[k] = mask ? fmaxf(mask[(int64_t)b * S + k] * kLog2e, -1e30f) : 0.f;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    settle(qf[s]);
+    settle(df[s]);
+  }
+  settle(lse_q);
+  settle(del_q);
+  if (nt > 1) {
+    dma_tile(Kb + TILE, base + 64 * ld + H, ld, wave, lane);
+    dma_tile(Vb + TILE, base + 64 * ld + 2 * H, ld, wave, lane);
+  }
 
   f32x16 dq0 = {}, dq1 = {};
-  const uint32_t rowbase = (uint32_t)(((int64_t)bh * S + q) * S);
-  const int nt = S / 64;
-#pragma unroll 1
-  for (int kt = 0; kt < nt; ++kt) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    const bf16_t* Ks = Kb + (kt & 1) * TILE;
-    const bf16_t* Vs = Vb + (kt & 1) * TILE;
-    if (kt + 1 < nt) {
-      const int64_t off = (int64_t)(kt + 1) * 64 * ld;
-      dma_tile(Kb + ((kt + 1) & 1) * TILE, base + off + H, ld, wave, lane);
-      dma_tile(Vb + ((kt + 1) & 1) * TILE, base + off + 2 * H, ld, wave, lane);
+  // dropout pair of (q, key): ((bh S + q) S + key) >> 1 = pair_q + key / 2 (key even in every hashed pair)
+  const uint32_t pair_q = (uint32_t)(((int64_t)bh * S + q) * (S / 2)) + 2 * hf;
+  auto tile = [&](const int stg, const int kt) {
+
+    if (kt + 1 < nt) tile_barrier<1>();
+    else tile_barrier<0>();
+    const bf16_t* Ks = Kb + stg * TILE;
+    const bf16_t* Vs = Vb + stg * TILE;
+    if (kt + 2 < nt) {
+      const int s2 = stg == 0 ? 2 : stg - 1;
+      const int64_t off = (int64_t)(kt + 2) * 64 * ld;
+      dma_tile(Kb + s2 * TILE, base + off + H, ld, wave, lane);
+      dma_tile(Vb + s2 * TILE, base + off + 2 * H, ld, wave, lane);
     }
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb) {
@@ -348,6 +430,7 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_q_kernel(const bf16_t* __res
         dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, df[s], dpacc, 0, 0, 0);
       }
       f32x16 ds;
+      const uint32_t pair_kb = pair_q + (uint32_t)(kt * 32 + kb * 16);
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const int kk = kt * 64 + kb * 32 + 8 * g4 + 4 * hf;  // keys kk .. kk+3 in regs 4g4 .. 4g4+3
@@ -358,8 +441,8 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_q_kernel(const bf16_t* __res
           const float p0 = __builtin_amdgcn_exp2f(fmaf(sacc[reg], sl2, mb[e]) - lse_q);
           const float p1 = __builtin_amdgcn_exp2f(fmaf(sacc[reg + 1], sl2, mb[e + 1]) - lse_q);
           float f0 = 1.f, f1 = 1.f;
-          if (dp.enabled) {
-            const uint32_t bits = dropout_bits((rowbase + kk + e) >> 1, dp);
+          if constexpr (DROP) {
+            const uint32_t bits = dropout_bits(pair_kb + (uint32_t)(4 * g4 + (e >> 1)), dp);
             f0 = keep_factor(bits, 0, dp);
             f1 = keep_factor(bits, 1, dp);
           }
@@ -375,7 +458,9 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_q_kernel(const bf16_t* __res
         dq1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(Ks, kb * 32, s, 1, lane), sb, dq1, 0, 0, 0);
       }
     }
-  }
+  };
+#pragma unroll 1
+  for (int t = 0, stg = 0; t < nt; ++t, stg = stg == NSTG - 1 ? 0 : stg + 1) tile(stg, t);
   __syncthreads();  // K images no longer read: reuse as staging
   store_rows(Kb + wave * 32 * D, dq0, dq1, scale, dqkv + ((int64_t)b * S + q0) * ld + hh * D, ld, lane,
              dbias ? bsum + wave * D : nullptr);
@@ -395,8 +480,12 @@ void launch_attnS_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* 
                       double p, uint64_t seed, hipStream_t st) {
   DropoutParams dp = make_dropout(p, seed);
   const float sl2 = attn::kLog2e / sqrtf((float)attn::D);
-  hipLaunchKernelGGL(aS::attnS_fwd_kernel, dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, out, lse2, S, heads,
-                     sl2, dp);
+  if (dp.enabled)
+    hipLaunchKernelGGL(aS::attnS_fwd_kernel<true>, dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, out, lse2, S,
+                       heads, sl2, dp);
+  else
+    hipLaunchKernelGGL(aS::attnS_fwd_kernel<false>, dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, out, lse2, S,
+                       heads, sl2, dp);
   HSD_CHECK_LAUNCH();
 }
 
@@ -411,11 +500,19 @@ void launch_attnS_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, con
   hipLaunchKernelGGL(aS::attnS_delta_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, o, dout,
                      delta_ws, B * S, S, heads);
   HSD_CHECK_LAUNCH();
-  hipLaunchKernelGGL(aS::attnS_bwd_kv_kernel, dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, dout, lse2,
-                     delta_ws, dqkv, dbias, S, heads, sl2, scale, dp);
-  HSD_CHECK_LAUNCH();
-  hipLaunchKernelGGL(aS::attnS_bwd_q_kernel, dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, dout, lse2,
-                     delta_ws, dqkv, dbias, S, heads, sl2, scale, dp);
+  if (dp.enabled) {
+    hipLaunchKernelGGL(aS::attnS_bwd_kv_kernel<true>, dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, dout,
+                       lse2, delta_ws, dqkv, dbias, S, heads, sl2, scale, dp);
+    HSD_CHECK_LAUNCH();
+    hipLaunchKernelGGL(aS::attnS_bwd_q_kernel<true>, dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, dout,
+                       lse2, delta_ws, dqkv, dbias, S, heads, sl2, scale, dp);
+  } else {
+    hipLaunchKernelGGL(aS::attnS_bwd_kv_kernel<false>, dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, dout,
+                       lse2, delta_ws, dqkv, dbias, S, heads, sl2, scale, dp);
+    HSD_CHECK_LAUNCH();
+    hipLaunchKernelGGL(aS::attnS_bwd_q_kernel<false>, dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, dout,
+                       lse2, delta_ws, dqkv, dbias, S, heads, sl2, scale, dp);
+  }
   HSD_CHECK_LAUNCH();
 }
 
