@@ -374,7 +374,16 @@ void gemm2(torch::Tensor A, torch::Tensor B, torch::Tensor C, int64_t la, int64_
                 ws->numel() >= (int64_t)sp * M * N, "gemm2 slab workspace too small");
     wsp = ws->data_ptr<float>();
   }
-  if (!f32out) TORCH_CHECK(sp == 1, "split-K only with fp32 output");
+  torch::Tensor nt_ws;
+  if (!f32out) {
+    // NT bf16 output: splits <= 0 = automatic (gemm2_nt_splits), 1 = one pass, > 1 = split-K slabs + epilogue pass
+    if (sp <= 0) sp = la == 0 ? hsd::gemm2_nt_splits((int)M, (int)N, (int)K) : 1;
+    TORCH_CHECK(la == 0 || sp == 1, "gemm2: split-K bf16 output is NT only");
+    if (sp > 1) {
+      nt_ws = torch::empty({(int64_t)sp * M * N}, A.options().dtype(torch::kFloat32));
+      wsp = nt_ws.data_ptr<float>();
+    }
+  }
   float* dbp = nullptr;
   if (dbias.has_value()) {
     TORCH_CHECK((epi == 5 || epi == 9) && N % 256 == 0, "gemm2 fused dbias: DGELU / MUL epilogue with N % 256 == 0");
@@ -417,6 +426,7 @@ void transpose_many(torch::Tensor desc, int64_t total_tiles) {
 }
 
 int64_t gemm2_splits(int64_t M, int64_t N, int64_t K) { return hsd::gemm2_wgrad_splits((int)M, (int)N, (int)K); }
+int64_t gemm2_nt_splits(int64_t M, int64_t N, int64_t K) { return hsd::gemm2_nt_splits((int)M, (int)N, (int)K); }
 bool gemm2_supported(int64_t la, int64_t lb, int64_t epi, int64_t M, int64_t N, int64_t K) {
   return la == lb && hsd::gemm2_supported((int)la, (int)lb, (int)epi, (int)M, (int)N, (int)K);
 }
@@ -458,6 +468,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm_variant", &gemm_variant);
   m.def("gemm2", &gemm2);
   m.def("gemm2_splits", &gemm2_splits);
+  m.def("gemm2_nt_splits", &gemm2_nt_splits);
   m.def("gemm2_supported", &gemm2_supported);
   m.def("transpose_many", &transpose_many);
   m.def("xent", &xent);

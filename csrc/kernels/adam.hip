@@ -9,43 +9,64 @@
 //   m = b1 m + (1-b1) g ;  v = b2 v + (1-b2) g² ;  θ = θ(1 - lr·wd·mask) - step·m/(√v + eps)
 #include "common.h"
 
+#include <stdlib.h>
+
 namespace hsd {
 
 template <bool kGradBf16, bool kWriteBf16>
+__device__ __forceinline__ f32x4 load_grad(const void* __restrict__ g_, int64_t i) {
+  if constexpr (kGradBf16) {
+    const u32x2 w = __builtin_nontemporal_load(reinterpret_cast<const u32x2*>(g_) + i);
+    return f32x4{lo_bf(w.x), hi_bf(w.x), lo_bf(w.y), hi_bf(w.y)};
+  } else {
+    return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(g_) + i);
+  }
+}
+
+// U chunks of 4 elements per thread per trip, all U x 4 loads issued before the first use (a one-chunk trip
+// leaves ~4 loads in flight per thread, too few to cover HBM latency at the occupancy a CU holds). Every
+// byte is touched once per step, so loads and stores are non-temporal (no L2 / MALL pollution).
+template <bool kGradBf16, bool kWriteBf16, int U>
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float* __restrict__ m,
                                                    float* __restrict__ v, const void* __restrict__ g_,
                                                    bf16_t* __restrict__ out, const uint8_t* __restrict__ decay,
                                                    int64_t n4, float step, float eps, float b1, float b2,
                                                    float gscale, float lr_wd) {
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    f32x4 g;
-    if constexpr (kGradBf16) {
-      u32x2 w = reinterpret_cast<const u32x2*>(g_)[i];
-      g = f32x4{lo_bf(w.x), hi_bf(w.x), lo_bf(w.y), hi_bf(w.y)};
-    } else {
-      g = reinterpret_cast<const f32x4*>(g_)[i];
-    }
-    f32x4 pp = reinterpret_cast<f32x4*>(p)[i];
-    f32x4 mm = reinterpret_cast<f32x4*>(m)[i];
-    f32x4 vv = reinterpret_cast<f32x4*>(v)[i];
-    float wdf = 1.0f;
-    if (decay != nullptr && lr_wd != 0.0f) wdf = decay[(i * 4) >> 6] ? (1.0f - lr_wd) : 1.0f;
+  for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < n4; i0 += stride * U) {
+    f32x4 g[U], pp[U], mm[U], vv[U];
 #pragma unroll
-    for (int k = 0; k < 4; ++k) {
-      float gk = g[k] * gscale;
-      mm[k] = b1 * mm[k] + (1.0f - b1) * gk;
-      vv[k] = b2 * vv[k] + (1.0f - b2) * gk * gk;
-      pp[k] = pp[k] * wdf - step * mm[k] / (sqrtf(vv[k]) + eps);
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i < n4) {
+        g[u] = load_grad<kGradBf16, kWriteBf16>(g_, i);
+        pp[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p) + i);
+        mm[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(m) + i);
+        vv[u] = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(v) + i);
+      }
     }
-    reinterpret_cast<f32x4*>(p)[i] = pp;
-    reinterpret_cast<f32x4*>(m)[i] = mm;
-    reinterpret_cast<f32x4*>(v)[i] = vv;
-    if constexpr (kWriteBf16) {
-      u32x2 o;
-      o.x = pack_bf2(pp[0], pp[1]);
-      o.y = pack_bf2(pp[2], pp[3]);
-      reinterpret_cast<u32x2*>(out)[i] = o;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int64_t i = i0 + u * stride;
+      if (i >= n4) break;
+      float wdf = 1.0f;
+      if (decay != nullptr && lr_wd != 0.0f) wdf = decay[(i * 4) >> 6] ? (1.0f - lr_wd) : 1.0f;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float gk = g[u][k] * gscale;
+        mm[u][k] = b1 * mm[u][k] + (1.0f - b1) * gk;
+        vv[u][k] = b2 * vv[u][k] + (1.0f - b2) * gk * gk;
+        pp[u][k] = pp[u][k] * wdf - step * mm[u][k] / (sqrtf(vv[u][k]) + eps);
+      }
+      __builtin_nontemporal_store(pp[u], reinterpret_cast<f32x4*>(p) + i);
+      __builtin_nontemporal_store(mm[u], reinterpret_cast<f32x4*>(m) + i);
+      __builtin_nontemporal_store(vv[u], reinterpret_cast<f32x4*>(v) + i);
+      if constexpr (kWriteBf16) {
+        u32x2 o;
+        o.x = pack_bf2(pp[u][0], pp[u][1]);
+        o.y = pack_bf2(pp[u][2], pp[u][3]);
+        reinterpret_cast<u32x2*>(out)[i] = o;
+      }
     }
   }
 }
@@ -54,12 +75,23 @@ void launch_adam(float* p, float* m, float* v, const void* g, bool grad_bf16, bf
                  const uint8_t* decay, int64_t n, float step, float eps, float b1, float b2, float gscale,
                  float lr_wd, hipStream_t stream) {
   int64_t n4 = n / 4;  // n is a multiple of 1024 (FlatParamStore)
+  const char* ue = getenv("HSD_ADAM_UNROLL");  // A/B: chunks per thread per trip (1, 2 or 4)
+  const int U = ue ? atoi(ue) : 2;
   int threads = 256;
   int64_t blocks = (n4 + threads - 1) / threads;
-  if (blocks > 256 * 16) blocks = 256 * 16;  // grid-stride: 16 blocks/CU over 256 CUs
-#define HSD_ADAM(GB, WB)                                                                          \
-  hipLaunchKernelGGL((adam_kernel<GB, WB>), dim3((unsigned)blocks), dim3(threads), 0, stream, p, m, v, g, \
-                     out_bf16, decay, n4, step, eps, b1, b2, gscale, lr_wd)
+  if (blocks > 256 * 8) blocks = 256 * 8;  // grid-stride: 8 blocks (32 waves) per CU over 256 CUs
+#define HSD_ADAM(GB, WB)                                                                                         \
+  do {                                                                                                           \
+    if (U >= 4)                                                                                                  \
+      hipLaunchKernelGGL((adam_kernel<GB, WB, 4>), dim3((unsigned)blocks), dim3(threads), 0, stream, p, m, v, g, \
+                         out_bf16, decay, n4, step, eps, b1, b2, gscale, lr_wd);                                 \
+    else if (U == 2)                                                                                             \
+      hipLaunchKernelGGL((adam_kernel<GB, WB, 2>), dim3((unsigned)blocks), dim3(threads), 0, stream, p, m, v, g, \
+                         out_bf16, decay, n4, step, eps, b1, b2, gscale, lr_wd);                                 \
+    else                                                                                                         \
+      hipLaunchKernelGGL((adam_kernel<GB, WB, 1>), dim3((unsigned)blocks), dim3(threads), 0, stream, p, m, v, g, \
+                         out_bf16, decay, n4, step, eps, b1, b2, gscale, lr_wd);                                 \
+  } while (0)
   if (grad_bf16) {
     if (out_bf16) HSD_ADAM(true, true); else HSD_ADAM(true, false);
   } else {

@@ -697,6 +697,57 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
   }
 }
 
+// Split-K NT (small tile counts, gemm2_nt_splits): the main loop wrote fp32 partials [splits][M][N]
+// (E2_F32_SLAB); this pass sums them in split order and runs the SAME per-chunk epilogue math as the fused
+// epilogue (epi_chunk on bf16(acc + bias)), so every epilogue kind, its dropout sites and the fused bias-gradient
+// column sums behave exactly as in the one-pass kernel (up to the fp32 summation order of the K-splits).
+// Block = 8 16-B column chunks (64 columns) x 32 row lanes; `rpb` rows per block.
+template <int EPI>
+__global__ __launch_bounds__(256) void splitk_epi_kernel(const float* __restrict__ ws, int splits, int rpb,
+                                                         G2Params p) {
+  p.dp = resolve_seed(p.dp);
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int c8 = tid & 7, rl = tid >> 3;
+  const int nb = blockIdx.x * 64;
+  const int n = nb + c8 * 8;
+  const int m0 = blockIdx.y * rpb;
+  const int m1 = min(p.M, m0 + rpb);
+  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  if (n < p.N) {
+    f32x4 b0 = {0.f, 0.f, 0.f, 0.f}, b1 = {0.f, 0.f, 0.f, 0.f};
+    if constexpr (epi_bias(EPI)) {
+      const u32x4 b = *reinterpret_cast<const u32x4*>(p.bias + n);
+      b0 = f32x4{lo_bf(b.x), hi_bf(b.x), lo_bf(b.y), hi_bf(b.y)};
+      b1 = f32x4{lo_bf(b.z), hi_bf(b.z), lo_bf(b.w), hi_bf(b.w)};
+    }
+    const int64_t plane = (int64_t)p.M * p.N;
+    bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
+    for (int m = m0 + rl; m < m1; m += 32) {
+      const float* w = ws + (int64_t)m * p.N + n;
+      f32x4 a0 = *reinterpret_cast<const f32x4*>(w);
+      f32x4 a1 = *reinterpret_cast<const f32x4*>(w + 4);
+      for (int sp = 1; sp < splits; ++sp) {
+        a0 += *reinterpret_cast<const f32x4*>(w + sp * plane);
+        a1 += *reinterpret_cast<const f32x4*>(w + sp * plane + 4);
+      }
+      if constexpr (epi_bias(EPI)) {
+        a0 += b0;
+        a1 += b1;
+      }
+      const u32x2 lo = pack4(a0), hi = pack4(a1);
+      u32x4 o = {lo.x, lo.y, hi.x, hi.y}, o2;
+      u32x4 x = {0, 0, 0, 0};
+      if constexpr (epi_aux(EPI)) x = *reinterpret_cast<const u32x4*>(p.aux + (int64_t)m * p.ldaux + n);
+      epi_chunk<EPI>(o, o2, x, m, n, p, csum);
+      st16(C + (int64_t)m * p.ldc + n, o, p.nt_store);
+      if constexpr (epi_two_out(EPI)) st16(p.C2 + (int64_t)m * p.ldc + n, o2, p.nt_store);
+    }
+  }
+  if constexpr (EPI == E2_DGELU || EPI == E2_MUL) {
+    if (p.dbias != nullptr) colsum_flush(csum, p.dbias, nb, p.N, lane);  // every lane: shuffles inside
+  }
+}
+
 }  // namespace g2
 
 // Main-loop schedule (tools/gemm_probe.py, interleaved rounds in one process, random operands, T = 131072
@@ -774,6 +825,21 @@ int gemm2_pick_bn(int M, int N) {
   return best;
 }
 
+// K-splits for a bf16-output NT GEMM. A 256 x 256 tile grid that leaves more than half of the 256 CUs idle
+// (the reference's own per-rank batch: bert-large, B = 8, S = 512 -> M = 4096: 64 tiles on the H-wide GEMMs)
+// is split over K into fp32 slabs plus one reduce-and-epilogue pass, keeping >= 8 K-tiles per split.
+// HSD_G2_SPLITK=0 disables, =n forces n.
+int gemm2_nt_splits(int M, int N, int K) {
+  const char* e = getenv("HSD_G2_SPLITK");
+  const int kt = K / 64;
+  if (e) return std::max(1, std::min(atoi(e), kt));
+  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  if (tiles * 2 > 256) return 1;
+  int s = 256 / tiles;
+  while (s > 1 && kt / s < 8) --s;
+  return s;
+}
+
 bool gemm2_supported(int la, int lb, int epi, int M, int N, int K) {
   if (K % 64 || M < 1 || N % 8) return false;
   if (la == 0 && lb == 0) return epi_bf16_out(epi) && gemm2_pick_bn(M, N) != 0;
@@ -827,6 +893,39 @@ void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const b
   p.A = A; p.lda = lda; p.B = B; p.ldb = ldb; p.M = M; p.N = N; p.K = K; p.C = C; p.ldc = ldc;
   p.bias = bias; p.aux = aux; p.ldaux = ldaux; p.C2 = C2;
   p.dp = make_dropout(p_drop, seed);
+  if (la == 0 && lb == 0 && splits > 1) {
+    if (ws == nullptr || !epi_bf16_out(epi)) abort();
+    G2Params q = p;
+    q.C = ws;
+    q.dbias = nullptr;
+    g2_launch<0, 0, E2_F32_SLAB, 256>(q, splits, st);
+    int kps = (K + splits - 1) / splits;
+    kps = (kps + 63) / 64 * 64;
+    const int real = (K + kps - 1) / kps;
+    const int gx = (N + 63) / 64;
+    const int gy_want = std::max(1, 2048 / gx);
+    int rpb = (M + gy_want - 1) / gy_want;
+    rpb = (rpb + 31) / 32 * 32;
+    const dim3 grid(gx, (M + rpb - 1) / rpb);
+#define G2_SK(E)                                                                                          \
+  case E:                                                                                                 \
+    hipLaunchKernelGGL(g2::splitk_epi_kernel<E>, grid, dim3(256), 0, st, (const float*)ws, real, rpb, p); \
+    break;
+    switch (epi) {
+      G2_SK(E2_STORE)
+      G2_SK(E2_BIAS)
+      G2_SK(E2_BIAS_GELU)
+      G2_SK(E2_BIAS_DROP_RES)
+      G2_SK(E2_RES)
+      G2_SK(E2_DGELU)
+      G2_SK(E2_BIAS_GELU_D)
+      G2_SK(E2_MUL)
+      default: abort();
+    }
+#undef G2_SK
+    HSD_CHECK_LAUNCH();
+    return;
+  }
   if (la == 0 && lb == 0) {
     int bn = gemm2_pick_bn(M, N);
     if (dbias != nullptr) {

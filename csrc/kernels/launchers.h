@@ -80,6 +80,7 @@ void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const b
                   double p_drop, uint64_t seed, int splits, float* ws, float* dbias, hipStream_t st);
 bool gemm2_supported(int la, int lb, int epi, int M, int N, int K);
 int gemm2_wgrad_splits(int M, int N, int K);
+int gemm2_nt_splits(int M, int N, int K);
 void launch_gemm_wgrad_variant(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, int M, int N, int K, float* C,
                                int64_t ldc, int splits, hipStream_t st);
 }  // namespace hsd

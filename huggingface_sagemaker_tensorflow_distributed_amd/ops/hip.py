@@ -439,7 +439,7 @@ def gemm_fwd(x, w, epi, bias=None, aux=None, out2=None, p=0.0, seed=0):
         _C.gemm8(qx, FP8_E4M3, sx, wq, FP8_E4M3, w._hsd_qs, y, epi, bias, aux, out2, float(p), _s64(seed), None)
         return y
     if _nt_ok(x.shape[0], w.shape[0], x.shape[1], epi):
-        _C.gemm2(x, w, y, 0, 0, epi, bias, aux, out2, float(p), _s64(seed), 1, None, None)
+        _C.gemm2(x, w, y, 0, 0, epi, bias, aux, out2, float(p), _s64(seed), 0, None, None)  # 0: auto split-K
     else:
         _C.gemm(x, w, y, 0, 0, epi, bias, aux, out2, float(p), _s64(seed), 1)
     return y
@@ -465,7 +465,7 @@ def gemm_dgrad(dy, w, epi=EPI_STORE, aux=None, dbias=None):
         if wt is None or wt.shape[0] != w.shape[1] or wt.shape[1] != w.shape[0]:
             wt = w.t().contiguous()
         fuse = dbias is not None and epi in (EPI_DGELU, EPI_MUL) and w.shape[1] % 256 == 0
-        _C.gemm2(dy, wt, dx, 0, 0, epi, None, aux, None, 0.0, 0, 1, None, dbias if fuse else None)
+        _C.gemm2(dy, wt, dx, 0, 0, epi, None, aux, None, 0.0, 0, 0, None, dbias if fuse else None)
         if dbias is not None and not fuse:
             _C.colsum(dx, dbias)
     else:

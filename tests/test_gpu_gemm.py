@@ -232,3 +232,33 @@ def test_gemm2_gelu_derivative_and_mul_epilogues(gpu):
     C_.gemm2(dy, W, out, 0, 0, 9, None, D, None, 0.0, 0, 1, None, db)
     _check(out, (dy.float() @ W.float().t()).bfloat16().float() * D.float())
     _check(db, out.float().sum(0), 1e-3)
+
+
+@pytest.mark.parametrize("M,N,K,splits", [(512, 768, 1024, 4), (300, 512, 3072, 3), (4096, 1024, 4096, 0)])
+@pytest.mark.parametrize("epi", [0, 1, 2, 3, 4, 5, 8, 9])
+def test_gemm2_nt_splitk_matches_one_pass(gpu, M, N, K, splits, epi):
+    """Split-K NT (fp32 slabs + reduce-and-epilogue pass) == the one-pass fused epilogue, for every epilogue kind
+    (same dropout sites, same fused bias-gradient column sums), up to the fp32 order of the K-split sums."""
+    torch.manual_seed(5 + epi)
+    C_ = _C()
+    if splits == 0:
+        assert C_.gemm2_nt_splits(M, N, K) > 1  # the reference's bert-large B=8 S=512 shape is split automatically
+    A, B = _mk((M, K), gpu), _mk((N, K), gpu, 0.05)
+    bias = _mk((N,), gpu)
+    aux = _mk((M, N), gpu) if epi != 9 else torch.rand(M, N, device=gpu).bfloat16()
+    two = epi in (2, 8)
+    p = 0.1 if epi == 3 else 0.0
+    outs = []
+    for sp in (1, splits):
+        C = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+        C2 = torch.empty_like(C) if two else None
+        db = torch.zeros(N, device=gpu) if epi in (5, 9) and N % 256 == 0 else None
+        C_.gemm2(A, B, C, 0, 0, epi, bias if epi in (1, 2, 3, 8) else None, aux if epi in (3, 4, 5, 9) else None,
+                 C2, p, 77, sp, None, db)
+        outs.append((C.float(), C2.float() if two else None, db))
+    (c1, c21, d1), (cs, c2s, ds) = outs
+    _check(cs, c1)
+    if two:
+        _check(c2s, c21)
+    if d1 is not None:
+        torch.testing.assert_close(ds, d1, rtol=2e-2, atol=1e-2 * float(d1.abs().max()) + 1e-3)
