@@ -302,3 +302,25 @@ def test_overlap_from_timeline():
     assert r["comm_ms"] == 8.0 and r["exposed_ms"] == 5.0 and r["tail_ms"] == 5.0
     assert r["overlap_pct"] == 37.5 and r["bytes"] == 600
     assert overlap_from_timeline(5.0, [])["overlap_pct"] == 100.0
+
+
+def _worker_agree(rank, world, port):
+    _setenv(rank, world, port)
+    import torch.distributed as dist
+
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel import backend, comm
+
+    backend.init(device="cpu")
+    dev = torch.device("cpu")
+    # the native engine is created only if EVERY rank succeeds; one failing rank makes all of them fall back
+    assert comm._all_ranks_ok(True, dev)
+    assert not comm._all_ranks_ok(rank != world - 1, dev)
+    assert comm._disable("test") is None and not comm.native_active()
+    assert comm.get_engine() is None  # disabled (and a CPU world never builds the engine anyway)
+    comm.reset()
+    dist.barrier()
+    backend.shutdown()
+
+
+def test_native_engine_creation_is_agreed_across_ranks():
+    mp.spawn(_worker_agree, args=(2, _port()), nprocs=2, join=True)

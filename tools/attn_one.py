@@ -1,5 +1,6 @@
-"""Runs the S=128 attention forward once and the backward `iters` times at the BERT-base B=1024 shape (for
-rocprofv3 --pmc passes); prints the mean times of both directions at p = 0 and p = 0.1."""
+"""Runs the attention forward and backward `iters` times (for rocprofv3 --pmc passes); prints the mean times of
+both directions at p = 0 and p = 0.1. Default shape: BERT-base B=1024 S=128; ATTN_SHAPE=B,S,heads overrides
+(bert-large S=512: ATTN_SHAPE=64,512,16)."""
 import os
 import sys
 
@@ -10,7 +11,8 @@ from huggingface_sagemaker_tensorflow_distributed_amd.ops import hip  # noqa: E4
 
 C_ = hip._C
 dev = "cuda"
-B, S, heads, H = 1024, 128, 12, 768
+B, S, heads = (int(v) for v in os.environ.get("ATTN_SHAPE", "1024,128,12").split(","))
+H = heads * 64
 T = B * S
 p = float(sys.argv[1]) if len(sys.argv) > 1 else 0.1
 iters = int(sys.argv[2]) if len(sys.argv) > 2 else 5
@@ -22,6 +24,7 @@ dqkv = torch.empty_like(qkv)
 dout = torch.randn(T, H, device=dev).bfloat16()
 mask = torch.zeros(B, S, device=dev)
 dbias = torch.zeros(3 * H, device=dev)
+ws = torch.empty(B * heads * S, device=dev) if S > 128 else None  # delta workspace of the streaming kernels
 st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
 for pp in sorted({0.0, p}):
     C_.attn_fwd(qkv, mask, out, lse, B, S, heads, pp, 123)
@@ -34,7 +37,7 @@ for pp in sorted({0.0, p}):
     f = st.elapsed_time(en) / iters * 1e3
     st.record()
     for _ in range(iters):
-        C_.attn_bwd(qkv, mask, out, dout, lse, dqkv, None, B, S, heads, pp, 123, dbias)
+        C_.attn_bwd(qkv, mask, out, dout, lse, dqkv, ws, B, S, heads, pp, 123, dbias)
     en.record()
     torch.cuda.synchronize()
     b = st.elapsed_time(en) / iters * 1e3

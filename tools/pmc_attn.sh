@@ -1,5 +1,5 @@
 #!/bin/bash
-# PMC passes over the S=128 attention kernels (tools/attn_one.py): kernel-trace + pmc only, one counter set per run.
+# PMC passes over the attention kernels (tools/attn_one.py; ATTN_SHAPE=B,S,heads selects the shape): kernel-trace + pmc only, one counter set per run.
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
