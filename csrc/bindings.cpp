@@ -25,7 +25,7 @@ void adam_step(torch::Tensor p, torch::Tensor m, torch::Tensor v, torch::Tensor 
   CHECK_CUDA(p); CHECK_CONTIG(p); CHECK_DTYPE(p, torch::kFloat32);
   CHECK_DTYPE(m, torch::kFloat32); CHECK_DTYPE(v, torch::kFloat32);
   TORCH_CHECK(p.numel() == m.numel() && p.numel() == v.numel() && p.numel() == g.numel(), "size mismatch");
-  TORCH_CHECK(p.numel() % 1024 == 0, "flat buffer must be a multiple of 1024 elements");
+  TORCH_CHECK(p.numel() % 64 == 0, "flat buffer (or slice) must be a multiple of 64 elements");
   bool gbf = g.scalar_type() == torch::kBFloat16;
   TORCH_CHECK(gbf || g.scalar_type() == torch::kFloat32, "grad must be fp32 or bf16");
   hsd::bf16_t* o = nullptr;

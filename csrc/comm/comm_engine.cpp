@@ -100,6 +100,8 @@ class CommEngine {
   }
 
   int64_t rank() const { return rank_; }
+  // the comm stream (the optimizer steps each bucket on it right after the bucket's all-reduce)
+  int64_t stream_ptr() const { return reinterpret_cast<int64_t>(stream_); }
   int64_t world() const { return world_; }
 
   // ---------------------------------------------------------------- one-shot collectives
@@ -333,6 +335,7 @@ void register_comm(pybind11::module& m) {
       .def("add_dependency_stream", &CommEngine::add_dependency_stream)
       .def("num_buckets", &CommEngine::num_buckets)
       .def("launched_count", &CommEngine::launched_count)
+      .def("stream_ptr", &CommEngine::stream_ptr)
       .def_property_readonly("rank", &CommEngine::rank)
       .def_property_readonly("world", &CommEngine::world);
 }

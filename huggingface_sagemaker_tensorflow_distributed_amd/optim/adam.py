@@ -11,11 +11,20 @@ PyTorch's form divides √v by √(1-β2ᵗ) before adding ε; both are ``θ -= 
 The DP ``1/N`` gradient average (``hvd.DistributedOptimizer`` semantics) and the optional
 gradient-accumulation ``1/k`` are folded into ``grad_scale``; with bf16 compute the kernel also
 writes the bf16 weight copy the next forward reads (no separate cast pass).
+
+Overlap with backward (:meth:`FusedAdam.enable_overlap`): the update is elementwise, so a contiguous slice of the
+flat buffers can be stepped as soon as its gradients are final. The store is laid out in backward order, so
+the slices complete front-to-back while the rest of backward still runs: one process runs each slice's Adam on
+a side stream the moment its last gradient is queued; data-parallel ranks run it on the RCCL engine's stream
+right after the slice's bucket all-reduce. The memory-bound update then shares the GPU with the compute-bound
+backward GEMMs instead of following them (the bert-large optimizer pass moves ~10 GB per step). What is left
+at ``step()`` is the join, the slices no gradient reached, and the batched Wᵀ refresh.
 """
 from __future__ import annotations
 
 import math
-from typing import Iterable, List, Optional
+import os
+from typing import Callable, Iterable, List, Optional, Tuple
 
 import torch
 
@@ -61,8 +70,62 @@ class FusedAdam:
         eps_eff = self.eps if self.eps_mode == "keras" else self.eps * math.sqrt(bc2)
         return step, eps_eff
 
+    # -------------------------------------------------------------------------- overlap with backward
+    def enable_overlap(self, ranges: List[Tuple[int, int]], on_ready: Optional[Callable] = None) -> None:
+        """Step the flat-buffer slices ``ranges`` (64-aligned, backward order) as their gradients complete.
+        ``on_ready``: the store-readiness callback to install (one process); data-parallel ranks call
+        :meth:`step_range` from the bucketer instead."""
+        self._ranges = list(ranges)
+        self._done = [False] * len(self._ranges)
+        self._began = False
+        if on_ready is not None:
+            self.store.ready_callback = on_ready
+
+    @property
+    def overlap_enabled(self) -> bool:
+        return bool(getattr(self, "_ranges", None))
+
+    def begin_step(self, grad_scale: float) -> None:
+        """Fix this step's coefficients before backward (the slices are stepped during it)."""
+        self.step_count += 1
+        step, eps_eff = self._coeffs()
+        self._coef = (step, eps_eff, float(grad_scale))
+        self._done = [False] * len(self._ranges)
+        self._began = True
+
+    @torch.no_grad()
+    def step_range(self, b: int) -> None:
+        """Adam on slice ``b`` on the CURRENT stream (the caller orders it after the slice's gradients)."""
+        if not self._began or self._done[b]:
+            return
+        from ..ops import hip
+
+        st, e = self._ranges[b]
+        s = self.store
+        step, eps_eff, gscale = self._coef
+        out = s.compute[st:e] if s.compute is not s.master else None
+        dm = self._decay_mask[st // ALIGN:(e + ALIGN - 1) // ALIGN] if self._decay_mask is not None else None
+        hip.adam_step(s.master[st:e], self.exp_avg[st:e], self.exp_avg_sq[st:e], s.grad[st:e], out, dm, step,
+                      eps_eff, self.beta1, self.beta2, gscale, self.lr * self.weight_decay)
+        self._done[b] = True
+
+    @torch.no_grad()
+    def _finish_overlapped(self, grad_scale: float) -> None:
+        from ..ops import hip
+
+        if abs(grad_scale - self._coef[2]) > 1e-12 * max(1.0, abs(grad_scale)):
+            raise RuntimeError("FusedAdam: grad_scale changed between begin_step and step")
+        hip.join_side_streams()
+        for b in range(len(self._ranges)):  # slices no gradient reached (unused parameters)
+            self.step_range(b)
+        self._began = False
+        self.store.refresh_transposed()
+
     @torch.no_grad()
     def step(self, grad_scale: float = 1.0) -> None:
+        if getattr(self, "_began", False):
+            self._finish_overlapped(grad_scale)
+            return
         self.step_count += 1
         step, eps_eff = self._coeffs()
         s = self.store
@@ -86,3 +149,58 @@ class FusedAdam:
         s.master.addcdiv_(self.exp_avg, self.exp_avg_sq.sqrt().add_(eps_eff), value=-step)
         if write_compute:
             s.compute.copy_(s.master)
+
+
+def plan_ranges(store: FlatParamStore, bucket_mb: float) -> Tuple[List[Tuple[int, int]], List[int]]:
+    """Contiguous slices of ~``bucket_mb`` of gradients over whole segments, and each parameter's slice."""
+    limit = int(bucket_mb * (1 << 20)) // store.grad.element_size()
+    ranges, owner, start = [], [0] * len(store.segments), 0
+    for i, _seg in enumerate(store.segments):
+        owner[i] = len(ranges)
+        end = store.segments[i + 1].offset if i + 1 < len(store.segments) else store.numel
+        if end - start >= limit or i + 1 == len(store.segments):
+            ranges.append((start, end))
+            start = end
+    return ranges, owner
+
+
+class LocalOverlap:
+    """One-process driver of :meth:`FusedAdam.enable_overlap`: counts each slice's ready gradients (the store's
+    post-accumulate hooks) and, when the last one is queued, runs the slice's Adam on a side stream that first
+    waits for everything queued so far on the compute (and wgrad) streams."""
+
+    def __init__(self, opt: FusedAdam, bucket_mb: Optional[float] = None):
+        store = opt.store
+        mb = bucket_mb if bucket_mb else float(os.environ.get("HSD_OPT_BUCKET_MB", "32"))
+        self.ranges, self.owner = plan_ranges(store, mb)
+        self.count = [0] * len(self.ranges)
+        for o in self.owner:
+            self.count[o] += 1
+        self.pending = list(self.count)
+        self.opt = opt
+        self.stream = torch.cuda.Stream(device=store.device)
+        self.sync = True
+        opt.enable_overlap(self.ranges, on_ready=self.mark_ready)
+
+    def begin(self) -> None:
+        self.pending = list(self.count)
+        self.sync = True
+
+    def mark_ready(self, i: int) -> None:
+        if not self.sync:  # accumulation micro-step: gradients are not final yet
+            return
+        b = self.owner[i]
+        self.pending[b] -= 1
+        if self.pending[b] == 0:
+            from ..ops import hip
+
+            cur = torch.cuda.current_stream(self.stream.device)
+            self.stream.wait_stream(cur)
+            side = hip.side_stream(self.stream.device)
+            if side is not None:
+                self.stream.wait_stream(side)
+            with torch.cuda.stream(self.stream):
+                self.opt.step_range(b)
+
+    def join(self) -> None:
+        torch.cuda.current_stream(self.stream.device).wait_stream(self.stream)

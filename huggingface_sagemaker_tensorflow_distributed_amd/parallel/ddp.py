@@ -87,6 +87,7 @@ class GradBucketer:
             for pi in b.params:
                 self._param_bucket[pi] = b
         self.sync_enabled = True
+        self._on_reduced = None
         self.engine = engine
         if engine is None and (native is None or native) and group is None:
             from .comm import get_engine
@@ -119,7 +120,9 @@ class GradBucketer:
             return
         if self.engine is not None:
             if self.overlap:
-                self.engine.mark_ready(i)
+                idx = self.engine.mark_ready(i)
+                if idx >= 0 and self._on_reduced is not None:
+                    self._on_reduced(idx)
             return
         b = self._param_bucket[i]
         if b.launched:
@@ -154,6 +157,8 @@ class GradBucketer:
             return
         if self.engine is not None:
             self.engine.finish()  # launches unlaunched buckets; compute stream waits (host does not)
+            if self._on_reduced is not None:
+                self.engine.wait_all()  # ... and for the optimizer slices queued behind the all-reduces
             return
         if self.world <= 1:
             return
@@ -174,6 +179,21 @@ class GradBucketer:
             yield
         finally:
             self.sync_enabled = prev
+
+    def attach_optimizer(self, opt) -> bool:
+        """Step each bucket's slice of ``opt`` (FusedAdam) on the RCCL engine's stream right after the bucket's
+        all-reduce, i.e. under the rest of backward (native engine with overlap only)."""
+        if self.engine is None or not self.overlap or self.store.device.type != "cuda":
+            return False
+        ext = torch.cuda.ExternalStream(self.engine.stream_ptr(), device=self.store.device)
+        opt.enable_overlap([(b.start, b.end) for b in self.buckets])
+
+        def on_reduced(idx: int) -> None:
+            with torch.cuda.stream(ext):
+                opt.step_range(idx)
+
+        self._on_reduced = on_reduced
+        return True
 
     # ---------------------------------------------------------------- overlap timeline
     def set_timing(self, on: bool) -> bool:

@@ -204,4 +204,7 @@ def run(argv: Optional[Sequence[str]] = None, mode: str = "train") -> dict:
         tokenizer.save_pretrained(args.model_dir)
     backend.barrier()
     out["global_step"] = trainer.global_step
+    # tear the process group down explicitly: left to interpreter exit, the c10d / gloo threads are destroyed in
+    # arbitrary order and a rank can abort ("terminate called without an active exception") after a good run
+    backend.shutdown()
     return out

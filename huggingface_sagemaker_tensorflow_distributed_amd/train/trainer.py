@@ -18,6 +18,7 @@ from __future__ import annotations
 import contextlib
 import logging
 import math
+import os
 import time
 from dataclasses import dataclass, field
 from typing import Callable, Dict, Iterable, List, Optional
@@ -96,8 +97,34 @@ class Trainer:
         self._graphs = {}
         self._seed = None
         self._graph_replay = True  # tests: False = graph-mode seeding with eager kernels
+        self._opt_overlap = None  # LocalOverlap (one process) | "engine" (DP ranks) | None
         if hip_graph:
             self.enable_hip_graph()
+        if self._seed is None:
+            self._setup_opt_overlap()
+
+    def _setup_opt_overlap(self) -> None:
+        """Optimizer slices stepped under backward (optim/adam.py). Off: HSD_OPT_OVERLAP=0, CPU, HIP-graph mode,
+        DP worlds without the native engine, and optimizers without the flat-slice API."""
+        if (os.environ.get("HSD_OPT_OVERLAP", "1") == "0" or self.device.type != "cuda"
+                or not hasattr(self.optimizer, "enable_overlap")):
+            return
+        if self.bucketer is None and self.world == 1:
+            from ..optim.adam import LocalOverlap
+
+            self._opt_overlap = LocalOverlap(self.optimizer)
+        elif self.bucketer is not None and self.bucketer.attach_optimizer(self.optimizer):
+            self._opt_overlap = "engine"
+
+    def _drop_opt_overlap(self) -> None:
+        if self._opt_overlap is None:
+            return
+        if self._opt_overlap != "engine":
+            self.store.ready_callback = None
+        elif self.bucketer is not None:
+            self.bucketer._on_reduced = None
+        self.optimizer._ranges = []
+        self._opt_overlap = None
 
     def enable_hip_graph(self) -> bool:
         """Replay forward + backward from captured HIP graphs (train/graph.py). Single-process GPU runs of
@@ -110,6 +137,7 @@ class Trainer:
             return False
         from .graph import DeviceStepSeed
 
+        self._drop_opt_overlap()  # captured steps keep the optimizer outside the graph
         self._seed = DeviceStepSeed(self.device, self.model.rng.base_seed, self.rank)
         return True
 
@@ -141,9 +169,16 @@ class Trainer:
         if self.bucketer is not None:
             self.bucketer.begin()
         k = len(micro_batches)
+        ov = self._opt_overlap
+        if ov is not None:
+            self.optimizer.begin_step(grad_scale=1.0 / (self.world * k))
+            if ov != "engine":
+                ov.begin()
         loss = None
         for i, mb in enumerate(micro_batches):
             last = i == k - 1
+            if ov is not None and ov != "engine":
+                ov.sync = last  # accumulation micro-steps: gradients not final
             if self._seed is not None and self._graph_replay:
                 with prange("graph-replay"):
                     loss, logits = self._graph_for(mb).run(mb)
@@ -163,6 +198,8 @@ class Trainer:
                 ops.join_side_streams()
             if self.bucketer is not None:
                 self.bucketer.finish()
+            if ov is not None and ov != "engine":
+                ov.join()
         with prange("optimizer"):
             self.optimizer.step(grad_scale=1.0 / (self.world * k))
         self.global_step += 1

@@ -114,3 +114,38 @@ def test_train_script_on_gpu_writes_reference_artifacts(gpu, tmp_path, model, se
     cfg = json.loads((tmp_path / "model" / "config.json").read_text())
     assert cfg["architectures"] == ["BertForSequenceClassification"]
     assert (tmp_path / "model" / "model.safetensors").exists()
+
+
+@pytest.mark.parametrize("accum", [1, 2])
+def test_optimizer_overlapped_with_backward_uses_final_gradients(gpu, monkeypatch, accum):
+    """Adam slices stepped under backward (LocalOverlap, the default on one GPU): after each step the master
+    weights, moments and bf16 copies equal ONE full Adam pass applied afterwards to the final gradients of that step
+    (bit for bit) -- a slice stepped before its last gradient landed, or with the wrong coefficients, would differ.
+    Run-to-run comparison is not bitwise (fp32 atomics in the backward), hence this per-step replay."""
+    from huggingface_sagemaker_tensorflow_distributed_amd import data as hdata
+    from huggingface_sagemaker_tensorflow_distributed_amd.ops import hip
+    from huggingface_sagemaker_tensorflow_distributed_amd.train.runner import build
+    from huggingface_sagemaker_tensorflow_distributed_amd.utils.args import build_parser
+
+    ds = hdata.synthetic_classification(8 * 4, 128, 30522, seed=0)
+    batches = [{k: torch.from_numpy(v[8 * i:8 * (i + 1)]).long().to(gpu) for k, v in
+                (("input_ids", ds.input_ids), ("attention_mask", ds.attention_mask), ("labels", ds.labels))}
+               for i in range(4)]
+    monkeypatch.setenv("HSD_OPT_OVERLAP", "1")
+    monkeypatch.setenv("HSD_OPT_BUCKET_MB", "4")  # many slices
+    args, _ = build_parser("train").parse_known_args(
+        ["--model_name_or_path", "bert-base-uncased", "--train_batch_size", "8", "--learning_rate", "1e-4",
+         "--dtype", "bf16", "--log_every", "0", "--seed", "3"])
+    parts = build(args, "train")
+    tr, st, opt = parts["trainer"], parts["store"], parts["optimizer"]
+    assert tr._opt_overlap is not None and len(opt._ranges) > 10
+    for step in range(3):
+        p0, m0, v0 = st.master.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone()
+        tr.train_step([batches[(step * accum + j) % 4] for j in range(accum)])
+        torch.cuda.synchronize()
+        s, eps = opt._coeffs()
+        out = torch.empty_like(st.compute)
+        hip.adam_step(p0, m0, v0, st.grad, out, None, s, eps, opt.beta1, opt.beta2, 1.0 / accum, 0.0)
+        torch.cuda.synchronize()
+        assert torch.equal(p0, st.master) and torch.equal(m0, opt.exp_avg) and torch.equal(v0, opt.exp_avg_sq)
+        assert torch.equal(out, st.compute)
