@@ -104,3 +104,42 @@ def test_hip_backward_through_native_engine(gpu):
     assert all(0 <= s <= e for s, e, _ in rep["buckets"])
     assert sum(s < rep["backward_ms"] for s, _, _ in rep["buckets"]) >= eng.num_buckets() - 2
     buck.detach()
+
+
+def test_optimizer_overlap_on_engine_stream(gpu, monkeypatch):
+    """DP form of the optimizer overlap: each bucket's Adam slice runs on the RCCL engine's stream right after the
+    bucket's all-reduce (world-of-one communicator here). Every step must equal one full Adam pass over that step's
+    final (reduced) gradients, bit for bit."""
+    from huggingface_sagemaker_tensorflow_distributed_amd import data as hdata
+    from huggingface_sagemaker_tensorflow_distributed_amd.ops import hip
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel import GradBucketer
+    from huggingface_sagemaker_tensorflow_distributed_amd.train.runner import build
+    from huggingface_sagemaker_tensorflow_distributed_amd.train.trainer import Trainer
+    from huggingface_sagemaker_tensorflow_distributed_amd.utils.args import build_parser
+
+    monkeypatch.setenv("HSD_OPT_OVERLAP", "1")
+    args, _ = build_parser("train").parse_known_args(
+        ["--model_name_or_path", "bert-base-uncased", "--train_batch_size", "8", "--dtype", "bf16",
+         "--learning_rate", "1e-4", "--log_every", "0"])
+    parts = build(args, "train")
+    model, store, opt = parts["model"], parts["store"], parts["optimizer"]
+    C = _C()
+    eng = C.CommEngine(0, 1, C.CommEngine.unique_id(), gpu.index, True)
+    buck = GradBucketer(store, bucket_mb=4, engine=eng)
+    tr = Trainer(model, store, opt, buck, gpu)
+    assert tr._opt_overlap == "engine" and len(opt._ranges) == len(buck.buckets) > 10
+    ds = hdata.synthetic_classification(16, 128, 30522, seed=0)
+    batches = [{k: torch.from_numpy(v[8 * i:8 * (i + 1)]).long().to(gpu) for k, v in
+                (("input_ids", ds.input_ids), ("attention_mask", ds.attention_mask), ("labels", ds.labels))}
+               for i in range(2)]
+    for step in range(3):
+        p0, m0, v0 = store.master.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone()
+        tr.train_step([batches[step % 2]])
+        torch.cuda.synchronize()
+        assert eng.launched_count() == len(buck.buckets)
+        s, eps = opt._coeffs()
+        out = torch.empty_like(store.compute)
+        hip.adam_step(p0, m0, v0, store.grad, out, None, s, eps, opt.beta1, opt.beta2, 1.0, 0.0)
+        torch.cuda.synchronize()
+        assert torch.equal(p0, store.master) and torch.equal(m0, opt.exp_avg) and torch.equal(v0, opt.exp_avg_sq)
+        assert torch.equal(out, store.compute)
