@@ -123,3 +123,35 @@ def test_fp8_dtype_falls_back_to_bf16_on_cpu(tmp_path, monkeypatch):
     out, d, m = _run_script(tmp_path, ["--model_name_or_path", "hsd-tiny-bert", "--dtype", "fp8",
                                        "--max_seq_length", "16"], monkeypatch)
     assert os.path.isfile(d / "eval_results.txt") and os.path.isfile(m / "model.safetensors")
+
+
+def test_optimizer_overlap_slices_cover_store_in_backward_order():
+    """The overlapped optimizer's slices (optim/adam.py plan_ranges): contiguous, 64-aligned, whole segments, in
+    the store's backward layout order, covering every element exactly once."""
+    from huggingface_sagemaker_tensorflow_distributed_amd.models import build_model, resolve_config
+    from huggingface_sagemaker_tensorflow_distributed_amd.optim.adam import plan_ranges
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel import FlatParamStore
+
+    m = build_model(resolve_config("hsd-tiny-bert"), seed=0)
+    store = FlatParamStore(m, "cpu")
+    for mb in (0.001, 0.01, 1000.0):
+        ranges, owner = plan_ranges(store, mb)
+        assert ranges[0][0] == 0 and ranges[-1][1] == store.numel
+        assert all(a[1] == b[0] for a, b in zip(ranges, ranges[1:]))
+        assert all(s % 64 == 0 and e % 64 == 0 and e > s for s, e in ranges)
+        assert owner == sorted(owner) and len(set(owner)) == len(ranges)
+        for i, seg in enumerate(store.segments):
+            s, e = ranges[owner[i]]
+            assert s <= seg.offset and seg.offset + seg.numel <= e
+    assert len(plan_ranges(store, 1000.0)[0]) == 1
+
+
+def test_gemm_nt_split_policy():
+    """Split-K only for NT grids that leave more than half of the 256 CUs idle, >= 8 K-tiles per split."""
+    from huggingface_sagemaker_tensorflow_distributed_amd.ops._ext import load
+
+    C = load()
+    assert C.gemm2_nt_splits(4096, 1024, 4096) == 4      # bert-large B=8 S=512: 64 tiles
+    assert C.gemm2_nt_splits(4096, 768, 3072) == 5       # 48 tiles, 48 K-tiles
+    assert C.gemm2_nt_splits(131072, 768, 768) == 1      # headline: 1536 tiles
+    assert C.gemm2_nt_splits(8192, 768, 768) == 1        # 96 tiles but only 12 K-tiles
