@@ -19,6 +19,7 @@ import sys
 from typing import Dict, Optional
 
 from ..utils.args import hyperparameters_to_argv
+from .smenv import node_topology
 from .spawn import launch, visible_gpu_count
 
 logger = logging.getLogger(__name__)
@@ -35,8 +36,11 @@ class LocalEstimator:
                  distribution: Optional[Dict] = None, instance_type: str = "local", instance_count: int = 1,
                  base_job_name: Optional[str] = None, nproc_per_node: Optional[int] = None,
                  output_path: str = "output", **aws_kwargs):
-        if instance_count != 1:
-            raise ValueError("the local launcher runs one node; instance_count must be 1")
+        # multi-node (instance_count > 1): the same estimator runs on every node; the node list and this node's
+        # index come from the SageMaker container contract (SM_HOSTS / SM_CURRENT_HOST) or HSD_HOSTS / HSD_NODE_RANK
+        self._hosts, self._node_rank = node_topology(instance_count)
+        if instance_count != len(self._hosts):
+            raise ValueError(f"instance_count={instance_count} but {len(self._hosts)} host(s) in the environment")
         self.entry_point = entry_point
         self.source_dir = source_dir
         self.hyperparameters = dict(hyperparameters or {})
@@ -77,8 +81,12 @@ class LocalEstimator:
         cmd = [sys.executable, "-u", script, *hyperparameters_to_argv(self.hyperparameters)]
         n = self.nproc()
         logger.info("job %s: %d process(es) running %s", name, n, " ".join(cmd))
+        nnodes = len(self._hosts)
         rc = launch(cmd, n, output_data_dir=data_dir, model_dir=model_dir, distribution=self.distribution,
-                    hyperparameters=self.hyperparameters, job_name=name)
+                    hyperparameters=self.hyperparameters, job_name=name, nnodes=nnodes, node_rank=self._node_rank,
+                    master_addr=self._hosts[0] if nnodes > 1 else "127.0.0.1",
+                    master_port=int(os.environ.get("HSD_MASTER_PORT", "29500")) if nnodes > 1 else None,
+                    hosts=self._hosts if nnodes > 1 else None)
         self.model_data = model_dir
         if rc != 0:
             raise RuntimeError(f"training job {name} failed with exit code {rc}")

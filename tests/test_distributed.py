@@ -324,3 +324,49 @@ def _worker_agree(rank, world, port):
 
 def test_native_engine_creation_is_agreed_across_ranks():
     mp.spawn(_worker_agree, args=(2, _port()), nprocs=2, join=True)
+
+
+def test_two_node_launch_on_one_machine(tmp_path):
+    """Multi-node launch (--nnodes/--node-rank/--master-addr, SageMaker SM_HOSTS contract): two 'nodes' of one rank
+    each, started as two launchers on this machine, form one world of 2 and train to completion."""
+    import io
+    import threading
+
+    from huggingface_sagemaker_tensorflow_distributed_amd.launcher.spawn import launch
+
+    port = _port()
+    rcs, bufs = [None, None], [io.StringIO(), io.StringIO()]
+
+    def node(i):
+        rcs[i] = launch([sys.executable, os.path.join(ROOT, "scripts", "train.py"), "--model_name_or_path",
+                         "hsd-tiny-bert", "--epochs", "1", "--train_batch_size", "8", "--eval_batch_size", "8",
+                         "--max_seq_length", "32", "--num_train_examples", "64", "--num_eval_examples", "32",
+                         "--device", "cpu"], 1, output_data_dir=str(tmp_path / f"data{i}"),
+                        model_dir=str(tmp_path / f"model{i}"), stdout=bufs[i], nnodes=2, node_rank=i,
+                        master_addr="127.0.0.1", master_port=port)
+
+    ts = [threading.Thread(target=node, args=(i,)) for i in range(2)]
+    for t in ts:
+        t.start()
+    for t in ts:
+        t.join(timeout=240)
+    assert rcs == [0, 0], bufs[0].getvalue()[-2000:] + bufs[1].getvalue()[-2000:]
+    out0 = bufs[0].getvalue()
+    assert "rank=0/2" in out0 and "[1] " in bufs[1].getvalue()  # global rank 1 lives on node 1
+    assert (tmp_path / "data0" / "train_results.txt").exists()  # rank-0 node writes the results
+
+
+def test_estimator_multi_node_topology(monkeypatch):
+    from huggingface_sagemaker_tensorflow_distributed_amd.launcher.estimator import LocalEstimator
+    from huggingface_sagemaker_tensorflow_distributed_amd.launcher.smenv import node_topology
+
+    monkeypatch.delenv("SM_HOSTS", raising=False)
+    monkeypatch.delenv("SM_CURRENT_HOST", raising=False)
+    monkeypatch.delenv("HSD_HOSTS", raising=False)
+    assert node_topology(1) == (["algo-1"], 0)
+    with pytest.raises(ValueError):
+        LocalEstimator("train.py", instance_count=2)
+    monkeypatch.setenv("SM_HOSTS", '["algo-1", "algo-2"]')
+    monkeypatch.setenv("SM_CURRENT_HOST", "algo-2")
+    est = LocalEstimator("train.py", instance_count=2)
+    assert est._hosts == ["algo-1", "algo-2"] and est._node_rank == 1
