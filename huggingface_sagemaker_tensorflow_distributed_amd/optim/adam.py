@@ -78,6 +78,9 @@ class FusedAdam:
         self._ranges = list(ranges)
         self._done = [False] * len(self._ranges)
         self._began = False
+        # each slice's Wᵀ copies are refreshed right after its update (fp8 weight copies, which need the whole
+        # step's amax, are still re-quantised once at the end)
+        self._tsub = self.store.transposed_subsets(self._ranges) if self.store.master.is_cuda else None
         if on_ready is not None:
             self.store.ready_callback = on_ready
 
@@ -107,6 +110,8 @@ class FusedAdam:
         dm = self._decay_mask[st // ALIGN:(e + ALIGN - 1) // ALIGN] if self._decay_mask is not None else None
         hip.adam_step(s.master[st:e], self.exp_avg[st:e], self.exp_avg_sq[st:e], s.grad[st:e], out, dm, step,
                       eps_eff, self.beta1, self.beta2, gscale, self.lr * self.weight_decay)
+        if self._tsub is not None:
+            s.refresh_transposed_subset(self._tsub[b])
         self._done[b] = True
 
     @torch.no_grad()
@@ -119,7 +124,10 @@ class FusedAdam:
         for b in range(len(self._ranges)):  # slices no gradient reached (unused parameters)
             self.step_range(b)
         self._began = False
-        self.store.refresh_transposed()
+        if self._tsub is None:
+            self.store.refresh_transposed()
+        else:
+            self.store.refresh_fp8()
 
     @torch.no_grad()
     def step(self, grad_scale: float = 1.0) -> None:

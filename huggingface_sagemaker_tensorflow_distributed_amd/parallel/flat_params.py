@@ -184,6 +184,26 @@ class FlatParamStore:
         self.fp8_amax.zero_()
         hip._C.fp8_quant_many(ad, ab, qd, qb, self.fp8_amax, self.fp8_sinv, 0)
 
+    def transposed_subsets(self, ranges) -> list:
+        """Per flat-buffer slice ``[start, end)``: the batched-transpose descriptor table of the weights inside it
+        (``(desc, tiles)`` or ``None``), so an optimizer that steps slices separately can refresh each slice's Wᵀ
+        right after the slice's update instead of in one pass at the end of the step."""
+        if self._tdesc is None:
+            return [None] * len(ranges)
+        rows_all = self._tdesc.cpu().tolist()
+        base = self.compute.data_ptr()
+        esize = self.compute.element_size()
+        out = []
+        for st, e in ranges:
+            desc, tiles = [], 0
+            for src, dst, rows, cols, _t in rows_all:
+                off = (src - base) // esize
+                if st <= off < e:
+                    desc.append([src, dst, rows, cols, tiles])
+                    tiles += ((rows + 63) // 64) * ((cols + 63) // 64)
+            out.append((torch.tensor(desc, dtype=torch.int64, device=self.device), tiles) if desc else None)
+        return out
+
     @torch.no_grad()
     def refresh_transposed(self) -> None:
         if self._tdesc is None:
@@ -192,6 +212,15 @@ class FlatParamStore:
 
         hip._C.transpose_many(self._tdesc, self._ttiles)
         self.refresh_fp8()
+
+    @torch.no_grad()
+    def refresh_transposed_subset(self, subset) -> None:
+        """Wᵀ refresh of one slice (a :meth:`transposed_subsets` entry) on the current stream."""
+        if subset is None:
+            return
+        from ..ops import hip
+
+        hip._C.transpose_many(subset[0], subset[1])
 
     def index_of(self, p: torch.Tensor) -> int:
         return self._index[id(p)]

@@ -149,3 +149,8 @@ def test_optimizer_overlapped_with_backward_uses_final_gradients(gpu, monkeypatc
         torch.cuda.synchronize()
         assert torch.equal(p0, st.master) and torch.equal(m0, opt.exp_avg) and torch.equal(v0, opt.exp_avg_sq)
         assert torch.equal(out, st.compute)
+        # each slice's Wᵀ copies are refreshed right after its update
+        tracked = [p for p in st.params if hasattr(p, "_hsd_wt")]
+        assert len(tracked) == 48
+        for p in tracked:
+            assert torch.equal(p._hsd_wt, p.detach().t())
