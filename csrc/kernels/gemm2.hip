@@ -872,7 +872,9 @@ int gemm2_wgrad_splits(int M, int N, int K) {
   int s = 256 / tiles;
   if (s < 1) s = 1;
   const int kt = K / 64;
-  while (s > 1 && kt / s < 4) --s;
+  const char* e = getenv("HSD_WGRAD_MIN_KT");  // A/B: minimum K-tiles per split
+  const int min_kt = e ? std::max(1, atoi(e)) : 4;
+  while (s > 1 && kt / s < min_kt) --s;
   return s;
 }
 
