@@ -441,7 +441,10 @@ static void ln_fwd_t(const bf16_t* y, const bf16_t* res, const bf16_t* gamma, co
   const char* env = getenv("HSD_LN_FWD_RPW");  // A/B: 1 = the one-row kernel; > 1 = rows per wave
   const int mode = env ? atoi(env) : 0;
   if (mode != 1 && res == nullptr && z == nullptr && !dp.enabled && H % 8 == 0 && H <= 1024) {
-    const int rpw = mode > 1 ? mode : std::max(2, std::min(16, rows / 8192));
+    // 2 rows per wave (the next row's loads in flight while one reduces): best at the HBM-bound headline shape
+    // (131072 x 768: 75 us vs 81 us at 16 rows per wave); every setting is equal once the tensors fit the MALL
+    // (tools/bench_ln_rpw.py, profiles/bench_ln_rpw_r2.jsonl)
+    const int rpw = mode > 1 ? mode : 2;
     const int waves = (rows + rpw - 1) / rpw;
     const int blocks = (waves + kLnWaves - 1) / kLnWaves;
     if (H <= 512)
