@@ -17,15 +17,17 @@ import os
 import sys
 
 T = int(os.environ.get("SOL_T", "131072"))
+H = int(os.environ.get("SOL_H", "768"))  # bert-large S=512 B=64: SOL_T=32768 SOL_H=1024
+I = 4 * H
 REPS = 6
 # name: (layout, M, N, K, epi)  -- NT: C[M][N] = A[M][K] B[N][K]^T;  TT: dW[N][K] += dY[T][N]^T X[T][K]
 GEMMS = [
-    ("qkv_fwd_bias", "NT", T, 2304, 768, 1), ("out_fwd_drop_res", "NT", T, 768, 768, 3),
-    ("ffn1_fwd_gelu_d", "NT", T, 3072, 768, 8), ("ffn2_fwd_drop_res", "NT", T, 768, 3072, 3),
-    ("ffn2_dgrad_mul_dbias", "NT", T, 3072, 768, 9), ("ffn1_dgrad_res", "NT", T, 768, 3072, 4),
-    ("out_dgrad", "NT", T, 768, 768, 0), ("qkv_dgrad_res", "NT", T, 768, 2304, 4),
-    ("qkv_wgrad", "TT", 2304, 768, T, 7), ("out_wgrad", "TT", 768, 768, T, 7),
-    ("ffn1_wgrad", "TT", 3072, 768, T, 7), ("ffn2_wgrad", "TT", 768, 3072, T, 7),
+    ("qkv_fwd_bias", "NT", T, 3 * H, H, 1), ("out_fwd_drop_res", "NT", T, H, H, 3),
+    ("ffn1_fwd_gelu_d", "NT", T, I, H, 8), ("ffn2_fwd_drop_res", "NT", T, H, I, 3),
+    ("ffn2_dgrad_mul_dbias", "NT", T, I, H, 9), ("ffn1_dgrad_res", "NT", T, H, I, 4),
+    ("out_dgrad", "NT", T, H, H, 0), ("qkv_dgrad_res", "NT", T, H, 3 * H, 4),
+    ("qkv_wgrad", "TT", 3 * H, H, T, 7), ("out_wgrad", "TT", H, H, T, 7),
+    ("ffn1_wgrad", "TT", I, H, T, 7), ("ffn2_wgrad", "TT", H, I, T, 7),
 ]
 
 
