@@ -14,7 +14,22 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def one(path: str, steps: int, bs: int, seq: int, lr: float) -> dict:
+def _model_dir(layers: int) -> str:
+    """bert-base width and vocab with ``layers`` encoder layers, as an HF config.json directory."""
+    import tempfile
+
+    d = tempfile.mkdtemp(prefix="hsd-conv-")
+    cfg = {"model_type": "bert", "architectures": ["BertForSequenceClassification"], "vocab_size": 30522,
+           "hidden_size": 768, "num_hidden_layers": layers, "num_attention_heads": 12, "intermediate_size": 3072,
+           "hidden_act": "gelu", "hidden_dropout_prob": 0.1, "attention_probs_dropout_prob": 0.1,
+           "max_position_embeddings": 512, "type_vocab_size": 2, "initializer_range": 0.02, "layer_norm_eps": 1e-12,
+           "pad_token_id": 0, "num_labels": 2}
+    with open(os.path.join(d, "config.json"), "w") as f:
+        json.dump(cfg, f)
+    return d
+
+
+def one(path: str, steps: int, bs: int, seq: int, lr: float, layers: int = 12) -> dict:
     sys.path.insert(0, ROOT)
     import torch
 
@@ -25,7 +40,8 @@ def one(path: str, steps: int, bs: int, seq: int, lr: float) -> dict:
     from huggingface_sagemaker_tensorflow_distributed_amd.utils.args import build_parser
 
     args, _ = build_parser("train").parse_known_args(
-        ["--model_name_or_path", "bert-base-uncased", "--train_batch_size", str(bs), "--learning_rate", str(lr),
+        ["--model_name_or_path", "bert-base-uncased" if layers == 12 else _model_dir(layers),
+         "--train_batch_size", str(bs), "--learning_rate", str(lr),
          "--dtype", "bf16", "--log_every", "0", "--seed", "7"])
     parts = build(args, "train")
     tr, dev = parts["trainer"], parts["device"]
@@ -43,7 +59,7 @@ def one(path: str, steps: int, bs: int, seq: int, lr: float) -> dict:
             window = []
     loader = BatchLoader(test, ShardSampler(len(test), 0, 1, shuffle=False, drop_last=False, batch_size=64), dev)
     ev = tr.evaluate(loader)
-    return {"path": path, "steps": steps, "batch": bs, "seq_len": seq, "lr": lr, "loss_curve_25": curve,
+    return {"path": path, "layers": layers, "steps": steps, "batch": bs, "seq_len": seq, "lr": lr, "loss_curve_25": curve,
             "eval_loss": round(ev["loss"], 4), "eval_accuracy": round(ev["sparse_categorical_accuracy"], 4)}
 
 
@@ -53,15 +69,16 @@ def main():
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--seq_len", type=int, default=128)
-    ap.add_argument("--lr", type=float, default=1e-4)
+    ap.add_argument("--lr", type=float, default=3e-5)
+    ap.add_argument("--layers", type=int, default=12, help="encoder layers (bert-base width)")
     a = ap.parse_args()
     if a.path:
-        print(json.dumps(one(a.path, a.steps, a.batch, a.seq_len, a.lr)), flush=True)
+        print(json.dumps(one(a.path, a.steps, a.batch, a.seq_len, a.lr, a.layers)), flush=True)
         return
     for path in ("hip", "torch"):
         env = dict(os.environ, HSD_OPS="torch" if path == "torch" else "")
         cmd = [sys.executable, os.path.abspath(__file__), "--path", path, "--steps", str(a.steps), "--batch",
-               str(a.batch), "--seq_len", str(a.seq_len), "--lr", str(a.lr)]
+               str(a.batch), "--seq_len", str(a.seq_len), "--lr", str(a.lr), "--layers", str(a.layers)]
         out = subprocess.run(cmd, env=env, capture_output=True, text=True)
         line = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
         print(line[-1] if line else json.dumps({"path": path, "error": out.stderr[-2000:]}), flush=True)
