@@ -155,3 +155,26 @@ def test_gemm_nt_split_policy():
     assert C.gemm2_nt_splits(4096, 768, 3072) == 5       # 48 tiles, 48 K-tiles
     assert C.gemm2_nt_splits(131072, 768, 768) == 1      # headline: 1536 tiles
     assert C.gemm2_nt_splits(8192, 768, 768) == 1        # 96 tiles but only 12 K-tiles
+
+
+def test_tiny_bert_learns_the_marker_task_on_cpu():
+    """The CPU (torch reference) path learns the synthetic marker task: the label is carried by one token at a
+    random position of a padded, variable-length sequence (the GPU tier checks the same on the HIP kernels)."""
+    import torch
+
+    from huggingface_sagemaker_tensorflow_distributed_amd import data as hdata
+    from huggingface_sagemaker_tensorflow_distributed_amd.train.runner import build
+    from huggingface_sagemaker_tensorflow_distributed_amd.utils.args import build_parser
+
+    args, _ = build_parser("train").parse_known_args(
+        ["--model_name_or_path", "hsd-tiny-bert", "--train_batch_size", "16", "--learning_rate", "2e-3",
+         "--log_every", "0", "--device", "cpu", "--seed", "7"])
+    tr = build(args, "train")["trainer"]
+    vocab = tr.model.cfg.vocab_size
+    ds = hdata.synthetic_classification(16 * 100, 32, vocab, seed=1)
+    losses = []
+    for i in range(100):
+        sl = slice(16 * i, 16 * (i + 1))
+        losses.append(float(tr.train_step([{k: torch.from_numpy(v[sl]).long() for k, v in (
+            ("input_ids", ds.input_ids), ("attention_mask", ds.attention_mask), ("labels", ds.labels))}]).detach()))
+    assert sum(losses[:10]) / 10 > 0.5 and sum(losses[-20:]) / 20 < 0.2, losses[::10]
