@@ -26,16 +26,18 @@ constexpr int S = 128;
 using namespace attn;
 
 // ------------------------------------------------------------------------------------------------
-__global__ __launch_bounds__(256, 2) void attn128_fwd_kernel(const bf16_t* __restrict__ qkv,
+__global__ __launch_bounds__(256, 4) void attn128_fwd_kernel(const bf16_t* __restrict__ qkv,
                                                              const float* __restrict__ mask, bf16_t* __restrict__ out,
                                                              float* __restrict__ lse2, int heads, float sl2,
                                                              DropoutParams dp) {
   dp = resolve_seed(dp);
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * S * D + 4 * 32 * D + 2 * S];
+  // [K | V | mask bias]; the output staging reuses K's slot after a barrier, so the 33 KiB footprint lets four
+  // workgroups share a CU (122 VGPRs: four waves per SIMD) for more memory-level parallelism
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * S * D + 2 * S];
   bf16_t* Ks = lds;
   bf16_t* Vs = lds + S * D;
-  bf16_t* stg_all = lds + 2 * S * D;
-  float* mbias = reinterpret_cast<float*>(lds + 2 * S * D + 4 * 32 * D);
+  bf16_t* stg_all = lds;
+  float* mbias = reinterpret_cast<float*>(lds + 2 * S * D);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hf = lane >> 5;
@@ -113,6 +115,9 @@ __global__ __launch_bounds__(256, 2) void attn128_fwd_kernel(const bf16_t* __res
       o1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(Vs, kb * 32, s, 1, lane), pb, o1, 0, 0, 0);
     }
   if (hf == 0) lse2[(int64_t)bh * S + q] = mx + __log2f(l);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();  // every wave's K reads done: K's slot becomes the output staging
+  asm volatile("" ::: "memory");
   store_rows(stg_all + wave * 32 * D, o0, o1, 1.0f / l, out + ((int64_t)b * S + wave * 32) * H + hh * D, H, lane);
 }
 
