@@ -30,6 +30,12 @@ def DistributedOptimizer(optimizer, store=None, bucket_mb=None):
     return optimizer, (GradBucketer(store, bucket_mb=bucket_mb) if size() > 1 else None)
 
 
+class callbacks:  # noqa: N801 - the ``hvd.callbacks`` namespace
+    """``hvd.callbacks.BroadcastGlobalVariablesCallback`` / ``MetricAverageCallback`` equivalents (train/callbacks.py)."""
+
+    from .train.callbacks import BroadcastGlobalVariablesCallback, MetricAverageCallback  # noqa: F401
+
+
 def broadcast_parameters(store, optimizer=None, root_rank: int = 0):
     from .parallel.collectives import broadcast_parameters as _b
 
@@ -37,4 +43,4 @@ def broadcast_parameters(store, optimizer=None, root_rank: int = 0):
 
 
 __all__ = ["init", "rank", "size", "local_rank", "local_size", "barrier", "is_distributed", "shutdown",
-           "DistributedOptimizer", "broadcast_parameters", "__version__"]
+           "DistributedOptimizer", "broadcast_parameters", "callbacks", "__version__"]

@@ -110,3 +110,25 @@ class FaultInjection(Callback):
     def on_batch_end(self, trainer, step):
         if backend.rank() == self.rank and trainer.global_step >= self.step >= 0:
             raise SystemExit(f"injected fault on rank {self.rank} at step {trainer.global_step}")
+
+
+class BroadcastGlobalVariablesCallback(Callback):
+    """``hvd.callbacks.BroadcastGlobalVariablesCallback(root_rank)`` (``scripts/train.py:133``): every rank starts
+    from ``root_rank``'s weights (and optimizer state). Horovod's Keras callback broadcasts at the end of the first
+    batch, after the optimizer slots exist; here the flat master / moment buffers exist from construction, so the
+    broadcast happens BEFORE step 1 and the first update is already identical on every rank."""
+
+    def __init__(self, root_rank: int = 0):
+        self.root_rank = int(root_rank)
+
+    def on_train_begin(self, trainer):
+        from ..parallel.collectives import broadcast_parameters
+
+        if backend.is_distributed():
+            broadcast_parameters(trainer.store, trainer.optimizer, src=self.root_rank)
+
+
+class MetricAverageCallback(Callback):
+    """``hvd.callbacks.MetricAverageCallback()``: the epoch metrics the Trainer reports are already exact global
+    averages (an all-reduce of loss-sum / correct / count), so this exists for source
+    compatibility and does nothing."""

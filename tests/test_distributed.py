@@ -370,3 +370,30 @@ def test_estimator_multi_node_topology(monkeypatch):
     monkeypatch.setenv("SM_CURRENT_HOST", "algo-2")
     est = LocalEstimator("train.py", instance_count=2)
     assert est._hosts == ["algo-1", "algo-2"] and est._node_rank == 1
+
+
+def _worker_hvd_callback(rank, world, port):
+    _setenv(rank, world, port)
+    import torch.distributed as dist
+
+    import huggingface_sagemaker_tensorflow_distributed_amd as hvd
+
+    hvd.init(device="cpu")
+    assert hvd.size() == world and hvd.rank() == rank
+    model, store, opt, tr = _make(seed_init=100 + rank)  # every rank starts from different weights
+    opt.exp_avg.fill_(float(rank))
+    cb = hvd.callbacks.BroadcastGlobalVariablesCallback(0)
+    cb.on_train_begin(tr)
+    ref = store.master.clone()
+    dist.broadcast(ref, 0)
+    assert torch.equal(store.master, ref)
+    assert torch.all(opt.exp_avg == 0.0)  # rank 0's optimizer state too
+    assert all(torch.equal(p.detach().float().reshape(-1), store.master[s.offset:s.offset + s.numel])
+               for p, s in zip(store.params, store.segments))
+    hvd.shutdown()
+
+
+def test_hvd_broadcast_callback_syncs_weights_and_optimizer_state():
+    """``hvd.callbacks.BroadcastGlobalVariablesCallback(0)`` (scripts/train.py:133) on the facade: ranks built from
+    different seeds hold rank 0's weights and Adam moments after on_train_begin."""
+    mp.spawn(_worker_hvd_callback, args=(2, _port()), nprocs=2, join=True)
