@@ -117,6 +117,8 @@ def build(args, mode: str):
                     weight_decay=args.weight_decay if args.optimizer == "adamw" else 0.0)
     bucketer = GradBucketer(store, bucket_mb=args.bucket_mb) if world > 1 else None
     trainer = Trainer(model, store, opt, bucketer, dev, grad_accum=args.gradient_accumulation_steps,
+                      lr_schedule=getattr(args, "lr_schedule", "constant"),
+                      lr_warmup_steps=getattr(args, "lr_warmup_steps", 0),
                       check_sync=args.check_sync, log_every=args.log_every, step_watchdog=args.step_watchdog,
                       hip_graph=bool(getattr(args, "hip_graph", False)))
     initial_epoch = 0

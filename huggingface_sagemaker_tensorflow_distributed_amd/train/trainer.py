@@ -81,7 +81,8 @@ class _Meter:
 
 class Trainer:
     def __init__(self, model, store, optimizer, bucketer=None, device=None, grad_accum: int = 1,
-                 check_sync: int = 0, log_every: int = 50, step_watchdog: float = 0.0, hip_graph: bool = False):
+                 check_sync: int = 0, log_every: int = 50, step_watchdog: float = 0.0, hip_graph: bool = False,
+                 lr_schedule: str = "constant", lr_warmup_steps: int = 0):
         self.model = model
         self.store = store
         self.optimizer = optimizer
@@ -98,6 +99,14 @@ class Trainer:
         self._seed = None
         self._graph_replay = True  # tests: False = graph-mode seeding with eager kernels
         self._opt_overlap = None  # LocalOverlap (one process) | "engine" (DP ranks) | None
+        # learning-rate schedule: the reference's Keras Adam uses a constant rate (scripts/train.py:113); linear =
+        # warmup to the base rate, then linear decay to 0 over the steps fit() is asked to run
+        if lr_schedule not in ("constant", "linear"):
+            raise ValueError(f"lr_schedule {lr_schedule!r}")
+        self.lr_schedule = lr_schedule
+        self.lr_warmup_steps = max(0, int(lr_warmup_steps))
+        self.base_lr = float(getattr(optimizer, "lr", 0.0))
+        self.total_steps: Optional[int] = None
         if hip_graph:
             self.enable_hip_graph()
         if self._seed is None:
@@ -151,6 +160,16 @@ class Trainer:
         return g
 
     # -------------------------------------------------------------------------- step
+    def lr_at(self, step: int) -> float:
+        """Learning rate of optimizer step ``step`` (0-based)."""
+        f = 1.0
+        w = self.lr_warmup_steps
+        if w and step < w:
+            f = (step + 1) / w
+        elif self.lr_schedule == "linear" and self.total_steps:
+            f = max(0.0, (self.total_steps - step) / max(1, self.total_steps - w))
+        return self.base_lr * f
+
     def _forward_loss(self, batch):
         loss, logits = self.model(batch["input_ids"], attention_mask=batch["attention_mask"],
                                   labels=batch["labels"])
@@ -169,6 +188,8 @@ class Trainer:
         if self.bucketer is not None:
             self.bucketer.begin()
         k = len(micro_batches)
+        if self.lr_schedule != "constant" or self.lr_warmup_steps:
+            self.optimizer.lr = self.lr_at(self.global_step)
         ov = self._opt_overlap
         if ov is not None:
             self.optimizer.begin_step(grad_scale=1.0 / (self.world * k))
@@ -215,6 +236,10 @@ class Trainer:
         run continues the epoch count of its checkpoint instead of training ``epochs`` more)."""
         hist = History()
         callbacks = list(callbacks)
+        per_epoch = len(loader) // self.grad_accum
+        if max_steps:
+            per_epoch = min(per_epoch, max_steps)
+        self.total_steps = self.global_step + per_epoch * max(0, epochs - int(initial_epoch))
         for cb in callbacks:
             cb.on_train_begin(self)
         for epoch in range(int(initial_epoch), epochs):

@@ -70,6 +70,9 @@ def _add_framework_flags(p: argparse.ArgumentParser) -> None:
     g.add_argument("--adam_eps_mode", choices=["keras", "torch"], default="keras")
     g.add_argument("--adam_epsilon", type=float, default=None)
     g.add_argument("--gradient_accumulation_steps", type=int, default=1)
+    g.add_argument("--lr_schedule", choices=["constant", "linear"], default="constant",
+                   help="constant = Keras Adam(learning_rate) (reference); linear = warmup then linear decay to 0")
+    g.add_argument("--lr_warmup_steps", type=int, default=0, help="linear warmup steps of the learning rate")
     g.add_argument("--benchmark", type=str2bool, default=False)
     g.add_argument("--warmup_steps", type=int, default=3, help="benchmark warmup steps")
     g.add_argument("--profile", type=str2bool, default=False)

@@ -178,3 +178,22 @@ def test_tiny_bert_learns_the_marker_task_on_cpu():
         losses.append(float(tr.train_step([{k: torch.from_numpy(v[sl]).long() for k, v in (
             ("input_ids", ds.input_ids), ("attention_mask", ds.attention_mask), ("labels", ds.labels))}]).detach()))
     assert sum(losses[:10]) / 10 > 0.5 and sum(losses[-20:]) / 20 < 0.2, losses[::10]
+
+
+def test_lr_schedule_linear_warmup_decay():
+    """--lr_schedule linear --lr_warmup_steps W: warmup to the base rate, then linear decay to 0; constant (the
+    Keras reference) leaves the rate alone."""
+    from huggingface_sagemaker_tensorflow_distributed_amd.models import build_model, resolve_config
+    from huggingface_sagemaker_tensorflow_distributed_amd.optim import FusedAdam
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel import FlatParamStore
+    from huggingface_sagemaker_tensorflow_distributed_amd.train.trainer import Trainer
+
+    m = build_model(resolve_config("hsd-tiny-bert"), seed=0)
+    store = FlatParamStore(m, "cpu")
+    tr = Trainer(m, store, FusedAdam(store, lr=1e-3), None, "cpu", lr_schedule="linear", lr_warmup_steps=2)
+    tr.total_steps = 10
+    lrs = [tr.lr_at(s) for s in range(10)]
+    assert lrs[0] == 0.5e-3 and lrs[1] == 1e-3
+    assert lrs[2] == 1e-3 and all(a > b for a, b in zip(lrs[2:], lrs[3:])) and abs(lrs[9] - 1e-3 / 8) < 1e-12
+    const = Trainer(m, store, FusedAdam(store, lr=1e-3), None, "cpu")
+    assert all(const.lr_at(s) == 1e-3 for s in range(5))
