@@ -36,7 +36,8 @@ distribution = {
 }[os.environ.get("HSD_DISTRIBUTION", "none")]
 # instance configurations: "mi355x" = every local GPU
 instance_type = os.environ.get("HSD_INSTANCE_TYPE", "mi355x")
-instance_count = 1
+# multi-node: set HSD_INSTANCE_COUNT and, on every node, SM_HOSTS / SM_CURRENT_HOST (or HSD_HOSTS / HSD_NODE_RANK)
+instance_count = int(os.environ.get("HSD_INSTANCE_COUNT", "1"))
 
 huggingface_estimator = HuggingFace(
     # distributed script,
