@@ -748,6 +748,90 @@ __global__ __launch_bounds__(256) void splitk_epi_kernel(const float* __restrict
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// gemm2s: NT GEMM on 128 x 128 tiles for grids the 256 x 256 kernel cannot fill (small token counts: the
+// reference's per-rank batch of 8 x 512 tokens, serving batches). 4 waves (2 x 2), 64 x 64 wave tiles of
+// v_mfma_f32_16x16x32_bf16, BK 64, two 32-KiB LDS stages (two workgroups per CU), the same swizzled k-contiguous
+// LDS images and epilogues as gemm2. The next K-tile's LDS-DMA is issued as inline asm right after the barrier that
+// frees its stage, so hipcc does not drain it with vmcnt(0) before the current tile's LDS reads (a builtin DMA
+// into a runtime-indexed stage makes hipcc assume aliasing); its completion is counted by hand at the next barrier.
+constexpr int SBM = 128, SBN = 128;
+
+__device__ __forceinline__ void dma_nt_asm(bf16_t* img, const bf16_t* __restrict__ X, int64_t ld, int r0, int Rmax,
+                                           int k0, int g, int lane) {
+  const int row = g * 8 + (lane >> 3);
+  const int lc = (lane & 7) ^ f1(row);
+  const int rr = min(r0 + row, Rmax - 1);
+  const bf16_t* src = X + (int64_t)rr * ld + k0 + lc * 8;
+  const uint32_t lds = (uint32_t)__builtin_amdgcn_readfirstlane(
+      (int)(uint32_t)(size_t)(__attribute__((address_space(3))) bf16_t*)(img + g * 512));
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(src), "s"(lds)
+               : "memory");
+}
+
+template <int EPI>
+__global__ __launch_bounds__(256, 2) void gemm2s_kernel(G2Params p) {
+  p.dp = resolve_seed(p.dp);
+  constexpr int TA = SBM * 64, STAGE = TA + SBN * 64;  // elements
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 1, wn = wave & 1;
+  // XCD-aware bijective remap (as gemm2): the tiles one XCD runs are neighbours
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int tm = v / p.tiles_n, tn = v % p.tiles_n;
+  const int m0 = tm * SBM, n0 = tn * SBN;
+  const int nt = p.K / BK;
+  HSD_DASSERT(v < nwg && m0 < p.M && n0 < p.N && p.K % BK == 0);
+
+  // 16 DMA wave-instructions per operand image per stage, 4 + 4 per wave
+  auto dma_tile = [&](bf16_t* stage, int k0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dma_nt_asm(stage, p.A, p.lda, m0, p.M, k0, wave * 4 + q, lane);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) dma_nt_asm(stage + TA, p.B, p.ldb, n0, p.N, k0, wave * 4 + q, lane);
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int arow = wm * 64, bcol = wn * 64;
+
+  dma_tile(smem, 0);
+  for (int t = 0; t < nt; ++t) {
+    const bf16_t* cA = smem + (t & 1) * STAGE;
+    const bf16_t* cB = cA + TA;
+    // tile t landed (this wave's part) and every wave's part visible; every wave finished reading tile t-1,
+    // whose stage tile t+1 now refills
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    G2_BARRIER();
+    if (t + 1 < nt) dma_tile(smem + ((t + 1) & 1) * STAGE, (t + 1) * BK);
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8 fa[4], fb[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) fa[i] = frag<0>(cA, arow + 16 * i, ks, lane);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) fb[j] = frag<0>(cB, bcol + 16 * j, ks, lane);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  // every wave done with the operand images: they become the epilogue staging (4 x 8 KiB slices)
+  G2_BARRIER();
+  epilogue_bf16<EPI, 256, 4>(acc, p, smem, wave, lane, m0 + arow, n0 + bcol);
+}
+
 }  // namespace g2
 
 // Main-loop schedule (tools/gemm_probe.py, interleaved rounds in one process, random operands, T = 131072
@@ -829,15 +913,29 @@ int gemm2_pick_bn(int M, int N) {
 // (the reference's own per-rank batch: bert-large, B = 8, S = 512 -> M = 4096: 64 tiles on the H-wide GEMMs)
 // is split over K into fp32 slabs plus one reduce-and-epilogue pass, keeping >= 8 K-tiles per split.
 // HSD_G2_SPLITK=0 disables, =n forces n.
+constexpr int SBN_HOST = 128;
+bool gemm2s_use(int M, int N, int K);
+
 int gemm2_nt_splits(int M, int N, int K) {
   const char* e = getenv("HSD_G2_SPLITK");
   const int kt = K / 64;
   if (e) return std::max(1, std::min(atoi(e), kt));
+  if (gemm2s_use(M, N, K)) return 1;  // the 128 x 128 kernel fills the GPU without K-splits
   const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
   if (tiles * 2 > 256) return 1;
   int s = 256 / tiles;
   while (s > 1 && kt / s < 8) --s;
   return s;
+}
+
+// gemm2s (128 x 128 tiles) for NT grids that 256 x 256 tiles leave mostly idle. HSD_G2_SMALL=0 disables,
+// =1 forces it for every shape it supports.
+bool gemm2s_use(int M, int N, int K) {
+  if (N % SBN_HOST != 0 || K % 64 != 0) return false;
+  const char* e = getenv("HSD_G2_SMALL");
+  if (e) return atoi(e) != 0;
+  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  return tiles * 2 <= 256;
 }
 
 bool gemm2_supported(int la, int lb, int epi, int M, int N, int K) {
@@ -895,6 +993,30 @@ void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const b
   p.A = A; p.lda = lda; p.B = B; p.ldb = ldb; p.M = M; p.N = N; p.K = K; p.C = C; p.ldc = ldc;
   p.bias = bias; p.aux = aux; p.ldaux = ldaux; p.C2 = C2;
   p.dp = make_dropout(p_drop, seed);
+  if (la == 0 && lb == 0 && splits <= 1 && gemm2s_use(M, N, K)) {
+    G2Params q = p;
+    q.tiles_n = N / g2::SBN;
+    q.ntiles = ((M + g2::SBM - 1) / g2::SBM) * q.tiles_n;
+    q.kps = K;
+#define G2_SMALL(E)                                                                                   \
+  case E:                                                                                             \
+    hipLaunchKernelGGL(g2::gemm2s_kernel<E>, dim3(q.ntiles), dim3(256), 0, st, q);                    \
+    break;
+    switch (epi) {
+      G2_SMALL(E2_STORE)
+      G2_SMALL(E2_BIAS)
+      G2_SMALL(E2_BIAS_GELU)
+      G2_SMALL(E2_BIAS_DROP_RES)
+      G2_SMALL(E2_RES)
+      G2_SMALL(E2_DGELU)
+      G2_SMALL(E2_BIAS_GELU_D)
+      G2_SMALL(E2_MUL)
+      default: abort();
+    }
+#undef G2_SMALL
+    HSD_CHECK_LAUNCH();
+    return;
+  }
   if (la == 0 && lb == 0 && splits > 1) {
     if (ws == nullptr || !epi_bf16_out(epi)) abort();
     G2Params q = p;

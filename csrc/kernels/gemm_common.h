@@ -149,9 +149,12 @@ __device__ __forceinline__ void colsum_flush(float (&csum)[8], float* dbias, int
 
 // bf16-output epilogue of a 256 x BN tile held as acc[8][BN/64] (acc[i][j] = D[n][m] block: lane l holds
 // m = 16i + (l&15), n = 16j + 4(l>>4) + r), staged through the wave's [64][BN/4 + 8] slice of `smem`.
-template <int EPI, int BN>
-__device__ __forceinline__ void epilogue_bf16(f32x4 (&acc)[8][BN / 64], const G2Params& p, bf16_t* smem, int wave,
+// MB = 16-row MFMA blocks per wave (8: the 128-row wave tiles of the 256 x BN kernels; 4: the 64-row wave tiles
+// of gemm2s_kernel), one 64-row staging pass per 4 blocks.
+template <int EPI, int BN, int MB = 8>
+__device__ __forceinline__ void epilogue_bf16(f32x4 (&acc)[MB][BN / 64], const G2Params& p, bf16_t* smem, int wave,
                                               int lane, int mw, int nw) {
+  static_assert(MB == 4 || MB == 8, "64 or 128 rows per wave");
   constexpr int WN = BN / 4, NREP = WN / 16;
   const int q4 = lane >> 4, lr = lane & 15;
   // stage bf16(acc [+ bias]) through a wave-private LDS slice ([64 rows][SROW]), then write whole
@@ -179,7 +182,7 @@ __device__ __forceinline__ void epilogue_bf16(f32x4 (&acc)[8][BN / 64], const G2
   constexpr bool kColsum = (EPI == E2_DGELU || EPI == E2_MUL) && CPR == 8;
   float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int h = 0; h < 2; ++h) {
+  for (int h = 0; h < MB / 4; ++h) {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll

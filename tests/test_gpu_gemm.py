@@ -236,11 +236,12 @@ def test_gemm2_gelu_derivative_and_mul_epilogues(gpu):
 
 @pytest.mark.parametrize("M,N,K,splits", [(512, 768, 1024, 4), (300, 512, 3072, 3), (4096, 1024, 4096, 0)])
 @pytest.mark.parametrize("epi", [0, 1, 2, 3, 4, 5, 8, 9])
-def test_gemm2_nt_splitk_matches_one_pass(gpu, M, N, K, splits, epi):
+def test_gemm2_nt_splitk_matches_one_pass(gpu, monkeypatch, M, N, K, splits, epi):
     """Split-K NT (fp32 slabs + reduce-and-epilogue pass) == the one-pass fused epilogue, for every epilogue kind
     (same dropout sites, same fused bias-gradient column sums), up to the fp32 order of the K-split sums."""
     torch.manual_seed(5 + epi)
     C_ = _C()
+    monkeypatch.setenv("HSD_G2_SMALL", "0")  # split-K is the small-grid path only when the 128-tile kernel is off
     if splits == 0:
         assert C_.gemm2_nt_splits(M, N, K) > 1  # the reference's bert-large B=8 S=512 shape is split automatically
     A, B = _mk((M, K), gpu), _mk((N, K), gpu, 0.05)
@@ -262,3 +263,33 @@ def test_gemm2_nt_splitk_matches_one_pass(gpu, M, N, K, splits, epi):
         _check(c2s, c21)
     if d1 is not None:
         torch.testing.assert_close(ds, d1, rtol=2e-2, atol=1e-2 * float(d1.abs().max()) + 1e-3)
+
+
+@pytest.mark.parametrize("M,N,K", [(300, 512, 1024), (4096, 1024, 1024), (128, 768, 3072)])
+@pytest.mark.parametrize("epi", [0, 1, 2, 3, 4, 5, 8, 9])
+def test_gemm2_small_tiles_match_256_tiles(gpu, monkeypatch, M, N, K, epi):
+    """gemm2s (128 x 128 tiles, for grids 256 x 256 tiles leave idle) == gemm2 bit for bit on every epilogue (same
+    K order per element, same dropout sites); fused bias-gradient column sums to fp32 rounding."""
+    torch.manual_seed(3 + epi)
+    C_ = _C()
+    A, B = _mk((M, K), gpu), _mk((N, K), gpu, 0.05)
+    bias = _mk((N,), gpu)
+    aux = _mk((M, N), gpu) if epi != 9 else torch.rand(M, N, device=gpu).bfloat16()
+    two = epi in (2, 8)
+    outs = []
+    for small in ("0", "1"):
+        monkeypatch.setenv("HSD_G2_SMALL", small)
+        monkeypatch.setenv("HSD_G2_SPLITK", "1")
+        C = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+        C2 = torch.empty_like(C) if two else None
+        db = torch.zeros(N, device=gpu) if epi in (5, 9) and N % 256 == 0 else None
+        C_.gemm2(A, B, C, 0, 0, epi, bias if epi in (1, 2, 3, 8) else None, aux if epi in (3, 4, 5, 9) else None,
+                 C2, 0.1 if epi == 3 else 0.0, 77, 0, None, db)
+        torch.cuda.synchronize()
+        outs.append((C, C2, db))
+    (c0, c20, d0), (c1, c21, d1) = outs
+    assert torch.equal(c0, c1)
+    if two:
+        assert torch.equal(c20, c21)
+    if d0 is not None:
+        torch.testing.assert_close(d1, d0, rtol=1e-4, atol=1e-4 * float(d0.abs().max()) + 1e-6)
