@@ -25,6 +25,8 @@
 #include "gemm_common.h"
 #include <stdlib.h>
 
+#include <cmath>
+
 namespace hsd {
 
 namespace g2 {
@@ -57,7 +59,7 @@ __device__ __forceinline__ void dma(bf16_t* img, const bf16_t* __restrict__ X, i
 }
 
 // 16x16x32 operand fragment: lane l holds rows (rbase + (l&15)), k = 32·ks + 8·(l>>4) + 0..7
-template <int L>
+template <int L, int W = 256>
 __device__ __forceinline__ bf16x8 frag(const bf16_t* img, int rbase, int ks, int lane) {
   if constexpr (L == 0) {
     const int row = rbase + (lane & 15);
@@ -69,9 +71,9 @@ __device__ __forceinline__ bf16x8 frag(const bf16_t* img, int rbase, int ks, int
     const int m = rbase + 4 * p;
     const int k2 = k + 4;
     bf16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (lds_bf16x4_t*)(img + k * 256 + (((m >> 3) ^ f2(k)) << 3) + (m & 7)));
+        (lds_bf16x4_t*)(img + k * W + (((m >> 3) ^ f2(k)) << 3) + (m & 7)));
     bf16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16(
-        (lds_bf16x4_t*)(img + k2 * 256 + (((m >> 3) ^ f2(k2)) << 3) + (m & 7)));
+        (lds_bf16x4_t*)(img + k2 * W + (((m >> 3) ^ f2(k2)) << 3) + (m & 7)));
     bf16x8 r;
     r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
     r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
@@ -749,20 +751,34 @@ __global__ __launch_bounds__(256) void splitk_epi_kernel(const float* __restrict
 }
 
 // ------------------------------------------------------------------------------------------------
-// gemm2s: NT GEMM on 128 x 128 tiles for grids the 256 x 256 kernel cannot fill (small token counts: the
+// gemm2s: GEMM on 128 x 128 tiles for grids the 256 x 256 kernel cannot fill (small token counts: the
 // reference's per-rank batch of 8 x 512 tokens, serving batches). 4 waves (2 x 2), 64 x 64 wave tiles of
-// v_mfma_f32_16x16x32_bf16, BK 64, two 32-KiB LDS stages (two workgroups per CU), the same swizzled k-contiguous
-// LDS images and epilogues as gemm2. The next K-tile's LDS-DMA is issued as inline asm right after the barrier that
-// frees its stage, so hipcc does not drain it with vmcnt(0) before the current tile's LDS reads (a builtin DMA
-// into a runtime-indexed stage makes hipcc assume aliasing); its completion is counted by hand at the next barrier.
+// v_mfma_f32_16x16x32_bf16, BK 64, NSTG 32-KiB LDS stages, the same swizzled LDS images (k-contiguous rows for NT;
+// 128-wide k-strided rows + transposing reads for the TT wgrad) and epilogues as gemm2. With one workgroup per CU
+// (<= 256 tiles) each SIMD runs ONE wave, so HBM latency is hidden by depth, not by occupancy: tiles t+1 .. t+NSTG-2
+// are in flight while tile t computes, retired by a counted vmcnt. The DMAs are inline asm issued right after the
+// barrier that frees their stage, so hipcc does not drain them with vmcnt(0) before the current tile's LDS reads (a
+// builtin DMA into a runtime-indexed stage makes hipcc assume aliasing).
+// TT (fp32 out): one split accumulates into C (unique owner, C += acc); split-K writes [split][M][N] slabs for
+// slab_reduce_kernel.
 constexpr int SBM = 128, SBN = 128;
 
-__device__ __forceinline__ void dma_nt_asm(bf16_t* img, const bf16_t* __restrict__ X, int64_t ld, int r0, int Rmax,
-                                           int k0, int g, int lane) {
-  const int row = g * 8 + (lane >> 3);
-  const int lc = (lane & 7) ^ f1(row);
-  const int rr = min(r0 + row, Rmax - 1);
-  const bf16_t* src = X + (int64_t)rr * ld + k0 + lc * 8;
+template <int L>
+__device__ __forceinline__ void dma_asm(bf16_t* img, const bf16_t* __restrict__ X, int64_t ld, int r0, int Rmax,
+                                        int k0, int g, int lane) {
+  const bf16_t* src;
+  if constexpr (L == 0) {
+    const int row = g * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ f1(row);
+    const int rr = min(r0 + row, Rmax - 1);
+    src = X + (int64_t)rr * ld + k0 + lc * 8;
+  } else {
+    // [64 k][128] image: 4 k-rows of 256 B per wave instruction
+    const int krow = g * 4 + (lane >> 4);
+    const int lc = (lane & 15) ^ f2(krow);
+    const int cc = min(r0 + lc * 8, Rmax - 8);
+    src = X + (int64_t)(k0 + krow) * ld + cc;
+  }
   const uint32_t lds = (uint32_t)__builtin_amdgcn_readfirstlane(
       (int)(uint32_t)(size_t)(__attribute__((address_space(3))) bf16_t*)(img + g * 512));
   unsigned keep;
@@ -772,29 +788,45 @@ __device__ __forceinline__ void dma_nt_asm(bf16_t* img, const bf16_t* __restrict
                : "memory");
 }
 
-template <int EPI>
-__global__ __launch_bounds__(256, 2) void gemm2s_kernel(G2Params p) {
+// wait until at most `left` (wave-uniform) K-tiles of DMA (8 instructions each) are still in flight
+template <int NSTG>
+__device__ __forceinline__ void wait_tiles(int left) {
+  if constexpr (NSTG >= 4) {
+    if (left >= 2) { vmcnt<16>(); return; }
+  }
+  if constexpr (NSTG >= 3) {
+    if (left >= 1) { vmcnt<8>(); return; }
+  }
+  vmcnt<0>();
+}
+
+template <int L, int EPI, int NSTG>
+__global__ __launch_bounds__(256, NSTG <= 2 ? 2 : 1) void gemm2s_kernel(G2Params p) {
+  static_assert(NSTG >= 2 && NSTG <= 4, "2-4 stages");
+  static_assert(L == 0 ? epi_bf16_out(EPI) : EPI == E2_F32_SLAB, "NT: bf16 epilogues; TT: fp32");
   p.dp = resolve_seed(p.dp);
   constexpr int TA = SBM * 64, STAGE = TA + SBN * 64;  // elements
-  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * STAGE];
+  __shared__ __attribute__((aligned(16))) bf16_t smem[NSTG * STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave >> 1, wn = wave & 1;
-  // XCD-aware bijective remap (as gemm2): the tiles one XCD runs are neighbours
+  // 1-D grid over (split, tile), XCD-aware bijective remap (as gemm2): the tiles one XCD runs are neighbours
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
   const int v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int tm = v / p.tiles_n, tn = v % p.tiles_n;
+  const int split = v / p.ntiles, wg = v % p.ntiles;
+  const int tm = wg / p.tiles_n, tn = wg % p.tiles_n;
   const int m0 = tm * SBM, n0 = tn * SBN;
-  const int nt = p.K / BK;
-  HSD_DASSERT(v < nwg && m0 < p.M && n0 < p.N && p.K % BK == 0);
+  const int kbeg = split * p.kps;
+  const int nt = (min(p.K, kbeg + p.kps) - kbeg) / BK;
+  HSD_DASSERT(v < nwg && m0 < p.M && n0 < p.N && kbeg < p.K && p.kps % BK == 0 && p.K % BK == 0);
 
   // 16 DMA wave-instructions per operand image per stage, 4 + 4 per wave
   auto dma_tile = [&](bf16_t* stage, int k0) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) dma_nt_asm(stage, p.A, p.lda, m0, p.M, k0, wave * 4 + q, lane);
+    for (int q = 0; q < 4; ++q) dma_asm<L>(stage, p.A, p.lda, m0, p.M, k0, wave * 4 + q, lane);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) dma_nt_asm(stage + TA, p.B, p.ldb, n0, p.N, k0, wave * 4 + q, lane);
+    for (int q = 0; q < 4; ++q) dma_asm<L>(stage + TA, p.B, p.ldb, n0, p.N, k0, wave * 4 + q, lane);
   };
 
   f32x4 acc[4][4];
@@ -804,32 +836,60 @@ __global__ __launch_bounds__(256, 2) void gemm2s_kernel(G2Params p) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
   const int arow = wm * 64, bcol = wn * 64;
 
-  dma_tile(smem, 0);
+#pragma unroll
+  for (int s = 0; s < NSTG - 1; ++s)
+    if (s < nt) dma_tile(smem + s * STAGE, kbeg + s * BK);
+  int rs = 0, ws = NSTG - 1;
   for (int t = 0; t < nt; ++t) {
-    const bf16_t* cA = smem + (t & 1) * STAGE;
+    const bf16_t* cA = smem + rs * STAGE;
     const bf16_t* cB = cA + TA;
     // tile t landed (this wave's part) and every wave's part visible; every wave finished reading tile t-1,
-    // whose stage tile t+1 now refills
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // whose stage tile t+NSTG-1 now refills
+    wait_tiles<NSTG>(min(NSTG - 2, nt - 1 - t));
     G2_BARRIER();
-    if (t + 1 < nt) dma_tile(smem + ((t + 1) & 1) * STAGE, (t + 1) * BK);
+    if (t + NSTG - 1 < nt) dma_tile(smem + ws * STAGE, kbeg + (t + NSTG - 1) * BK);
 #pragma unroll
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 fa[4], fb[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = frag<0>(cA, arow + 16 * i, ks, lane);
+      for (int i = 0; i < 4; ++i) fa[i] = frag<L, SBM>(cA, arow + 16 * i, ks, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = frag<0>(cB, bcol + 16 * j, ks, lane);
+      for (int j = 0; j < 4; ++j) fb[j] = frag<L, SBN>(cB, bcol + 16 * j, ks, lane);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
     }
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    rs = rs == NSTG - 1 ? 0 : rs + 1;
+    ws = ws == NSTG - 1 ? 0 : ws + 1;
   }
-  // every wave done with the operand images: they become the epilogue staging (4 x 8 KiB slices)
-  G2_BARRIER();
-  epilogue_bf16<EPI, 256, 4>(acc, p, smem, wave, lane, m0 + arow, n0 + bcol);
+  const int mw = m0 + arow, nw = n0 + bcol;
+  if constexpr (L == 1) {
+    // acc[i][j]: lane l holds m = 16i + (l&15), n = 16j + 4(l>>4) + r
+    const bool direct = nwg == p.ntiles;
+    const int q4 = lane >> 4, lr = lane & 15;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int m = mw + 16 * i + lr;
+      if (m >= p.M) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = nw + 16 * j + 4 * q4;
+        if (direct) {
+          f32x4* c = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.C) + (int64_t)m * p.ldc + n);
+          *c = *c + acc[i][j];
+        } else {
+          float* c = reinterpret_cast<float*>(p.C) + (int64_t)split * p.M * p.N + (int64_t)m * p.N + n;
+          *reinterpret_cast<f32x4*>(c) = acc[i][j];
+        }
+      }
+    }
+  } else {
+    // every wave done with the operand images: they become the epilogue staging (4 x 8 KiB slices)
+    G2_BARRIER();
+    epilogue_bf16<EPI, 256, 4>(acc, p, smem, wave, lane, mw, nw);
+  }
 }
 
 }  // namespace g2
@@ -938,10 +998,71 @@ bool gemm2s_use(int M, int N, int K) {
   return tiles * 2 <= 256;
 }
 
+// Weight-gradient plan: 256 x 256 tiles (gemm2, split-K slabs) or 128 x 128 tiles (gemm2s TT), and the K-split
+// count, by a cost model fitted to tools/wgrad_ab.py on MI355X (24 BERT shapes x T = 4096 / 8192 / 16384; it
+// picks the faster path on all 24, profiles/wgrad_ab_r2.json): us = rounds x (a·K-tiles per split + b) + c·MB of
+// slab / C traffic, rounds = ceil(workgroups / 256) (one workgroup per CU on both). HSD_G2_SMALL_TT=0 / 1 forces
+// the tile size (the split count is still chosen by the model); HSD_WGRAD_MIN_KT sets the minimum K-tiles per split.
+struct WgradPlan {
+  bool small;
+  int splits;
+};
+
+static double wgrad_cost(int M, int N, int K, int s, bool small) {
+  const int tile = small ? 128 : 256;
+  const double tiles = (double)((M + tile - 1) / tile) * ((N + tile - 1) / tile);
+  const int kt_all = K / 64;
+  const int kt = (kt_all + s - 1) / s;
+  const int real = (kt_all + kt - 1) / kt;
+  const double rounds = std::ceil(tiles * real / 256.0);
+  const double mb = ((real > 1 ? 8.0 * real : 0.0) + 8.0) * M * N / 1e6;
+  return small ? rounds * (0.658 * kt + 5.02) + 0.176 * mb : rounds * (1.637 * kt + 15.9) + 0.0847 * mb;
+}
+
+static WgradPlan wgrad_plan(int M, int N, int K) {
+  const char* e = getenv("HSD_G2_SMALL_TT");
+  const int force = e ? atoi(e) : -1;
+  const bool can_small = N % SBN_HOST == 0 && M % 8 == 0 && K % 64 == 0 && force != 0;
+  const bool can_big = N % 256 == 0 && force != 1;
+  const char* m = getenv("HSD_WGRAD_MIN_KT");
+  const int min_kt = m ? std::max(1, atoi(m)) : 2;
+  const int kt_all = K / 64;
+  WgradPlan best{can_small && !can_big, 1};
+  double best_cost = 1e30;
+  for (int small = 0; small < 2; ++small) {
+    if (small ? !can_small : !can_big) continue;
+    for (int sp = 1; sp <= 32 && (sp == 1 || kt_all / sp >= min_kt); ++sp) {
+      const double c = wgrad_cost(M, N, K, sp, small);
+      if (c < best_cost) { best_cost = c; best = WgradPlan{small != 0, sp}; }
+    }
+  }
+  return best;
+}
+
+bool gemm2st_use(int M, int N, int K) { return wgrad_plan(M, N, K).small; }
+
+// LDS stages of gemm2s (HSD_G2S_STAGES: 2 -> two workgroups per CU; 3 / 4 -> one, deeper DMA prefetch)
+static int g2s_stages() {
+  const char* e = getenv("HSD_G2S_STAGES");
+  const int v = e ? atoi(e) : 3;
+  return v < 2 ? 2 : (v > 4 ? 4 : v);
+}
+
+template <int L, int EPI>
+static void g2s_launch(const G2Params& q, int grid, hipStream_t st) {
+  const int ns = g2s_stages();
+  if (ns == 2) hipLaunchKernelGGL((g2::gemm2s_kernel<L, EPI, 2>), dim3(grid), dim3(256), 0, st, q);
+  else if (ns == 3) hipLaunchKernelGGL((g2::gemm2s_kernel<L, EPI, 3>), dim3(grid), dim3(256), 0, st, q);
+  else hipLaunchKernelGGL((g2::gemm2s_kernel<L, EPI, 4>), dim3(grid), dim3(256), 0, st, q);
+  HSD_CHECK_LAUNCH();
+}
+
 bool gemm2_supported(int la, int lb, int epi, int M, int N, int K) {
   if (K % 64 || M < 1 || N % 8) return false;
   if (la == 0 && lb == 0) return epi_bf16_out(epi) && gemm2_pick_bn(M, N) != 0;
-  if (la == 1 && lb == 1) return (epi == E2_F32_ATOMIC || epi == E2_F32_SLAB) && M % 8 == 0 && N % 256 == 0;
+  if (la == 1 && lb == 1)
+    return (epi == E2_F32_ATOMIC || epi == E2_F32_SLAB) && M % 8 == 0 &&
+           (N % 256 == 0 || (epi == E2_F32_SLAB && gemm2st_use(M, N, K)));
   return false;
 }
 
@@ -963,17 +1084,10 @@ static bool use_gemm3(int la, int lb, int epi, int M, int N, int K) {
   return (gemm3_mask() & bit) && gemm3_supported(la, lb, epi, M, N, K);
 }
 
-// splits for the TT wgrad: fill ~one wave of 256 CUs with >= 4 K-tiles per block
+// K-splits of the TT wgrad (wgrad_plan)
 int gemm2_wgrad_splits(int M, int N, int K) {
   if (use_gemm3(1, 1, E2_F32_SLAB, M, N, K)) return gemm3_wgrad_splits(M, N, K);
-  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
-  int s = 256 / tiles;
-  if (s < 1) s = 1;
-  const int kt = K / 64;
-  const char* e = getenv("HSD_WGRAD_MIN_KT");  // A/B: minimum K-tiles per split
-  const int min_kt = e ? std::max(1, atoi(e)) : 4;
-  while (s > 1 && kt / s < min_kt) --s;
-  return s;
+  return wgrad_plan(M, N, K).splits;
 }
 
 void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, int M, int N,
@@ -998,9 +1112,9 @@ void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const b
     q.tiles_n = N / g2::SBN;
     q.ntiles = ((M + g2::SBM - 1) / g2::SBM) * q.tiles_n;
     q.kps = K;
-#define G2_SMALL(E)                                                                                   \
-  case E:                                                                                             \
-    hipLaunchKernelGGL(g2::gemm2s_kernel<E>, dim3(q.ntiles), dim3(256), 0, st, q);                    \
+#define G2_SMALL(E)                   \
+  case E:                             \
+    g2s_launch<0, E>(q, q.ntiles, st); \
     break;
     switch (epi) {
       G2_SMALL(E2_STORE)
@@ -1014,7 +1128,6 @@ void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const b
       default: abort();
     }
 #undef G2_SMALL
-    HSD_CHECK_LAUNCH();
     return;
   }
   if (la == 0 && lb == 0 && splits > 1) {
@@ -1075,7 +1188,24 @@ void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const b
 #undef G2_NT
   } else if (la == 1 && lb == 1) {
     if (splits <= 0) splits = gemm2_wgrad_splits(M, N, K);
-    if (epi == E2_F32_SLAB && splits > 1 && ws != nullptr) {
+    if (epi == E2_F32_SLAB && gemm2st_use(M, N, K) && (splits == 1 || ws != nullptr)) {
+      G2Params q = p;
+      q.tiles_n = N / g2::SBN;
+      q.ntiles = ((M + g2::SBM - 1) / g2::SBM) * q.tiles_n;
+      int kps = (K + splits - 1) / splits;
+      kps = (kps + 63) / 64 * 64;
+      const int real = (K + kps - 1) / kps;
+      q.kps = kps;
+      if (real > 1) q.C = ws;
+      g2s_launch<1, E2_F32_SLAB>(q, q.ntiles * real, st);
+      if (real > 1) {
+        const int64_t n4 = (int64_t)M * N / 4;
+        int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
+        hipLaunchKernelGGL(g2::slab_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, reinterpret_cast<float*>(C),
+                           ldc, M, N, real);
+        HSD_CHECK_LAUNCH();
+      }
+    } else if (epi == E2_F32_SLAB && splits > 1 && ws != nullptr) {
       G2Params q = p;
       q.C = ws;
       g2_launch<1, 1, E2_F32_SLAB, 256>(q, splits, st);

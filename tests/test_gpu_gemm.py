@@ -265,9 +265,10 @@ def test_gemm2_nt_splitk_matches_one_pass(gpu, monkeypatch, M, N, K, splits, epi
         torch.testing.assert_close(ds, d1, rtol=2e-2, atol=1e-2 * float(d1.abs().max()) + 1e-3)
 
 
+@pytest.mark.parametrize("stages", [2, 3, 4])
 @pytest.mark.parametrize("M,N,K", [(300, 512, 1024), (4096, 1024, 1024), (128, 768, 3072)])
 @pytest.mark.parametrize("epi", [0, 1, 2, 3, 4, 5, 8, 9])
-def test_gemm2_small_tiles_match_256_tiles(gpu, monkeypatch, M, N, K, epi):
+def test_gemm2_small_tiles_match_256_tiles(gpu, monkeypatch, M, N, K, epi, stages):
     """gemm2s (128 x 128 tiles, for grids 256 x 256 tiles leave idle) == gemm2 bit for bit on every epilogue (same
     K order per element, same dropout sites); fused bias-gradient column sums to fp32 rounding."""
     torch.manual_seed(3 + epi)
@@ -277,6 +278,7 @@ def test_gemm2_small_tiles_match_256_tiles(gpu, monkeypatch, M, N, K, epi):
     aux = _mk((M, N), gpu) if epi != 9 else torch.rand(M, N, device=gpu).bfloat16()
     two = epi in (2, 8)
     outs = []
+    monkeypatch.setenv("HSD_G2S_STAGES", str(stages))
     for small in ("0", "1"):
         monkeypatch.setenv("HSD_G2_SMALL", small)
         monkeypatch.setenv("HSD_G2_SPLITK", "1")
@@ -293,3 +295,22 @@ def test_gemm2_small_tiles_match_256_tiles(gpu, monkeypatch, M, N, K, epi):
         assert torch.equal(c20, c21)
     if d0 is not None:
         torch.testing.assert_close(d1, d0, rtol=1e-4, atol=1e-4 * float(d0.abs().max()) + 1e-6)
+
+
+@pytest.mark.parametrize("stages", [2, 3, 4])
+@pytest.mark.parametrize("M,N,K,splits", [(1024, 1024, 4096, 0), (1024, 1024, 4096, 1), (3072, 1024, 4096, 0),
+                                          (1000, 768, 512, 0), (1024, 4096, 128, 0), (200, 384, 1024, 3)])
+def test_gemm2_small_tt_wgrad(gpu, monkeypatch, M, N, K, splits, stages):
+    """gemm2s TT (128 x 128 tiles): weight gradient C += Aᵀ·B in fp32, one split accumulating in place or K-splits
+    into slabs + reduce, every stage depth, against the fp32 reference."""
+    monkeypatch.setenv("HSD_G2_SMALL_TT", "1")
+    monkeypatch.setenv("HSD_G2S_STAGES", str(stages))
+    torch.manual_seed(31)
+    C_ = _C()
+    A, B = _mk((K, M), gpu), _mk((K, N), gpu)
+    C0 = torch.randn(M, N, device=gpu)
+    C = C0.clone()
+    sp = splits or C_.gemm2_splits(M, N, K)
+    ws = torch.empty(sp * M * N, device=gpu)
+    C_.gemm2(A, B, C, 1, 1, 7, None, None, None, 0.0, 0, sp, ws, None)
+    _check(C, C0 + A.float().t() @ B.float(), 1e-3)
