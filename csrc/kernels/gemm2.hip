@@ -1041,16 +1041,19 @@ static WgradPlan wgrad_plan(int M, int N, int K) {
 
 bool gemm2st_use(int M, int N, int K) { return wgrad_plan(M, N, K).small; }
 
-// LDS stages of gemm2s (HSD_G2S_STAGES: 2 -> two workgroups per CU; 3 / 4 -> one, deeper DMA prefetch)
-static int g2s_stages() {
+// LDS stages of gemm2s: 2 -> two workgroups per CU, 3 -> one with a deeper DMA prefetch. A grid that fits one
+// workgroup per CU takes 3 stages, a larger one 2 (tools/nt_ab.py, profiles/nt_ab_r2.jsonl: at T = 8192 the 384-tile
+// bert-base GEMMs run 19-49 us at 2 stages vs 26-68 us at 3; at <= 256 tiles 3 stages are equal or up to 5 % faster).
+// HSD_G2S_STAGES (2-4) overrides.
+static int g2s_stages(int grid) {
   const char* e = getenv("HSD_G2S_STAGES");
-  const int v = e ? atoi(e) : 3;
+  const int v = e ? atoi(e) : (grid <= 256 ? 3 : 2);
   return v < 2 ? 2 : (v > 4 ? 4 : v);
 }
 
 template <int L, int EPI>
 static void g2s_launch(const G2Params& q, int grid, hipStream_t st) {
-  const int ns = g2s_stages();
+  const int ns = g2s_stages(grid);
   if (ns == 2) hipLaunchKernelGGL((g2::gemm2s_kernel<L, EPI, 2>), dim3(grid), dim3(256), 0, st, q);
   else if (ns == 3) hipLaunchKernelGGL((g2::gemm2s_kernel<L, EPI, 3>), dim3(grid), dim3(256), 0, st, q);
   else hipLaunchKernelGGL((g2::gemm2s_kernel<L, EPI, 4>), dim3(grid), dim3(256), 0, st, q);
