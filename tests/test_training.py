@@ -146,15 +146,23 @@ def test_optimizer_overlap_slices_cover_store_in_backward_order():
     assert len(plan_ranges(store, 1000.0)[0]) == 1
 
 
-def test_gemm_nt_split_policy():
-    """Split-K only for NT grids that leave more than half of the 256 CUs idle, >= 8 K-tiles per split."""
+def test_gemm_nt_split_policy(monkeypatch):
+    """Small NT grids go to the 128 x 128 kernel (no K-splits); with it off, split-K only for NT grids that leave
+    more than half of the 256 CUs idle, >= 8 K-tiles per split. Weight gradients: the cost model keeps the
+    headline's split counts and takes 128 x 128 tiles where 256 x 256 tiles would need many thin splits."""
     from huggingface_sagemaker_tensorflow_distributed_amd.ops._ext import load
 
     C = load()
-    assert C.gemm2_nt_splits(4096, 1024, 4096) == 4      # bert-large B=8 S=512: 64 tiles
-    assert C.gemm2_nt_splits(4096, 768, 3072) == 5       # 48 tiles, 48 K-tiles
+    assert C.gemm2_nt_splits(4096, 1024, 4096) == 1      # bert-large B=8 S=512: gemm2s, 256 tiles of 128^2
     assert C.gemm2_nt_splits(131072, 768, 768) == 1      # headline: 1536 tiles
+    monkeypatch.setenv("HSD_G2_SMALL", "0")
+    assert C.gemm2_nt_splits(4096, 1024, 4096) == 4      # 64 tiles of 256^2
+    assert C.gemm2_nt_splits(4096, 768, 3072) == 5       # 48 tiles, 48 K-tiles
     assert C.gemm2_nt_splits(8192, 768, 768) == 1        # 96 tiles but only 12 K-tiles
+    monkeypatch.delenv("HSD_G2_SMALL")
+    assert C.gemm2_splits(2304, 768, 131072) == 9        # headline wgrads: 256^2 tiles, one wave of 256 CUs
+    assert C.gemm2_splits(768, 768, 131072) == 28
+    assert C.gemm2_splits(1024, 1024, 4096) == 4         # 128^2 tiles x 4 splits (256^2 would need 13+)
 
 
 def test_tiny_bert_learns_the_marker_task_on_cpu():
