@@ -479,8 +479,15 @@ static void ln_bwd_t(const bf16_t* dout, const bf16_t* z, const float* mean, con
                      bf16_t* dz, bf16_t* dy, const bf16_t* dres_add, float* dgamma, float* dbeta, float* dbias,
                      int rows, int H, const DropoutParams& dp, hipStream_t st) {
   if (!getenv("HSD_LN_SPLIT")) {
-    // ~16 rows per wave: 2048 waves = 8 per CU, a few thousand column atomics per block
-    const int rpw = std::max(4, (rows + 2047) / 2048);
+    // ~16 rows per wave at the headline's 131072 rows: 2048 waves = 8 per CU, a few thousand column atomics per
+    // block; at least 4 rows per wave (a floor of 2 for small row counts, twice the waves and the column atomics,
+    // measured 1-2 % slower end to end at bert-large B = 8 and bert-base B = 32: profiles/small_tiles_r2.log;
+    // HSD_LN_BWD_MIN_RPW overrides the floor)
+    static const int min_rpw = [] {
+      const char* e = getenv("HSD_LN_BWD_MIN_RPW");
+      return e ? std::max(1, atoi(e)) : 4;
+    }();
+    const int rpw = std::max(min_rpw, (rows + 2047) / 2048);
     const int waves = (rows + rpw - 1) / rpw;
     const int blocks = (waves + kLnWaves - 1) / kLnWaves;
     // dbias sums the gradient that enters the GEMM: dy (or dz, which equals dy when there is no dropout)
