@@ -803,7 +803,8 @@ __device__ __forceinline__ void wait_tiles(int left) {
 template <int L, int EPI, int NSTG>
 __global__ __launch_bounds__(256, NSTG <= 2 ? 2 : 1) void gemm2s_kernel(G2Params p) {
   static_assert(NSTG >= 2 && NSTG <= 4, "2-4 stages");
-  static_assert(L == 0 ? epi_bf16_out(EPI) : EPI == E2_F32_SLAB, "NT: bf16 epilogues; TT: fp32");
+  static_assert(L == 0 ? (epi_bf16_out(EPI) || EPI == E2_F32_SLAB) : EPI == E2_F32_SLAB,
+                "NT: bf16 epilogues or split-K slabs; TT: fp32");
   p.dp = resolve_seed(p.dp);
   constexpr int TA = SBM * 64, STAGE = TA + SBN * 64;  // elements
   __shared__ __attribute__((aligned(16))) bf16_t smem[NSTG * STAGE];
@@ -865,9 +866,10 @@ __global__ __launch_bounds__(256, NSTG <= 2 ? 2 : 1) void gemm2s_kernel(G2Params
     ws = ws == NSTG - 1 ? 0 : ws + 1;
   }
   const int mw = m0 + arow, nw = n0 + bcol;
-  if constexpr (L == 1) {
-    // acc[i][j]: lane l holds m = 16i + (l&15), n = 16j + 4(l>>4) + r
-    const bool direct = nwg == p.ntiles;
+  if constexpr (EPI == E2_F32_SLAB) {
+    // acc[i][j]: lane l holds m = 16i + (l&15), n = 16j + 4(l>>4) + r. One TT split accumulates into C; NT always
+    // writes its slab (splitk_epi_kernel reduces and runs the bf16 epilogue).
+    const bool direct = L == 1 && nwg == p.ntiles;
     const int q4 = lane >> 4, lr = lane & 15;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -980,7 +982,15 @@ int gemm2_nt_splits(int M, int N, int K) {
   const char* e = getenv("HSD_G2_SPLITK");
   const int kt = K / 64;
   if (e) return std::max(1, std::min(atoi(e), kt));
-  if (gemm2s_use(M, N, K)) return 1;  // the 128 x 128 kernel fills the GPU without K-splits
+  if (gemm2s_use(M, N, K)) {
+    // 128 x 128 tiles: split only grids that leave more than half of the CUs idle (serving batches: B = 1 has 6-24
+    // tiles, each a latency-bound chain of 12-48 K-steps), >= 2 K-tiles per split
+    const int tiles = ((M + 127) / 128) * (N / 128);
+    if (tiles * 2 > 256) return 1;
+    int s = 256 / tiles;
+    while (s > 1 && kt / s < 2) --s;
+    return s;
+  }
   const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
   if (tiles * 2 > 256) return 1;
   int s = 256 / tiles;
@@ -1138,10 +1148,17 @@ void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const b
     G2Params q = p;
     q.C = ws;
     q.dbias = nullptr;
-    g2_launch<0, 0, E2_F32_SLAB, 256>(q, splits, st);
     int kps = (K + splits - 1) / splits;
     kps = (kps + 63) / 64 * 64;
     const int real = (K + kps - 1) / kps;
+    if (gemm2s_use(M, N, K)) {
+      q.tiles_n = N / g2::SBN;
+      q.ntiles = ((M + g2::SBM - 1) / g2::SBM) * q.tiles_n;
+      q.kps = kps;
+      g2s_launch<0, E2_F32_SLAB>(q, q.ntiles * real, st);
+    } else {
+      g2_launch<0, 0, E2_F32_SLAB, 256>(q, splits, st);
+    }
     const int gx = (N + 63) / 64;
     const int gy_want = std::max(1, 2048 / gx);
     int rpb = (M + gy_want - 1) / gy_want;

@@ -234,16 +234,19 @@ def test_gemm2_gelu_derivative_and_mul_epilogues(gpu):
     _check(db, out.float().sum(0), 1e-3)
 
 
-@pytest.mark.parametrize("M,N,K,splits", [(512, 768, 1024, 4), (300, 512, 3072, 3), (4096, 1024, 4096, 0)])
+@pytest.mark.parametrize("small", ["0", "1"])
+@pytest.mark.parametrize("M,N,K,splits", [(512, 768, 1024, 4), (300, 512, 3072, 3), (4096, 1024, 4096, 0),
+                                          (128, 768, 3072, 0), (128, 3072, 768, 0)])
 @pytest.mark.parametrize("epi", [0, 1, 2, 3, 4, 5, 8, 9])
-def test_gemm2_nt_splitk_matches_one_pass(gpu, monkeypatch, M, N, K, splits, epi):
+def test_gemm2_nt_splitk_matches_one_pass(gpu, monkeypatch, M, N, K, splits, epi, small):
     """Split-K NT (fp32 slabs + reduce-and-epilogue pass) == the one-pass fused epilogue, for every epilogue kind
     (same dropout sites, same fused bias-gradient column sums), up to the fp32 order of the K-split sums."""
     torch.manual_seed(5 + epi)
     C_ = _C()
-    monkeypatch.setenv("HSD_G2_SMALL", "0")  # split-K is the small-grid path only when the 128-tile kernel is off
-    if splits == 0:
-        assert C_.gemm2_nt_splits(M, N, K) > 1  # the reference's bert-large B=8 S=512 shape is split automatically
+    # split-K slabs from the 256 x 256 kernel (small = "0") or the 128 x 128 kernel ("1": serving batches)
+    monkeypatch.setenv("HSD_G2_SMALL", small)
+    if splits == 0 and (small == "0") == (M != 128):
+        assert C_.gemm2_nt_splits(M, N, K) > 1  # small tile grids are split automatically
     A, B = _mk((M, K), gpu), _mk((N, K), gpu, 0.05)
     bias = _mk((N,), gpu)
     aux = _mk((M, N), gpu) if epi != 9 else torch.rand(M, N, device=gpu).bfloat16()
