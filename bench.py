@@ -21,7 +21,7 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from huggingface_sagemaker_tensorflow_distributed_amd import data as hdata  # noqa: E402
 from huggingface_sagemaker_tensorflow_distributed_amd.parallel import backend  # noqa: E402
 from huggingface_sagemaker_tensorflow_distributed_amd.train.runner import build  # noqa: E402
-from huggingface_sagemaker_tensorflow_distributed_amd.utils.args import build_parser  # noqa: E402
+from huggingface_sagemaker_tensorflow_distributed_amd.utils.args import batch_size_arg, build_parser  # noqa: E402
 
 METRIC = "sequences/sec (whole node) BERT-base seq128 at 1/2/4/8 MI355X"
 BASELINE_VALUE = None  # the reference publishes no number
@@ -32,8 +32,8 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--batch_size", type=int, default=int(os.environ.get("HSD_BENCH_BATCH", "1024")),
-                    help="per-GPU batch")
+    ap.add_argument("--batch_size", type=batch_size_arg, default=batch_size_arg(os.environ.get("HSD_BENCH_BATCH", "1024")),
+                    help="per-GPU batch, or 'auto' (sized for the device memory, train/batch_planner.py)")
     ap.add_argument("--seq_len", type=int, default=128)
     ap.add_argument("--model", default="bert-base-uncased")
     ap.add_argument("--bucket_mb", type=float, default=None)
@@ -50,12 +50,13 @@ def main():
     targs, _ = build_parser("train").parse_known_args(
         ["--model_name_or_path", a.model, "--train_batch_size", str(a.batch_size), "--dtype", a.dtype,
          "--task", a.task, "--hip_graph", str(a.hip_graph),
-         "--learning_rate", "5e-5", "--log_every", "0"]
+         "--learning_rate", "5e-5", "--log_every", "0", "--max_seq_length", str(a.seq_len)]
         + (["--bucket_mb", str(a.bucket_mb)] if a.bucket_mb else [])
         + (["--grad_dtype", a.grad_dtype] if a.grad_dtype else []))
     parts = build(targs, "train")
     trainer, dev, world, rank = parts["trainer"], parts["device"], parts["world"], parts["rank"]
     cfg = parts["model"].cfg
+    a.batch_size = targs.train_batch_size  # resolved when --batch_size auto
     n_batches = 4
     if a.task == "masked-lm":
         ds = hdata.synthetic_mlm(a.batch_size * n_batches, a.seq_len, cfg.vocab_size, seed=1234 + rank)

@@ -30,6 +30,7 @@ from ..utils.args import parse_args
 from ..utils.env import is_sagemaker_dp_enabled
 from ..utils.logging import setup_logging
 from ..utils.results_io import write_eval_results, write_train_results
+from . import batch_planner
 from .callbacks import FaultInjection, ModelCheckpoint, load_checkpoint, master_state_dict
 from .trainer import Trainer
 
@@ -64,7 +65,7 @@ def _datasets(args, cfg, tokenizer, max_len: int):
     return tr, te
 
 
-def _provenance(args, model, rank: int, n_train: int, n_eval: int) -> dict:
+def _provenance(args, model, rank: int, n_train: int, n_eval: int, batch_plan=None) -> dict:
     """Say loudly when the run is not the reference's imdb fine-tune of pretrained weights: results files keep
     the reference's exact format, so the data / weights they came from go to ``run_provenance.json`` beside
     them and to a WARNING in the log."""
@@ -72,7 +73,9 @@ def _provenance(args, model, rank: int, n_train: int, n_eval: int) -> dict:
     synthetic = args.dataset == "synthetic"
     info = {"dataset": args.dataset, "synthetic_data": synthetic, "weights": weights,
             "model_name_or_path": args.model_name_or_path, "num_train_examples": n_train,
-            "num_eval_examples": n_eval}
+            "num_eval_examples": n_eval, "train_batch_size": args.train_batch_size}
+    if batch_plan is not None:
+        info["auto_batch"] = batch_plan.as_dict()
     if synthetic or weights == "random-init":
         what = " and ".join(x for x in (("synthetic random data" if synthetic else ""),
                                          ("random-init weights" if weights == "random-init" else "")) if x)
@@ -115,6 +118,20 @@ def build(args, mode: str):
     lr = base_lr * world if mode == "train" else base_lr  # scripts/train.py:112 vs singe_node_train.py:78
     opt = FusedAdam(store, lr=lr, eps=args.adam_epsilon, eps_mode=args.adam_eps_mode,
                     weight_decay=args.weight_decay if args.optimizer == "adamw" else 0.0)
+    tokenizer = hdata.load_tokenizer(args.model_name_or_path, model.cfg.vocab_size, model.cfg.model_max_length)
+    max_len = args.max_seq_length or min(tokenizer.model_max_length, model.cfg.max_position_embeddings)
+    batch_plan = None
+    if args.train_batch_size == "auto":
+        # sized on the device before any readiness hook / bucketer exists (the probes are plain fwd + bwd)
+        batch_plan = batch_planner.plan(model, store, max_len, dev, headroom=args.auto_batch_headroom,
+                                        max_tokens=args.auto_batch_max_tokens or None)
+        per_gpu = batch_planner.agree_min(batch_plan.per_gpu_batch, dev)
+        batch_plan.per_gpu_batch = per_gpu
+        args.train_batch_size = per_gpu if mode == "train" else per_gpu * world
+        logger.info("--train_batch_size auto: %d per GPU (%s, %.1f MB/sequence, fixed %.2f GB, budget %.1f of "
+                    "%.1f GB, capped by %s) -> train_batch_size %d", per_gpu, batch_plan.method,
+                    batch_plan.per_seq_bytes / 2**20, batch_plan.fixed_bytes / 2**30, batch_plan.budget_bytes / 2**30,
+                    batch_plan.total_bytes / 2**30, batch_plan.capped_by, args.train_batch_size)
     bucketer = GradBucketer(store, bucket_mb=args.bucket_mb) if world > 1 else None
     trainer = Trainer(model, store, opt, bucketer, dev, grad_accum=args.gradient_accumulation_steps,
                       lr_schedule=getattr(args, "lr_schedule", "constant"),
@@ -125,7 +142,8 @@ def build(args, mode: str):
     if args.resume_from:
         initial_epoch = int(load_checkpoint(args.resume_from, trainer).get("epoch", 0))
     broadcast_parameters(store, opt if args.resume_from else None)
-    return {"initial_epoch": initial_epoch, "model": model, "store": store, "optimizer": opt, "bucketer": bucketer, "trainer": trainer,
+    return {"initial_epoch": initial_epoch, "tokenizer": tokenizer, "max_len": max_len, "batch_plan": batch_plan,
+            "model": model, "store": store, "optimizer": opt, "bucketer": bucketer, "trainer": trainer,
             "device": dev, "world": world, "rank": rank, "lr": lr, "dtype": dtype_name}
 
 
@@ -142,8 +160,7 @@ def run(argv: Optional[Sequence[str]] = None, mode: str = "train") -> dict:
     world, rank = parts["world"], parts["rank"]
     cfg = model.cfg
 
-    tokenizer = hdata.load_tokenizer(args.model_name_or_path, cfg.vocab_size, cfg.model_max_length)
-    max_len = args.max_seq_length or min(tokenizer.model_max_length, cfg.max_position_embeddings)
+    tokenizer, max_len = parts["tokenizer"], parts["max_len"]
     train_ds, test_ds = _datasets(args, cfg, tokenizer, max_len)
 
     if mode == "train":
@@ -161,7 +178,7 @@ def run(argv: Optional[Sequence[str]] = None, mode: str = "train") -> dict:
     test_loader = hdata.BatchLoader(test_ds, ShardSampler(len(test_ds), rank, world, shuffle=False, seed=args.seed,
                                                            drop_last=False, mark_padding=True,
                                                            batch_size=per_rank_eval), dev)
-    _provenance(args, model, rank, len(train_ds), len(test_ds))
+    _provenance(args, model, rank, len(train_ds), len(test_ds), parts["batch_plan"])
     out = {"args": args}
     callbacks = [FaultInjection()]
     if args.benchmark or args.profile:

@@ -33,10 +33,21 @@ def str2bool(v) -> bool:
     raise argparse.ArgumentTypeError(f"expected a boolean, got {v!r}")
 
 
+def batch_size_arg(v):
+    """``--train_batch_size``: an int (the reference's ``type=int``) or ``auto`` = sized for the device's HBM
+    (train/batch_planner.py)."""
+    if isinstance(v, int):
+        return v
+    if str(v).strip().lower() == "auto":
+        return "auto"
+    return int(v)
+
+
 def _add_reference_flags(p: argparse.ArgumentParser, *, with_n_gpus: bool) -> None:
     # scripts/train.py:39-45
     p.add_argument("--epochs", type=int, default=3)
-    p.add_argument("--train_batch_size", type=int, default=8)
+    p.add_argument("--train_batch_size", type=batch_size_arg, default=8,
+                   help="int, or 'auto': the largest per-GPU batch that fits the HBM (capped at the throughput knee)")
     p.add_argument("--eval_batch_size", type=int, default=4)
     p.add_argument("--model_name_or_path", type=str, default=None)
     p.add_argument("--learning_rate", type=float, default=5e-5)
@@ -88,6 +99,10 @@ def _add_framework_flags(p: argparse.ArgumentParser) -> None:
     g.add_argument("--num_labels", type=int, default=2)
     g.add_argument("--task", choices=["sequence-classification", "masked-lm"], default="sequence-classification",
                    help="masked-lm: RoBERTa MLM pretraining (BASELINE.json config 5)")
+    g.add_argument("--auto_batch_max_tokens", type=int, default=131072,
+                   help="--train_batch_size auto: cap per-GPU tokens (0 = fill the memory budget)")
+    g.add_argument("--auto_batch_headroom", type=float, default=0.9,
+                   help="--train_batch_size auto: fraction of the device memory the step may use")
     g.add_argument("--fp8_grad_format", choices=["e4m3", "e5m2"], default="e4m3",
                    help="--dtype fp8: format of the quantised gradients in the dgrad GEMMs")
 
