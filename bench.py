@@ -34,6 +34,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=5)
     ap.add_argument("--batch_size", type=batch_size_arg, default=batch_size_arg(os.environ.get("HSD_BENCH_BATCH", "1024")),
                     help="per-GPU batch, or 'auto' (sized for the device memory, train/batch_planner.py)")
+    ap.add_argument("--auto_batch_max_tokens", type=int, default=131072,
+                    help="--batch_size auto: per-GPU token cap (0 = fill the HBM budget)")
     ap.add_argument("--seq_len", type=int, default=128)
     ap.add_argument("--model", default="bert-base-uncased")
     ap.add_argument("--bucket_mb", type=float, default=None)
@@ -50,7 +52,8 @@ def main():
     targs, _ = build_parser("train").parse_known_args(
         ["--model_name_or_path", a.model, "--train_batch_size", str(a.batch_size), "--dtype", a.dtype,
          "--task", a.task, "--hip_graph", str(a.hip_graph),
-         "--learning_rate", "5e-5", "--log_every", "0", "--max_seq_length", str(a.seq_len)]
+         "--learning_rate", "5e-5", "--log_every", "0", "--max_seq_length", str(a.seq_len),
+         "--auto_batch_max_tokens", str(a.auto_batch_max_tokens)]
         + (["--bucket_mb", str(a.bucket_mb)] if a.bucket_mb else [])
         + (["--grad_dtype", a.grad_dtype] if a.grad_dtype else []))
     parts = build(targs, "train")
@@ -112,6 +115,7 @@ def main():
                        "comm": ("native-rccl" if getattr(trainer.bucketer, "engine", None) is not None
                                 else ("torch-" + backend.state().backend if world > 1 else "none"))},
             **({"comm_overlap": overlap} if overlap is not None else {}),
+            **({"batch_plan": parts["batch_plan"].as_dict()} if parts.get("batch_plan") is not None else {}),
         }), flush=True)
     backend.shutdown()
 
