@@ -56,7 +56,13 @@ import os as _os
 
 _WGRAD_STREAM = _os.environ.get("HSD_WGRAD_STREAM", "0") == "1"  # opt-in: +1% at B=256, but record_stream
 # keeps freed activations from being reused promptly and collapses large-batch throughput
+# HSD_WGRAD_STASH=1 (default): instead of record_stream, the side stream's operands stay referenced until the
+# next join_side_streams() (the compute stream has then waited for the side stream, so their blocks go back to
+# the compute stream's pool with no cross-stream event bookkeeping in the allocator). Costs the operands' memory
+# until the end of the backward (~40 GB at bert-base B = 1024).
+_WGRAD_STASH = _os.environ.get("HSD_WGRAD_STASH", "1") == "1"
 _SIDE = {}
+_STASH = []
 
 
 def side_stream(device) -> Optional[torch.cuda.Stream]:
@@ -76,6 +82,7 @@ def join_side_streams() -> None:
     for s in _SIDE.values():
         if s.device == cur.device:
             cur.wait_stream(s)
+    _STASH.clear()
 
 
 def wgrad_done(g: "_Grad", dy: torch.Tensor, x: torch.Tensor):
@@ -89,8 +96,11 @@ def wgrad_done(g: "_Grad", dy: torch.Tensor, x: torch.Tensor):
     with torch.cuda.stream(s):
         gemm_wgrad_(g, dy, x)
         r = g.done()
-    dy.record_stream(s)
-    x.record_stream(s)
+    if _WGRAD_STASH:
+        _STASH.append((dy, x))
+    else:
+        dy.record_stream(s)
+        x.record_stream(s)
     return r
 
 
