@@ -1,0 +1,43 @@
+"""bench.py under the driver's multi-GPU launch line, rehearsed on CPU (gloo, world 2 and 8).
+
+The driver runs ``python -m torch.distributed.run --nnodes=1 --nproc-per-node N --master-addr 127.0.0.1
+--master-port P bench.py --gpus N --steps K --warmup W`` and parses ONE JSON line from rank 0. Here the same line
+runs 2 and 8 CPU ranks of a tiny BERT: exactly one JSON line, the contract's keys, whole-job value = global batch x
+steps / time (max over ranks), DP degree in the config.
+"""
+import json
+import os
+
+import pytest
+import socket
+import subprocess
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+        "vs_baseline", "dtype", "data", "config"}
+
+
+def _port() -> int:
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+@pytest.mark.parametrize("n", [2, 8])
+def test_bench_driver_line_cpu(n):
+    env = dict(os.environ, OMP_NUM_THREADS="1", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", str(n),
+           "--steps", "2", "--warmup", "1", "--batch_size", "2", "--seq_len", "16", "--model", "hsd-tiny-bert"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout
+    d = json.loads(lines[0])
+    assert KEYS <= set(d), set(d) ^ KEYS
+    assert d["n_gpus"] == n and d["steps"] == 2 and d["warmup"] == 1
+    assert d["config"]["global_batch"] == 2 * n and d["config"]["parallelism"] == f"dp{n}"
+    assert d["higher_is_better"] is True and d["scaling"] == "weak"
+    assert d["value"] > 0
+    assert abs(d["value"] - 2 * n * 2 / (d["ms_per_step"] * 2 / 1e3)) / d["value"] < 0.01
