@@ -7,11 +7,11 @@ steps / time (max over ranks), DP degree in the config.
 """
 import json
 import os
-
-import pytest
 import socket
 import subprocess
 import sys
+
+import pytest
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 KEYS = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
