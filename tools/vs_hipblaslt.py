@@ -1,0 +1,84 @@
+"""This framework's GEMMs vs hipBLASLt (torch.addmm / torch.mm) on the headline layer's shapes, one process.
+
+    python tools/vs_hipblaslt.py [T]      (default T = 131072 tokens = bert-base B = 1024, S = 128)
+
+For each bert-base projection (QKV, attention output, FFN1, FFN2) and each of its three GEMMs:
+  forward  y = x Wᵀ + b        ours: gemm2 NT, bias epilogue      library: torch.addmm(b, x, Wᵀ)
+  dgrad    dx = dy W           ours: gemm2 NT on the stored Wᵀ    library: torch.mm(dy, W)
+  wgrad    dW += dyᵀ x (fp32)  ours: gemm2 TT split-K + reduce    library: main_grad += torch.mm(dyᵀ, x) (bf16 out)
+Random operands, HIP-event timing, interleaved rounds (ours / library alternate) so both see the same clocks.
+Prints one JSON object (TFLOP/s per GEMM and the layer totals); also writes gpurun_out/vs_hipblaslt.json.
+"""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from huggingface_sagemaker_tensorflow_distributed_amd.ops import hip  # noqa: E402
+
+
+def timed(fn, iters=10):
+    st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    st.record()
+    for _ in range(iters):
+        fn()
+    en.record()
+    torch.cuda.synchronize()
+    return st.elapsed_time(en) / iters * 1e-3
+
+
+def main():
+    T = int(sys.argv[1]) if len(sys.argv) > 1 else 131072
+    dev = torch.device("cuda", 0)
+    torch.manual_seed(0)
+    out = {"tokens": T}
+    tot = {"ours_s": 0.0, "lib_s": 0.0, "flop": 0.0}
+    for name, (N, K) in {"qkv": (2304, 768), "attn_out": (768, 768), "ffn1": (3072, 768),
+                         "ffn2": (768, 3072)}.items():
+        x = torch.randn(T, K, device=dev).bfloat16()
+        w = torch.randn(N, K, device=dev).bfloat16() * 0.05
+        wt = w.t().contiguous()
+        b = torch.randn(N, device=dev).bfloat16()
+        dy = torch.randn(T, N, device=dev).bfloat16()
+        gw = torch.zeros(N, K, device=dev)
+        w.main_grad = gw
+        g = hip._Grad(w)
+        fl = 2.0 * T * N * K
+        cases = {
+            "fwd": (lambda: hip.gemm_fwd(x, w, hip.EPI_BIAS, bias=b), lambda: torch.addmm(b, x, w.t())),
+            "dgrad": (lambda: hip._C.gemm2(dy, wt, torch.empty(T, K, device=dev, dtype=torch.bfloat16), 0, 0,
+                                           hip.EPI_STORE, None, None, None, 0.0, 0, 0, None, None),
+                      lambda: torch.mm(dy, w)),
+            "wgrad": (lambda: hip.gemm_wgrad_(g, dy, x), lambda: gw.add_(torch.mm(dy.t(), x))),
+        }
+        r = {}
+        for case, (ours, lib) in cases.items():
+            for f in (ours, lib):  # warm-up (kernel selection, workspaces)
+                f()
+                f()
+            torch.cuda.synchronize()
+            t_o, t_l = [], []
+            for _ in range(3):
+                t_o.append(timed(ours))
+                t_l.append(timed(lib))
+            to, tl = min(t_o), min(t_l)
+            r[case] = {"ours_TFLOPs": round(fl / to / 1e12, 1), "hipblaslt_TFLOPs": round(fl / tl / 1e12, 1),
+                       "ours_us": round(to * 1e6, 1), "hipblaslt_us": round(tl * 1e6, 1), "speedup": round(tl / to, 3)}
+            tot["ours_s"] += to
+            tot["lib_s"] += tl
+            tot["flop"] += fl
+        out[name] = r
+        print(name, json.dumps(r), flush=True)
+        del w.main_grad
+    out["layer"] = {"ours_TFLOPs": round(tot["flop"] / tot["ours_s"] / 1e12, 1),
+                    "hipblaslt_TFLOPs": round(tot["flop"] / tot["lib_s"] / 1e12, 1),
+                    "speedup": round(tot["lib_s"] / tot["ours_s"], 3)}
+    print(json.dumps(out), flush=True)
+    os.makedirs("gpurun_out", exist_ok=True)
+    json.dump(out, open("gpurun_out/vs_hipblaslt.json", "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
