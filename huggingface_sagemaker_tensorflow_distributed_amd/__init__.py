@@ -9,6 +9,7 @@ The top level doubles as the ``hvd``-style facade the reference script programs 
 
     import huggingface_sagemaker_tensorflow_distributed_amd as hvd
     hvd.init(); hvd.rank(); hvd.size(); hvd.local_rank()
+    hvd.allreduce(t) / hvd.allgather(t) / hvd.broadcast(t, 0) / hvd.broadcast_object(obj, 0)
 """
 from __future__ import annotations
 
@@ -36,6 +37,20 @@ class callbacks:  # noqa: N801 - the ``hvd.callbacks`` namespace
     from .train.callbacks import BroadcastGlobalVariablesCallback, MetricAverageCallback  # noqa: F401
 
 
+from .parallel.collectives import Average, Max, Min, Sum  # noqa: E402
+from .parallel.collectives import hvd_allgather as allgather  # noqa: E402
+from .parallel.collectives import hvd_allgather_object as allgather_object  # noqa: E402
+from .parallel.collectives import hvd_allreduce as allreduce  # noqa: E402
+from .parallel.collectives import hvd_broadcast as broadcast  # noqa: E402
+
+
+def broadcast_object(obj, root_rank: int = 0):
+    """``hvd.broadcast_object``: ``root_rank``'s picklable object on every rank."""
+    from .parallel.collectives import broadcast_object as _bo
+
+    return _bo(obj, src=root_rank)
+
+
 def broadcast_parameters(store, optimizer=None, root_rank: int = 0):
     from .parallel.collectives import broadcast_parameters as _b
 
@@ -43,4 +58,5 @@ def broadcast_parameters(store, optimizer=None, root_rank: int = 0):
 
 
 __all__ = ["init", "rank", "size", "local_rank", "local_size", "barrier", "is_distributed", "shutdown",
-           "DistributedOptimizer", "broadcast_parameters", "callbacks", "__version__"]
+           "DistributedOptimizer", "broadcast_parameters", "callbacks", "allreduce", "allgather", "broadcast",
+           "broadcast_object", "allgather_object", "Average", "Sum", "Min", "Max", "__version__"]

@@ -67,3 +67,66 @@ def params_in_sync(store) -> bool:
     dist.all_reduce(lo, op=dist.ReduceOp.MIN)
     dist.all_reduce(hi, op=dist.ReduceOp.MAX)
     return bool(torch.equal(lo, hi))
+
+
+# ---------------------------------------------------------------------------------------------- hvd tensor API
+# Horovod's tensor collectives (``hvd.allreduce / allgather / broadcast / broadcast_object``), for code that calls
+# them directly next to the reference's DistributedOptimizer / broadcast callback (Horovod
+# also allgathers IndexedSlices). Out of place like Horovod; on GPUs the all-reduce and broadcast go through the
+# native RCCL engine, everything else through torch.distributed (RCCL or gloo).
+Average, Sum, Min, Max = "average", "sum", "min", "max"
+_OPS = {Sum: dist.ReduceOp.SUM, Min: dist.ReduceOp.MIN, Max: dist.ReduceOp.MAX}
+
+
+def hvd_allreduce(tensor: torch.Tensor, average=None, op=None) -> torch.Tensor:
+    """``hvd.allreduce``: the reduced copy of ``tensor`` (default op Average; ``average=False`` means Sum)."""
+    if op is None:
+        op = Sum if average is False else Average
+    out = tensor.detach().clone().contiguous()
+    if not backend.is_distributed():
+        return out
+    if op in (Sum, Average):
+        from .comm import allreduce_
+
+        if not out.is_floating_point() and op == Average:
+            raise TypeError("hvd.allreduce(op=Average) needs a floating-point tensor")
+        allreduce_(out)
+        if op == Average:
+            out /= backend.size()
+    else:
+        dist.all_reduce(out, op=_OPS[op])
+    return out
+
+
+def hvd_allgather(tensor: torch.Tensor) -> torch.Tensor:
+    """``hvd.allgather``: concatenation over ranks along dim 0; the first dimension may differ per rank."""
+    t = tensor.detach().contiguous()
+    if not backend.is_distributed():
+        return t.clone()
+    world = backend.size()
+    n = torch.tensor([t.shape[0]], dtype=torch.int64, device=t.device)
+    sizes = [torch.zeros_like(n) for _ in range(world)]
+    dist.all_gather(sizes, n)
+    sizes = [int(s.item()) for s in sizes]
+    mx = max(sizes)
+    pad = t
+    if t.shape[0] < mx:
+        pad = torch.cat([t, t.new_zeros((mx - t.shape[0],) + tuple(t.shape[1:]))])
+    parts = [torch.empty_like(pad) for _ in range(world)]
+    dist.all_gather(parts, pad)
+    return torch.cat([p[:s] for p, s in zip(parts, sizes)])
+
+
+def hvd_broadcast(tensor: torch.Tensor, root_rank: int = 0) -> torch.Tensor:
+    """``hvd.broadcast``: a copy of ``root_rank``'s tensor on every rank."""
+    out = tensor.detach().clone().contiguous()
+    return broadcast_tensor(out, root_rank) if backend.is_distributed() else out
+
+
+def hvd_allgather_object(obj) -> list:
+    """``hvd.allgather_object``: every rank's picklable object, in rank order (objects this process made)."""
+    if not backend.is_distributed():
+        return [obj]
+    out = [None] * backend.size()
+    dist.all_gather_object(out, obj)
+    return out

@@ -397,3 +397,31 @@ def test_hvd_broadcast_callback_syncs_weights_and_optimizer_state():
     """``hvd.callbacks.BroadcastGlobalVariablesCallback(0)`` (scripts/train.py:133) on the facade: ranks built from
     different seeds hold rank 0's weights and Adam moments after on_train_begin."""
     mp.spawn(_worker_hvd_callback, args=(2, _port()), nprocs=2, join=True)
+
+
+def _worker_hvd_tensor_ops(rank, world, port):
+    _setenv(rank, world, port)
+    import huggingface_sagemaker_tensorflow_distributed_amd as hvd
+
+    hvd.init(device="cpu")
+    x = torch.full((3, 2), float(rank + 1))
+    avg = hvd.allreduce(x)
+    assert torch.allclose(avg, torch.full((3, 2), (world + 1) / 2.0)) and torch.equal(x, torch.full((3, 2), rank + 1.0))
+    assert torch.equal(hvd.allreduce(x, average=False), torch.full((3, 2), world * (world + 1) / 2.0))
+    assert torch.equal(hvd.allreduce(x, op=hvd.Max), torch.full((3, 2), float(world)))
+    assert torch.equal(hvd.allreduce(torch.tensor([rank + 5]), op=hvd.Min), torch.tensor([5]))
+    # variable first dimension, like Horovod's allgather of IndexedSlices rows
+    g = hvd.allgather(torch.arange(rank + 1, dtype=torch.float32).reshape(-1, 1) + 10 * rank)
+    want = torch.cat([torch.arange(r + 1, dtype=torch.float32).reshape(-1, 1) + 10 * r for r in range(world)])
+    assert torch.equal(g, want)
+    b = hvd.broadcast(torch.tensor([float(rank), 7.0]), root_rank=world - 1)
+    assert torch.equal(b, torch.tensor([float(world - 1), 7.0]))
+    assert hvd.broadcast_object({"r": rank}, root_rank=1) == {"r": 1}
+    assert hvd.allgather_object(rank * 3) == [r * 3 for r in range(world)]
+    hvd.shutdown()
+
+
+def test_hvd_tensor_collectives_world3():
+    """Horovod tensor API on the facade (allreduce Average / Sum / Min / Max, variable-length allgather,
+    broadcast from a non-zero root, object broadcast / allgather), gloo world 3."""
+    mp.spawn(_worker_hvd_tensor_ops, args=(3, _port()), nprocs=3, join=True)
