@@ -50,23 +50,31 @@ class _Grad:
 # Weight-gradient GEMMs are independent of the rest of the backward chain (dgrad -> previous layer), so
 # they run on a side stream: their compute overlaps the dgrad GEMMs' memory-bound epilogues and the
 # attention / LayerNorm kernels on other CUs. Gradient readiness (bucket all-reduce) is signalled from
-# the side stream; the comm engine also orders every collective after it, and the trainer joins it
-# before the optimizer (join_side_streams).
+# the side stream; the comm engine and the overlapped optimizer order their work after it, and every backward
+# pass ends with the compute stream joined to it (an autograd final callback), so gradients read after
+# ``loss.backward()`` are complete on the compute stream.
+#
+# HSD_WGRAD_STREAM: "auto" (default) = on for steps of < 65,536 tokens, where the GEMM grids leave CUs idle and
+# the side stream measured +1.6 % (bert-base B = 256) to +8.4 % (bert-base B = 64) and +5.8 % at the reference's
+# bert-large B = 8 S = 512 (profiles/wgrad_stream_small_ab_r2.log); off above (neutral at B = 1024, where one
+# weight-gradient grid holds every CU). "1" = always, "0" = never. Never while a HIP graph is being captured.
 import os as _os
 
-_WGRAD_STREAM = _os.environ.get("HSD_WGRAD_STREAM", "0") == "1"  # opt-in: +1% at B=256, but record_stream
-# keeps freed activations from being reused promptly and collapses large-batch throughput
+_WGRAD_MODE = _os.environ.get("HSD_WGRAD_STREAM", "auto").strip().lower()
+_WGRAD_AUTO_MAX_TOKENS = int(_os.environ.get("HSD_WGRAD_STREAM_MAX_TOKENS", "65535"))
 # HSD_WGRAD_STASH=1 (default): instead of record_stream, the side stream's operands stay referenced until the
 # next join_side_streams() (the compute stream has then waited for the side stream, so their blocks go back to
-# the compute stream's pool with no cross-stream event bookkeeping in the allocator). Costs the operands' memory
-# until the end of the backward (~40 GB at bert-base B = 1024).
+# the compute stream's pool with no cross-stream event bookkeeping in the allocator; record_stream collapsed
+# throughput 7x at B = 256-1024). Costs the operands' memory until the end of the backward.
 _WGRAD_STASH = _os.environ.get("HSD_WGRAD_STASH", "1") == "1"
 _SIDE = {}
 _STASH = []
+_JOIN_QUEUED = [False]
 
 
 def side_stream(device) -> Optional[torch.cuda.Stream]:
-    if not _WGRAD_STREAM:
+    """The device's wgrad side stream (created on first use), or None when HSD_WGRAD_STREAM=0."""
+    if _WGRAD_MODE in ("0", "off", "false"):
         return None
     key = device.index if device.index is not None else torch.cuda.current_device()
     s = _SIDE.get(key)
@@ -76,6 +84,12 @@ def side_stream(device) -> Optional[torch.cuda.Stream]:
     return s
 
 
+def _use_side_stream(tokens: int) -> bool:
+    if _WGRAD_MODE in ("0", "off", "false") or torch.cuda.is_current_stream_capturing():
+        return False
+    return _WGRAD_MODE in ("1", "on", "true") or tokens <= _WGRAD_AUTO_MAX_TOKENS
+
+
 def join_side_streams() -> None:
     """Make the current stream wait for every side stream (call before consuming gradients)."""
     cur = torch.cuda.current_stream() if _SIDE else None
@@ -83,15 +97,24 @@ def join_side_streams() -> None:
         if s.device == cur.device:
             cur.wait_stream(s)
     _STASH.clear()
+    _JOIN_QUEUED[0] = False
+
+
+def _end_of_backward() -> None:
+    join_side_streams()
 
 
 def wgrad_done(g: "_Grad", dy: torch.Tensor, x: torch.Tensor):
     """``g += dyᵀ·x`` then ``g.done()`` — on the wgrad side stream when the gradient lands in the flat
-    fp32 main_grad buffer (training with a FlatParamStore), synchronously otherwise."""
-    s = side_stream(dy.device) if (g.mg is not None and g.buf is g.mg) else None
+    fp32 main_grad buffer (training with a FlatParamStore) and the step is small enough, synchronously otherwise."""
+    s = side_stream(dy.device) if (g.mg is not None and g.buf is g.mg and _use_side_stream(dy.shape[0])) else None
     if s is None:
         gemm_wgrad_(g, dy, x)
         return g.done()
+    if not _JOIN_QUEUED[0]:
+        # join the compute stream to the side stream when this backward pass finishes
+        torch.autograd.Variable._execution_engine.queue_callback(_end_of_backward)
+        _JOIN_QUEUED[0] = True
     s.wait_stream(torch.cuda.current_stream())
     with torch.cuda.stream(s):
         gemm_wgrad_(g, dy, x)
