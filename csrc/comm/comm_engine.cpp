@@ -12,7 +12,11 @@
 //   backward kernels mark parameters ready in a deterministic order on every rank, so the engine
 //   launches bucket b's in-place ncclAllReduce as soon as its last parameter is ready — the role of
 //   Horovod's 64 MiB fusion buffer + coordinator, without the coordinator.
+// * Optional wire compression (Horovod's hvd.Compression.fp16): a bucket is cast to a bf16 /
+//   fp16 shadow on the comm stream, all-reduced in that type (half the xGMI bytes) and cast back into the fp32
+//   gradient buffer, all on the comm stream.
 #include <torch/extension.h>
+#include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
 #include <c10/hip/HIPCachingAllocator.h>
 #include <hip/hip_runtime.h>
@@ -161,6 +165,18 @@ class CommEngine {
     begin_step();
   }
 
+  // 0 = none (all-reduce the gradient buffer in place), 1 = bf16 on the wire, 2 = fp16 on the wire
+  void set_compression(int64_t mode) {
+    if (mode < 0 || mode > 2) throw std::runtime_error("set_compression: mode 0 (none), 1 (bf16) or 2 (fp16)");
+    comp_ = (int)mode;
+    if (comp_ != 0) {
+      if (!flat_.defined()) throw std::runtime_error("set_compression: call set_buckets first");
+      const auto dt = comp_ == 1 ? at::kBFloat16 : at::kHalf;
+      if (!shadow_.defined() || shadow_.numel() != flat_.numel() || shadow_.scalar_type() != dt)
+        shadow_ = at::empty({flat_.numel()}, flat_.options().dtype(dt));
+    }
+  }
+
   void begin_step() {
     for (auto& b : buckets_) {
       b.pending = b.nparams;
@@ -289,7 +305,16 @@ class CommEngine {
     order_after_caller();
     const int64_t n = b.end - b.start;
     if (timing_) HIP_OK(hipEventRecord(b.t_start, stream_));
-    if (n > 0) {
+    if (n > 0 && comp_ != 0 && flat_.scalar_type() == at::kFloat) {
+      // cast -> all-reduce in 16 bits -> cast back, all ordered on the comm stream
+      c10::hip::HIPStreamGuard guard(c10::hip::getStreamFromExternal(stream_, device_));
+      at::Tensor src = flat_.narrow(0, b.start, n);
+      at::Tensor wire = shadow_.narrow(0, b.start, n);
+      wire.copy_(src);
+      NCCL_OK(ncclAllReduce(wire.data_ptr(), wire.data_ptr(), (size_t)n, to_nccl(wire.scalar_type()), ncclSum, comm_,
+                            stream_));
+      src.copy_(wire);
+    } else if (n > 0) {
       char* base = static_cast<char*>(flat_.data_ptr()) + b.start * flat_.element_size();
       NCCL_OK(ncclAllReduce(base, base, (size_t)n, to_nccl(flat_.scalar_type()), ncclSum, comm_, stream_));
     }
@@ -311,6 +336,8 @@ class CommEngine {
   std::vector<hipStream_t> deps_;
   std::vector<hipEvent_t> dep_events_;
   torch::Tensor flat_;
+  torch::Tensor shadow_;
+  int comp_ = 0;
 };
 
 }  // namespace
@@ -326,6 +353,7 @@ void register_comm(pybind11::module& m) {
       .def("allreduce", &CommEngine::allreduce, py::arg("t"), py::arg("wait") = true)
       .def("broadcast", &CommEngine::broadcast, py::arg("t"), py::arg("root") = 0)
       .def("set_buckets", &CommEngine::set_buckets)
+      .def("set_compression", &CommEngine::set_compression)
       .def("begin_step", &CommEngine::begin_step)
       .def("set_timing", &CommEngine::set_timing)
       .def("timings", &CommEngine::timings)

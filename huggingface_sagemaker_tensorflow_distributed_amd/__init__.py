@@ -18,17 +18,26 @@ __version__ = "0.1.0"
 from .parallel.backend import barrier, init, is_distributed, local_rank, local_size, rank, shutdown, size
 
 
-def DistributedOptimizer(optimizer, store=None, bucket_mb=None):
+class Compression:  # noqa: N801 - Horovod's ``hvd.Compression`` namespace
+    """Wire dtype of the gradient all-reduce: ``none`` (fp32), ``fp16`` (Horovod's), ``bf16`` (MI355X-native)."""
+
+    none = "none"
+    fp16 = "fp16"
+    bf16 = "bf16"
+
+
+def DistributedOptimizer(optimizer, store=None, bucket_mb=None, compression=Compression.none):
     """Horovod-compatible spelling: returns ``(optimizer, bucketer)`` wired to the flat store.
 
     In this framework gradient averaging lives in :class:`parallel.GradBucketer` (all-reduce overlapped
     with backward) and the ``1/N`` scale is folded into :class:`optim.FusedAdam`; this helper exists so
-    code written against ``hvd.DistributedOptimizer`` has a direct equivalent.
+    code written against ``hvd.DistributedOptimizer(opt, compression=hvd.Compression.fp16)`` has a direct
+    equivalent.
     """
     from .parallel.ddp import GradBucketer
 
     store = store or optimizer.store
-    return optimizer, (GradBucketer(store, bucket_mb=bucket_mb) if size() > 1 else None)
+    return optimizer, (GradBucketer(store, bucket_mb=bucket_mb, compression=compression) if size() > 1 else None)
 
 
 class callbacks:  # noqa: N801 - the ``hvd.callbacks`` namespace
@@ -58,5 +67,5 @@ def broadcast_parameters(store, optimizer=None, root_rank: int = 0):
 
 
 __all__ = ["init", "rank", "size", "local_rank", "local_size", "barrier", "is_distributed", "shutdown",
-           "DistributedOptimizer", "broadcast_parameters", "callbacks", "allreduce", "allgather", "broadcast",
+           "DistributedOptimizer", "Compression", "broadcast_parameters", "callbacks", "allreduce", "allgather", "broadcast",
            "broadcast_object", "allgather_object", "Average", "Sum", "Min", "Max", "__version__"]

@@ -35,6 +35,8 @@ from .flat_params import FlatParamStore
 logger = logging.getLogger(__name__)
 
 DEFAULT_BUCKET_MB = float(os.environ.get("HSD_BUCKET_MB", "64"))
+# wire compression of fp32 gradient buckets: name -> (CommEngine mode, torch dtype on the wire)
+COMPRESSION = {"none": (0, None), "bf16": (1, torch.bfloat16), "fp16": (2, torch.float16)}
 
 
 def overlap_from_timeline(backward_ms: float, buckets) -> dict:
@@ -51,22 +53,28 @@ def overlap_from_timeline(backward_ms: float, buckets) -> dict:
 
 
 class _Bucket:
-    __slots__ = ("index", "start", "end", "params", "ready", "handle", "launched")
+    __slots__ = ("index", "start", "end", "params", "ready", "handle", "launched", "wire")
 
     def __init__(self, index: int, start: int, end: int, params: List[int]):
         self.index, self.start, self.end, self.params = index, start, end, params
         self.ready = set()
         self.handle = None
         self.launched = False
+        self.wire = None
 
 
 class GradBucketer:
     """Static buckets over a :class:`FlatParamStore`'s gradient buffer."""
 
     def __init__(self, store: FlatParamStore, bucket_mb: Optional[float] = None, group=None,
-                 overlap: bool = True, native: Optional[bool] = None, engine=None):
+                 overlap: bool = True, native: Optional[bool] = None, engine=None, compression: str = "none"):
         """``engine``: an explicit native CommEngine (tests drive a world-of-one RCCL communicator through
-        the full HIP backward with it; overlap is then on regardless of the world size)."""
+        the full HIP backward with it; overlap is then on regardless of the world size).
+        ``compression``: ``none`` | ``bf16`` | ``fp16`` — the dtype fp32 gradient buckets travel in
+        (Horovod's ``hvd.Compression.fp16``): half the all-reduce bytes, gradients stay fp32 on either side."""
+        if compression not in COMPRESSION:
+            raise ValueError(f"compression {compression!r}: one of {sorted(COMPRESSION)}")
+        self.compression = compression
         self.store = store
         self.group = group
         self.world = engine.world if engine is not None else backend.size()
@@ -110,6 +118,8 @@ class GradBucketer:
                     param_bucket[pi] = b.index
             self.engine.set_buckets(store.grad, [b.start for b in self.buckets], [b.end for b in self.buckets],
                                     [len(b.params) for b in self.buckets], param_bucket)
+            if compression != "none" and store.grad.dtype == torch.float32:
+                self.engine.set_compression(COMPRESSION[compression][0])
         store.ready_callback = self.mark_ready
 
     # ---------------------------------------------------------------- hooks
@@ -138,7 +148,13 @@ class GradBucketer:
             from ..ops import hip as _hip
 
             _hip.join_side_streams()  # gradients of this bucket may come from the wgrad stream
-        b.handle = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        wire_dtype = COMPRESSION[self.compression][1]
+        if wire_dtype is not None and view.dtype == torch.float32:
+            b.wire = view.to(wire_dtype)
+            b.handle = dist.all_reduce(b.wire, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
+        else:
+            b.wire = None
+            b.handle = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         b.launched = True
 
     # ---------------------------------------------------------------- step API
@@ -169,6 +185,9 @@ class GradBucketer:
             if b.handle is not None:
                 b.handle.wait()
                 b.handle = None
+                if b.wire is not None:
+                    self.store.grad[b.start:b.end].copy_(b.wire)
+                    b.wire = None
 
     @contextlib.contextmanager
     def no_sync(self):

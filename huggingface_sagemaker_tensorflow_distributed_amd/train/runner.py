@@ -132,7 +132,8 @@ def build(args, mode: str):
                     "%.1f GB, capped by %s) -> train_batch_size %d", per_gpu, batch_plan.method,
                     batch_plan.per_seq_bytes / 2**20, batch_plan.fixed_bytes / 2**30, batch_plan.budget_bytes / 2**30,
                     batch_plan.total_bytes / 2**30, batch_plan.capped_by, args.train_batch_size)
-    bucketer = GradBucketer(store, bucket_mb=args.bucket_mb) if world > 1 else None
+    bucketer = (GradBucketer(store, bucket_mb=args.bucket_mb, compression=getattr(args, "grad_compression", "none"))
+                if world > 1 else None)
     trainer = Trainer(model, store, opt, bucketer, dev, grad_accum=args.gradient_accumulation_steps,
                       lr_schedule=getattr(args, "lr_schedule", "constant"),
                       lr_warmup_steps=getattr(args, "lr_warmup_steps", 0),

@@ -425,3 +425,40 @@ def test_hvd_tensor_collectives_world3():
     """Horovod tensor API on the facade (allreduce Average / Sum / Min / Max, variable-length allgather,
     broadcast from a non-zero root, object broadcast / allgather), gloo world 3."""
     mp.spawn(_worker_hvd_tensor_ops, args=(3, _port()), nprocs=3, join=True)
+
+
+def _worker_compression(rank, world, port, mode):
+    _setenv(rank, world, port)
+    import torch.distributed as dist
+
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel import GradBucketer, backend
+
+    backend.init(device="cpu")
+    model, store, opt, tr = _make(seed_init=7)
+    buck = GradBucketer(store, bucket_mb=0.05, compression=mode)
+    g = torch.Generator().manual_seed(100 + rank)
+    mine = torch.randn(store.numel, generator=g)
+    store.grad.copy_(mine)
+    buck.begin()
+    for i in range(len(store.params)):
+        buck.mark_ready(i)
+    buck.finish()
+    full = mine.clone()
+    dist.all_reduce(full)  # fp32 reference sum
+    wire = {"bf16": torch.bfloat16, "fp16": torch.float16}[mode]
+    assert store.grad.dtype == torch.float32
+    torch.testing.assert_close(store.grad, full, rtol=0, atol=world * 2.0 ** -6 * float(full.abs().max()))
+    assert not torch.equal(store.grad, full)  # the sum did travel in 16 bits
+    # every rank holds the same reduced gradient, and it is exactly representable in the wire dtype
+    ref = store.grad.clone()
+    dist.broadcast(ref, 0)
+    assert torch.equal(store.grad, ref)
+    assert torch.equal(store.grad.to(wire).float(), store.grad)
+    backend.shutdown()
+
+
+@pytest.mark.parametrize("mode", ["bf16", "fp16"])
+def test_gradient_wire_compression_world2(mode):
+    """Horovod's ``hvd.Compression.fp16`` (``--grad_compression``): fp32 gradient buckets all-reduced in 16 bits,
+    cast back to fp32, identical on every rank, within 16-bit rounding of the fp32 sum (gloo world 2)."""
+    mp.spawn(_worker_compression, args=(2, _port(), mode), nprocs=2, join=True)

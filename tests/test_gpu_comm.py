@@ -143,3 +143,25 @@ def test_optimizer_overlap_on_engine_stream(gpu, monkeypatch):
         torch.cuda.synchronize()
         assert torch.equal(p0, store.master) and torch.equal(m0, opt.exp_avg) and torch.equal(v0, opt.exp_avg_sq)
         assert torch.equal(out, store.compute)
+
+
+@pytest.mark.parametrize("mode,dtype", [(1, torch.bfloat16), (2, torch.float16)])
+def test_comm_engine_wire_compression(gpu, mode, dtype):
+    """set_compression (Horovod's hvd.Compression.fp16): each fp32 bucket is cast to 16 bits on the comm stream,
+    all-reduced, cast back. With a world of one the result is the 16-bit rounding of the gradients, bucket by
+    bucket, including the bucket finish() launches; a bad mode is refused."""
+    C = _C()
+    eng = C.CommEngine(0, 1, C.CommEngine.unique_id(), gpu.index, True)
+    flat = torch.randn(10_000, device=gpu)
+    ref = flat.to(dtype).float()
+    eng.set_buckets(flat, [0, 4000, 5000], [4000, 5000, 10_000], [2, 1, 3], [0, 0, 1, 2, 2, 2])
+    eng.set_compression(mode)
+    eng.begin_step()
+    assert eng.mark_ready(2) == 1
+    eng.mark_ready(0)
+    eng.mark_ready(1)
+    eng.finish()
+    torch.cuda.synchronize()
+    assert torch.equal(flat, ref)
+    with pytest.raises(RuntimeError):
+        eng.set_compression(3)
