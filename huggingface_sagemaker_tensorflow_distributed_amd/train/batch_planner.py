@@ -15,7 +15,8 @@ planner measures instead of guessing:
    across data-parallel ranks (minimum).
 
 Without a GPU the same formula runs on an analytic activation estimate (:func:`activation_bytes_per_seq`) against
-``fallback_budget_bytes``.
+``fallback_budget_bytes``. With ``--dtype fp8`` the probes' forward passes also record the first amax values of the
+delayed-scaling sites (a random batch of the training shape), as a warm-up step would.
 """
 from __future__ import annotations
 
