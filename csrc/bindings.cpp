@@ -230,24 +230,6 @@ void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int64_t la, int64_t
                    C2.has_value() ? BF(*C2) : nullptr, p, (uint64_t)seed, (int)splits, cur_stream());
 }
 
-void gemm_variant(torch::Tensor A, torch::Tensor B, torch::Tensor C, int64_t la, int64_t lb, int64_t variant) {
-  const int64_t M = la == 0 ? A.size(0) : A.size(1);
-  const int64_t K = la == 0 ? A.size(1) : A.size(0);
-  const int64_t N = lb == 0 ? B.size(0) : B.size(1);
-  TORCH_CHECK(C.size(0) == M && C.size(1) == N && K % 64 == 0 && M >= 256 && N >= 256, "gemm_variant shapes");
-  TORCH_CHECK(A.scalar_type() == torch::kBFloat16 && B.scalar_type() == torch::kBFloat16 &&
-              C.scalar_type() == torch::kBFloat16, "bf16");
-  hsd::launch_gemm_variant((int)la, (int)lb, (int)variant, CBF(A), A.stride(0), CBF(B), B.stride(0), (int)M, (int)N,
-                           (int)K, BF(C), C.stride(0), cur_stream());
-}
-
-void gemm_wgrad_variant(torch::Tensor dy, torch::Tensor x, torch::Tensor C, int64_t splits) {
-  TORCH_CHECK(dy.size(0) == x.size(0) && C.size(0) == dy.size(1) && C.size(1) == x.size(1), "shapes");
-  TORCH_CHECK(C.scalar_type() == torch::kFloat32 && dy.size(0) % 64 == 0, "wgrad variant");
-  hsd::launch_gemm_wgrad_variant(CBF(dy), dy.stride(0), CBF(x), x.stride(0), (int)dy.size(1), (int)x.size(1),
-                                 (int)dy.size(0), C.data_ptr<float>(), C.stride(0), (int)splits, cur_stream());
-}
-
 // gemm2: la=lb=0 -> NT (A [M,K], B [N,K]) bf16 C with epilogue 0..5;
 //        la=lb=1 -> TT (A [K,M], B [K,N]) fp32 C += A^T B, epi 6 atomics / 7 slabs in ws.
 // fp8 per-tensor quantisation: q = sat(x · FMT_MAX / amax), sinv = amax / FMT_MAX (device scalars)
@@ -465,12 +447,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("dqkv"), py::arg("dq_acc"), py::arg("B"), py::arg("S"), py::arg("heads"), py::arg("p"), py::arg("seed"),
         py::arg("dbias") = py::none());
   m.def("gemm", &gemm);
-  m.def("gemm_variant", &gemm_variant);
   m.def("gemm2", &gemm2);
   m.def("gemm2_splits", &gemm2_splits);
   m.def("gemm2_nt_splits", &gemm2_nt_splits);
   m.def("gemm2_supported", &gemm2_supported);
   m.def("transpose_many", &transpose_many);
   m.def("xent", &xent);
-  m.def("gemm_wgrad_variant", &gemm_wgrad_variant);
 }

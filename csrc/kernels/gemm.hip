@@ -457,149 +457,6 @@ static void gemm_launch(const GemmParams& p0, int splits, hipStream_t st) {
 }
 
 
-// ================================================================================================
-// v4: 1 wave per SIMD, 4 waves (2x2), 128x128-class wave tiles whose 256 accumulator registers live in
-// the AGPR half of the unified register file. LDS read bytes per MFMA are a quarter of the 8-wave
-// kernels' (the PMC run showed those feeding MFMA only ~35% of the time); DMA pieces of stage t+1 are
-// spread between the MFMA groups of stage t; one barrier per K-tile.
-template <int LA, int LB, int EPI, int BM_, int BN_>
-__global__ __launch_bounds__(256, 1) void gemm_big_kernel(GemmParams p) {
-  p.dp = resolve_seed(p.dp);
-  constexpr bool SWAP = EPI != EPI_F32_ATOMIC;
-  constexpr int NS = 2;
-  constexpr int TA = BM_ * 64, TB = BN_ * 64, STAGE = TA + TB;
-  constexpr int MB = BM_ / 2 / 32, NB = BN_ / 2 / 32;
-  constexpr int GA = BM_ / 32, GB = BN_ / 32;  // DMA pieces per wave per stage (4 waves)
-  constexpr int G = GA + GB;
-  static_assert(LA == 0 || BM_ == 128 || BM_ == 256, "k-strided tiles are 128 or 256 wide");
-  static_assert(LB == 0 || BN_ == 128 || BN_ == 256, "k-strided tiles are 128 or 256 wide");
-  __shared__ __attribute__((aligned(16))) bf16_t smem[NS * STAGE];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
-
-  const int nwg = gridDim.x;
-  const int bid = blockIdx.x;
-  const int xcd = bid & 7;
-  const int q8 = nwg >> 3, r8 = nwg & 7;
-  const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
-  const int tm = wg / p.tiles_n, tn = wg % p.tiles_n;
-  const int m0 = tm * BM_, n0 = tn * BN_;
-  const int kbeg = blockIdx.y * p.kps;
-  const int kend = min(p.K, kbeg + p.kps);
-  const int nt = (kend - kbeg) / BK;
-
-  f32x16 acc[MB][NB];
-#pragma unroll
-  for (int i = 0; i < MB; ++i)
-#pragma unroll
-    for (int j = 0; j < NB; ++j) acc[i][j] = f32x16{};
-
-#pragma unroll
-  for (int j = 0; j < G; ++j) {
-    if (j < GA) dma_piece<LA, BM_, 4>(j, smem, p.A, p.lda, m0, p.M, kbeg, wave, lane);
-    else dma_piece<LB, BN_, 4>(j - GA, smem + TA, p.B, p.ldb, n0, p.N, kbeg, wave, lane);
-  }
-  for (int t = 0; t < nt; ++t) {
-    wait_vmcnt<0>();
-    __builtin_amdgcn_s_barrier();
-    const bool issue = t + 1 < nt;
-    const bf16_t* tA = smem + (t & 1) * STAGE;
-    const bf16_t* tB = tA + TA;
-    bf16_t* nA = smem + ((t + 1) & 1) * STAGE;
-    const int kn = kbeg + (t + 1) * BK;
-#pragma unroll
-    for (int ks = 0; ks < 4; ++ks) {
-      bf16x8 fa[MB], fb[NB];
-#pragma unroll
-      for (int i = 0; i < MB; ++i) fa[i] = frag<LA, BM_>(tA, wm * (BM_ / 2) + 32 * i, ks, lane);
-#pragma unroll
-      for (int j = 0; j < NB; ++j) fb[j] = frag<LB, BN_>(tB, wn * (BN_ / 2) + 32 * j, ks, lane);
-#pragma unroll
-      for (int i = 0; i < MB; ++i) {
-        // DMA pieces of the next stage spread over the MFMA groups: piece q goes with (ks, i) slot q
-        if (issue) {
-#pragma unroll
-          for (int q = 0; q < G; ++q) {
-            if ((q * 4 * MB) / G == ks * MB + i) {
-              if (q < GA) dma_piece<LA, BM_, 4>(q, nA, p.A, p.lda, m0, p.M, kn, wave, lane);
-              else dma_piece<LB, BN_, 4>(q - GA, nA + TA, p.B, p.ldb, n0, p.N, kn, wave, lane);
-            }
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < NB; ++j) {
-          if constexpr (SWAP) acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fb[j], fa[i], acc[i][j], 0, 0, 0);
-          else acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[i], fb[j], acc[i][j], 0, 0, 0);
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int i = 0; i < MB; ++i)
-#pragma unroll
-    for (int j = 0; j < NB; ++j)
-      epi_block<EPI, SWAP>(acc[i][j], m0 + wm * (BM_ / 2) + 32 * i, n0 + wn * (BN_ / 2) + 32 * j, lane, p);
-}
-
-template <int LA, int LB, int EPI, int BM_, int BN_>
-static void gemm_big_launch(const GemmParams& p0, int splits, hipStream_t st) {
-  GemmParams p = p0;
-  p.tiles_m = (p.M + BM_ - 1) / BM_;
-  p.tiles_n = (p.N + BN_ - 1) / BN_;
-  if (splits < 1) splits = 1;
-  int kps = (p.K + splits - 1) / splits;
-  kps = (kps + BK - 1) / BK * BK;
-  splits = (p.K + kps - 1) / kps;
-  p.kps = kps;
-  dim3 grid(p.tiles_m * p.tiles_n, splits);
-  hipLaunchKernelGGL((gemm_big_kernel<LA, LB, EPI, BM_, BN_>), grid, dim3(256), 0, st, p);
-  HSD_CHECK_LAUNCH();
-}
-
-// Sweep entry (tools/bench_gemm.py): fixed EPI_STORE, config chosen by `variant`.
-void launch_gemm_variant(int la, int lb, int variant, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb,
-                         int M, int N, int K, bf16_t* C, int64_t ldc, hipStream_t st) {
-  GemmParams p{};
-  p.A = A; p.lda = lda; p.B = B; p.ldb = ldb; p.M = M; p.N = N; p.K = K; p.C = C; p.ldc = ldc;
-  p.dp = make_dropout(0.0, 0);
-  if (la == 0 && lb == 0) {
-    switch (variant) {
-      case 0: gemm_dma_launch<0, 0, EPI_STORE, 256, 192, 4, 2, 2>(p, 1, st); break;
-      case 1: gemm_dma_launch<0, 0, EPI_STORE, 256, 128, 4, 2, 3>(p, 1, st); break;
-      case 2: gemm_dma_launch<0, 0, EPI_STORE, 256, 128, 4, 2, 2>(p, 1, st); break;
-      case 3: gemm_dma_launch<0, 0, EPI_STORE, 256, 256, 2, 4, 2>(p, 1, st); break;
-      case 4: gemm_dma_launch<0, 0, EPI_STORE, 128, 256, 2, 4, 3>(p, 1, st); break;
-      case 5: gemm_big_launch<0, 0, EPI_STORE, 256, 256>(p, 1, st); break;
-      case 6: gemm_big_launch<0, 0, EPI_STORE, 256, 192>(p, 1, st); break;
-      case 7: gemm_big_launch<0, 0, EPI_STORE, 192, 256>(p, 1, st); break;
-      default: abort();
-    }
-  } else if (la == 0 && lb == 1) {
-    switch (variant) {
-      case 0: gemm_dma_launch<0, 1, EPI_STORE, 256, 128, 4, 2, 2>(p, 1, st); break;
-      case 1: gemm_dma_launch<0, 1, EPI_STORE, 256, 128, 4, 2, 3>(p, 1, st); break;
-      case 2: gemm_dma_launch<0, 1, EPI_STORE, 128, 256, 2, 4, 3>(p, 1, st); break;
-      case 3: gemm_dma_launch<0, 1, EPI_STORE, 256, 256, 2, 4, 2>(p, 1, st); break;
-      case 4: gemm_dma_launch<0, 1, EPI_STORE, 192, 256, 2, 4, 2>(p, 1, st); break;
-      case 5: gemm_big_launch<0, 1, EPI_STORE, 256, 256>(p, 1, st); break;
-      case 6: gemm_big_launch<0, 1, EPI_STORE, 192, 256>(p, 1, st); break;
-      case 7: gemm_big_launch<0, 1, EPI_STORE, 256, 128>(p, 1, st); break;
-      default: abort();
-    }
-  } else {
-    abort();
-  }
-}
-
-void launch_gemm_wgrad_variant(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, int M, int N, int K, float* C,
-                               int64_t ldc, int splits, hipStream_t st) {
-  GemmParams p{};
-  p.A = A; p.lda = lda; p.B = B; p.ldb = ldb; p.M = M; p.N = N; p.K = K; p.C = C; p.ldc = ldc;
-  p.dp = make_dropout(0.0, 0);
-  gemm_big_launch<1, 1, EPI_F32_ATOMIC, 256, 256>(p, splits, st);
-}
-
 // Public entry: layouts + epilogue chosen at run time.
 void launch_gemm(int la, int lb, int epi, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, int M, int N,
                  int K, void* C, int64_t ldc, const bf16_t* bias, const bf16_t* aux, int64_t ldaux, bf16_t* C2,

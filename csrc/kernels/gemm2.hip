@@ -58,6 +58,27 @@ __device__ __forceinline__ void dma(bf16_t* img, const bf16_t* __restrict__ X, i
                                    (__attribute__((address_space(3))) void*)(img + g * 512), 16, 0, 0);
 }
 
+// TT (both operands k-strided) DMA: inline asm, a per-lane byte offset computed once per workgroup and a scalar
+// (SGPR) base per K-tile. With the builtin, hipcc does not tell the transposing LDS reads (ds_read_b64_tr_b16) apart
+// from the LDS-DMA destination and drains EVERY DMA (s_waitcnt vmcnt(0)) before the first read of each K-tile, so
+// tile t+2's DMA had one MFMA phase to land instead of a K-tile. The asm DMA is invisible to hipcc's wait
+// bookkeeping; the kernel's counted vmcnt<N>() waits retire it.
+__device__ __forceinline__ uint32_t tt_lane_off(int64_t ld, int r0, int Rmax, int g, int lane) {
+  const int krow = g * 2 + (lane >> 5);
+  const int lc = (lane & 31) ^ f2(krow);
+  const int cc = min(r0 + lc * 8, Rmax - 8);
+  return (uint32_t)(((int64_t)krow * ld + cc) * 2);
+}
+
+__device__ __forceinline__ void dma_lds_asm(const bf16_t* sbase, uint32_t voff, uint32_t lds_addr) {
+  const uint32_t lds = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds_addr);
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(voff), "s"(sbase), "s"(lds)
+               : "memory");
+}
+
 // 16x16x32 operand fragment: lane l holds rows (rbase + (l&15)), k = 32·ks + 8·(l>>4) + 0..7
 template <int L, int W = 256>
 __device__ __forceinline__ bf16x8 frag(const bf16_t* img, int rbase, int ks, int lane) {
@@ -118,9 +139,25 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
   const int nt = (kend - kbeg) / BK;
   HSD_DASSERT(v < nwg && m0 < p.M && n0 < p.N && kbeg < p.K && (kend - kbeg) % BK == 0);
 
+  constexpr bool TT = LA == 1 && LB == 1;
+  uint32_t ttoff[TT ? G : 1];
+  if constexpr (TT) {
+#pragma unroll
+    for (int q = 0; q < G; ++q)
+      ttoff[q] = q < GA ? tt_lane_off(p.lda, m0, p.M, wave * GA + q, lane)
+                        : tt_lane_off(p.ldb, n0, p.N, wave * GB + (q - GA), lane);
+  }
+  // LDS byte address of smem (one generic -> LDS conversion; stage / slot offsets are plain integer adds)
+  const uint32_t smem_lds = (uint32_t)(size_t)(__attribute__((address_space(3))) bf16_t*)smem;
   auto dma_slot = [&](int q, bf16_t* stage, int k0) {
-    if (q < GA) dma<LA, BM>(stage, p.A, p.lda, m0, p.M, k0, wave * GA + q, lane);
-    else dma<LB, BN>(stage + TA, p.B, p.ldb, n0, p.N, k0, wave * GB + (q - GA), lane);
+    if constexpr (TT) {
+      const uint32_t st = smem_lds + (uint32_t)(stage - smem) * 2u;
+      if (q < GA) dma_lds_asm(p.A + (int64_t)k0 * p.lda, ttoff[q], st + (wave * GA + q) * 1024u);
+      else dma_lds_asm(p.B + (int64_t)k0 * p.ldb, ttoff[q], st + (TA + (wave * GB + (q - GA)) * 512) * 2u);
+    } else {
+      if (q < GA) dma<LA, BM>(stage, p.A, p.lda, m0, p.M, k0, wave * GA + q, lane);
+      else dma<LB, BN>(stage + TA, p.B, p.ldb, n0, p.N, k0, wave * GB + (q - GA), lane);
+    }
   };
 
   f32x4 acc[8][NREP];
@@ -504,427 +541,6 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
   }
 }
 
-// Persistent NT variant: each workgroup walks tiles blockIdx.x, +gridDim.x, ... as ONE sequence of K-steps
-// (stage = step & 1), so the next tile's first K-step is DMA'd during the current tile's last K-step and
-// its epilogue, and the epilogue's stores drain while the next tile's MFMAs run. The epilogue stages one
-// 16-row MFMA block at a time through a wave-private LDS slice placed AFTER the two operand stages.
-template <int EPI, int BN>
-__global__ __launch_bounds__(512, 1) void gemm2p_kernel(G2Params p, int ntiles) {
-  p.dp = resolve_seed(p.dp);
-  constexpr int WN = BN / 4, NREP = WN / 16, NB0 = 2, NB1 = NREP - NB0;
-  constexpr int TA = BM * 64, TB = BN * 64, STAGE = TA + TB;
-  constexpr int GA = 4, GB = BN / 64, G = GA + GB;
-  constexpr int SROW = WN + 8, CPR = WN / 8;
-  constexpr int ITER = (16 * CPR + 63) / 64;
-  constexpr bool kBias = epi_bias(EPI);
-  constexpr bool kAux = epi_aux(EPI);
-  constexpr bool kColsum = (EPI == E2_DGELU || EPI == E2_MUL) && CPR == 8;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * STAGE + 8 * 16 * SROW];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const int arow = wm * 128, bcol = wn * WN;
-  const int q4 = lane >> 4, lr = lane & 15;
-  const int nt = p.K / BK;
-  bf16_t* stg = smem + 2 * STAGE + wave * 16 * SROW;
-  bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
-
-  auto tile_origin = [&](int tile, int& m0, int& n0) {
-    const int xcd = tile & 7, q8 = ntiles >> 3, r8 = ntiles & 7;
-    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (tile >> 3);
-    m0 = (wg / p.tiles_n) * BM;
-    n0 = (wg % p.tiles_n) * BN;
-  };
-  auto dma_step = [&](int m0, int n0, int kt, bf16_t* stage) {
-#pragma unroll
-    for (int q = 0; q < G; ++q) {
-      if (q < GA) dma<0, BM>(stage, p.A, p.lda, m0, p.M, kt * BK, wave * GA + q, lane);
-      else dma<0, BN>(stage + TA, p.B, p.ldb, n0, p.N, kt * BK, wave * GB + (q - GA), lane);
-    }
-  };
-
-  f32x4 acc[8][NREP];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < NREP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 fa[4][2], fb0[NB0][2], fb1[NB1][2];
-
-  int tile = blockIdx.x;
-  if (tile >= ntiles) return;
-  int m0, n0;
-  tile_origin(tile, m0, n0);
-  dma_step(m0, n0, 0, smem);
-  vmcnt<0>();
-  G2_BARRIER();
-  int step = 0;
-  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-  while (true) {
-    const int next_tile = tile + gridDim.x;
-    int nm0 = 0, nn0 = 0;
-    if (next_tile < ntiles) tile_origin(next_tile, nm0, nn0);
-    for (int t = 0; t < nt; ++t, ++step) {
-      const bf16_t* cA = smem + (step & 1) * STAGE;
-      const bf16_t* cB = cA + TA;
-      bf16_t* nS = smem + ((step + 1) & 1) * STAGE;
-      if (t + 1 < nt) dma_step(m0, n0, t + 1, nS);
-      else if (next_tile < ntiles) dma_step(nm0, nn0, 0, nS);
-#pragma unroll
-      for (int j = 0; j < NB0; ++j)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) fb0[j][ks] = frag<0>(cB, bcol + 16 * j, ks, lane);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<0>(cA, arow + 16 * i, ks, lane);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < NB0; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][ks], fa[i][ks], acc[i][j], 0, 0, 0);
-#pragma unroll
-      for (int j = 0; j < NB1; ++j)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) fb1[j][ks] = frag<0>(cB, bcol + 16 * (NB0 + j), ks, lane);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < NB1; ++j)
-            acc[i][NB0 + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][ks], fa[i][ks], acc[i][NB0 + j], 0, 0, 0);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<0>(cA, arow + 64 + 16 * i, ks, lane);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-#pragma unroll
-          for (int j = 0; j < NB1; ++j)
-            acc[4 + i][NB0 + j] =
-                __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][ks], fa[i][ks], acc[4 + i][NB0 + j], 0, 0, 0);
-#pragma unroll
-          for (int j = 0; j < NB0; ++j)
-            acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][ks], fa[i][ks], acc[4 + i][j], 0, 0, 0);
-        }
-      if (t + 1 < nt) {
-        vmcnt<0>();
-        G2_BARRIER();
-      }
-    }
-    // the next tile's first K-step (DMA'd at the start of this tile's last K-step) has landed for every
-    // wave, and every wave is past its last LDS read of this tile: one barrier publishes / frees both.
-    // The epilogue's stores then stay in flight until the next K-step's vmcnt(0).
-    vmcnt<0>();
-    G2_BARRIER();
-
-    // ---------------------------------------------------------------- epilogue (16-row passes)
-    const int mw = m0 + arow, nw = n0 + bcol;
-    f32x4 bv[NREP];
-    if constexpr (kBias) {
-#pragma unroll
-      for (int j = 0; j < NREP; ++j) {
-        const int n = min(nw + 16 * j + 4 * q4, p.N - 4);
-        const u32x2 b = *reinterpret_cast<const u32x2*>(p.bias + n);
-        bv[j] = f32x4{lo_bf(b.x), hi_bf(b.x), lo_bf(b.y), hi_bf(b.y)};
-      }
-    }
-    u32x4 xv[8][ITER];
-    if constexpr (kAux) {
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int it = 0; it < ITER; ++it) {
-          const int idx = min(lane + 64 * it, 16 * CPR - 1);
-          const int row = idx / CPR, c8 = idx % CPR;
-          const int m = min(mw + 16 * i + row, p.M - 1);
-          xv[i][it] = *reinterpret_cast<const u32x4*>(p.aux + (int64_t)m * p.ldaux + nw + c8 * 8);
-        }
-    }
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-#pragma unroll
-      for (int j = 0; j < NREP; ++j) {
-        f32x4 v = acc[i][j];
-        if constexpr (kBias) v += bv[j];
-        *reinterpret_cast<u32x2*>(stg + lr * SROW + 16 * j + 4 * q4) = pack4(v);
-        acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-      }
-      __builtin_amdgcn_wave_barrier();
-#pragma unroll
-      for (int it = 0; it < ITER; ++it) {
-        const int idx = lane + 64 * it;
-        if (idx >= 16 * CPR) continue;
-        const int row = idx / CPR, c8 = idx % CPR;
-        const int m = mw + 16 * i + row;
-        const int n = nw + c8 * 8;
-        u32x4 o = *reinterpret_cast<const u32x4*>(stg + row * SROW + c8 * 8);
-        if (m >= p.M) continue;
-        const int64_t co = (int64_t)m * p.ldc + n;
-        u32x4 o2;
-        u32x4 x = u32x4{0, 0, 0, 0};
-        if constexpr (kAux) x = xv[i][it];
-        epi_chunk<EPI>(o, o2, x, m, n, p, csum);
-        st16(C + co, o, p.nt_store);
-        if constexpr (epi_two_out(EPI)) st16(p.C2 + co, o2, p.nt_store);
-      }
-      __builtin_amdgcn_wave_barrier();
-    }
-    if constexpr (kColsum) {
-      if (p.dbias != nullptr) colsum_flush(csum, p.dbias, nw, p.N, lane);
-#pragma unroll
-      for (int e = 0; e < 8; ++e) csum[e] = 0.f;  // per-tile column sums (flush adds the whole vector)
-    }
-    if (next_tile >= ntiles) break;
-    tile = next_tile;
-    m0 = nm0;
-    n0 = nn0;
-  }
-}
-
-// Persistent NT kernel on the staggered 4-phase main loop (SYNC 4) -- gemm2p's tile walk with gemm2's fastest
-// schedule. A workgroup walks tiles blockIdx.x, +gridDim.x, ... as ONE sequence of K-steps s = 0 .. tiles x nt - 1,
-// so the DMA of the next tile's first K-steps is issued during the current tile's last K-steps (no pipeline
-// refill, no workgroup relaunch between tiles). At a tile's last K-step the two wave groups meet (the leading
-// group wm = 0 takes one extra barrier), both run the epilogue through a wave-private 16-row LDS slice placed
-// AFTER the two operand stages (which already hold the next tile's first K-steps), and wm = 1 takes one extra
-// barrier to re-open the one-barrier stagger. HSD_G2_PERSIST=1 selects it.
-template <int EPI, int BN>
-__global__ __launch_bounds__(512, 1) void gemm2p4_kernel(G2Params p, int ntiles) {
-  p.dp = resolve_seed(p.dp);
-  constexpr int WN = BN / 4, NREP = WN / 16, NB0 = 2, NB1 = NREP - NB0;
-  constexpr int TA = BM * 64, TB = BN * 64, STAGE = TA + TB;
-  constexpr int GA = 4, GB = BN / 64, G = GA + GB;
-  constexpr int D0 = 2;
-  constexpr int E1 = D0 + (G - D0 + 1) / 2;
-  constexpr int SROW = WN + 8, CPR = WN / 8;
-  constexpr int ITER = (16 * CPR + 63) / 64;
-  constexpr bool kBias = epi_bias(EPI);
-  constexpr bool kAux = epi_aux(EPI);
-  constexpr bool kColsum = (EPI == E2_DGELU || EPI == E2_MUL) && CPR == 8;
-  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * STAGE + 8 * 16 * SROW];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const int arow = wm * 128, bcol = wn * WN;
-  const int q4 = lane >> 4, lr = lane & 15;
-  const int nt = p.K / BK;
-  if ((int)blockIdx.x >= ntiles) return;
-  const int my_tiles = (ntiles - (int)blockIdx.x + (int)gridDim.x - 1) / (int)gridDim.x;
-  const int nsteps = my_tiles * nt;
-  bf16_t* stg = smem + 2 * STAGE + wave * 16 * SROW;
-  bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
-
-  // K-step s -> (m0, n0, k0) of its tile (same XCD-aware tile order as gemm2p)
-  auto origin = [&](int s, int& m0, int& n0, int& k0) {
-    const int ti = s / nt;
-    const int tile = (int)blockIdx.x + ti * (int)gridDim.x;
-    const int xcd = tile & 7, q8 = ntiles >> 3, r8 = ntiles & 7;
-    const int wg = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (tile >> 3);
-    m0 = (wg / p.tiles_n) * BM;
-    n0 = (wg % p.tiles_n) * BN;
-    k0 = (s - ti * nt) * BK;
-  };
-  // Per-lane source offsets of each DMA slot are loop-invariant for every tile that lies inside the matrix
-  // (row = slot row + lane row, 16-B chunk swizzled by row); only a tile crossing the M / N edge clamps rows, on a
-  // slow path. The fast path is uniform base (SGPR) + invariant lane offset + k0, no per-step multiplies.
-  int offA[GA], offB[GB];
-#pragma unroll
-  for (int q = 0; q < GA; ++q) {
-    const int row = (wave * GA + q) * 8 + (lane >> 3);
-    offA[q] = row * p.lda + ((lane & 7) ^ f1(row)) * 8;
-  }
-#pragma unroll
-  for (int q = 0; q < GB; ++q) {
-    const int row = (wave * GB + q) * 8 + (lane >> 3);
-    offB[q] = row * p.ldb + ((lane & 7) ^ f1(row)) * 8;
-  }
-  auto dma_slot = [&](int q, bf16_t* stage, int m0, int n0, int k0) {
-    if (q < GA) {
-      if (m0 + BM <= p.M) {
-        const bf16_t* src = p.A + (int64_t)m0 * p.lda + k0 + offA[q];
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                         (__attribute__((address_space(3))) void*)(stage + (wave * GA + q) * 512),
-                                         16, 0, 0);
-      } else {
-        dma<0, BM>(stage, p.A, p.lda, m0, p.M, k0, wave * GA + q, lane);
-      }
-    } else {
-      if (n0 + BN <= p.N) {
-        const bf16_t* src = p.B + (int64_t)n0 * p.ldb + k0 + offB[q - GA];
-        __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)src,
-                                         (__attribute__((address_space(3))) void*)(stage + TA + (wave * GB + q - GA) * 512),
-                                         16, 0, 0);
-      } else {
-        dma<0, BN>(stage + TA, p.B, p.ldb, n0, p.N, k0, wave * GB + (q - GA), lane);
-      }
-    }
-  };
-
-  f32x4 acc[8][NREP];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < NREP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 fa[4][2], fb0[NB0][2], fb1[NB1][2];
-  float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
-
-  int cm0, cn0, ck0;  // the current K-step's tile
-  origin(0, cm0, cn0, ck0);
-  {
-#pragma unroll
-    for (int q = 0; q < G; ++q) dma_slot(q, smem, cm0, cn0, ck0);
-    if (nsteps > 1) {
-      int m1, n1, k1;
-      origin(1, m1, n1, k1);
-#pragma unroll
-      for (int q = 0; q < D0; ++q) dma_slot(q, smem + STAGE, m1, n1, k1);
-      vmcnt<D0>();
-    } else {
-      vmcnt<0>();
-    }
-  }
-  G2_BARRIER();
-  if (wm == 1) G2_BARRIER();
-#define G2P_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
-#define G2P_CLUSTER(ACC_I0, FA, FB, NBX, J0)                                                                 \
-  __builtin_amdgcn_s_setprio(1);                                                                             \
-  _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) _Pragma("unroll") for (int i = 0; i < 4; ++i)               \
-      _Pragma("unroll") for (int j = 0; j < NBX; ++j) acc[ACC_I0 + i][J0 + j] =                                \
-          __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[j][ks], FA[i][ks], acc[ACC_I0 + i][J0 + j], 0, 0, 0);     \
-  __builtin_amdgcn_s_setprio(0);
-  for (int s = 0; s < nsteps; ++s) {
-    const bf16_t* cA = smem + (s & 1) * STAGE;
-    const bf16_t* cB = cA + TA;
-    bf16_t* nS = smem + ((s + 1) & 1) * STAGE;
-    const bool n1 = s + 1 < nsteps, n2 = s + 2 < nsteps;
-    int m1 = cm0, nn1 = cn0, k1 = ck0 + BK, m2 = cm0, nn2 = cn0, k2 = ck0 + 2 * BK;
-    if (k1 >= p.K && n1) origin(s + 1, m1, nn1, k1);
-    if (k2 >= p.K && n2) origin(s + 2, m2, nn2, k2);
-    // P1: A-sub0 + B-sub0 reads, first half of step s+1's DMA
-#pragma unroll
-    for (int j = 0; j < NB0; ++j)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) fb0[j][ks] = frag<0>(cB, bcol + 16 * j, ks, lane);
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<0>(cA, arow + 16 * i, ks, lane);
-    if (n1) {
-#pragma unroll
-      for (int q = D0; q < E1; ++q) dma_slot(q, nS, m1, nn1, k1);
-    }
-    G2P_LGKM0();
-    G2_BARRIER();
-    G2P_CLUSTER(0, fa, fb0, NB0, 0)
-    G2_BARRIER();
-    // P2: B-sub1 reads, rest of step s+1's DMA
-#pragma unroll
-    for (int j = 0; j < NB1; ++j)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) fb1[j][ks] = frag<0>(cB, bcol + 16 * (NB0 + j), ks, lane);
-    if (n1) {
-#pragma unroll
-      for (int q = E1; q < G; ++q) dma_slot(q, nS, m1, nn1, k1);
-    }
-    G2P_LGKM0();
-    G2_BARRIER();
-    G2P_CLUSTER(0, fa, fb1, NB1, NB0)
-    G2_BARRIER();
-    // P3: A-sub1 reads
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<0>(cA, arow + 64 + 16 * i, ks, lane);
-    G2P_LGKM0();
-    G2_BARRIER();
-    G2P_CLUSTER(4, fa, fb1, NB1, NB0)
-    G2_BARRIER();
-    // P4: no reads; D0 slots of step s+2 into this stage; retire step s+1
-    if (n2) {
-#pragma unroll
-      for (int q = 0; q < D0; ++q) dma_slot(q, const_cast<bf16_t*>(cA), m2, nn2, k2);
-      vmcnt<D0>();
-    } else {
-      vmcnt<0>();
-    }
-    G2_BARRIER();
-    G2P_CLUSTER(4, fa, fb0, NB0, 0)
-    G2_BARRIER();
-
-    if (ck0 + BK == p.K) {
-      // ---------------------------------------------------------------- tile epilogue (16-row passes)
-      if (wm == 0) G2_BARRIER();  // meet the lagging group: every MFMA of this tile is done
-      const int mw = cm0 + arow, nw = cn0 + bcol;
-      f32x4 bv[NREP];
-      if constexpr (kBias) {
-#pragma unroll
-        for (int j = 0; j < NREP; ++j) {
-          const int n = min(nw + 16 * j + 4 * q4, p.N - 4);
-          const u32x2 b = *reinterpret_cast<const u32x2*>(p.bias + n);
-          bv[j] = f32x4{lo_bf(b.x), hi_bf(b.x), lo_bf(b.y), hi_bf(b.y)};
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        u32x4 xv[ITER];
-        if constexpr (kAux) {
-#pragma unroll
-          for (int it = 0; it < ITER; ++it) {
-            const int idx = min(lane + 64 * it, 16 * CPR - 1);
-            const int row = idx / CPR, c8 = idx % CPR;
-            const int m = min(mw + 16 * i + row, p.M - 1);
-            xv[it] = *reinterpret_cast<const u32x4*>(p.aux + (int64_t)m * p.ldaux + nw + c8 * 8);
-          }
-        }
-#pragma unroll
-        for (int j = 0; j < NREP; ++j) {
-          f32x4 v = acc[i][j];
-          if constexpr (kBias) v += bv[j];
-          *reinterpret_cast<u32x2*>(stg + lr * SROW + 16 * j + 4 * q4) = pack4(v);
-          acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-        __builtin_amdgcn_wave_barrier();
-#pragma unroll
-        for (int it = 0; it < ITER; ++it) {
-          const int idx = lane + 64 * it;
-          if (idx >= 16 * CPR) continue;
-          const int row = idx / CPR, c8 = idx % CPR;
-          const int m = mw + 16 * i + row;
-          const int n = nw + c8 * 8;
-          u32x4 o = *reinterpret_cast<const u32x4*>(stg + row * SROW + c8 * 8);
-          if (m >= p.M) continue;
-          const int64_t co = (int64_t)m * p.ldc + n;
-          u32x4 o2;
-          u32x4 x = u32x4{0, 0, 0, 0};
-          if constexpr (kAux) x = xv[it];
-          epi_chunk<EPI>(o, o2, x, m, n, p, csum);
-          st16(C + co, o, p.nt_store);
-          if constexpr (epi_two_out(EPI)) st16(p.C2 + co, o2, p.nt_store);
-        }
-        __builtin_amdgcn_wave_barrier();
-      }
-      if constexpr (kColsum) {
-        if (p.dbias != nullptr) colsum_flush(csum, p.dbias, nw, p.N, lane);
-#pragma unroll
-        for (int e = 0; e < 8; ++e) csum[e] = 0.f;
-      }
-      if (wm == 1 && n1) G2_BARRIER();  // re-open the one-barrier stagger for the next tile
-    }
-    if (n1) {
-      cm0 = m1;
-      cn0 = nn1;
-      ck0 = k1;
-    }
-  }
-#undef G2P_CLUSTER
-#undef G2P_LGKM0
-}
-
 // main_grad[i] += Σ_s ws[s][i]   (float4 lanes, grid-stride)
 __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ ws, float* __restrict__ C,
                                                           int64_t ldc, int M, int N, int splits) {
@@ -1149,42 +765,8 @@ static int g2_sync_mode(int la, int K) {
   return la == 0 ? 4 : 7;
 }
 
-// Persistent SYNC-4 NT kernel (gemm2p4) for bf16-output GEMMs: HSD_G2_PERSIST=1 on, =0 off (A/B switch).
-static bool g2_persist(const G2Params& p) {
-  const char* v = getenv("HSD_G2_PERSIST");
-  (void)p;
-  return v != nullptr && atoi(v) != 0;
-}
-
-template <int EPI, int BN>
-static void g2p_launch(const G2Params& p0, hipStream_t st, bool sync4 = false) {
-  G2Params p = p0;
-  const int tiles_m = (p.M + g2::BM - 1) / g2::BM;
-  p.tiles_n = (p.N + BN - 1) / BN;
-  p.kps = p.K;
-  const int ntiles = tiles_m * p.tiles_n;
-  p.ntiles = ntiles;
-  static int cus = [] {
-    int dev = 0, n = 0;
-    hipGetDevice(&dev);
-    hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-    return n > 0 ? n : 256;
-  }();
-  const int grid = ntiles < cus ? ntiles : cus;
-  if (sync4) hipLaunchKernelGGL((g2::gemm2p4_kernel<EPI, BN>), dim3(grid), dim3(512), 0, st, p, ntiles);
-  else hipLaunchKernelGGL((g2::gemm2p_kernel<EPI, BN>), dim3(grid), dim3(512), 0, st, p, ntiles);
-  HSD_CHECK_LAUNCH();
-}
-
 template <int LA, int LB, int EPI, int BN>
 static void g2_launch(const G2Params& p0, int splits, hipStream_t st) {
-  if constexpr (LA == 0 && LB == 0 && epi_bf16_out(EPI)) {
-    const bool p4 = g2_persist(p0);
-    if (p4 || g2_sync_mode(LA, p0.K) == 3) {
-      g2p_launch<EPI, BN>(p0, st, p4);
-      return;
-    }
-  }
   G2Params p = p0;
   const int tiles_m = (p.M + g2::BM - 1) / g2::BM;
   p.tiles_n = (p.N + BN - 1) / BN;
@@ -1329,38 +911,14 @@ bool gemm2_supported(int la, int lb, int epi, int M, int N, int K) {
   return false;
 }
 
-// gemm3.hip: the two-workgroups-per-CU 256 x 128 body. HSD_GEMM3 selects it per layout: bit 0 = NT (forward /
-// dgrad, bf16 epilogues), bit 1 = TT (weight gradients); shapes it does not tile stay on gemm2.
-bool gemm3_supported(int la, int lb, int epi, int M, int N, int K);
-int gemm3_wgrad_splits(int M, int N, int K);
-void launch_gemm3(int la, int lb, int epi, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, int M, int N,
-                  int K, void* C, int64_t ldc, const bf16_t* bias, const bf16_t* aux, int64_t ldaux, bf16_t* C2,
-                  double p_drop, uint64_t seed, int splits, float* ws, float* dbias, hipStream_t st);
-
-static int gemm3_mask() {
-  const char* e = getenv("HSD_GEMM3");
-  return e ? atoi(e) : 0;
-}
-
-static bool use_gemm3(int la, int lb, int epi, int M, int N, int K) {
-  const int bit = la == 0 ? 1 : 2;
-  return (gemm3_mask() & bit) && gemm3_supported(la, lb, epi, M, N, K);
-}
-
 // K-splits of the TT wgrad (wgrad_plan)
 int gemm2_wgrad_splits(int M, int N, int K) {
-  if (use_gemm3(1, 1, E2_F32_SLAB, M, N, K)) return gemm3_wgrad_splits(M, N, K);
   return wgrad_plan(M, N, K).splits;
 }
 
 void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, int M, int N,
                   int K, void* C, int64_t ldc, const bf16_t* bias, const bf16_t* aux, int64_t ldaux, bf16_t* C2,
                   double p_drop, uint64_t seed, int splits, float* ws, float* dbias, hipStream_t st) {
-  if (use_gemm3(la, lb, epi, M, N, K)) {
-    launch_gemm3(la, lb, epi, A, lda, B, ldb, M, N, K, C, ldc, bias, aux, ldaux, C2, p_drop, seed, splits, ws, dbias,
-                 st);
-    return;
-  }
   G2Params p{};
   p.dbias = dbias;
   {

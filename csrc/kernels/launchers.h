@@ -57,8 +57,6 @@ namespace hsd {
 void launch_gemm(int la, int lb, int epi, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, int M, int N,
                  int K, void* C, int64_t ldc, const bf16_t* bias, const bf16_t* aux, int64_t ldaux, bf16_t* C2,
                  double p_drop, uint64_t seed, int splits, hipStream_t st);
-void launch_gemm_variant(int la, int lb, int variant, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb,
-                         int M, int N, int K, bf16_t* C, int64_t ldc, hipStream_t st);
 // gemm2.hip — 256-row-tile 8-phase MFMA GEMM: (0,0) NT bf16 out with epilogues 0..5; (1,1) TT fp32 out
 // (epi 6 = atomics, 7 = split-K slabs in `ws` [splits][M][N] + reduce into C)
 // device step seed for dropout (common.h g_dropout_dev_seed); nullptr = off
@@ -81,6 +79,4 @@ void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const b
 bool gemm2_supported(int la, int lb, int epi, int M, int N, int K);
 int gemm2_wgrad_splits(int M, int N, int K);
 int gemm2_nt_splits(int M, int N, int K);
-void launch_gemm_wgrad_variant(const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, int M, int N, int K, float* C,
-                               int64_t ldc, int splits, hipStream_t st);
 }  // namespace hsd

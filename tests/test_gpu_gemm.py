@@ -101,29 +101,6 @@ def test_gemm_dgrad_epilogues(gpu):
     _check(C, ref.bfloat16().float() * x.grad, 3e-2)
 
 
-@pytest.mark.parametrize("variant", range(8))
-@pytest.mark.parametrize("la,lb", [(0, 0), (0, 1)])
-def test_gemm_variants(gpu, variant, la, lb):
-    torch.manual_seed(6)
-    M, N, K = 640, 768, 512
-    A = _mk((M, K), gpu)
-    B = _mk((N, K) if lb == 0 else (K, N), gpu)
-    C = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
-    _C().gemm_variant(A, B, C, la, lb, variant)
-    _check(C, _ref(A, B, la, lb))
-
-
-@pytest.mark.parametrize("splits", [1, 4])
-def test_gemm_wgrad_big(gpu, splits):
-    torch.manual_seed(7)
-    T, N, K = 1024, 768, 320
-    dy, x = _mk((T, N), gpu), _mk((T, K), gpu)
-    C0 = torch.randn(N, K, device=gpu)
-    C = C0.clone()
-    _C().gemm_wgrad_variant(dy, x, C, splits)
-    _check(C, C0 + dy.float().t() @ x.float(), 1e-3)
-
-
 # ---------------------------------------------------------------- gemm2 (8-phase 256-row tiles)
 G2_SHAPES = [(256, 768, 768), (300, 768, 128), (1000, 960, 192), (512, 2304, 256), (768, 3072, 512)]
 
@@ -319,33 +296,3 @@ def test_gemm2_small_tt_wgrad(gpu, monkeypatch, M, N, K, splits, stages):
     _check(C, C0 + A.float().t() @ B.float(), 1e-3)
 
 
-@pytest.mark.parametrize("M,N,K", [(3000, 768, 768), (8192, 3072, 768), (6000, 768, 3072), (1024, 2304, 768)])
-@pytest.mark.parametrize("epi", [0, 1, 2, 3, 4, 5, 8, 9])
-def test_gemm2_persistent_sync4_matches_gemm2(gpu, monkeypatch, M, N, K, epi):
-    """gemm2p4 (persistent tile walk on the staggered 4-phase main loop, HSD_G2_PERSIST=1) == gemm2 bit for bit
-    on every bf16 epilogue (same K order per element, same dropout sites; partial last row tile included);
-    fused bias-gradient column sums (reset per tile) to fp32 rounding."""
-    torch.manual_seed(5 + epi)
-    C_ = _C()
-    A, B = _mk((M, K), gpu), _mk((N, K), gpu, 0.05)
-    bias = _mk((N,), gpu)
-    aux = _mk((M, N), gpu) if epi != 9 else torch.rand(M, N, device=gpu).bfloat16()
-    two = epi in (2, 8)
-    outs = []
-    monkeypatch.setenv("HSD_G2_SPLITK", "1")
-    monkeypatch.setenv("HSD_G2_SMALL", "0")
-    for persist in ("0", "1"):
-        monkeypatch.setenv("HSD_G2_PERSIST", persist)
-        C = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
-        C2 = torch.empty_like(C) if two else None
-        db = torch.zeros(N, device=gpu) if epi in (5, 9) and N % 256 == 0 else None
-        C_.gemm2(A, B, C, 0, 0, epi, bias if epi in (1, 2, 3, 8) else None, aux if epi in (3, 4, 5, 9) else None,
-                 C2, 0.1 if epi == 3 else 0.0, 77, 0, None, db)
-        torch.cuda.synchronize()
-        outs.append((C, C2, db))
-    (c0, c20, d0), (c1, c21, d1) = outs
-    assert torch.equal(c0, c1)
-    if two:
-        assert torch.equal(c20, c21)
-    if d0 is not None:
-        torch.testing.assert_close(d1, d0, rtol=1e-4, atol=1e-4 * float(d0.abs().max()) + 1e-6)
