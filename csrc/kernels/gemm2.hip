@@ -753,16 +753,17 @@ __global__ __launch_bounds__(256, NSTG <= 2 ? 2 : 1) void gemm2s_kernel(G2Params
 
 }  // namespace g2
 
-// Main-loop schedule (tools/gemm_probe.py, interleaved rounds in one process, random operands, T = 131072
-// tokens; profiles/gemm_probe_r1_sync.json): NT (forward / dgrad) runs best with the staggered 4-phase
-// form (SYNC 4: +5-10 % over one-barrier-per-K-tile SYNC 1 on every BERT shape, +15 % at 8192^3); the TT
-// wgrad with the unstaggered 8-phase form (SYNC 0; the stagger is neutral there). The persistent NT kernel
-// (3) and the pipelined-read form (2) measured within noise / slower. HSD_G2_SYNC overrides for A/B runs;
-// HSD_G2_NT=1 makes the epilogue stores non-temporal (measured neutral).
+// Main-loop schedule (interleaved rounds in one process, random operands, T = 131072 tokens): the staggered 4-phase
+// form (SYNC 4) is the fastest on both layouts. NT (forward / dgrad): +5-10 % over one-barrier-per-K-tile SYNC 1 on
+// every BERT shape (tools/gemm_probe.py, profiles/gemm_probe_r1_sync.json). TT (weight gradients), once its LDS-DMA
+// stopped draining every K-tile (dma_lds_asm): 1,018-1,134 TFLOP/s vs 920-1,065 for SYNC 7 and 979-1,074 for SYNC 0
+// on the four bert-base weights (tools/tt_probe.py, profiles/tt_probe_r3_sync_splits.json). HSD_G2_SYNC overrides
+// for A/B runs; HSD_G2_NT=1 makes the epilogue stores non-temporal (measured neutral).
 static int g2_sync_mode(int la, int K) {
   const char* e = getenv("HSD_G2_SYNC");
   if (e) return atoi(e);
-  return la == 0 ? 4 : 7;
+  (void)la;
+  return 4;
 }
 
 template <int LA, int LB, int EPI, int BN>

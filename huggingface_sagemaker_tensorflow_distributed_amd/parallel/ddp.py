@@ -96,6 +96,7 @@ class GradBucketer:
                 self._param_bucket[pi] = b
         self.sync_enabled = True
         self._on_reduced = None
+        self.last_launched: Optional[int] = None  # index of the last bucket whose all-reduce was issued (watchdog)
         self.engine = engine
         if engine is None and (native is None or native) and group is None:
             from .comm import get_engine
@@ -131,8 +132,10 @@ class GradBucketer:
         if self.engine is not None:
             if self.overlap:
                 idx = self.engine.mark_ready(i)
-                if idx >= 0 and self._on_reduced is not None:
-                    self._on_reduced(idx)
+                if idx >= 0:
+                    self.last_launched = idx
+                    if self._on_reduced is not None:
+                        self._on_reduced(idx)
             return
         b = self._param_bucket[i]
         if b.launched:
@@ -156,9 +159,11 @@ class GradBucketer:
             b.wire = None
             b.handle = dist.all_reduce(view, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         b.launched = True
+        self.last_launched = b.index
 
     # ---------------------------------------------------------------- step API
     def begin(self) -> None:
+        self.last_launched = None
         if self.engine is not None:
             self.engine.begin_step()
             return

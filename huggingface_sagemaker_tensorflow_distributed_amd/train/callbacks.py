@@ -12,6 +12,7 @@ import json
 import logging
 import os
 import random
+import time
 
 import numpy as np
 import torch
@@ -101,14 +102,29 @@ class ModelCheckpoint(Callback):
 
 
 class FaultInjection(Callback):
-    """Test hook: ``HSD_FAULT_RANK`` / ``HSD_FAULT_STEP`` crash one rank mid-training."""
+    """Test hook (SURVEY.md §5): ``HSD_FAULT_RANK`` / ``HSD_FAULT_STEP`` crash one rank mid-training;
+    with ``HSD_FAULT_HANG=1`` that rank hangs inside its next step instead (a stand-in for a stuck kernel or
+    collective), which only the step watchdog (``--step_watchdog``) can turn into a failed job."""
 
     def __init__(self):
         self.rank = int(os.environ.get("HSD_FAULT_RANK", "-1"))
         self.step = int(os.environ.get("HSD_FAULT_STEP", "-1"))
+        self.hang = os.environ.get("HSD_FAULT_HANG", "0") == "1"
+
+    def on_train_begin(self, trainer):
+        if self.hang and backend.rank() == self.rank and self.step >= 0:
+            inner = trainer._forward_loss
+
+            def hanging_forward(batch):
+                if trainer.global_step >= self.step:
+                    while True:  # never returns: the watchdog ends the process
+                        time.sleep(3600)
+                return inner(batch)
+
+            trainer._forward_loss = hanging_forward
 
     def on_batch_end(self, trainer, step):
-        if backend.rank() == self.rank and trainer.global_step >= self.step >= 0:
+        if not self.hang and backend.rank() == self.rank and trainer.global_step >= self.step >= 0:
             raise SystemExit(f"injected fault on rank {self.rank} at step {trainer.global_step}")
 
 

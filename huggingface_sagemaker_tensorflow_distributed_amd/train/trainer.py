@@ -92,6 +92,8 @@ class Trainer:
         self.check_sync = int(check_sync)
         self.log_every = int(log_every)
         self.step_watchdog = float(step_watchdog)
+        self._watchdog = None
+        self._phase = "idle"
         self.global_step = 0
         self.world = backend.size()
         self.rank = backend.rank()
@@ -208,12 +210,15 @@ class Trainer:
                 continue
             ctx = self.bucketer.no_sync() if (self.bucketer is not None and not last) else contextlib.nullcontext()
             with ctx:
+                self._phase = "forward"
                 with prange("forward"):
                     loss, logits = self._forward_loss(mb)
+                self._phase = "backward+allreduce"
                 with prange("backward+allreduce"):
                     loss.backward()
             if meter is not None:
                 meter.update(loss, logits, mb["labels"])
+        self._phase = "allreduce-wait"
         with prange("allreduce-wait"):
             if self.device.type == "cuda":
                 ops.join_side_streams()
@@ -221,13 +226,36 @@ class Trainer:
                 self.bucketer.finish()
             if ov is not None and ov != "engine":
                 ov.join()
+        self._phase = "optimizer"
         with prange("optimizer"):
             self.optimizer.step(grad_scale=1.0 / (self.world * k))
+        self._phase = "idle"
         self.global_step += 1
         if self.check_sync and self.global_step % self.check_sync == 0:
             if not params_in_sync(self.store):
                 raise RuntimeError(f"ranks diverged at step {self.global_step} (--check_sync)")
         return loss
+
+    # -------------------------------------------------------------------------- stall watchdog
+    def _watchdog_context(self) -> str:
+        last = None
+        if self.bucketer is not None:
+            last = getattr(self.bucketer, "last_launched", None)
+        return (f"phase {self._phase}; last launched gradient bucket {last if last is not None else '-'}"
+                + (f" of {len(self.bucketer.buckets)}" if self.bucketer is not None else ""))
+
+    def start_watchdog(self) -> None:
+        """--step_watchdog S: a monitor thread ends the process if no step completes (on the device) for S
+        seconds (train/watchdog.py); the launcher then tears the group down."""
+        if self.step_watchdog > 0 and self._watchdog is None:
+            from .watchdog import StepWatchdog
+
+            self._watchdog = StepWatchdog(self.step_watchdog, rank=self.rank, describe=self._watchdog_context).start()
+
+    def stop_watchdog(self) -> None:
+        if self._watchdog is not None:
+            self._watchdog.stop()
+            self._watchdog = None
 
     # -------------------------------------------------------------------------- fit
     def fit(self, loader, epochs: int, callbacks: Iterable = (), verbose: bool = True,
@@ -242,6 +270,17 @@ class Trainer:
         self.total_steps = self.global_step + per_epoch * max(0, epochs - int(initial_epoch))
         for cb in callbacks:
             cb.on_train_begin(self)
+        self.start_watchdog()
+        try:
+            self._fit_epochs(loader, epochs, callbacks, verbose, max_steps, initial_epoch, hist)
+        finally:
+            self.stop_watchdog()
+        for cb in callbacks:
+            cb.on_train_end(self)
+        return hist
+
+    def _fit_epochs(self, loader, epochs, callbacks, verbose, max_steps, initial_epoch, hist) -> None:
+        wd = self._watchdog
         for epoch in range(int(initial_epoch), epochs):
             if hasattr(loader, "sampler"):
                 loader.sampler.set_epoch(epoch)
@@ -253,10 +292,11 @@ class Trainer:
             it = iter(loader)
             for step in range(nsteps):
                 mbs = [next(it) for _ in range(self.grad_accum)]
-                ts = time.time()
+                if wd is not None:
+                    wd.step_begin(self.global_step)
                 self.train_step(mbs, meter)
-                if self.step_watchdog and time.time() - ts > self.step_watchdog:
-                    raise RuntimeError(f"step {self.global_step} exceeded watchdog {self.step_watchdog}s")
+                if wd is not None:
+                    wd.step_end(self.global_step - 1, self.device)
                 if verbose and self.rank == 0 and self.log_every and (step + 1) % self.log_every == 0:
                     r = meter.result(global_=False)
                     logger.info("epoch %d step %d/%d - loss: %.4f - sparse_categorical_accuracy: %.4f - %.1f ms/step",
@@ -273,9 +313,6 @@ class Trainer:
                             time.time() - t0, logs["loss"], logs["sparse_categorical_accuracy"])
             for cb in callbacks:
                 cb.on_epoch_end(self, epoch, logs)
-        for cb in callbacks:
-            cb.on_train_end(self)
-        return hist
 
     # -------------------------------------------------------------------------- evaluate
     @torch.no_grad()

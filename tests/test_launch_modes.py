@@ -5,6 +5,8 @@
 * the ``HuggingFace`` estimator look-alike with an ``smdistributed`` distribution spawns one rank per process slot and
   writes the reference artifacts (reference ``launch.py:20,36-55``);
 * an injected fault on one rank (``HSD_FAULT_RANK`` / ``HSD_FAULT_STEP``) fails the whole job with a non-zero code;
+* an injected HANG on one rank (``HSD_FAULT_HANG=1``) is turned into a failed job by ``--step_watchdog`` within its
+  timeout (the stalled rank, and the rank blocked in the all-reduce behind it, exit non-zero; the launcher tears down);
 * ``--check_sync`` detects ranks whose parameters diverged.
 """
 import io
@@ -73,6 +75,26 @@ def test_injected_fault_fails_the_job(tmp_path):
                 model_dir=str(tmp_path / "model"), env_extra={"HSD_FAULT_RANK": "1", "HSD_FAULT_STEP": "1"},
                 stdout=buf, kill_grace_s=5)
     assert rc != 0, buf.getvalue()[-3000:]
+    assert not (tmp_path / "model" / "model.safetensors").exists()
+
+
+def test_injected_hang_is_caught_by_step_watchdog(tmp_path):
+    import time
+
+    from huggingface_sagemaker_tensorflow_distributed_amd.launcher.spawn import launch
+
+    buf = io.StringIO()
+    t0 = time.time()
+    rc = launch([sys.executable, os.path.join(ROOT, "scripts", "train.py"), "--train_batch_size", "8",
+                 "--eval_batch_size", "8", "--step_watchdog", "4"] + TINY, 2, output_data_dir=str(tmp_path / "data"),
+                model_dir=str(tmp_path / "model"),
+                env_extra={"HSD_FAULT_RANK": "1", "HSD_FAULT_STEP": "2", "HSD_FAULT_HANG": "1"},
+                stdout=buf, kill_grace_s=5)
+    elapsed = time.time() - t0
+    log = buf.getvalue()
+    assert rc != 0, log[-3000:]
+    assert "step watchdog: rank" in log, log[-3000:]
+    assert elapsed < 120, elapsed
     assert not (tmp_path / "model" / "model.safetensors").exists()
 
 
