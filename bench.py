@@ -19,7 +19,8 @@ import torch
 sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 from huggingface_sagemaker_tensorflow_distributed_amd import data as hdata  # noqa: E402
-from huggingface_sagemaker_tensorflow_distributed_amd.parallel import backend  # noqa: E402
+from huggingface_sagemaker_tensorflow_distributed_amd.parallel import backend, rccl_env  # noqa: E402
+from huggingface_sagemaker_tensorflow_distributed_amd.parallel.collectives import params_in_sync  # noqa: E402
 from huggingface_sagemaker_tensorflow_distributed_amd.train.runner import build  # noqa: E402
 from huggingface_sagemaker_tensorflow_distributed_amd.utils.args import batch_size_arg, build_parser  # noqa: E402
 
@@ -101,6 +102,22 @@ def main():
         if overlap is not None:
             overlap.pop("buckets", None)
     value = a.batch_size * world * a.steps / dt
+    # untimed self-validation (the driver's N > 1 runs): every rank ends the timed steps with bit-identical
+    # parameters, and the gradient path really spans the job (native RCCL engine of `world` ranks, its buckets)
+    div = os.environ.get("HSD_FAULT_DIVERGE_RANK")  # test hook: perturb one rank's weights after the timed steps
+    if div is not None and int(div) == rank:
+        with torch.no_grad():
+            trainer.store.master[0] += 1e-3
+    in_sync = params_in_sync(trainer.store)
+    engine = getattr(trainer.bucketer, "engine", None)
+    rccl_world = int(engine.world) if engine is not None else None
+    validation = {"ranks_in_sync": in_sync, "rccl_world": rccl_world, "native_engine": engine is not None,
+                  "n_buckets": len(trainer.bucketer.buckets) if trainer.bucketer is not None else 0,
+                  "grad_bytes_per_step": trainer.store.grad.numel() * trainer.store.grad.element_size()
+                  if world > 1 else 0}
+    if world > 1:
+        validation["rccl_env"] = rccl_env.effective()
+    ok = in_sync and (engine is None or rccl_world == world)
     if rank == 0:
         print(json.dumps({
             "metric": METRIC, "value": round(value, 2), "unit": "sequences/sec", "n_gpus": world,
@@ -114,10 +131,14 @@ def main():
                        "hip_graph": trainer._seed is not None,
                        "comm": ("native-rccl" if getattr(trainer.bucketer, "engine", None) is not None
                                 else ("torch-" + backend.state().backend if world > 1 else "none"))},
+            "validation": validation,
             **({"comm_overlap": overlap} if overlap is not None else {}),
             **({"batch_plan": parts["batch_plan"].as_dict()} if parts.get("batch_plan") is not None else {}),
         }), flush=True)
     backend.shutdown()
+    if not ok:
+        print(f"bench: rank {rank}: validation failed {validation}", file=sys.stderr, flush=True)
+        sys.exit(3)
 
 
 if __name__ == "__main__":

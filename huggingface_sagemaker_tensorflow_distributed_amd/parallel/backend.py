@@ -47,6 +47,10 @@ def init(device: Optional[str] = None, timeout_s: float = 1800.0, backend: Optio
     env = dist_env()
     use_cuda = _want_cuda(device)
     if use_cuda:
+        from . import rccl_env
+
+        rccl_env.apply(env["world_size"])  # before any communicator exists
+    if use_cuda:
         torch.cuda.set_device(env["local_rank"] % max(1, torch.cuda.device_count()))
         dev = torch.device("cuda", torch.cuda.current_device())
     else:

@@ -15,6 +15,7 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (HIP kernels / RCCL)")
     config.addinivalue_line("markers", "dist: multi-process (gloo) test")
     config.addinivalue_line("markers", "slow: long-running test")
+    config.addinivalue_line("markers", "multigpu: needs >= 2 GPUs on one node (skips cleanly otherwise)")
 
 
 @pytest.fixture

@@ -41,3 +41,23 @@ def test_bench_driver_line_cpu(n):
     assert d["higher_is_better"] is True and d["scaling"] == "weak"
     assert d["value"] > 0
     assert abs(d["value"] - 2 * n * 2 / (d["ms_per_step"] * 2 / 1e3)) / d["value"] < 0.01
+    # self-validation after the timed loop: parameters identical on every rank, buckets in use
+    v = d["validation"]
+    assert v["ranks_in_sync"] is True
+    assert v["n_buckets"] >= 1
+    assert v["native_engine"] is False and v["rccl_world"] is None  # gloo on CPU: torch collectives
+    assert v["grad_bytes_per_step"] > 0
+
+
+def test_bench_exits_nonzero_when_ranks_diverge():
+    """The self-validation is real: a rank whose parameters differ after the timed loop fails the job (exit 3) and
+    the line says ranks_in_sync false."""
+    env = dict(os.environ, OMP_NUM_THREADS="1", CUDA_VISIBLE_DEVICES="", HIP_VISIBLE_DEVICES="",
+               HSD_FAULT_DIVERGE_RANK="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+           "--master-addr", "127.0.0.1", "--master-port", str(_port()), "bench.py", "--gpus", "2",
+           "--steps", "1", "--warmup", "1", "--batch_size", "2", "--seq_len", "16", "--model", "hsd-tiny-bert"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=600)
+    assert r.returncode != 0
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1 and json.loads(lines[0])["validation"]["ranks_in_sync"] is False
