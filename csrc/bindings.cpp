@@ -401,6 +401,75 @@ void xent(torch::Tensor logits, torch::Tensor labels, c10::optional<torch::Tenso
                    n_valid.data_ptr<float>(), (int)logits.size(0), (int)logits.size(1), cur_stream());
 }
 
+// fused classification head (cls_head.hip). pre [R][H] bf16 (row stride ld), W2 [C][H], b2 [C] bf16, labels int64 [R]
+// (or none: logits only); t_out [R][H], logits [R][C] bf16; partials fp32 [cls_head_blocks(R)][4]; stats fp32 [4]
+void cls_head_fwd(torch::Tensor pre, torch::Tensor W2, torch::Tensor b2, c10::optional<torch::Tensor> labels,
+                  torch::Tensor t_out, torch::Tensor logits, torch::Tensor partials, torch::Tensor stats, int64_t act,
+                  double p, int64_t seed) {
+  TORCH_CHECK(pre.is_cuda() && pre.dim() == 2 && pre.stride(1) == 1 && pre.stride(0) % 8 == 0 &&
+              pre.scalar_type() == torch::kBFloat16, "cls_head pre");
+  const int64_t R = pre.size(0), H = pre.size(1), C = W2.size(0);
+  TORCH_CHECK(H % 8 == 0 && H <= 1024 && C >= 1 && C <= 4, "cls_head: H % 8 == 0, H <= 1024, 1 <= classes <= 4");
+  TORCH_CHECK(W2.is_contiguous() && W2.size(1) == H && W2.scalar_type() == torch::kBFloat16, "cls_head W2");
+  TORCH_CHECK(b2.is_contiguous() && b2.numel() == C && b2.scalar_type() == torch::kBFloat16, "cls_head b2");
+  TORCH_CHECK(t_out.is_contiguous() && t_out.sizes() == pre.sizes() && t_out.scalar_type() == torch::kBFloat16, "cls t");
+  TORCH_CHECK(logits.is_contiguous() && logits.size(0) == R && logits.size(1) == C &&
+              logits.scalar_type() == torch::kBFloat16, "cls_head logits");
+  check_f32(partials, "partials");
+  check_f32(stats, "stats");
+  TORCH_CHECK(partials.numel() >= 4 * (int64_t)hsd::cls_head_blocks((int)R) && stats.numel() >= 4, "cls_head stats");
+  const int64_t* lab = nullptr;
+  if (labels.has_value()) {
+    TORCH_CHECK(labels->scalar_type() == torch::kInt64 && labels->is_contiguous() && labels->numel() == R, "labels");
+    lab = labels->data_ptr<int64_t>();
+  }
+  TORCH_CHECK(act == 0 || act == 1, "cls_head act: 0 tanh, 1 relu");
+  hsd::launch_cls_head_fwd(CBF(pre), pre.stride(0), CBF(W2), CBF(b2), lab, BF(t_out), BF(logits),
+                           partials.data_ptr<float>(), stats.data_ptr<float>(), (int)R, (int)H, (int)C, (int)act, p,
+                           (uint64_t)seed, cur_stream());
+}
+
+void cls_head_bwd(torch::Tensor t, torch::Tensor W2, torch::Tensor logits, torch::Tensor labels, torch::Tensor stats,
+                  torch::Tensor dloss, torch::Tensor dpre, torch::Tensor dW2, torch::Tensor db2, int64_t act, double p,
+                  int64_t seed) {
+  TORCH_CHECK(t.is_cuda() && t.dim() == 2 && t.is_contiguous() && t.scalar_type() == torch::kBFloat16, "cls t");
+  const int64_t R = t.size(0), H = t.size(1), C = W2.size(0);
+  TORCH_CHECK(H % 8 == 0 && H <= 1024 && C >= 1 && C <= 4, "cls_head shape");
+  TORCH_CHECK(W2.is_contiguous() && W2.size(1) == H && W2.scalar_type() == torch::kBFloat16, "cls_head W2");
+  TORCH_CHECK(logits.is_contiguous() && logits.size(0) == R && logits.size(1) == C &&
+              logits.scalar_type() == torch::kBFloat16, "cls_head logits");
+  TORCH_CHECK(labels.scalar_type() == torch::kInt64 && labels.is_contiguous() && labels.numel() == R, "labels");
+  check_f32(stats, "stats");
+  check_f32(dloss, "dloss");
+  TORCH_CHECK(dpre.is_contiguous() && dpre.sizes() == t.sizes() && dpre.scalar_type() == torch::kBFloat16, "dpre");
+  check_f32(dW2, "dW2");
+  check_f32(db2, "db2");
+  TORCH_CHECK(dW2.numel() == C * H && db2.numel() == C, "cls_head grads");
+  hsd::launch_cls_head_bwd(CBF(t), CBF(W2), CBF(logits), labels.data_ptr<int64_t>(), stats.data_ptr<float>(),
+                           dloss.data_ptr<float>(), BF(dpre), dW2.data_ptr<float>(), db2.data_ptr<float>(), (int)R,
+                           (int)H, (int)C, (int)act, p, (uint64_t)seed, cur_stream());
+}
+
+// C [N][K] fp32 += dy [T][N]ᵀ · x [T][K] for small T (row strides allowed; unit inner strides)
+void small_wgrad(torch::Tensor dy, torch::Tensor x, torch::Tensor C) {
+  TORCH_CHECK(dy.is_cuda() && x.is_cuda() && dy.dim() == 2 && x.dim() == 2 && dy.size(0) == x.size(0), "small_wgrad");
+  TORCH_CHECK(dy.scalar_type() == torch::kBFloat16 && x.scalar_type() == torch::kBFloat16 && dy.stride(1) == 1 &&
+              x.stride(1) == 1 && x.stride(0) % 4 == 0, "small_wgrad inputs");
+  TORCH_CHECK(C.scalar_type() == torch::kFloat32 && C.dim() == 2 && C.size(0) == dy.size(1) && C.size(1) == x.size(1) &&
+              C.stride(1) == 1 && C.stride(0) % 4 == 0 && x.size(1) % 4 == 0, "small_wgrad C");
+  hsd::launch_small_wgrad(CBF(dy), dy.stride(0), CBF(x), x.stride(0), C.data_ptr<float>(), C.stride(0),
+                          (int)dy.size(0), (int)dy.size(1), (int)x.size(1), cur_stream());
+}
+
+int64_t cls_head_blocks(int64_t R) { return hsd::cls_head_blocks((int)R); }
+
+// stream-ordered zero fill (hipMemsetAsync): gradient buffers and scatter targets without an at::native fill kernel
+void memset0(torch::Tensor x) {
+  TORCH_CHECK(x.is_cuda() && x.is_contiguous(), "memset0: contiguous GPU tensor");
+  const auto err = hipMemsetAsync(x.data_ptr(), 0, x.numel() * x.element_size(), cur_stream());
+  TORCH_CHECK(err == hipSuccess, "hipMemsetAsync failed");
+}
+
 void transpose_many(torch::Tensor desc, int64_t total_tiles) {
   TORCH_CHECK(desc.is_cuda() && desc.scalar_type() == torch::kInt64 && desc.dim() == 2 && desc.size(1) == 5 &&
               desc.is_contiguous(), "transpose_many: int64 [n, 5] device descriptor table");
@@ -453,4 +522,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm2_supported", &gemm2_supported);
   m.def("transpose_many", &transpose_many);
   m.def("xent", &xent);
+  m.def("cls_head_fwd", &cls_head_fwd);
+  m.def("cls_head_bwd", &cls_head_bwd);
+  m.def("cls_head_blocks", &cls_head_blocks);
+  m.def("memset0", &memset0);
+  m.def("small_wgrad", &small_wgrad);
 }

@@ -134,6 +134,37 @@ void launch_colsum(const bf16_t* x, float* dbias, int rows, int N, hipStream_t s
   colsum_launch(false, x, nullptr, nullptr, dbias, rows, N, st);
 }
 
+// C[n][k] += Σ_t dy[t][n] · x[t][k]  (bf16 in, fp32 C) for token counts below one 64-token K-tile: the weight gradient of
+// the classification head's dense layer at small batches (the reference's own B = 8), where gemm2's TT path does not
+// tile. One thread per 4 consecutive k; the dy element is a wave-wide broadcast, the x row chunk an 8-B load.
+__global__ __launch_bounds__(256) void small_wgrad_kernel(const bf16_t* __restrict__ dy, int64_t ldy,
+                                                          const bf16_t* __restrict__ x, int64_t ldx, float* __restrict__ C,
+                                                          int64_t ldc, int T, int N, int K) {
+  const int64_t n4 = (int64_t)N * (K / 4);
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
+    const int n = (int)(i / (K / 4));
+    const int k = (int)(i % (K / 4)) * 4;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int t = 0; t < T; ++t) {
+      const float d = bf2f(dy[(int64_t)t * ldy + n]);
+      const u32x2 w = *reinterpret_cast<const u32x2*>(x + (int64_t)t * ldx + k);
+      acc[0] = fmaf(d, lo_bf(w.x), acc[0]);
+      acc[1] = fmaf(d, hi_bf(w.x), acc[1]);
+      acc[2] = fmaf(d, lo_bf(w.y), acc[2]);
+      acc[3] = fmaf(d, hi_bf(w.y), acc[3]);
+    }
+    f32x4* c = reinterpret_cast<f32x4*>(C + (int64_t)n * ldc + k);
+    *c = *c + acc;
+  }
+}
+
+void launch_small_wgrad(const bf16_t* dy, int64_t ldy, const bf16_t* x, int64_t ldx, float* C, int64_t ldc, int T,
+                        int N, int K, hipStream_t st) {
+  const int64_t n4 = (int64_t)N * (K / 4);
+  hipLaunchKernelGGL(small_wgrad_kernel, dim3(grid_for(n4)), dim3(256), 0, st, dy, ldy, x, ldx, C, ldc, T, N, K);
+  HSD_CHECK_LAUNCH();
+}
+
 void launch_dropout(const bf16_t* x, bf16_t* out, int64_t n, double p, uint64_t seed, hipStream_t st) {
   DropoutParams dp = make_dropout(p, seed);
   int64_t n4 = n / 4;  // caller guarantees n % 4 == 0

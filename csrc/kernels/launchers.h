@@ -37,11 +37,22 @@ void launch_gelu_bwd_colsum(const bf16_t* dg, const bf16_t* y, bf16_t* da, float
                             hipStream_t st);
 void launch_colsum(const bf16_t* x, float* dbias, int rows, int N, hipStream_t st);
 void launch_dropout(const bf16_t* x, bf16_t* out, int64_t n, double p, uint64_t seed, hipStream_t st);
+// C[N][K] (fp32, ldc) += dy[T][N]ᵀ · x[T][K] for small T (K % 4 == 0)
+void launch_small_wgrad(const bf16_t* dy, int64_t ldy, const bf16_t* x, int64_t ldx, float* C, int64_t ldc, int T,
+                        int N, int K, hipStream_t st);
 // xent.hip: fused softmax cross-entropy (+ gradient, + argmax-correct count); stats = {Σloss, correct}
 void launch_xent(const void* logits, bool bf16, const int64_t* labels, void* dlogits, float* stats,
                  const float* n_valid, int rows, int V, hipStream_t st);
 // desc: int64 [n][5] = {src, dst, rows, cols, first_tile}; rows, cols multiples of 4
 void launch_transpose_many(const int64_t* desc, int n, int total_tiles, hipStream_t st);
+// cls_head.hip: fused sequence-classification head after the dense GEMM (act, dropout, classifier, CE, accuracy)
+int cls_head_blocks(int R);
+void launch_cls_head_fwd(const bf16_t* pre, int64_t ld_pre, const bf16_t* W2, const bf16_t* b2, const int64_t* labels,
+                         bf16_t* t_out, bf16_t* logits, float* partials, float* stats, int R, int H, int C, int act,
+                         double p, uint64_t seed, hipStream_t st);
+void launch_cls_head_bwd(const bf16_t* t_in, const bf16_t* W2, const bf16_t* logits, const int64_t* labels,
+                         const float* stats, const float* dloss, bf16_t* dpre, float* dW2, float* db2, int R, int H,
+                         int C, int act, double p, uint64_t seed, hipStream_t st);
 // attention.hip
 bool attn_streaming(int S);
 void launch_attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse2, int B, int S, int heads,

@@ -172,26 +172,23 @@ class TransformerForSequenceClassification(_Base):
         c = self.cfg
         training = self.training
         h = self.encoder(input_ids, attention_mask, token_type_ids, self.rng, training)
-        x = h[:, 0].contiguous()  # [CLS] / <s>
+        # head on the [CLS] / <s> row (ops.cls_head: one fused kernel per direction after the dense GEMM on GPUs);
+        # the dropout seeds are drawn in the same order as the unfused head always drew them
         if c.model_type == "bert":
             p = (c.classifier_dropout if c.classifier_dropout is not None else c.hidden_dropout_prob) if training else 0.0
-            pooled = torch.tanh(ops.linear(x, self.pooler_weight, self.pooler_bias))
-            pooled = ops.dropout(pooled, p, self.rng.next() if p else 0)
-            logits = ops.linear(pooled, self.classifier_weight, self.classifier_bias)
+            w1, b1, act, p_in, seed_in = self.pooler_weight, self.pooler_bias, "tanh", 0.0, 0
         elif c.model_type == "roberta":
             p = (c.classifier_dropout if c.classifier_dropout is not None else c.hidden_dropout_prob) if training else 0.0
-            x = ops.dropout(x, p, self.rng.next() if p else 0)
-            x = torch.tanh(ops.linear(x, self.head_dense_weight, self.head_dense_bias))
-            x = ops.dropout(x, p, self.rng.next() if p else 0)
-            logits = ops.linear(x, self.classifier_weight, self.classifier_bias)
+            w1, b1, act, p_in = self.head_dense_weight, self.head_dense_bias, "tanh", p
+            seed_in = self.rng.next() if p else 0
         else:
             p = c.seq_classif_dropout if training else 0.0
-            x = torch.relu(ops.linear(x, self.head_dense_weight, self.head_dense_bias))
-            x = ops.dropout(x, p, self.rng.next() if p else 0)
-            logits = ops.linear(x, self.classifier_weight, self.classifier_bias)
+            w1, b1, act, p_in, seed_in = self.head_dense_weight, self.head_dense_bias, "relu", 0.0, 0
+        seed = self.rng.next() if p else 0
+        out = ops.cls_head(h, w1, b1, self.classifier_weight, self.classifier_bias, labels, act, p_in, seed_in, p, seed)
         if labels is not None:
-            return ops.cross_entropy(logits, labels), logits
-        return logits
+            return out  # (loss, logits)
+        return out
 
 
 class RobertaForMaskedLM(_Base):

@@ -127,5 +127,31 @@ def cross_entropy(logits, labels):
     return _ref.cross_entropy(logits, labels)
 
 
+def cls_head(h, w1, b1, w2, b2, labels, act: str, p_in: float, seed_in: int, p: float, seed: int):
+    """Classification head on the first token of ``h`` [B, S, H] (+ the loss when ``labels`` is given).
+
+    Returns ``logits`` without labels, else ``(loss, logits)`` with the argmax-hit count on ``loss._hsd_correct``
+    and the fused {mean loss, hits, rows, loss sum} on ``loss._hsd_stats`` (HIP path). On GPUs the dense layer runs on gemm2 and everything after it (activation, dropout, classifier, CE,
+    accuracy) in one fused kernel per direction (csrc/kernels/cls_head.hip); the first-token rows are read in place
+    (no gather copy) and their gradient is written straight into the zeroed ``dh`` rows."""
+    if _hip(h) and labels is not None and _hipmod().cls_head_ok(h, w1, w2):
+        loss, logits, stats = _hipmod().cls_head(h, w1, b1, w2, b2, labels, act, p_in, seed_in, p, seed)
+        loss._hsd_correct = stats[1]
+        loss._hsd_stats = stats  # {mean loss, hits, rows, loss sum}: the metric meter folds these lazily
+        return loss, logits
+    x = h[:, 0].contiguous()
+    if _hip(h):
+        x = dropout(x, p_in, seed_in)
+        y = linear(x, w1, b1)
+        y = torch.tanh(y) if act == "tanh" else torch.relu(y)
+        y = dropout(y, p, seed)
+        logits = linear(y, w2, b2)
+    else:
+        logits = _ref.cls_head(x, w1, b1, w2, b2, act, p_in, seed_in, p, seed, True)
+    if labels is None:
+        return logits
+    return cross_entropy(logits, labels), logits
+
+
 def accuracy_count(logits, labels):
     return _ref.accuracy_count(logits, labels)

@@ -634,6 +634,84 @@ def ffn_block(h, w1, b1, w2, b2, ln_w, ln_b, eps, p, seed):
     return _FFNBlock.apply(h, w1, b1, w2, b2, ln_w, ln_b, eps, p, seed)
 
 
+# ------------------------------------------------------------------------------------------ classification head
+_ACT = {"tanh": 0, "relu": 1}
+
+
+def cls_head_ok(h, w1, w2) -> bool:
+    H = h.shape[-1]
+    return (h.dtype == torch.bfloat16 and h.dim() == 3 and H % 8 == 0 and H <= 1024 and 1 <= w2.shape[0] <= 4
+            and w1.shape[0] == H and (h.shape[1] * H) % 8 == 0)
+
+
+class _ClsHead(torch.autograd.Function):
+    """First-token rows of h -> dense (gemm2, bias epilogue) -> fused act / dropout / classifier / CE / accuracy
+    (cls_head.hip). Backward: one fused kernel (CE grad, classifier dgrad + fp32 dW2 / db2 into main_grad, dropout,
+    act') -> dense dgrad written into the first-token rows of a zeroed dh, wgrad, bias column sums."""
+
+    @staticmethod
+    def forward(ctx, h, w1, b1, w2, b2, labels, act, p_in, seed_in, p, seed):
+        B, S, H = h.shape
+        C = w2.shape[0]
+        x = h.reshape(B, S * H)[:, :H]  # the [CLS] rows, read in place (row stride S*H)
+        if p_in > 0:
+            x = dropout(x.contiguous(), p_in, seed_in)
+        pre = gemm_fwd(x, w1, EPI_BIAS, bias=b1) if _nt_ok(B, H, H, EPI_BIAS) else torch.addmm(b1, x, w1.t())
+        t = torch.empty_like(pre)
+        logits = torch.empty((B, C), dtype=h.dtype, device=h.device)
+        nblk = _C.cls_head_blocks(B)
+        partials = torch.empty(nblk * 4, dtype=torch.float32, device=h.device)
+        stats = torch.empty(4, dtype=torch.float32, device=h.device)
+        lab = labels.contiguous().long()
+        _C.cls_head_fwd(pre, w2, b2, lab, t, logits, partials, stats, _ACT[act], float(p), _s64(seed))
+        ctx.save_for_backward(x, w1, b1, t, w2, b2, logits, lab, stats)
+        ctx.cfg = (act, float(p_in), seed_in, float(p), seed, B, S, H)
+        ctx.mark_non_differentiable(logits, stats)
+        return stats[0], logits, stats
+
+    @staticmethod
+    def backward(ctx, dloss, _dlogits, _dstats):
+        x, w1, b1, t, w2, b2, logits, lab, stats = ctx.saved_tensors
+        act, p_in, seed_in, p, seed, B, S, H = ctx.cfg
+        g_w1, g_b1, g_w2, g_b2 = _Grad(w1), _Grad(b1), _Grad(w2), _Grad(b2)
+        dpre = torch.empty_like(t)
+        dl = dloss.reshape(1).to(torch.float32).contiguous()
+        _C.cls_head_bwd(t, w2, logits, lab, stats, dl, dpre, g_w2.buf, g_b2.buf, _ACT[act], p, _s64(seed))
+        r_w2, r_b2 = g_w2.done(), g_b2.done()
+        _C.colsum(dpre, g_b1.buf)
+        r_b1 = g_b1.done()
+        if _C.gemm2_supported(1, 1, 7, H, H, B):
+            gemm_wgrad_(g_w1, dpre, x)
+        elif B < 64:
+            _C.small_wgrad(dpre, x, g_w1.buf.view(H, H))
+        else:
+            _wgrad_(g_w1, dpre, x)
+        r_w1 = g_w1.done()
+        dh = None
+        if ctx.needs_input_grad[0]:
+            dh = torch.empty((B, S, H), dtype=dpre.dtype, device=dpre.device)
+            _C.memset0(dh)
+            dst = dh.reshape(B, S * H)[:, :H]  # the [CLS] rows of dh (row stride S*H)
+            if p_in > 0:
+                dx = gemm_dgrad(dpre, w1) if _nt_ok(B, H, H, EPI_STORE) else torch.mm(dpre, w1)
+                _C.dropout(dx, dx, p_in, _s64(seed_in))
+                dst.copy_(dx)
+            elif _nt_ok(B, H, H, EPI_STORE):
+                wt = getattr(w1, "_hsd_wt", None)
+                if wt is None or wt.shape[0] != H:
+                    wt = w1.t().contiguous()
+                _C.gemm2(dpre, wt, dst, 0, 0, EPI_STORE, None, None, None, 0.0, 0, 0, None, None)
+            else:
+                dst.copy_(torch.mm(dpre, w1))
+        return dh, r_w1, r_b1, r_w2, r_b2, None, None, None, None, None, None
+
+
+def cls_head(h, w1, b1, w2, b2, labels, act, p_in, seed_in, p, seed):
+    """(loss, logits, stats) of the fused classification head (labels required); stats = fp32
+    {mean loss, argmax hits, rows scored, loss sum}."""
+    return _ClsHead.apply(h, w1, b1, w2, b2, labels, act, p_in, seed_in, p, seed)
+
+
 # ------------------------------------------------------------------------------------------ loss
 class _CrossEntropy(torch.autograd.Function):
     """Mean softmax cross-entropy over non-ignored rows (-100) with the gradient produced by the same

@@ -87,3 +87,14 @@ def cross_entropy(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
 
 def accuracy_count(logits: torch.Tensor, labels: torch.Tensor) -> torch.Tensor:
     return (logits.argmax(dim=-1) == labels.long()).sum()
+
+
+def cls_head(x, w1, b1, w2, b2, act: str, p_in: float, seed_in: int, p: float, seed: int, training: bool):
+    """Sequence-classification head on the first-token rows ``x`` [B, H] -> logits [B, C]:
+    ``W2·dropout(act(W1·dropout_in(x) + b1)) + b2`` (HF BertPooler + classifier, RobertaClassificationHead,
+    DistilBERT pre_classifier; act = "tanh" | "relu")."""
+    x = dropout(x, p_in, seed_in, training)
+    h = F.linear(x, w1, b1)
+    h = torch.tanh(h) if act == "tanh" else torch.relu(h)
+    h = dropout(h, p, seed, training)
+    return F.linear(h, w2, b2)

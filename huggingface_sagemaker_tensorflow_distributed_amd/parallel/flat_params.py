@@ -44,6 +44,12 @@ def _no_decay(name: str) -> bool:
     return leaf.endswith("bias") or any(t in ("ln", "ln1", "ln2") for t in toks)
 
 
+def hip_kernels_active() -> bool:
+    import os
+
+    return os.environ.get("HSD_OPS", "").lower() != "torch"
+
+
 class FlatParamStore:
     def __init__(self, model: nn.Module, device: torch.device, compute_dtype: torch.dtype = torch.float32,
                  grad_dtype: torch.dtype = torch.float32, fp8: bool = False):
@@ -229,7 +235,12 @@ class FlatParamStore:
         return self.segments[self._index[id(p)]]
 
     def zero_grad(self) -> None:
-        self.grad.zero_()
+        if self.grad.is_cuda and hip_kernels_active():
+            from ..ops import hip
+
+            hip._C.memset0(self.grad)  # hipMemsetAsync: no elementwise fill kernel in the step
+        else:
+            self.grad.zero_()
 
     @torch.no_grad()
     def sync_compute_from_master(self) -> None:

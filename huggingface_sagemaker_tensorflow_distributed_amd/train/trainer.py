@@ -52,8 +52,23 @@ class _Meter:
 
     def __init__(self, device):
         self.t = torch.zeros(3, dtype=torch.float64, device=device)
+        self._pending: List[torch.Tensor] = []
+
+    def _fold(self) -> None:
+        if self._pending:
+            s = torch.stack(self._pending).double().sum(0)
+            self.t += s[[3, 1, 2]]
+            self._pending.clear()
 
     def update(self, loss: torch.Tensor, logits: torch.Tensor, labels: torch.Tensor) -> None:
+        fused_stats = getattr(loss, "_hsd_stats", None)
+        if fused_stats is not None:
+            # the fused head already counted {loss sum, hits, rows} on the device: keep the tensor, add them up
+            # when the metrics are read (no kernels per step)
+            self._pending.append(fused_stats)
+            if len(self._pending) >= 256:
+                self._fold()
+            return
         # classification: one label per logits row, -100 on the rows that only pad the eval shards;
         # MLM: logits only for the non-ignored (masked) tokens. Either way n counts the scored rows.
         n = labels.ne(-100).sum()
@@ -71,6 +86,7 @@ class _Meter:
         self.t += upd
 
     def result(self, global_: bool = True) -> Dict[str, float]:
+        self._fold()
         vals = self.t.tolist()
         if global_:
             vals = allreduce_sums(vals, self.t.device)
