@@ -217,7 +217,7 @@ def test_fused_blocks_vs_reference(gpu, p, S, H, heads):
     w1, b1, w2, b2 = mk(I, H), mk(I), mk(H, I), mk(H)
     l2w, l2b = (1 + 0.1 * torch.randn(H, device=gpu)).bfloat16().requires_grad_(), mk(H)
     am = torch.ones(B, S, dtype=torch.long, device=gpu)
-    am[2, 100:] = 0
+    am[B // 2, 100:] = 0
     mb = ref.key_mask_bias(am)
     params = [h, qw, qb, ow, ob, lw, lb, w1, b1, w2, b2, l2w, l2b]
 
