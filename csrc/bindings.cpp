@@ -324,7 +324,7 @@ void gemm2(torch::Tensor A, torch::Tensor B, torch::Tensor C, int64_t la, int64_
   TORCH_CHECK(A.scalar_type() == torch::kBFloat16 && B.scalar_type() == torch::kBFloat16, "gemm2 inputs must be bf16");
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "gemm2 operands must be 2-D");
   TORCH_CHECK(A.stride(1) == 1 && B.stride(1) == 1 && C.stride(1) == 1, "gemm2 operands need unit inner stride");
-  TORCH_CHECK(la == lb, "gemm2 layouts: NT (0,0) or TT (1,1)");
+  TORCH_CHECK(la == lb || (la == 0 && lb == 1), "gemm2 layouts: NT (0,0), NT with B = W[K][N] (0,1) or TT (1,1)");
   const int64_t M = la == 0 ? A.size(0) : A.size(1);
   const int64_t K = la == 0 ? A.size(1) : A.size(0);
   const int64_t N = lb == 0 ? B.size(0) : B.size(1);
@@ -461,6 +461,15 @@ void small_wgrad(torch::Tensor dy, torch::Tensor x, torch::Tensor C) {
                           (int)dy.size(0), (int)dy.size(1), (int)x.size(1), cur_stream());
 }
 
+void mask_bias(torch::Tensor mask, torch::Tensor out) {
+  TORCH_CHECK(mask.is_cuda() && mask.is_contiguous() &&
+              (mask.scalar_type() == torch::kInt64 || mask.scalar_type() == torch::kInt32), "mask_bias mask");
+  check_f32(out, "mask_bias out");
+  TORCH_CHECK(out.numel() == mask.numel(), "mask_bias shape");
+  hsd::launch_mask_bias(mask.data_ptr(), mask.scalar_type() == torch::kInt64, out.data_ptr<float>(), mask.numel(),
+                        cur_stream());
+}
+
 int64_t cls_head_blocks(int64_t R) { return hsd::cls_head_blocks((int)R); }
 
 // stream-ordered zero fill (hipMemsetAsync): gradient buffers and scatter targets without an at::native fill kernel
@@ -479,7 +488,7 @@ void transpose_many(torch::Tensor desc, int64_t total_tiles) {
 int64_t gemm2_splits(int64_t M, int64_t N, int64_t K) { return hsd::gemm2_wgrad_splits((int)M, (int)N, (int)K); }
 int64_t gemm2_nt_splits(int64_t M, int64_t N, int64_t K) { return hsd::gemm2_nt_splits((int)M, (int)N, (int)K); }
 bool gemm2_supported(int64_t la, int64_t lb, int64_t epi, int64_t M, int64_t N, int64_t K) {
-  return la == lb && hsd::gemm2_supported((int)la, (int)lb, (int)epi, (int)M, (int)N, (int)K);
+  return hsd::gemm2_supported((int)la, (int)lb, (int)epi, (int)M, (int)N, (int)K);
 }
 
 }  // namespace
@@ -527,4 +536,5 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cls_head_blocks", &cls_head_blocks);
   m.def("memset0", &memset0);
   m.def("small_wgrad", &small_wgrad);
+  m.def("mask_bias", &mask_bias);
 }

@@ -177,6 +177,9 @@ class CommEngine {
     }
   }
 
+  // fp16 wire pre-scale for the coming step(s): 1 / (world x gradient-accumulation micro-steps)
+  void set_prescale(double s) { prescale_ = s > 0.0 ? s : 1.0; }
+
   void begin_step() {
     for (auto& b : buckets_) {
       b.pending = b.nparams;
@@ -310,10 +313,17 @@ class CommEngine {
       c10::hip::HIPStreamGuard guard(c10::hip::getStreamFromExternal(stream_, device_));
       at::Tensor src = flat_.narrow(0, b.start, n);
       at::Tensor wire = shadow_.narrow(0, b.start, n);
-      wire.copy_(src);
+      if (comp_ == 2 && prescale_ != 1.0) {
+        // fp16 on the wire: pre-scale by 1/(world x micro-steps) so the rank SUM of k accumulated micro-steps stays
+        // inside fp16's range (65504); scaled back in fp32 after the all-reduce (exact for powers of two)
+        wire.copy_(src.mul(prescale_));
+      } else {
+        wire.copy_(src);
+      }
       NCCL_OK(ncclAllReduce(wire.data_ptr(), wire.data_ptr(), (size_t)n, to_nccl(wire.scalar_type()), ncclSum, comm_,
                             stream_));
       src.copy_(wire);
+      if (comp_ == 2 && prescale_ != 1.0) src.mul_(1.0 / prescale_);
     } else if (n > 0) {
       char* base = static_cast<char*>(flat_.data_ptr()) + b.start * flat_.element_size();
       NCCL_OK(ncclAllReduce(base, base, (size_t)n, to_nccl(flat_.scalar_type()), ncclSum, comm_, stream_));
@@ -338,6 +348,7 @@ class CommEngine {
   torch::Tensor flat_;
   torch::Tensor shadow_;
   int comp_ = 0;
+  double prescale_ = 1.0;
 };
 
 }  // namespace
@@ -354,6 +365,7 @@ void register_comm(pybind11::module& m) {
       .def("broadcast", &CommEngine::broadcast, py::arg("t"), py::arg("root") = 0)
       .def("set_buckets", &CommEngine::set_buckets)
       .def("set_compression", &CommEngine::set_compression)
+      .def("set_prescale", &CommEngine::set_prescale)
       .def("begin_step", &CommEngine::begin_step)
       .def("set_timing", &CommEngine::set_timing)
       .def("timings", &CommEngine::timings)

@@ -165,6 +165,19 @@ void launch_small_wgrad(const bf16_t* dy, int64_t ldy, const bf16_t* x, int64_t 
   HSD_CHECK_LAUNCH();
 }
 
+// additive key-padding bias of attention: out = (1 - mask) * FLT_MIN (ops/reference.py key_mask_bias, bit for bit)
+template <typename T>
+__global__ __launch_bounds__(256) void mask_bias_kernel(const T* __restrict__ m, float* __restrict__ out, int64_t n) {
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (int64_t)gridDim.x * blockDim.x)
+    out[i] = (1.0f - (float)m[i]) * -3.4028234663852886e+38f;
+}
+
+void launch_mask_bias(const void* mask, bool i64, float* out, int64_t n, hipStream_t st) {
+  if (i64) hipLaunchKernelGGL(mask_bias_kernel<int64_t>, dim3(grid_for(n)), dim3(256), 0, st, (const int64_t*)mask, out, n);
+  else hipLaunchKernelGGL(mask_bias_kernel<int32_t>, dim3(grid_for(n)), dim3(256), 0, st, (const int32_t*)mask, out, n);
+  HSD_CHECK_LAUNCH();
+}
+
 void launch_dropout(const bf16_t* x, bf16_t* out, int64_t n, double p, uint64_t seed, hipStream_t st) {
   DropoutParams dp = make_dropout(p, seed);
   int64_t n4 = n / 4;  // caller guarantees n % 4 == 0

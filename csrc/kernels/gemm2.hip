@@ -58,16 +58,32 @@ __device__ __forceinline__ void dma(bf16_t* img, const bf16_t* __restrict__ X, i
                                    (__attribute__((address_space(3))) void*)(img + g * 512), 16, 0, 0);
 }
 
-// TT (both operands k-strided) DMA: inline asm, a per-lane byte offset computed once per workgroup and a scalar
+// DMA of kernels with a k-strided operand (TT weight gradients, NT dgrad reading W directly): inline asm, a per-lane byte offset computed once per workgroup and a scalar
 // (SGPR) base per K-tile. With the builtin, hipcc does not tell the transposing LDS reads (ds_read_b64_tr_b16) apart
 // from the LDS-DMA destination and drains EVERY DMA (s_waitcnt vmcnt(0)) before the first read of each K-tile, so
 // tile t+2's DMA had one MFMA phase to land instead of a K-tile. The asm DMA is invisible to hipcc's wait
 // bookkeeping; the kernel's counted vmcnt<N>() waits retire it.
-__device__ __forceinline__ uint32_t tt_lane_off(int64_t ld, int r0, int Rmax, int g, int lane) {
-  const int krow = g * 2 + (lane >> 5);
-  const int lc = (lane & 31) ^ f2(krow);
-  const int cc = min(r0 + lc * 8, Rmax - 8);
-  return (uint32_t)(((int64_t)krow * ld + cc) * 2);
+// Per-lane byte offset of DMA slot g from the operand's per-K-tile scalar base (asm_base): k-strided images
+// (L = 1, base X + k0·ld) and k-contiguous images (L = 0, base X + r0·ld + k0; rows clamped to the matrix).
+template <int L>
+__device__ __forceinline__ uint32_t lane_off(int64_t ld, int r0, int Rmax, int g, int lane) {
+  if constexpr (L == 1) {
+    const int krow = g * 2 + (lane >> 5);
+    const int lc = (lane & 31) ^ f2(krow);
+    const int cc = min(r0 + lc * 8, Rmax - 8);
+    return (uint32_t)(((int64_t)krow * ld + cc) * 2);
+  } else {
+    const int row = g * 8 + (lane >> 3);
+    const int lc = (lane & 7) ^ f1(row);
+    const int rr = min(row, Rmax - 1 - r0);
+    return (uint32_t)(((int64_t)rr * ld + lc * 8) * 2);
+  }
+}
+
+template <int L>
+__device__ __forceinline__ const bf16_t* asm_base(const bf16_t* X, int64_t ld, int r0, int k0) {
+  if constexpr (L == 1) return X + (int64_t)k0 * ld;
+  else return X + (int64_t)r0 * ld + k0;
 }
 
 __device__ __forceinline__ void dma_lds_asm(const bf16_t* sbase, uint32_t voff, uint32_t lds_addr) {
@@ -139,21 +155,23 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
   const int nt = (kend - kbeg) / BK;
   HSD_DASSERT(v < nwg && m0 < p.M && n0 < p.N && kbeg < p.K && (kend - kbeg) % BK == 0);
 
-  constexpr bool TT = LA == 1 && LB == 1;
-  uint32_t ttoff[TT ? G : 1];
-  if constexpr (TT) {
+  // any k-strided operand: every DMA of the kernel is inline asm (a builtin DMA beside the transposing reads draws
+  // hipcc's vmcnt(0) drain, see dma_lds_asm); k-contiguous-only (NT) kernels keep the builtin
+  constexpr bool ASM = LA == 1 || LB == 1;
+  uint32_t aoff[ASM ? G : 1];
+  if constexpr (ASM) {
 #pragma unroll
     for (int q = 0; q < G; ++q)
-      ttoff[q] = q < GA ? tt_lane_off(p.lda, m0, p.M, wave * GA + q, lane)
-                        : tt_lane_off(p.ldb, n0, p.N, wave * GB + (q - GA), lane);
+      aoff[q] = q < GA ? lane_off<LA>(p.lda, m0, p.M, wave * GA + q, lane)
+                       : lane_off<LB>(p.ldb, n0, p.N, wave * GB + (q - GA), lane);
   }
   // LDS byte address of smem (one generic -> LDS conversion; stage / slot offsets are plain integer adds)
   const uint32_t smem_lds = (uint32_t)(size_t)(__attribute__((address_space(3))) bf16_t*)smem;
   auto dma_slot = [&](int q, bf16_t* stage, int k0) {
-    if constexpr (TT) {
+    if constexpr (ASM) {
       const uint32_t st = smem_lds + (uint32_t)(stage - smem) * 2u;
-      if (q < GA) dma_lds_asm(p.A + (int64_t)k0 * p.lda, ttoff[q], st + (wave * GA + q) * 1024u);
-      else dma_lds_asm(p.B + (int64_t)k0 * p.ldb, ttoff[q], st + (TA + (wave * GB + (q - GA)) * 512) * 2u);
+      if (q < GA) dma_lds_asm(asm_base<LA>(p.A, p.lda, m0, k0), aoff[q], st + (wave * GA + q) * 1024u);
+      else dma_lds_asm(asm_base<LB>(p.B, p.ldb, n0, k0), aoff[q], st + (TA + (wave * GB + (q - GA)) * 512) * 2u);
     } else {
       if (q < GA) dma<LA, BM>(stage, p.A, p.lda, m0, p.M, k0, wave * GA + q, lane);
       else dma<LB, BN>(stage + TA, p.B, p.ldb, n0, p.N, k0, wave * GB + (q - GA), lane);
@@ -657,11 +675,11 @@ __device__ __forceinline__ void wait_tiles(int left) {
   vmcnt<0>();
 }
 
-template <int L, int EPI, int NSTG>
+template <int LA, int LB, int EPI, int NSTG>
 __global__ __launch_bounds__(256, NSTG <= 2 ? 2 : 1) void gemm2s_kernel(G2Params p) {
   static_assert(NSTG >= 2 && NSTG <= 4, "2-4 stages");
-  static_assert(L == 0 ? (epi_bf16_out(EPI) || EPI == E2_F32_SLAB) : EPI == E2_F32_SLAB,
-                "NT: bf16 epilogues or split-K slabs; TT: fp32");
+  static_assert(LA == 0 ? (epi_bf16_out(EPI) || EPI == E2_F32_SLAB) : (LB == 1 && EPI == E2_F32_SLAB),
+                "NT / NT with k-strided B: bf16 epilogues or split-K slabs; TT: fp32");
   p.dp = resolve_seed(p.dp);
   constexpr int TA = SBM * 64, STAGE = TA + SBN * 64;  // elements
   __shared__ __attribute__((aligned(16))) bf16_t smem[NSTG * STAGE];
@@ -682,9 +700,9 @@ __global__ __launch_bounds__(256, NSTG <= 2 ? 2 : 1) void gemm2s_kernel(G2Params
   // 16 DMA wave-instructions per operand image per stage, 4 + 4 per wave
   auto dma_tile = [&](bf16_t* stage, int k0) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) dma_asm<L>(stage, p.A, p.lda, m0, p.M, k0, wave * 4 + q, lane);
+    for (int q = 0; q < 4; ++q) dma_asm<LA>(stage, p.A, p.lda, m0, p.M, k0, wave * 4 + q, lane);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) dma_asm<L>(stage + TA, p.B, p.ldb, n0, p.N, k0, wave * 4 + q, lane);
+    for (int q = 0; q < 4; ++q) dma_asm<LB>(stage + TA, p.B, p.ldb, n0, p.N, k0, wave * 4 + q, lane);
   };
 
   f32x4 acc[4][4];
@@ -710,9 +728,9 @@ __global__ __launch_bounds__(256, NSTG <= 2 ? 2 : 1) void gemm2s_kernel(G2Params
     for (int ks = 0; ks < 2; ++ks) {
       bf16x8 fa[4], fb[4];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) fa[i] = frag<L, SBM>(cA, arow + 16 * i, ks, lane);
+      for (int i = 0; i < 4; ++i) fa[i] = frag<LA, SBM>(cA, arow + 16 * i, ks, lane);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) fb[j] = frag<L, SBN>(cB, bcol + 16 * j, ks, lane);
+      for (int j = 0; j < 4; ++j) fb[j] = frag<LB, SBN>(cB, bcol + 16 * j, ks, lane);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -726,7 +744,7 @@ __global__ __launch_bounds__(256, NSTG <= 2 ? 2 : 1) void gemm2s_kernel(G2Params
   if constexpr (EPI == E2_F32_SLAB) {
     // acc[i][j]: lane l holds m = 16i + (l&15), n = 16j + 4(l>>4) + r. One TT split accumulates into C; NT always
     // writes its slab (splitk_epi_kernel reduces and runs the bf16 epilogue).
-    const bool direct = L == 1 && nwg == p.ntiles;
+    const bool direct = LA == 1 && nwg == p.ntiles;
     const int q4 = lane >> 4, lr = lane & 15;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -894,18 +912,19 @@ static int g2s_stages(int grid) {
   return v < 2 ? 2 : (v > 4 ? 4 : v);
 }
 
-template <int L, int EPI>
+template <int LA, int LB, int EPI>
 static void g2s_launch(const G2Params& q, int grid, hipStream_t st) {
   const int ns = g2s_stages(grid);
-  if (ns == 2) hipLaunchKernelGGL((g2::gemm2s_kernel<L, EPI, 2>), dim3(grid), dim3(256), 0, st, q);
-  else if (ns == 3) hipLaunchKernelGGL((g2::gemm2s_kernel<L, EPI, 3>), dim3(grid), dim3(256), 0, st, q);
-  else hipLaunchKernelGGL((g2::gemm2s_kernel<L, EPI, 4>), dim3(grid), dim3(256), 0, st, q);
+  if (ns == 2) hipLaunchKernelGGL((g2::gemm2s_kernel<LA, LB, EPI, 2>), dim3(grid), dim3(256), 0, st, q);
+  else if (ns == 3) hipLaunchKernelGGL((g2::gemm2s_kernel<LA, LB, EPI, 3>), dim3(grid), dim3(256), 0, st, q);
+  else hipLaunchKernelGGL((g2::gemm2s_kernel<LA, LB, EPI, 4>), dim3(grid), dim3(256), 0, st, q);
   HSD_CHECK_LAUNCH();
 }
 
 bool gemm2_supported(int la, int lb, int epi, int M, int N, int K) {
   if (K % 64 || M < 1 || N % 8) return false;
   if (la == 0 && lb == 0) return epi_bf16_out(epi) && gemm2_pick_bn(M, N) != 0;
+  if (la == 0 && lb == 1) return epi_bf16_out(epi) && (N % 256 == 0 || gemm2s_use(M, N, K));
   if (la == 1 && lb == 1)
     return (epi == E2_F32_ATOMIC || epi == E2_F32_SLAB) && M % 8 == 0 &&
            (N % 256 == 0 || (epi == E2_F32_SLAB && gemm2st_use(M, N, K)));
@@ -917,26 +936,20 @@ int gemm2_wgrad_splits(int M, int N, int K) {
   return wgrad_plan(M, N, K).splits;
 }
 
-void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, int M, int N,
-                  int K, void* C, int64_t ldc, const bf16_t* bias, const bf16_t* aux, int64_t ldaux, bf16_t* C2,
-                  double p_drop, uint64_t seed, int splits, float* ws, float* dbias, hipStream_t st) {
-  G2Params p{};
-  p.dbias = dbias;
-  {
-    const char* e = getenv("HSD_G2_NT");
-    p.nt_store = e ? atoi(e) : 0;
-  }
-  p.A = A; p.lda = lda; p.B = B; p.ldb = ldb; p.M = M; p.N = N; p.K = K; p.C = C; p.ldc = ldc;
-  p.bias = bias; p.aux = aux; p.ldaux = ldaux; p.C2 = C2;
-  p.dp = make_dropout(p_drop, seed);
-  if (la == 0 && lb == 0 && splits <= 1 && gemm2s_use(M, N, K)) {
+// NT-shaped GEMM (bf16 out, fused epilogues): B k-contiguous (LB = 0: B[N][K], e.g. the stored Wᵀ for dgrad) or
+// k-strided (LB = 1: B[K][N], the dgrad reading W[N_out][K_in] directly, no Wᵀ copy). 128 x 128 tiles for grids the
+// 256 x 256 kernel leaves mostly idle, split-K slabs + one reduce-and-epilogue pass for the smallest grids.
+template <int LB>
+static void launch_nt(const G2Params& p, int epi, int M, int N, int K, int splits, float* ws, float* dbias,
+                      hipStream_t st) {
+  if (splits <= 1 && gemm2s_use(M, N, K)) {
     G2Params q = p;
     q.tiles_n = N / g2::SBN;
     q.ntiles = ((M + g2::SBM - 1) / g2::SBM) * q.tiles_n;
     q.kps = K;
 #define G2_SMALL(E)                   \
   case E:                             \
-    g2s_launch<0, E>(q, q.ntiles, st); \
+    g2s_launch<0, LB, E>(q, q.ntiles, st); \
     break;
     switch (epi) {
       G2_SMALL(E2_STORE)
@@ -952,7 +965,7 @@ void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const b
 #undef G2_SMALL
     return;
   }
-  if (la == 0 && lb == 0 && splits > 1) {
+  if (splits > 1) {
     if (ws == nullptr || !epi_bf16_out(epi)) abort();
     G2Params q = p;
     q.C = ws;
@@ -964,9 +977,9 @@ void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const b
       q.tiles_n = N / g2::SBN;
       q.ntiles = ((M + g2::SBM - 1) / g2::SBM) * q.tiles_n;
       q.kps = kps;
-      g2s_launch<0, E2_F32_SLAB>(q, q.ntiles * real, st);
+      g2s_launch<0, LB, E2_F32_SLAB>(q, q.ntiles * real, st);
     } else {
-      g2_launch<0, 0, E2_F32_SLAB, 256>(q, splits, st);
+      g2_launch<0, LB, E2_F32_SLAB, 256>(q, splits, st);
     }
     const int gx = (N + 63) / 64;
     const int gy_want = std::max(1, 2048 / gx);
@@ -992,16 +1005,16 @@ void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const b
     HSD_CHECK_LAUNCH();
     return;
   }
-  if (la == 0 && lb == 0) {
-    int bn = gemm2_pick_bn(M, N);
+  {
+    int bn = LB == 1 ? 256 : gemm2_pick_bn(M, N);  // k-strided B images are 256 wide
     if (dbias != nullptr) {
       if ((epi != E2_DGELU && epi != E2_MUL) || N % 256) abort();  // fused column sums: 8 columns per lane (BN 256)
       bn = 256;
     }
 #define G2_NT(E)                                                     \
   case E:                                                            \
-    if (bn == 256) g2_launch<0, 0, E, 256>(p, 1, st);                \
-    else g2_launch<0, 0, E, 192>(p, 1, st);                          \
+    if (bn == 256 || LB == 1) g2_launch<0, LB, E, 256>(p, 1, st);    \
+    else g2_launch<0, LB, E, LB == 1 ? 256 : 192>(p, 1, st);         \
     return;
     switch (epi) {
       G2_NT(E2_STORE)
@@ -1015,6 +1028,23 @@ void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const b
       default: abort();
     }
 #undef G2_NT
+  }
+}
+
+void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, int M, int N,
+                  int K, void* C, int64_t ldc, const bf16_t* bias, const bf16_t* aux, int64_t ldaux, bf16_t* C2,
+                  double p_drop, uint64_t seed, int splits, float* ws, float* dbias, hipStream_t st) {
+  G2Params p{};
+  p.dbias = dbias;
+  {
+    const char* e = getenv("HSD_G2_NT");
+    p.nt_store = e ? atoi(e) : 0;
+  }
+  p.A = A; p.lda = lda; p.B = B; p.ldb = ldb; p.M = M; p.N = N; p.K = K; p.C = C; p.ldc = ldc;
+  p.bias = bias; p.aux = aux; p.ldaux = ldaux; p.C2 = C2;
+  p.dp = make_dropout(p_drop, seed);
+  if (la == 0 && lb == 0) {
+    launch_nt<0>(p, epi, M, N, K, splits, ws, dbias, st);
   } else if (la == 1 && lb == 1) {
     if (splits <= 0) splits = gemm2_wgrad_splits(M, N, K);
     if (epi == E2_F32_SLAB && gemm2st_use(M, N, K) && (splits == 1 || ws != nullptr)) {
@@ -1026,7 +1056,7 @@ void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const b
       const int real = (K + kps - 1) / kps;
       q.kps = kps;
       if (real > 1) q.C = ws;
-      g2s_launch<1, E2_F32_SLAB>(q, q.ntiles * real, st);
+      g2s_launch<1, 1, E2_F32_SLAB>(q, q.ntiles * real, st);
       if (real > 1) {
         const int64_t n4 = (int64_t)M * N / 4;
         int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
@@ -1049,6 +1079,8 @@ void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const b
     } else {
       g2_launch<1, 1, E2_F32_ATOMIC, 256>(p, splits, st);
     }
+  } else if (la == 0 && lb == 1) {
+    launch_nt<1>(p, epi, M, N, K, splits, ws, dbias, st);
   } else {
     abort();
   }

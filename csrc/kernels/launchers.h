@@ -37,6 +37,7 @@ void launch_gelu_bwd_colsum(const bf16_t* dg, const bf16_t* y, bf16_t* da, float
                             hipStream_t st);
 void launch_colsum(const bf16_t* x, float* dbias, int rows, int N, hipStream_t st);
 void launch_dropout(const bf16_t* x, bf16_t* out, int64_t n, double p, uint64_t seed, hipStream_t st);
+void launch_mask_bias(const void* mask, bool i64, float* out, int64_t n, hipStream_t st);
 // C[N][K] (fp32, ldc) += dy[T][N]ᵀ · x[T][K] for small T (K % 4 == 0)
 void launch_small_wgrad(const bf16_t* dy, int64_t ldy, const bf16_t* x, int64_t ldx, float* C, int64_t ldc, int T,
                         int N, int K, hipStream_t st);

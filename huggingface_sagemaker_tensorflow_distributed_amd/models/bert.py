@@ -39,13 +39,25 @@ class Embeddings(nn.Module):
             pad = self.cfg.pad_token_id
             m = input_ids.ne(pad).int()
             return (torch.cumsum(m, dim=1).type_as(m) * m).long() + pad
-        return torch.arange(S, device=input_ids.device).unsqueeze(0).expand(B, S)
+        return self._cached("pos", input_ids, lambda: torch.arange(S, device=input_ids.device).unsqueeze(0)
+                            .expand(B, S).contiguous())
+
+    def _cached(self, kind: str, input_ids: torch.Tensor, make):
+        """Per-shape constant id tensors (arange positions, zero token types), built once instead of every step."""
+        key = (kind, tuple(input_ids.shape), input_ids.device)
+        cache = self.__dict__.setdefault("_id_cache", {})
+        t = cache.get(key)
+        if t is None:
+            if len(cache) > 16:
+                cache.clear()
+            t = cache[key] = make()
+        return t
 
     def forward(self, input_ids, token_type_ids, rng: DropoutSeeds, training: bool) -> torch.Tensor:
         c = self.cfg
         pos = self.position_ids(input_ids)
         if token_type_ids is None and self.token_type_embeddings is not None:
-            token_type_ids = torch.zeros_like(input_ids)
+            token_type_ids = self._cached("type0", input_ids, lambda: torch.zeros_like(input_ids))
         p = c.hidden_dropout_prob if training else 0.0
         return ops.embed_ln(input_ids, pos, token_type_ids, self.word_embeddings, self.position_embeddings,
                             self.token_type_embeddings, self.ln_weight, self.ln_bias, c.layer_norm_eps,

@@ -3,7 +3,8 @@
 * CUDA (=HIP on ROCm) tensors -> hand-written gfx950 kernels in ``csrc/kernels`` via
   :mod:`.hip` (custom autograd Functions). If the compiled extension is missing on a GPU box this
   raises — there is no silent eager fallback.
-* CPU tensors -> :mod:`.reference` (plain torch; also the numerics oracle for the kernel tests).
+* CPU tensors, and fp32 GPU tensors (``--dtype fp32``) -> :mod:`.reference` (plain torch; also the numerics oracle
+  for the kernel tests).
 
 ``HSD_OPS=torch`` forces the reference path on GPU (only for A/B measurements of the kernels).
 """
@@ -20,7 +21,9 @@ _FORCE_TORCH = os.environ.get("HSD_OPS", "").lower() == "torch"
 
 
 def _hip(x: torch.Tensor) -> bool:
-    return x.is_cuda and not _FORCE_TORCH
+    # fp32 tensors (``--dtype fp32``, the reference's own precision: scripts/train.py:113-123 has no mixed-precision
+    # policy) run the fp32 reference ops on the GPU (hipBLASLt / rocBLAS fp32 GEMMs); the HIP kernels are bf16 / fp8
+    return x.is_cuda and not _FORCE_TORCH and x.dtype != torch.float32
 
 
 def _hipmod():
@@ -30,6 +33,9 @@ def _hipmod():
 
 
 def key_mask_bias(attention_mask: Optional[torch.Tensor]):
+    if attention_mask is not None and attention_mask.is_cuda and not _FORCE_TORCH and \
+            attention_mask.dtype in (torch.int64, torch.int32):
+        return _hipmod().key_mask_bias(attention_mask)
     return _ref.key_mask_bias(attention_mask)
 
 

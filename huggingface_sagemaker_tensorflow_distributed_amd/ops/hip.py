@@ -493,11 +493,18 @@ def gemm_dgrad(dy, w, epi=EPI_STORE, aux=None, dbias=None):
         if dbias is not None and not fuse:
             _C.colsum(dx, dbias)
         return dx
-    if _nt_ok(dy.shape[0], w.shape[1], dy.shape[1], epi):
-        wt = getattr(w, "_hsd_wt", None)  # FlatParamStore keeps Wᵀ fresh (one batched transpose per step)
-        if wt is None or wt.shape[0] != w.shape[1] or wt.shape[1] != w.shape[0]:
+    wt = getattr(w, "_hsd_wt", None)  # FlatParamStore keeps Wᵀ fresh (one batched transpose per step)
+    if wt is not None and (wt.shape[0] != w.shape[1] or wt.shape[1] != w.shape[0]):
+        wt = None
+    fuse = dbias is not None and epi in (EPI_DGELU, EPI_MUL) and w.shape[1] % 256 == 0
+    if wt is None and w.is_contiguous() and _C.gemm2_supported(0, 1, epi, dy.shape[0], w.shape[1], dy.shape[1]):
+        # no stored Wᵀ (small steps): the NT kernel reads W [N_out][K_in] itself as its k-strided B operand
+        _C.gemm2(dy, w, dx, 0, 1, epi, None, aux, None, 0.0, 0, 0, None, dbias if fuse else None)
+        if dbias is not None and not fuse:
+            _C.colsum(dx, dbias)
+    elif _nt_ok(dy.shape[0], w.shape[1], dy.shape[1], epi):
+        if wt is None:
             wt = w.t().contiguous()
-        fuse = dbias is not None and epi in (EPI_DGELU, EPI_MUL) and w.shape[1] % 256 == 0
         _C.gemm2(dy, wt, dx, 0, 0, epi, None, aux, None, 0.0, 0, 0, None, dbias if fuse else None)
         if dbias is not None and not fuse:
             _C.colsum(dx, dbias)
@@ -634,6 +641,15 @@ def ffn_block(h, w1, b1, w2, b2, ln_w, ln_b, eps, p, seed):
     return _FFNBlock.apply(h, w1, b1, w2, b2, ln_w, ln_b, eps, p, seed)
 
 
+# ------------------------------------------------------------------------------------------ attention mask
+def key_mask_bias(attention_mask):
+    """[B, S] 0/1 mask -> additive fp32 bias (0 keep, float32 min masked), one kernel (ops/reference.py formula)."""
+    am = attention_mask.contiguous()
+    out = torch.empty(am.shape, dtype=torch.float32, device=am.device)
+    _C.mask_bias(am, out)
+    return out
+
+
 # ------------------------------------------------------------------------------------------ classification head
 _ACT = {"tanh": 0, "relu": 1}
 
@@ -667,6 +683,7 @@ class _ClsHead(torch.autograd.Function):
         ctx.save_for_backward(x, w1, b1, t, w2, b2, logits, lab, stats)
         ctx.cfg = (act, float(p_in), seed_in, float(p), seed, B, S, H)
         ctx.mark_non_differentiable(logits, stats)
+        ctx.set_materialize_grads(False)  # no zero-filled gradients for the non-differentiable outputs
         return stats[0], logits, stats
 
     @staticmethod
@@ -675,6 +692,8 @@ class _ClsHead(torch.autograd.Function):
         act, p_in, seed_in, p, seed, B, S, H = ctx.cfg
         g_w1, g_b1, g_w2, g_b2 = _Grad(w1), _Grad(b1), _Grad(w2), _Grad(b2)
         dpre = torch.empty_like(t)
+        if dloss is None:
+            dloss = torch.zeros((), dtype=torch.float32, device=t.device)
         dl = dloss.reshape(1).to(torch.float32).contiguous()
         _C.cls_head_bwd(t, w2, logits, lab, stats, dl, dpre, g_w2.buf, g_b2.buf, _ACT[act], p, _s64(seed))
         r_w2, r_b2 = g_w2.done(), g_b2.done()
@@ -696,11 +715,8 @@ class _ClsHead(torch.autograd.Function):
                 dx = gemm_dgrad(dpre, w1) if _nt_ok(B, H, H, EPI_STORE) else torch.mm(dpre, w1)
                 _C.dropout(dx, dx, p_in, _s64(seed_in))
                 dst.copy_(dx)
-            elif _nt_ok(B, H, H, EPI_STORE):
-                wt = getattr(w1, "_hsd_wt", None)
-                if wt is None or wt.shape[0] != H:
-                    wt = w1.t().contiguous()
-                _C.gemm2(dpre, wt, dst, 0, 0, EPI_STORE, None, None, None, 0.0, 0, 0, None, None)
+            elif _C.gemm2_supported(0, 1, EPI_STORE, B, H, H):
+                _C.gemm2(dpre, w1, dst, 0, 1, EPI_STORE, None, None, None, 0.0, 0, 0, None, None)  # reads W1 as is
             else:
                 dst.copy_(torch.mm(dpre, w1))
         return dh, r_w1, r_b1, r_w2, r_b2, None, None, None, None, None, None

@@ -73,6 +73,14 @@ class FusedAdam:
     # -------------------------------------------------------------------------- overlap with backward
     def enable_overlap(self, ranges: List[Tuple[int, int]], on_ready: Optional[Callable] = None) -> None:
         """Step the flat-buffer slices ``ranges`` (64-aligned, backward order) as their gradients complete.
+
+        INVARIANT (the overlap is correct only under it): every kernel that READS a parameter -- its bf16 copy, its
+        Wᵀ / fp8 copies -- is queued before that parameter's post-accumulate hook fires. Autograd runs the hook after
+        the last node that used the parameter, and the HIP backward kernels read weights inside those nodes, so this
+        holds for the model code here; it would NOT hold for activation recompute (a re-run forward reads weights
+        after their hook) or a head that reads weights outside autograd after the hook. A model that breaks it sets
+        ``opt_overlap_safe = False`` and the Trainer then steps the optimizer once after backward.
+
         ``on_ready``: the store-readiness callback to install (one process); data-parallel ranks call
         :meth:`step_range` from the bucketer instead."""
         self._ranges = list(ranges)
@@ -95,6 +103,14 @@ class FusedAdam:
         self._coef = (step, eps_eff, float(grad_scale))
         self._done = [False] * len(self._ranges)
         self._began = True
+
+    def abort_step(self) -> None:
+        """Undo :meth:`begin_step` when the step fails before :meth:`step` (an exception in backward, an OOM at an
+        auto-planned batch): the bias-correction step count must not drift by one per failed step. Slices already
+        stepped under the failed backward cannot be undone; the caller is expected to stop or restore a checkpoint."""
+        if getattr(self, "_began", False):
+            self.step_count -= 1
+            self._began = False
 
     @torch.no_grad()
     def step_range(self, b: int) -> None:

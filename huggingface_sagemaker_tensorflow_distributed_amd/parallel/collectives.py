@@ -82,14 +82,15 @@ def hvd_allreduce(tensor: torch.Tensor, average=None, op=None) -> torch.Tensor:
     """``hvd.allreduce``: the reduced copy of ``tensor`` (default op Average; ``average=False`` means Sum)."""
     if op is None:
         op = Sum if average is False else Average
+    if op == Average and not tensor.is_floating_point():
+        # checked before the world-size early return: the same call fails the same way in a world of one
+        raise TypeError("hvd.allreduce(op=Average) needs a floating-point tensor")
     out = tensor.detach().clone().contiguous()
     if not backend.is_distributed():
         return out
     if op in (Sum, Average):
         from .comm import allreduce_
 
-        if not out.is_floating_point() and op == Average:
-            raise TypeError("hvd.allreduce(op=Average) needs a floating-point tensor")
         allreduce_(out)
         if op == Average:
             out /= backend.size()

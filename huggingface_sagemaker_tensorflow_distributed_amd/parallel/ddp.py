@@ -97,6 +97,7 @@ class GradBucketer:
         self.sync_enabled = True
         self._on_reduced = None
         self.last_launched: Optional[int] = None  # index of the last bucket whose all-reduce was issued (watchdog)
+        self._prescale = 1.0
         self.engine = engine
         if engine is None and (native is None or native) and group is None:
             from .comm import get_engine
@@ -153,7 +154,9 @@ class GradBucketer:
             _hip.join_side_streams()  # gradients of this bucket may come from the wgrad stream
         wire_dtype = COMPRESSION[self.compression][1]
         if wire_dtype is not None and view.dtype == torch.float32:
-            b.wire = view.to(wire_dtype)
+            # fp16: pre-scaled by 1/(world x micro-steps) so the rank sum stays inside fp16's range (undone in
+            # finish); bf16 has fp32's range and travels unscaled
+            b.wire = (view * self._prescale).to(wire_dtype) if self._prescale != 1.0 else view.to(wire_dtype)
             b.handle = dist.all_reduce(b.wire, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         else:
             b.wire = None
@@ -162,9 +165,12 @@ class GradBucketer:
         self.last_launched = b.index
 
     # ---------------------------------------------------------------- step API
-    def begin(self) -> None:
+    def begin(self, micro_steps: int = 1) -> None:
         self.last_launched = None
+        self._prescale = 1.0 / (self.world * max(1, int(micro_steps))) if self.compression == "fp16" else 1.0
         if self.engine is not None:
+            if self.compression == "fp16":
+                self.engine.set_prescale(self._prescale)
             self.engine.begin_step()
             return
         for b in self.buckets:
@@ -191,7 +197,10 @@ class GradBucketer:
                 b.handle.wait()
                 b.handle = None
                 if b.wire is not None:
-                    self.store.grad[b.start:b.end].copy_(b.wire)
+                    g = self.store.grad[b.start:b.end]
+                    g.copy_(b.wire)
+                    if self._prescale != 1.0:
+                        g.mul_(1.0 / self._prescale)
                     b.wire = None
 
     @contextlib.contextmanager

@@ -12,6 +12,7 @@ complete front-to-back while backward is still running.
 """
 from __future__ import annotations
 
+import os
 import re
 from dataclasses import dataclass
 from typing import Dict, List, Optional
@@ -44,17 +45,33 @@ def _no_decay(name: str) -> bool:
     return leaf.endswith("bias") or any(t in ("ln", "ln1", "ln2") for t in toks)
 
 
-def hip_kernels_active() -> bool:
-    import os
+# Below this many tokens per rank the dgrad GEMMs read W directly (gemm2 NT with a k-strided B operand) instead of a
+# stored Wᵀ copy: the per-step Wᵀ refresh (2 x the encoder's bf16 weights through HBM) is a fixed cost that small
+# steps cannot amortise (3 % of the reference's own bert-large B = 8 S = 512 step), while at large token counts the
+# k-contiguous B read is the cheaper main loop. HSD_WT: auto (default) | 1 (always keep Wᵀ) | 0 (never).
+WT_MIN_TOKENS = int(os.environ.get("HSD_WT_MIN_TOKENS", "32768"))
 
+
+def keep_transposed_weights(rank_tokens) -> bool:
+    mode = os.environ.get("HSD_WT", "auto").lower()
+    if mode in ("0", "1"):
+        return mode == "1"
+    return rank_tokens is None or rank_tokens >= WT_MIN_TOKENS
+
+
+def hip_kernels_active() -> bool:
     return os.environ.get("HSD_OPS", "").lower() != "torch"
 
 
 class FlatParamStore:
     def __init__(self, model: nn.Module, device: torch.device, compute_dtype: torch.dtype = torch.float32,
-                 grad_dtype: torch.dtype = torch.float32, fp8: bool = False):
+                 grad_dtype: torch.dtype = torch.float32, fp8: bool = False, transposed: bool = True):
+        """``transposed``: keep bf16 Wᵀ copies of the encoder weights for the dgrad GEMMs (refreshed after every
+        optimizer step); False = the dgrads read W directly (small steps, see keep_transposed_weights). fp8 always
+        keeps them (the fp8 dgrad reads the quantised Wᵀ)."""
         self.device = torch.device(device)
         self.fp8 = fp8
+        self.keep_wt = bool(transposed) or fp8
         self.compute_dtype = compute_dtype
         self.grad_dtype = grad_dtype
         named = [(n, p) for n, p in model.named_parameters() if p.requires_grad]
@@ -101,6 +118,8 @@ class FlatParamStore:
                 cb(i)
         return ready
 
+    # The post-accumulate hook below is also where the overlapped optimizer (optim/adam.py enable_overlap) may
+    # start updating this parameter: see the invariant documented there.
     def _make_accum_hook(self, i: int):
         def hook(p):
             if p.grad is not None:
@@ -116,7 +135,7 @@ class FlatParamStore:
         self.transposed = None
         self._tdesc = None
         self._fp8_desc = None
-        if self.device.type != "cuda" or self.compute_dtype != torch.bfloat16:
+        if self.device.type != "cuda" or self.compute_dtype != torch.bfloat16 or not self.keep_wt:
             return
         idx = [i for i, n in enumerate(self.names) if TRANSPOSED_WEIGHTS.search(n) and len(self.segments[i].shape) == 2
                and self.segments[i].shape[0] % 4 == 0 and self.segments[i].shape[1] % 4 == 0]

@@ -25,6 +25,7 @@ from .. import data as hdata
 from .. import ops
 from ..models import from_pretrained, save_pretrained
 from ..optim import FusedAdam
+from ..parallel.flat_params import keep_transposed_weights
 from ..parallel import FlatParamStore, GradBucketer, ShardSampler, backend, broadcast_parameters
 from ..utils.args import parse_args
 from ..utils.env import is_sagemaker_dp_enabled
@@ -108,18 +109,26 @@ def build(args, mode: str):
     model.rng.rank = rank
     # --dtype fp8: bf16 activations / master-weight copies plus fp8 (e4m3) weight copies and per-tensor
     # quantised fp8 forward + dgrad GEMMs on the HIP path (ops/hip.py set_fp8); CPU runs stay bf16.
+    if dtype_name == "fp32" and on_gpu:
+        logger.warning("--dtype fp32 on the GPU: the reference's precision, computed by the fp32 PyTorch ops "
+                       "(hipBLASLt / rocBLAS fp32 GEMMs) with the fused fp32 Adam; the hand-written HIP kernels are "
+                       "bf16 / fp8 (use --dtype bf16 for speed)")
     fp8 = dtype_name == "fp8" and on_gpu and ops.hip_active(dev)
     if dtype_name == "fp8" and not fp8:
         logger.warning("--dtype fp8 needs the HIP path on a GPU; computing in bf16")
     if fp8:
         ops.set_fp8(True, getattr(args, "fp8_grad_format", "e4m3"))
-    store = FlatParamStore(model, dev, compute_dtype=compute_dtype, grad_dtype=grad_dtype, fp8=fp8)
+    tokenizer = hdata.load_tokenizer(args.model_name_or_path, model.cfg.vocab_size, model.cfg.model_max_length)
+    max_len = args.max_seq_length or min(tokenizer.model_max_length, model.cfg.max_position_embeddings)
+    rank_tokens = None
+    if args.train_batch_size != "auto":
+        rank_tokens = (int(args.train_batch_size) // (1 if mode == "train" else world)) * max_len
+    store = FlatParamStore(model, dev, compute_dtype=compute_dtype, grad_dtype=grad_dtype, fp8=fp8,
+                           transposed=keep_transposed_weights(rank_tokens))
     base_lr = float(args.learning_rate)
     lr = base_lr * world if mode == "train" else base_lr  # scripts/train.py:112 vs singe_node_train.py:78
     opt = FusedAdam(store, lr=lr, eps=args.adam_epsilon, eps_mode=args.adam_eps_mode,
                     weight_decay=args.weight_decay if args.optimizer == "adamw" else 0.0)
-    tokenizer = hdata.load_tokenizer(args.model_name_or_path, model.cfg.vocab_size, model.cfg.model_max_length)
-    max_len = args.max_seq_length or min(tokenizer.model_max_length, model.cfg.max_position_embeddings)
     batch_plan = None
     if args.train_batch_size == "auto":
         # sized on the device before any readiness hook / bucketer exists (the probes are plain fwd + bwd)

@@ -136,6 +136,10 @@ class Trainer:
         if (os.environ.get("HSD_OPT_OVERLAP", "1") == "0" or self.device.type != "cuda"
                 or not hasattr(self.optimizer, "enable_overlap")):
             return
+        if not getattr(self.model, "opt_overlap_safe", True):
+            # the model reads weights after their gradient hook (FusedAdam.enable_overlap's invariant): no overlap
+            logger.info("optimizer overlap off: %s sets opt_overlap_safe = False", type(self.model).__name__)
+            return
         if self.bucketer is None and self.world == 1:
             from ..optim.adam import LocalOverlap
 
@@ -203,9 +207,9 @@ class Trainer:
         else:
             self.model.rng.new_step(self.global_step)
         self.store.zero_grad()
-        if self.bucketer is not None:
-            self.bucketer.begin()
         k = len(micro_batches)
+        if self.bucketer is not None:
+            self.bucketer.begin(micro_steps=k)
         if self.lr_schedule != "constant" or self.lr_warmup_steps:
             self.optimizer.lr = self.lr_at(self.global_step)
         ov = self._opt_overlap
@@ -213,6 +217,35 @@ class Trainer:
             self.optimizer.begin_step(grad_scale=1.0 / (self.world * k))
             if ov != "engine":
                 ov.begin()
+        loss = None
+        try:
+            loss = self._micro_steps(micro_batches, meter, ov, k)
+        except BaseException:
+            if ov is not None:
+                self.optimizer.abort_step()  # the step count must not advance for a step that never happened
+            self._phase = "idle"
+            raise
+        self._phase = "allreduce-wait"
+        with prange("allreduce-wait"):
+            if self.device.type == "cuda":
+                ops.join_side_streams()
+            if self.bucketer is not None:
+                self.bucketer.finish()
+            if ov is not None and ov != "engine":
+                ov.join()
+        self._phase = "optimizer"
+        with prange("optimizer"):
+            self.optimizer.step(grad_scale=1.0 / (self.world * k))
+        self._phase = "idle"
+        self.global_step += 1
+        if self.check_sync and self.global_step % self.check_sync == 0:
+            if not params_in_sync(self.store):
+                raise RuntimeError(f"ranks diverged at step {self.global_step} (--check_sync)")
+        return loss
+
+    def _micro_steps(self, micro_batches, meter, ov, k):
+        """Forward + backward of every accumulation micro-step (the bucket all-reduces and, with the optimizer
+        overlap, the Adam slices start under the last backward)."""
         loss = None
         for i, mb in enumerate(micro_batches):
             last = i == k - 1
@@ -234,22 +267,6 @@ class Trainer:
                     loss.backward()
             if meter is not None:
                 meter.update(loss, logits, mb["labels"])
-        self._phase = "allreduce-wait"
-        with prange("allreduce-wait"):
-            if self.device.type == "cuda":
-                ops.join_side_streams()
-            if self.bucketer is not None:
-                self.bucketer.finish()
-            if ov is not None and ov != "engine":
-                ov.join()
-        self._phase = "optimizer"
-        with prange("optimizer"):
-            self.optimizer.step(grad_scale=1.0 / (self.world * k))
-        self._phase = "idle"
-        self.global_step += 1
-        if self.check_sync and self.global_step % self.check_sync == 0:
-            if not params_in_sync(self.store):
-                raise RuntimeError(f"ranks diverged at step {self.global_step} (--check_sync)")
         return loss
 
     # -------------------------------------------------------------------------- stall watchdog

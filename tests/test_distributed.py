@@ -462,3 +462,29 @@ def test_gradient_wire_compression_world2(mode):
     """Horovod's ``hvd.Compression.fp16`` (``--grad_compression``): fp32 gradient buckets all-reduced in 16 bits,
     cast back to fp32, identical on every rank, within 16-bit rounding of the fp32 sum (gloo world 2)."""
     mp.spawn(_worker_compression, args=(2, _port(), mode), nprocs=2, join=True)
+
+
+def _worker_fp16_range(rank, world, port):
+    _setenv(rank, world, port)
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel import GradBucketer, backend
+
+    backend.init(device="cpu")
+    model, store, opt, tr = _make(seed_init=7)
+    buck = GradBucketer(store, bucket_mb=0.05, compression="fp16")
+    # two accumulated micro-steps of ~40,000 per element on each of two ranks: the rank sum (~160,000) is far beyond
+    # fp16's 65,504; the 1/(world x micro-steps) pre-scale keeps the wire inside the range
+    store.grad.fill_(40000.0 + rank)
+    buck.begin(micro_steps=2)
+    for i in range(len(store.params)):
+        buck.mark_ready(i)
+    buck.finish()
+    want = 40000.0 * world + sum(range(world))
+    assert torch.isfinite(store.grad).all()
+    torch.testing.assert_close(store.grad, torch.full_like(store.grad, want), rtol=2e-3, atol=0)
+    backend.shutdown()
+
+
+def test_fp16_wire_compression_keeps_large_accumulated_gradients_finite():
+    """fp16 buckets are pre-scaled by 1/(world x micro-steps) before the cast, so large accumulated
+    gradients do not overflow to inf on the wire (gloo world 2, gradient accumulation 2)."""
+    mp.spawn(_worker_fp16_range, args=(2, _port()), nprocs=2, join=True)

@@ -185,3 +185,62 @@ def test_two_layer_bert_learns_the_marker_task(gpu, tmp_path):
     test = hdata.synthetic_classification(512, 128, 30522, seed=2)
     ev = tr.evaluate(BatchLoader(test, ShardSampler(512, 0, 1, shuffle=False, drop_last=False, batch_size=64), gpu))
     assert ev["sparse_categorical_accuracy"] > 0.95, ev
+
+
+def test_small_step_without_stored_wt_matches_with(gpu, monkeypatch):
+    """bert-large at the reference's own per-rank shape class (B = 2, S = 512: under the Wᵀ token threshold): the
+    store without Wᵀ copies (dgrads read W directly) trains exactly like the store with them -- same losses and
+    the same weights after 3 steps (the two dgrad layouts are bit-identical)."""
+    from huggingface_sagemaker_tensorflow_distributed_amd.optim import FusedAdam
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel import FlatParamStore
+    from huggingface_sagemaker_tensorflow_distributed_amd.train.trainer import Trainer
+
+    monkeypatch.setenv("HSD_OPT_OVERLAP", "0")
+    cfg = resolve_config("bert-large-uncased").replace(num_hidden_layers=2, hidden_dropout_prob=0.0,
+                                                        attention_probs_dropout_prob=0.0)
+    g = torch.Generator().manual_seed(0)
+    batches = [{"input_ids": torch.randint(5, cfg.vocab_size, (2, 512), generator=g).to(gpu),
+                "attention_mask": torch.ones(2, 512, dtype=torch.long, device=gpu),
+                "labels": torch.randint(0, 2, (2,), generator=g).to(gpu)} for _ in range(3)]
+    runs = []
+    for keep in (True, False):
+        m = build_model(cfg, seed=0).to(gpu)
+        store = FlatParamStore(m, gpu, compute_dtype=torch.bfloat16, transposed=keep)
+        assert (store.transposed is not None) == keep
+        tr = Trainer(m, store, FusedAdam(store, lr=1e-4), None, gpu)
+        losses = [float(tr.train_step([b]).detach()) for b in batches]
+        torch.cuda.synchronize()
+        runs.append((losses, store.master.clone()))
+    (l0, m0), (l1, m1) = runs
+    assert l0[0] == l1[0]
+    assert max(abs(a - b) for a, b in zip(l0, l1)) < 1e-3, (l0, l1)
+    assert float((m0 - m1).abs().max()) < 1e-3
+
+
+def test_fp32_mode_on_gpu_matches_cpu_fp32(gpu, tmp_path):
+    """--dtype fp32 (the reference's precision, scripts/train.py:113-123) trains on the GPU -- fp32 reference ops,
+    fused fp32 Adam -- and reproduces the CPU fp32 run of the same job (same seeds, data, dropout masks): the epoch
+    loss / accuracy and the eval metrics agree to fp32 summation-order noise."""
+    import os
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    out = {}
+    for device in ("cuda", "cpu"):
+        d = tmp_path / device
+        env = dict(os.environ, SM_OUTPUT_DATA_DIR=str(d / "data"), SM_MODEL_DIR=str(d / "model"), SM_NUM_GPUS="1",
+                   SM_FRAMEWORK_PARAMS="{}")
+        cmd = [sys.executable, os.path.join(root, "scripts", "train.py"), "--epochs", "1", "--train_batch_size", "8",
+               "--eval_batch_size", "8", "--model_name_or_path", "hsd-tiny-bert", "--max_seq_length", "64",
+               "--num_train_examples", "64", "--num_eval_examples", "32", "--dtype", "fp32", "--device", device,
+               "--log_every", "0"]
+        r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
+        assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+        ev = dict(line.split(" = ") for line in (d / "data" / "eval_results.txt").read_text().splitlines())
+        tr = (d / "data" / "train_results.txt").read_text().splitlines()[0]
+        out[device] = (float(ev["loss"]), float(ev["sparse_categorical_accuracy"]), float(tr.split("[")[1].split("]")[0]))
+    (gl, ga, gt), (cl, ca, ct) = out["cuda"], out["cpu"]
+    assert abs(gl - cl) < 1e-3 * max(1.0, abs(cl)), (gl, cl)
+    assert abs(gt - ct) < 1e-3 * max(1.0, abs(ct)), (gt, ct)
+    assert abs(ga - ca) <= 1.0 / 32 + 1e-9, (ga, ca)

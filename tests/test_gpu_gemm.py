@@ -296,3 +296,32 @@ def test_gemm2_small_tt_wgrad(gpu, monkeypatch, M, N, K, splits, stages):
     _check(C, C0 + A.float().t() @ B.float(), 1e-3)
 
 
+
+
+@pytest.mark.parametrize("M,N,K", [(4096, 1024, 1024), (4096, 4096, 1024), (4096, 1024, 4096), (1000, 768, 3072),
+                                   (131072 // 16, 768, 3072), (64, 1024, 1024)])
+@pytest.mark.parametrize("epi", [0, 4, 5, 9])
+def test_gemm2_dgrad_reading_w_directly_matches_stored_wt(gpu, M, N, K, epi):
+    """The dgrad on W [K][N] as the NT kernel's k-strided B operand (layout (0, 1): small steps keep no Wᵀ copy)
+    equals the dgrad on the stored Wᵀ [N][K] (layout (0, 0)) bit for bit: same fragments, same K order. Shapes cover
+    the 128 x 128 kernel, the 256 x 256 kernel, split-K slabs and a fused bias-gradient column sum."""
+    torch.manual_seed(31 + epi)
+    C_ = _C()
+    dy, w = _mk((M, K), gpu), _mk((K, N), gpu, 0.05)
+    aux = _mk((M, N), gpu) if epi != 9 else torch.rand(M, N, device=gpu).bfloat16()
+    outs = []
+    for la_lb, B in (((0, 0), w.t().contiguous()), ((0, 1), w)):
+        C = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+        db = torch.zeros(N, device=gpu) if epi in (5, 9) and N % 256 == 0 else None
+        if not C_.gemm2_supported(la_lb[0], la_lb[1], epi, M, N, K):
+            pytest.skip("shape not tiled")
+        C_.gemm2(dy, B, C, la_lb[0], la_lb[1], epi, None, aux if epi in (4, 5, 9) else None, None, 0.0, 0, 0, None, db)
+        torch.cuda.synchronize()
+        outs.append((C, db))
+    (c0, d0), (c1, d1) = outs
+    assert torch.equal(c0, c1)
+    if d0 is not None:
+        torch.testing.assert_close(d1, d0, rtol=1e-4, atol=1e-4 * float(d0.abs().max()) + 1e-6)
+    ref = dy.float() @ w.float()
+    if epi == 0:
+        _check(c1, ref)

@@ -205,3 +205,33 @@ def test_lr_schedule_linear_warmup_decay():
     assert lrs[2] == 1e-3 and all(a > b for a, b in zip(lrs[2:], lrs[3:])) and abs(lrs[9] - 1e-3 / 8) < 1e-12
     const = Trainer(m, store, FusedAdam(store, lr=1e-3), None, "cpu")
     assert all(const.lr_at(s) == 1e-3 for s in range(5))
+
+
+def test_failed_step_does_not_advance_adam_step_count():
+    """an exception between begin_step (overlapped optimizer) and step() leaves step_count unchanged."""
+    import torch
+
+    from huggingface_sagemaker_tensorflow_distributed_amd.models import build_model, resolve_config
+    from huggingface_sagemaker_tensorflow_distributed_amd.optim import FusedAdam
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel import FlatParamStore
+
+    m = build_model(resolve_config("hsd-tiny-bert"), seed=0)
+    store = FlatParamStore(m, torch.device("cpu"))
+    opt = FusedAdam(store, lr=1e-3)
+    opt.enable_overlap([(0, store.numel)])
+    opt.begin_step(grad_scale=1.0)
+    assert opt.step_count == 1
+    opt.abort_step()
+    assert opt.step_count == 0 and not opt._began
+
+
+def test_hvd_allreduce_average_rejects_integers_in_a_world_of_one():
+    """the dtype check runs before the world-size early return (same error at any world size)."""
+    import pytest
+    import torch
+
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel.collectives import hvd_allreduce
+
+    with pytest.raises(TypeError):
+        hvd_allreduce(torch.arange(4))
+    assert torch.equal(hvd_allreduce(torch.arange(4), average=False), torch.arange(4))
