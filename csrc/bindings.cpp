@@ -381,13 +381,18 @@ void gemm2(torch::Tensor A, torch::Tensor B, torch::Tensor C, int64_t la, int64_
 
 // logits [R, V] (bf16 | fp32), labels int64 [R] (-100 = ignore); stats fp32 [2] += {Σ loss, correct};
 // dlogits (optional, same dtype/shape) = (softmax - onehot) / n_valid
+// logits [rows][ld] (unit inner stride), the first V columns scored (V = 0: all); dlogits same shape / strides
 void xent(torch::Tensor logits, torch::Tensor labels, c10::optional<torch::Tensor> dlogits, torch::Tensor stats,
-          torch::Tensor n_valid) {
-  TORCH_CHECK(logits.is_cuda() && logits.dim() == 2 && logits.is_contiguous(), "xent logits");
+          torch::Tensor n_valid, int64_t V) {
+  TORCH_CHECK(logits.is_cuda() && logits.dim() == 2 && logits.stride(1) == 1, "xent logits");
   const bool bf = logits.scalar_type() == torch::kBFloat16;
   TORCH_CHECK(bf || logits.scalar_type() == torch::kFloat32, "xent logits dtype");
   TORCH_CHECK(labels.scalar_type() == torch::kInt64 && labels.is_contiguous() && labels.numel() == logits.size(0),
               "xent labels");
+  const int64_t ld = logits.size(0) > 1 ? logits.stride(0) : logits.size(1);
+  TORCH_CHECK(ld == logits.size(1), "xent: rows must be dense (the padding is the columns beyond V)");
+  if (V <= 0) V = logits.size(1);
+  TORCH_CHECK(V <= logits.size(1), "xent V");
   check_f32(stats, "stats");
   check_f32(n_valid, "n_valid");
   TORCH_CHECK(stats.numel() >= 2 && n_valid.numel() == 1, "xent stats");
@@ -398,7 +403,7 @@ void xent(torch::Tensor logits, torch::Tensor labels, c10::optional<torch::Tenso
     dl = dlogits->data_ptr();
   }
   hsd::launch_xent(logits.data_ptr(), bf, labels.data_ptr<int64_t>(), dl, stats.data_ptr<float>(),
-                   n_valid.data_ptr<float>(), (int)logits.size(0), (int)logits.size(1), cur_stream());
+                   n_valid.data_ptr<float>(), (int)logits.size(0), (int)V, ld, cur_stream());
 }
 
 // fused classification head (cls_head.hip). pre [R][H] bf16 (row stride ld), W2 [C][H], b2 [C] bf16, labels int64 [R]
@@ -530,7 +535,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm2_nt_splits", &gemm2_nt_splits);
   m.def("gemm2_supported", &gemm2_supported);
   m.def("transpose_many", &transpose_many);
-  m.def("xent", &xent);
+  m.def("xent", &xent, py::arg("logits"), py::arg("labels"), py::arg("dlogits"), py::arg("stats"),
+        py::arg("n_valid"), py::arg("V") = 0);
   m.def("cls_head_fwd", &cls_head_fwd);
   m.def("cls_head_bwd", &cls_head_bwd);
   m.def("cls_head_blocks", &cls_head_blocks);

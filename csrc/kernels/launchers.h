@@ -43,7 +43,7 @@ void launch_small_wgrad(const bf16_t* dy, int64_t ldy, const bf16_t* x, int64_t 
                         int N, int K, hipStream_t st);
 // xent.hip: fused softmax cross-entropy (+ gradient, + argmax-correct count); stats = {Σloss, correct}
 void launch_xent(const void* logits, bool bf16, const int64_t* labels, void* dlogits, float* stats,
-                 const float* n_valid, int rows, int V, hipStream_t st);
+                 const float* n_valid, int rows, int V, int64_t ld, hipStream_t st);
 // desc: int64 [n][5] = {src, dst, rows, cols, first_tile}; rows, cols multiples of 4
 void launch_transpose_many(const int64_t* desc, int n, int total_tiles, hipStream_t st);
 // cls_head.hip: fused sequence-classification head after the dense GEMM (act, dropout, classifier, CE, accuracy)

@@ -27,50 +27,48 @@ __device__ __forceinline__ void st1(void* x, int64_t i, float v) {
 template <bool kBF16>
 __global__ __launch_bounds__(256) void xent_kernel(const void* __restrict__ logits, const int64_t* __restrict__ labels,
                                                    void* __restrict__ dlogits, float* __restrict__ stats,
-                                                   const float* __restrict__ n_valid, int rows, int V) {
+                                                   const float* __restrict__ n_valid, int rows, int V, int64_t ld) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
-  const int64_t base = (int64_t)row * V;
+  const int64_t base = (int64_t)row * ld;
   const int64_t y = labels[row];
   const bool valid = y >= 0 && y < V;
   float m = -INFINITY, s = 0.f, best = -INFINITY;
   int besti = 0;
-  // vector path: 8 bf16 (or 4 fp32) per 16-B load when the row is 16-B aligned
+  // vector path: 8 bf16 (or 4 fp32) per 16-B load over the 16-B-aligned part of the row, scalar tail
   constexpr int VEC = kBF16 ? 8 : 4;
-  const bool vec = (V % VEC) == 0;
-  if (vec) {
-    for (int j = lane * VEC; j < V; j += 64 * VEC) {
-      float v[VEC];
-      if constexpr (kBF16) {
-        const u32x4 w = *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(logits) + base + j);
+  const bool vec = (ld % VEC) == 0;
+  const int Vv = vec ? V - V % VEC : 0;
+  for (int j = lane * VEC; j < Vv; j += 64 * VEC) {
+    float v[VEC];
+    if constexpr (kBF16) {
+      const u32x4 w = *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(logits) + base + j);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) { v[2 * k] = lo_bf(w[k]); v[2 * k + 1] = hi_bf(w[k]); }
-      } else {
-        const f32x4 w = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(logits) + base + j);
+      for (int k = 0; k < 4; ++k) { v[2 * k] = lo_bf(w[k]); v[2 * k + 1] = hi_bf(w[k]); }
+    } else {
+      const f32x4 w = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(logits) + base + j);
 #pragma unroll
-        for (int k = 0; k < 4; ++k) v[k] = w[k];
-      }
-      float cm = v[0];
-#pragma unroll
-      for (int k = 1; k < VEC; ++k) cm = fmaxf(cm, v[k]);
-      const float nm = fmaxf(m, cm);
-      s = s * __expf(m - nm);
-#pragma unroll
-      for (int k = 0; k < VEC; ++k) {
-        s += __expf(v[k] - nm);
-        if (v[k] > best) { best = v[k]; besti = j + k; }
-      }
-      m = nm;
+      for (int k = 0; k < 4; ++k) v[k] = w[k];
     }
-  } else {
-    for (int j = lane; j < V; j += 64) {
-      const float v = ld1<kBF16>(logits, base + j);
-      const float nm = fmaxf(m, v);
-      s = s * __expf(m - nm) + __expf(v - nm);
-      m = nm;
-      if (v > best) { best = v; besti = j; }
+    float cm = v[0];
+#pragma unroll
+    for (int k = 1; k < VEC; ++k) cm = fmaxf(cm, v[k]);
+    const float nm = fmaxf(m, cm);
+    s = s * __expf(m - nm);
+#pragma unroll
+    for (int k = 0; k < VEC; ++k) {
+      s += __expf(v[k] - nm);
+      if (v[k] > best) { best = v[k]; besti = j + k; }
     }
+    m = nm;
+  }
+  for (int j = Vv + lane; j < V; j += 64) {
+    const float v = ld1<kBF16>(logits, base + j);
+    const float nm = fmaxf(m, v);
+    s = s * __expf(m - nm) + __expf(v - nm);
+    m = nm;
+    if (v > best || (v == best && j < besti)) { best = v; besti = j; }
   }
   // wave reduction of (m, s) and argmax (lowest index on ties, like torch.argmax)
 #pragma unroll
@@ -90,21 +88,40 @@ __global__ __launch_bounds__(256) void xent_kernel(const void* __restrict__ logi
     atomicAdd(stats + 1, besti == (int)y ? 1.0f : 0.0f);
   }
   if (dlogits) {
+    // gradient over the whole padded row: columns >= V (a padded vocabulary) get exact zeros
     const float scale = valid ? inv_n : 0.f;
-    for (int j = lane; j < V; j += 64) {
-      const float p = __expf(ld1<kBF16>(logits, base + j) - lse);
-      st1<kBF16>(dlogits, base + j, scale * (p - (j == y ? 1.0f : 0.0f)));
+    if (vec) {
+      for (int j = lane * VEC; j < ld; j += 64 * VEC) {
+        float g[VEC];
+#pragma unroll
+        for (int k = 0; k < VEC; ++k) {
+          const int jj = j + k;
+          g[k] = jj < V ? scale * (__expf(ld1<kBF16>(logits, base + jj) - lse) - (jj == y ? 1.0f : 0.0f)) : 0.0f;
+        }
+        if constexpr (kBF16) {
+          *reinterpret_cast<u32x4*>(reinterpret_cast<bf16_t*>(dlogits) + base + j) =
+              u32x4{pack_bf2(g[0], g[1]), pack_bf2(g[2], g[3]), pack_bf2(g[4], g[5]), pack_bf2(g[6], g[7])};
+        } else {
+          *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(dlogits) + base + j) = f32x4{g[0], g[1], g[2], g[3]};
+        }
+      }
+    } else {
+      for (int j = lane; j < ld; j += 64) {
+        const float g = j < V ? scale * (__expf(ld1<kBF16>(logits, base + j) - lse) - (j == y ? 1.0f : 0.0f)) : 0.0f;
+        st1<kBF16>(dlogits, base + j, g);
+      }
     }
   }
 }
 
 // stats[0] += Σ loss terms, stats[1] += correct; n_valid: device scalar (number of non-ignored rows)
+// ld: row stride of logits / dlogits (>= V; a padded vocabulary's extra columns are ignored and get zero gradient)
 void launch_xent(const void* logits, bool bf16, const int64_t* labels, void* dlogits, float* stats,
-                 const float* n_valid, int rows, int V, hipStream_t st) {
+                 const float* n_valid, int rows, int V, int64_t ld, hipStream_t st) {
   const int blocks = (rows + 3) / 4;
   if (blocks == 0) return;
-  if (bf16) hipLaunchKernelGGL(xent_kernel<true>, dim3(blocks), dim3(256), 0, st, logits, labels, dlogits, stats, n_valid, rows, V);
-  else hipLaunchKernelGGL(xent_kernel<false>, dim3(blocks), dim3(256), 0, st, logits, labels, dlogits, stats, n_valid, rows, V);
+  if (bf16) hipLaunchKernelGGL(xent_kernel<true>, dim3(blocks), dim3(256), 0, st, logits, labels, dlogits, stats, n_valid, rows, V, ld);
+  else hipLaunchKernelGGL(xent_kernel<false>, dim3(blocks), dim3(256), 0, st, logits, labels, dlogits, stats, n_valid, rows, V, ld);
   HSD_CHECK_LAUNCH();
 }
 

@@ -209,12 +209,32 @@ class RobertaForMaskedLM(_Base):
     base_prefix = "roberta"
     graph_safe = False  # the masked-token gather has a data-dependent size (no HIP-graph capture)
 
+    # The decoder's vocabulary dimension (tied word embeddings, lm_head.bias) is padded to a multiple of this many
+    # rows: 50265 -> 50432 for RoBERTa, so every GEMM of the head (logits forward, its dgrad and the tied-embedding
+    # weight gradient) tiles on the hand-written MFMA kernels. The padding rows stay exactly zero (zero init, zero
+    # gradient), the loss and the returned logits cover the real vocabulary only, and checkpoints keep HF's shapes
+    # (models/hf_io.py slices on save, zero-pads on load).
+    VOCAB_PAD = 256
+
     def __init__(self, cfg: ModelConfig):
         super().__init__(cfg)
         H = cfg.hidden_size
+        self.vocab = cfg.vocab_size
+        self.vocab_padded = -(-cfg.vocab_size // self.VOCAB_PAD) * self.VOCAB_PAD
+        if self.vocab_padded != self.vocab:
+            self.encoder.embeddings.word_embeddings = _param(self.vocab_padded, H)
         self.lm_dense_weight, self.lm_dense_bias = _param(H, H), _param(H)
         self.lm_ln_weight, self.lm_ln_bias = _param(H), _param(H)
-        self.lm_bias = _param(cfg.vocab_size)
+        self.lm_bias = _param(self.vocab_padded)
+
+    def padded_rows(self):
+        """Internal parameter -> its HF row count (the rows beyond it are the zero vocabulary padding)."""
+        return {"encoder.embeddings.word_embeddings": self.vocab, "lm_bias": self.vocab}
+
+    @torch.no_grad()
+    def zero_padding_rows(self) -> None:
+        self.encoder.embeddings.word_embeddings[self.vocab:].zero_()
+        self.lm_bias[self.vocab:].zero_()
 
     def architecture(self) -> str:
         return "RobertaForMaskedLM"
@@ -231,16 +251,15 @@ class RobertaForMaskedLM(_Base):
         h = self.encoder(input_ids, attention_mask, token_type_ids, self.rng, self.training)
         B, S, H = h.shape
         x = h.view(B * S, H)
+        wemb = self.encoder.embeddings.word_embeddings
         if labels is not None:
-            # only masked positions feed the (large-vocab) decoder
-            sel = labels.view(-1).ne(-100).nonzero(as_tuple=True)[0]
-            x = x.index_select(0, sel)
-            tgt = labels.view(-1).index_select(0, sel)
+            # only masked positions feed the (large-vocab) decoder: dense + GELU -> LN -> tied decoder -> CE
+            loss, logits = ops.mlm_head(x, labels.view(-1), self.lm_dense_weight, self.lm_dense_bias, self.lm_ln_weight,
+                                        self.lm_ln_bias, c.layer_norm_eps, wemb, self.lm_bias, self.vocab)
+            return loss, logits
         x = ops.linear_gelu(x, self.lm_dense_weight, self.lm_dense_bias)
         x = ops.layer_norm(x, self.lm_ln_weight, self.lm_ln_bias, c.layer_norm_eps)
-        logits = ops.linear(x, self.encoder.embeddings.word_embeddings, self.lm_bias)
-        if labels is not None:
-            return ops.cross_entropy(logits, tgt), logits
+        logits = ops.linear(x, wemb[:self.vocab], self.lm_bias[:self.vocab])
         return logits.view(B, S, -1)
 
 
@@ -258,4 +277,6 @@ def build_model(cfg: ModelConfig, task: str = "sequence-classification", seed: O
         g = torch.Generator()
         g.manual_seed(int(seed))
     _init_(m, cfg, g)
+    if hasattr(m, "zero_padding_rows"):
+        m.zero_padding_rows()
     return m

@@ -26,9 +26,12 @@ CONFIG_NAME = "config.json"
 def hf_state_dict(model: _Base, dtype: Optional[torch.dtype] = torch.float32) -> Dict[str, torch.Tensor]:
     """Internal (fused) parameters -> HF-named tensors (Q/K/V split back apart)."""
     params = dict(model.named_parameters())
+    padded = model.padded_rows() if hasattr(model, "padded_rows") else {}
     out: Dict[str, torch.Tensor] = {}
     for hf_key, ikey, split, nsplit in model.hf_names():
         t = params[ikey].detach()
+        if ikey in padded:
+            t = t[:padded[ikey]]  # drop the zero vocabulary padding rows
         if split is not None:
             t = t.chunk(nsplit, dim=0)[split]
         t = t.to("cpu")
@@ -51,6 +54,7 @@ def load_hf_state_dict(model: _Base, sd: Dict[str, torch.Tensor], strict: bool =
             return k[len(base):]
         return None
 
+    padded = model.padded_rows() if hasattr(model, "padded_rows") else {}
     pending: Dict[str, list] = {}
     for hf_key, ikey, split, nsplit in model.hf_names():
         k = lookup(hf_key)
@@ -66,6 +70,10 @@ def load_hf_state_dict(model: _Base, sd: Dict[str, torch.Tensor], strict: bool =
                 continue
             t = parts[0] if len(parts) == 1 else torch.cat(parts, dim=0)
             dst = params[ikey]
+            if ikey in padded and t.shape[0] == padded[ikey] and tuple(t.shape[1:]) == tuple(dst.shape[1:]):
+                dst.zero_()  # HF rows, then the zero vocabulary padding
+                dst[:t.shape[0]].copy_(t.to(dst.dtype))
+                continue
             if tuple(t.shape) != tuple(dst.shape):
                 raise ValueError(f"shape mismatch for {ikey}: checkpoint {tuple(t.shape)} vs model {tuple(dst.shape)}")
             dst.copy_(t.to(dst.dtype))

@@ -159,5 +159,24 @@ def cls_head(h, w1, b1, w2, b2, labels, act: str, p_in: float, seed_in: int, p: 
     return cross_entropy(logits, labels), logits
 
 
+def mlm_head(h2d, labels, w1, b1, ln_w, ln_b, eps, wemb, bias, vocab):
+    """Masked-LM head (RoBERTa) on the masked rows of ``h2d`` -> (loss, logits over the real vocabulary).
+
+    GPU: every GEMM on gemm2 (dense + GELU epilogue, LN kernel, the tied decoder over the 256-padded vocabulary, its
+    dgrad reading the embedding table directly and the embedding-table weight gradient), the chunked-vocabulary CE
+    kernel; the argmax-hit count rides on ``loss._hsd_correct``."""
+    if _hip(h2d) and h2d.dtype == torch.bfloat16 and _hipmod().mlm_head_ok(h2d, w1, wemb):
+        loss, logits, correct = _hipmod().mlm_head(h2d, labels, w1, b1, ln_w, ln_b, eps, wemb, bias, vocab)
+        loss._hsd_correct = correct
+        return loss, logits
+    if _hip(h2d):
+        sel = labels.ne(-100).nonzero(as_tuple=True)[0]
+        x = h2d.index_select(0, sel)
+        x = layer_norm(linear_gelu(x, w1, b1), ln_w, ln_b, eps)
+        logits = linear(x, wemb[:vocab], bias[:vocab])
+        return cross_entropy(logits, labels.index_select(0, sel)), logits
+    return _ref.mlm_head(h2d, labels, w1, b1, ln_w, ln_b, eps, wemb, bias, vocab)
+
+
 def accuracy_count(logits, labels):
     return _ref.accuracy_count(logits, labels)

@@ -184,12 +184,19 @@ def linear(x, w, b):
 
 
 class _LinearGelu(torch.autograd.Function):
+    """gelu(x Wᵀ + b): gemm2 with the bias + GELU epilogue (pre-activation and activation out) when the shape tiles;
+    backward: GELU' + bias column sums in one kernel, then gemm2 dgrad / wgrad."""
+
     @staticmethod
     def forward(ctx, x, w, b):
-        x2 = x.reshape(-1, x.shape[-1])
-        y = torch.addmm(b, x2, w.t())
-        g = torch.empty_like(y)
-        _C.gelu_fwd(y, g)
+        x2 = x.reshape(-1, x.shape[-1]).contiguous()
+        if x2.dtype == torch.bfloat16 and _nt_ok(x2.shape[0], w.shape[0], x2.shape[1], EPI_BIAS_GELU):
+            g = torch.empty((x2.shape[0], w.shape[0]), dtype=x2.dtype, device=x2.device)
+            y = gemm_fwd(x2, w, EPI_BIAS_GELU, bias=b, out2=g)
+        else:
+            y = torch.addmm(b, x2, w.t())
+            g = torch.empty_like(y)
+            _C.gelu_fwd(y, g)
         ctx.save_for_backward(x2, w, b, y)
         ctx.xshape = x.shape
         return g.view(*x.shape[:-1], w.shape[0])
@@ -201,8 +208,16 @@ class _LinearGelu(torch.autograd.Function):
         gw, gb = _Grad(w), _Grad(b)
         da = torch.empty_like(y)
         _C.gelu_bwd_colsum(dg2, y, da, gb.buf)
-        dx = torch.mm(da, w).view(ctx.xshape) if ctx.needs_input_grad[0] else None
-        _wgrad_(gw, da, x2)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if da.dtype == torch.bfloat16 and _nt_ok(da.shape[0], w.shape[1], da.shape[1], EPI_STORE):
+                dx = gemm_dgrad(da, w).view(ctx.xshape)
+            else:
+                dx = torch.mm(da, w).view(ctx.xshape)
+        if da.dtype == torch.bfloat16 and _C.gemm2_supported(1, 1, 7, w.shape[0], w.shape[1], da.shape[0]):
+            gemm_wgrad_(gw, da, x2)
+        else:
+            _wgrad_(gw, da, x2)
         return dx, gw.done(), gb.done()
 
 
@@ -214,8 +229,11 @@ def linear_gelu(x, w, b):
 class _DenseResidualLN(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, res, ln_w, ln_b, eps, p, seed):
-        x2 = x.reshape(-1, x.shape[-1])
-        y = torch.addmm(b, x2, w.t())
+        x2 = x.reshape(-1, x.shape[-1]).contiguous()
+        if x2.dtype == torch.bfloat16 and _nt_ok(x2.shape[0], w.shape[0], x2.shape[1], EPI_BIAS):
+            y = gemm_fwd(x2, w, EPI_BIAS, bias=b)
+        else:
+            y = torch.addmm(b, x2, w.t())
         rows, H = y.shape
         z = torch.empty_like(y)
         out = torch.empty_like(y)
@@ -239,8 +257,16 @@ class _DenseResidualLN(torch.autograd.Function):
             _C.ln_bwd(dout2, z, mean, rstd, ln_w, None, dy, None, gg.buf, gbe.buf, gb.buf, 0.0, 0)
             dz = dy
         gln_w, gln_b = gg.done(), gbe.done()
-        dx = torch.mm(dy, w).view(ctx.xshape) if ctx.needs_input_grad[0] else None
-        _wgrad_(gw, dy, x2)
+        dx = None
+        if ctx.needs_input_grad[0]:
+            if _nt_ok(dy.shape[0], w.shape[1], dy.shape[1], EPI_STORE):
+                dx = gemm_dgrad(dy, w).view(ctx.xshape)
+            else:
+                dx = torch.mm(dy, w).view(ctx.xshape)
+        if _C.gemm2_supported(1, 1, 7, w.shape[0], w.shape[1], dy.shape[0]):
+            gemm_wgrad_(gw, dy, x2)
+        else:
+            _wgrad_(gw, dy, x2)
         return dx, gw.done(), gb.done(), dz.view(dout.shape), gln_w, gln_b, None, None, None
 
 
@@ -726,6 +752,91 @@ def cls_head(h, w1, b1, w2, b2, labels, act, p_in, seed_in, p, seed):
     """(loss, logits, stats) of the fused classification head (labels required); stats = fp32
     {mean loss, argmax hits, rows scored, loss sum}."""
     return _ClsHead.apply(h, w1, b1, w2, b2, labels, act, p_in, seed_in, p, seed)
+
+
+# ------------------------------------------------------------------------------------------ masked-LM head
+def mlm_head_ok(h2d, w1, wemb) -> bool:
+    T, H = h2d.shape
+    Vp = wemb.shape[0]
+    return (H % 64 == 0 and w1.shape == (H, H) and Vp % 256 == 0 and wemb.shape[1] == H and wemb.is_contiguous()
+            and _C.gemm2_supported(0, 0, EPI_BIAS, 64, Vp, H) and _C.gemm2_supported(0, 1, EPI_STORE, 64, H, Vp))
+
+
+class _MlmHead(torch.autograd.Function):
+    """RoBERTa LM head on the masked rows, every GEMM on gemm2 (SURVEY.md §2.10 K16 MLM variant):
+
+    forward   x = h[masked] (row count padded to a multiple of 64 with ignored rows) -> gemm2 NT, bias + GELU
+              epilogue writing pre-activation and activation -> LN kernel -> gemm2 NT against the tied word
+              embeddings [Vp, H] (Vp = vocabulary padded to 256) with the lm_head bias -> xent kernel over the real
+              vocabulary columns (the padding columns get zero gradient)
+    backward  decoder bias grad = column sums of dlogits; tied-embedding grad += dlogitsᵀ · y (gemm2 TT: the
+              padded token count is a whole number of 64-token K-tiles); dy = dlogits · Wemb (gemm2 NT reading the
+              table directly as its k-strided B); LN bwd; GELU' + dense bias grad (one kernel); dense wgrad / dgrad;
+              the masked rows' gradient into a zeroed dh."""
+
+    @staticmethod
+    def forward(ctx, h2d, labels, w1, b1, ln_w, ln_b, eps, wemb, bias, vocab):
+        T, H = h2d.shape
+        Vp = wemb.shape[0]
+        lab = labels.reshape(-1)
+        sel = lab.ne(-100).nonzero(as_tuple=True)[0]
+        n = int(sel.numel())
+        npad = max(64, -(-n // 64) * 64)
+        idx = torch.zeros(npad, dtype=torch.long, device=h2d.device)
+        idx[:n] = sel
+        tgt = torch.full((npad,), -100, dtype=torch.long, device=h2d.device)
+        tgt[:n] = lab.index_select(0, sel)
+        x = h2d.index_select(0, idx)
+        act = torch.empty((npad, H), dtype=h2d.dtype, device=h2d.device)
+        pre = gemm_fwd(x, w1, EPI_BIAS_GELU, bias=b1, out2=act)
+        y, mean, rstd = _ln_fwd(act, ln_w, ln_b, eps)
+        logits = gemm_fwd(y, wemb, EPI_BIAS, bias=bias)
+        stats = torch.zeros(2, dtype=torch.float32, device=h2d.device)
+        n_valid = torch.full((1,), float(n), dtype=torch.float32, device=h2d.device)
+        dlogits = torch.empty_like(logits)
+        _C.xent(logits, tgt, dlogits, stats, n_valid, vocab)
+        loss = stats[0] * (1.0 / max(n, 1))
+        ctx.save_for_backward(x, sel, w1, b1, pre, act, y, mean, rstd, ln_w, ln_b, wemb, bias, dlogits)
+        ctx.cfg = (T, H, n)
+        ctx.mark_non_differentiable(stats)
+        ctx.set_materialize_grads(False)
+        return loss, logits[:n, :vocab], stats[1]
+
+    @staticmethod
+    def backward(ctx, dloss, _dlogits, _dcorrect):
+        x, sel, w1, b1, pre, act, y, mean, rstd, ln_w, ln_b, wemb, bias, dlogits = ctx.saved_tensors
+        T, H, n = ctx.cfg
+        g_wemb, g_w1, g_b1, g_lnw, g_lnb, g_bias = _Grad(wemb), _Grad(w1), _Grad(b1), _Grad(ln_w), _Grad(ln_b), _Grad(bias)
+        if dloss is None:
+            dloss = torch.zeros((), dtype=torch.float32, device=x.device)
+        dl = dloss.reshape(1).to(torch.float32)
+        # decoder bias: column sums of dlogits, scaled by the incoming loss gradient
+        cs = torch.zeros(dlogits.shape[1], dtype=torch.float32, device=x.device)
+        _C.colsum(dlogits, cs)
+        g_bias.buf.add_(cs * dl)
+        # tied embedding table: += dlogitsᵀ · (y · dloss)   (dlogits is already 1/n-scaled by the CE kernel)
+        gemm_wgrad_(g_wemb, dlogits, (y * dl.to(y.dtype)).contiguous())
+        r_wemb = g_wemb.done()
+        dy = torch.empty_like(y)
+        _C.gemm2(dlogits, wemb, dy, 0, 1, EPI_STORE, None, None, None, 0.0, 0, 0, None, None)
+        dy.mul_(dl.to(dy.dtype))
+        dact = torch.empty_like(act)
+        _C.ln_bwd(dy, act, mean, rstd, ln_w, None, dact, None, g_lnw.buf, g_lnb.buf, None, 0.0, 0)
+        dpre = torch.empty_like(pre)
+        _C.gelu_bwd_colsum(dact, pre, dpre, g_b1.buf)
+        gemm_wgrad_(g_w1, dpre, x)
+        dh = None
+        if ctx.needs_input_grad[0]:
+            dx = gemm_dgrad(dpre, w1)
+            dh = torch.empty((T, H), dtype=dx.dtype, device=dx.device)
+            _C.memset0(dh)
+            dh.index_copy_(0, sel, dx[:n])
+        return (dh, None, g_w1.done(), g_b1.done(), g_lnw.done(), g_lnb.done(), None, r_wemb, g_bias.done(), None)
+
+
+def mlm_head(h2d, labels, w1, b1, ln_w, ln_b, eps, wemb, bias, vocab):
+    """(loss, logits [n_masked, vocab], argmax hits) of the fused masked-LM head."""
+    return _MlmHead.apply(h2d, labels, w1, b1, ln_w, ln_b, eps, wemb, bias, vocab)
 
 
 # ------------------------------------------------------------------------------------------ loss

@@ -98,3 +98,13 @@ def cls_head(x, w1, b1, w2, b2, act: str, p_in: float, seed_in: int, p: float, s
     h = torch.tanh(h) if act == "tanh" else torch.relu(h)
     h = dropout(h, p, seed, training)
     return F.linear(h, w2, b2)
+
+
+def mlm_head(h2d, labels, w1, b1, ln_w, ln_b, eps: float, wemb, bias, vocab: int):
+    """RoBERTa LM head on the masked positions (labels != -100) of ``h2d`` [T, H]: ``LN(gelu(x W1ᵀ + b1))`` ->
+    tied decoder (``wemb[:vocab]``, ``bias[:vocab]``) -> mean CE. Returns (loss, logits [n_masked, vocab])."""
+    sel = labels.ne(-100).nonzero(as_tuple=True)[0]
+    x = h2d.index_select(0, sel)
+    x = layer_norm(linear_gelu(x, w1, b1), ln_w, ln_b, eps)
+    logits = F.linear(x, wemb[:vocab], bias[:vocab])
+    return cross_entropy(logits, labels.index_select(0, sel)), logits

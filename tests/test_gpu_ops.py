@@ -330,3 +330,42 @@ def test_fused_cls_head_vs_reference(gpu, model, B, C, H, p):
         rel = (a - b).norm() / (b.norm() + 1e-6)
         assert rel < 4e-2, f"{n}: rel err {rel:.3g}"
     assert torch.count_nonzero(g_hip[0][:, 1:]) == 0  # only the first-token rows receive gradient
+
+
+@pytest.mark.parametrize("H", [256, 1024])
+def test_mlm_head_vs_reference(gpu, H):
+    """The masked-LM head at RoBERTa's vocabulary (V = 50265, padded to 50432 inside the model): every GEMM on gemm2
+    (no library GEMM), CE over the real vocabulary only, vs the fp32 reference on the unpadded table."""
+    from huggingface_sagemaker_tensorflow_distributed_amd import ops
+
+    torch.manual_seed(23)
+    V, Vp, T = 50265, 50432, 512
+    mk = lambda *s, sc=0.05: (torch.randn(*s, device=gpu) * sc).bfloat16()  # noqa: E731
+    h = torch.randn(T, H, device=gpu).bfloat16().requires_grad_()
+    w1, b1 = mk(H, H).requires_grad_(), mk(H).requires_grad_()
+    lw = (1 + 0.1 * torch.randn(H, device=gpu)).bfloat16().requires_grad_()
+    lb = mk(H).requires_grad_()
+    wemb = mk(Vp, H)
+    wemb[V:] = 0
+    wemb.requires_grad_()
+    bias = mk(Vp)
+    bias[V:] = 0
+    bias.requires_grad_()
+    labels = torch.full((T,), -100, device=gpu, dtype=torch.long)
+    m = torch.rand(T, device=gpu) < 0.15
+    labels[m] = torch.randint(0, V, (int(m.sum()),), device=gpu)
+    params = [h, w1, b1, lw, lb, wemb, bias]
+    loss, logits = ops.mlm_head(h, labels, w1, b1, lw, lb, 1e-5, wemb, bias, V)
+    assert getattr(loss, "_hsd_correct", None) is not None, "the fused HIP head did not run"
+    assert logits.shape == (int(m.sum()), V)
+    loss.backward()
+    g_hip = [t.grad.float() for t in params]
+    f = [t.detach().float().requires_grad_() for t in params]
+    loss_ref, lg_ref = ref.mlm_head(f[0], labels, f[1], f[2], f[3], f[4], 1e-5, f[5], f[6], V)
+    loss_ref.backward()
+    assert abs(loss.item() - loss_ref.item()) < 1e-2 * abs(loss_ref.item()), (loss.item(), loss_ref.item())
+    _close(logits, lg_ref, 3e-2, 3e-2, "logits")
+    for n, a, b in zip(["h", "w1", "b1", "ln_w", "ln_b", "wemb", "bias"], g_hip, [t.grad for t in f]):
+        rel = (a - b).norm() / (b.norm() + 1e-6)
+        assert rel < 5e-2, f"{n}: rel err {rel:.3g}"
+    assert torch.count_nonzero(g_hip[5][V:]) == 0 and torch.count_nonzero(g_hip[6][V:]) == 0  # padding stays 0
