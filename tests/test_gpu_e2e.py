@@ -133,6 +133,7 @@ def test_optimizer_overlapped_with_backward_uses_final_gradients(gpu, monkeypatc
                for i in range(4)]
     monkeypatch.setenv("HSD_OPT_OVERLAP", "1")
     monkeypatch.setenv("HSD_OPT_BUCKET_MB", "4")  # many slices
+    monkeypatch.setenv("HSD_WT", "1")  # keep the Wᵀ copies at this small step (their per-slice refresh is checked)
     args, _ = build_parser("train").parse_known_args(
         ["--model_name_or_path", "bert-base-uncased", "--train_batch_size", "8", "--learning_rate", "1e-4",
          "--dtype", "bf16", "--log_every", "0", "--seed", "3"])
