@@ -118,6 +118,114 @@ __device__ __forceinline__ bf16x8 frag(const bf16_t* img, int rbase, int ks, int
   }
 }
 
+// Staggered 4-phase main loop (SYNC 4 / 5 / 7) over nt K-tiles from kbeg, shared by gemm2_kernel and the persistent
+// gemm2pk_kernel. PRO: issue the prologue (tile 0 whole + D0 slots of tile 1 -> stage 0 / 1, retire tile 0, first
+// barrier) here; without it the caller has done exactly that (the persistent kernel, under the previous tile's
+// epilogue). Enters with every wave at the same barrier count; leaves the same way.
+template <int LA, int LB, int BN, int SYNC, int G, int D0, bool PRO, class DMA>
+__device__ __forceinline__ void mainloop_staggered(f32x4 (&acc)[8][BN / 64], bf16_t* smem, const DMA& dma_slot,
+                                                   int nt, int kbeg, int wm, int arow, int bcol, int lane) {
+  constexpr int WN = BN / 4, NREP = WN / 16, NB0 = 2, NB1 = NREP - NB0;
+  constexpr int TA = BM * 64, STAGE = TA + BN * 64;
+  bf16x8 fa[4][2], fb0[NB0][2], fb1[NB1][2];
+  // Staggered 4-phase schedule (cdna_hip_programming.md §5 "256² 8-phase template"; MI355X_MICROARCH.md
+  // "Two waves per SIMD" item 9): the wave groups wm = 0 / 1 — one wave of each on every SIMD — run ONE
+  // barrier apart, so on every SIMD one wave's MFMA cluster overlaps the other wave's LDS reads and DMA
+  // issue. Each phase is   reads (+ DMA issue) -> lgkmcnt(0) -> barrier -> MFMA cluster -> barrier.
+  // * lgkmcnt(0) before the barrier: a group one barrier behind has COMPLETED (not just issued) the reads
+  //   of the phase it is in, so the P4 DMA into the current stage (tile t+2) cannot overwrite live data.
+  // * the counted vmcnt sits before P4's FIRST barrier (one barrier earlier than the unstaggered form), so
+  //   the lagging group's DMAs of tile t+1 have landed before the leading group reads them in P1(t+1).
+  // Tile t+1's DMA: SYNC 4 issues it in P1 / P2 (two MFMA phases to land), SYNC 5 spreads it over
+  // P1 / P2 / P3 (2 pieces per phase, fewer issue stalls per phase); D0 slots of tile t+2 go out in P4.
+  constexpr int E1 = SYNC != 5 ? D0 + (G - D0 + 1) / 2 : D0 + 2;
+  constexpr int E2 = SYNC != 5 ? G : (D0 + 4 < G ? D0 + 4 : G);
+#define G2_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
+#define G2_CLUSTER(ACC_I0, FA, FB, NBX, J0)                                                                  \
+  __builtin_amdgcn_s_setprio(1);                                                                             \
+  _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) _Pragma("unroll") for (int i = 0; i < 4; ++i)               \
+      _Pragma("unroll") for (int j = 0; j < NBX; ++j) acc[ACC_I0 + i][J0 + j] =                                \
+          __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[j][ks], FA[i][ks], acc[ACC_I0 + i][J0 + j], 0, 0, 0);     \
+  __builtin_amdgcn_s_setprio(0);
+  if constexpr (PRO) {
+#pragma unroll
+    for (int q = 0; q < G; ++q) dma_slot(q, smem, kbeg);
+    if (nt > 1) {
+#pragma unroll
+      for (int q = 0; q < D0; ++q) dma_slot(q, smem + STAGE, kbeg + BK);
+      vmcnt<D0>();
+    } else {
+      vmcnt<0>();
+    }
+    G2_BARRIER();
+  }
+  if (wm == 1) G2_BARRIER();
+  for (int t = 0; t < nt; ++t) {
+    const bf16_t* cA = smem + (t & 1) * STAGE;
+    const bf16_t* cB = cA + TA;
+    bf16_t* nS = smem + ((t + 1) & 1) * STAGE;
+    const bool n1 = t + 1 < nt, n2 = t + 2 < nt;
+    const int k1 = kbeg + (t + 1) * BK, k2 = kbeg + (t + 2) * BK;
+    // P1: A-sub0 + B-sub0 reads, first part of tile t+1's DMA
+#pragma unroll
+    for (int j = 0; j < NB0; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) fb0[j][ks] = frag<LB>(cB, bcol + 16 * j, ks, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<LA>(cA, arow + 16 * i, ks, lane);
+    if (n1) {
+#pragma unroll
+      for (int q = D0; q < E1; ++q) dma_slot(q, nS, k1);
+    }
+    G2_LGKM0();
+    G2_BARRIER();
+    G2_CLUSTER(0, fa, fb0, NB0, 0)
+    G2_BARRIER();
+    // P2: B-sub1 reads, more of tile t+1's DMA
+#pragma unroll
+    for (int j = 0; j < NB1; ++j)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) fb1[j][ks] = frag<LB>(cB, bcol + 16 * (NB0 + j), ks, lane);
+    if (n1) {
+#pragma unroll
+      for (int q = E1; q < E2; ++q) dma_slot(q, nS, k1);
+    }
+    G2_LGKM0();
+    G2_BARRIER();
+    G2_CLUSTER(0, fa, fb1, NB1, NB0)
+    G2_BARRIER();
+    // P3: A-sub1 reads (+ the rest of tile t+1's DMA, SYNC 5)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<LA>(cA, arow + 64 + 16 * i, ks, lane);
+    if (n1) {
+#pragma unroll
+      for (int q = E2; q < G; ++q) dma_slot(q, nS, k1);
+    }
+    G2_LGKM0();
+    G2_BARRIER();
+    G2_CLUSTER(4, fa, fb1, NB1, NB0)
+    G2_BARRIER();
+    // P4: no reads; D0 slots of tile t+2 into this stage; retire tile t+1
+    if (n2) {
+#pragma unroll
+      for (int q = 0; q < D0; ++q) dma_slot(q, const_cast<bf16_t*>(cA), k2);
+      vmcnt<D0>();
+    } else {
+      vmcnt<0>();
+    }
+    G2_BARRIER();
+    G2_CLUSTER(4, fa, fb0, NB0, 0)
+    G2_BARRIER();
+  }
+  if (wm == 0) G2_BARRIER();
+#undef G2_CLUSTER
+#undef G2_LGKM0
+}
+
 template <int LA, int LB, int EPI, int BN, int SYNC>
 __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
   p.dp = resolve_seed(p.dp);
@@ -365,100 +473,7 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
 #undef G2_MMA
 #undef G2_SB
   } else if constexpr (SYNC == 4 || SYNC == 5 || SYNC == 7) {
-    // Staggered 4-phase schedule (cdna_hip_programming.md §5 "256² 8-phase template"; MI355X_MICROARCH.md
-    // "Two waves per SIMD" item 9): the wave groups wm = 0 / 1 — one wave of each on every SIMD — run ONE
-    // barrier apart, so on every SIMD one wave's MFMA cluster overlaps the other wave's LDS reads and DMA
-    // issue. Each phase is   reads (+ DMA issue) -> lgkmcnt(0) -> barrier -> MFMA cluster -> barrier.
-    // * lgkmcnt(0) before the barrier: a group one barrier behind has COMPLETED (not just issued) the reads
-    //   of the phase it is in, so the P4 DMA into the current stage (tile t+2) cannot overwrite live data.
-    // * the counted vmcnt sits before P4's FIRST barrier (one barrier earlier than the unstaggered form), so
-    //   the lagging group's DMAs of tile t+1 have landed before the leading group reads them in P1(t+1).
-    // Tile t+1's DMA: SYNC 4 issues it in P1 / P2 (two MFMA phases to land), SYNC 5 spreads it over
-    // P1 / P2 / P3 (2 pieces per phase, fewer issue stalls per phase); D0 slots of tile t+2 go out in P4.
-    constexpr int E1 = SYNC != 5 ? D0 + (G - D0 + 1) / 2 : D0 + 2;
-    constexpr int E2 = SYNC != 5 ? G : (D0 + 4 < G ? D0 + 4 : G);
-#define G2_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
-#define G2_CLUSTER(ACC_I0, FA, FB, NBX, J0)                                                                  \
-  __builtin_amdgcn_s_setprio(1);                                                                             \
-  _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) _Pragma("unroll") for (int i = 0; i < 4; ++i)               \
-      _Pragma("unroll") for (int j = 0; j < NBX; ++j) acc[ACC_I0 + i][J0 + j] =                                \
-          __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[j][ks], FA[i][ks], acc[ACC_I0 + i][J0 + j], 0, 0, 0);     \
-  __builtin_amdgcn_s_setprio(0);
-#pragma unroll
-    for (int q = 0; q < G; ++q) dma_slot(q, smem, kbeg);
-    if (nt > 1) {
-#pragma unroll
-      for (int q = 0; q < D0; ++q) dma_slot(q, smem + STAGE, kbeg + BK);
-      vmcnt<D0>();
-    } else {
-      vmcnt<0>();
-    }
-    G2_BARRIER();
-    if (wm == 1) G2_BARRIER();
-    for (int t = 0; t < nt; ++t) {
-      const bf16_t* cA = smem + (t & 1) * STAGE;
-      const bf16_t* cB = cA + TA;
-      bf16_t* nS = smem + ((t + 1) & 1) * STAGE;
-      const bool n1 = t + 1 < nt, n2 = t + 2 < nt;
-      const int k1 = kbeg + (t + 1) * BK, k2 = kbeg + (t + 2) * BK;
-      // P1: A-sub0 + B-sub0 reads, first part of tile t+1's DMA
-#pragma unroll
-      for (int j = 0; j < NB0; ++j)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) fb0[j][ks] = frag<LB>(cB, bcol + 16 * j, ks, lane);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<LA>(cA, arow + 16 * i, ks, lane);
-      if (n1) {
-#pragma unroll
-        for (int q = D0; q < E1; ++q) dma_slot(q, nS, k1);
-      }
-      G2_LGKM0();
-      G2_BARRIER();
-      G2_CLUSTER(0, fa, fb0, NB0, 0)
-      G2_BARRIER();
-      // P2: B-sub1 reads, more of tile t+1's DMA
-#pragma unroll
-      for (int j = 0; j < NB1; ++j)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) fb1[j][ks] = frag<LB>(cB, bcol + 16 * (NB0 + j), ks, lane);
-      if (n1) {
-#pragma unroll
-        for (int q = E1; q < E2; ++q) dma_slot(q, nS, k1);
-      }
-      G2_LGKM0();
-      G2_BARRIER();
-      G2_CLUSTER(0, fa, fb1, NB1, NB0)
-      G2_BARRIER();
-      // P3: A-sub1 reads (+ the rest of tile t+1's DMA, SYNC 5)
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<LA>(cA, arow + 64 + 16 * i, ks, lane);
-      if (n1) {
-#pragma unroll
-        for (int q = E2; q < G; ++q) dma_slot(q, nS, k1);
-      }
-      G2_LGKM0();
-      G2_BARRIER();
-      G2_CLUSTER(4, fa, fb1, NB1, NB0)
-      G2_BARRIER();
-      // P4: no reads; D0 slots of tile t+2 into this stage; retire tile t+1
-      if (n2) {
-#pragma unroll
-        for (int q = 0; q < D0; ++q) dma_slot(q, const_cast<bf16_t*>(cA), k2);
-        vmcnt<D0>();
-      } else {
-        vmcnt<0>();
-      }
-      G2_BARRIER();
-      G2_CLUSTER(4, fa, fb0, NB0, 0)
-      G2_BARRIER();
-    }
-    if (wm == 0) G2_BARRIER();
-#undef G2_CLUSTER
-#undef G2_LGKM0
+    mainloop_staggered<LA, LB, BN, SYNC, G, D0, true>(acc, smem, dma_slot, nt, kbeg, wm, arow, bcol, lane);
   } else {
     // ONE barrier per K-tile: tile t+1's DMA (into the other stage, free since the previous barrier) is
     // issued in two halves at the start of P1 / P2 and retired by vmcnt(0) before the end-of-tile
@@ -556,6 +571,111 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
     }
   } else {
     epilogue_bf16<EPI, BN>(acc, p, smem, wave, lane, mw, nw);
+  }
+}
+
+// Persistent NT GEMM (k-contiguous A and B, bf16 epilogues, no split-K): grid = min(tiles, CUs), one workgroup per
+// CU walking tiles v = bid, bid + grid, ... through the same XCD-aware remap as gemm2_kernel (grid is a multiple of
+// 8, so tile L and workgroup bid share an XCD). Main loop = gemm2_kernel's SYNC 4 schedule, unchanged. What changes
+// is the seam between tiles: a one-shot kernel pays, per tile, the new workgroup's prologue (address setup + the
+// first K-tile's DMA round trip, ~1-2 us at HBM latency under load) AFTER the previous workgroup's stores drained.
+// Here the next tile's prologue DMA (K-tile 0 into stage 0, D0 slots of K-tile 1 into stage 1) is issued right after
+// the main loop, BEFORE the epilogue, and lands while the epilogue stages and stores the finished tile through its
+// own 32 KiB LDS area (32-row passes; 2 x 64 KiB operand stages + 32 KiB = the whole 160 KiB).
+// Ordering rules (gfx9-family vector-memory counter: loads AND stores retire in issue order -- hipcc itself emits
+// counted vmcnt waits with stores outstanding):
+// * the epilogue's bias and first-pass residual loads are issued BEFORE the DMA, so waiting on them never waits on
+//   the DMA; later passes' residual loads do -- by then the DMA has had a pass to land;
+// * the DMA is inline asm (invisible to hipcc), so hipcc's wait for an epilogue LDS store cannot turn into a drain;
+// * after the epilogue, vmcnt<D0 + stores issued since> + barrier retires the next tile's K-tile 0 for every wave
+//   while the epilogue's stores are still in flight (they drain under the next tile's first K-tile).
+template <int EPI, int BN>
+__global__ __launch_bounds__(512, 1) void gemm2pk_kernel(G2Params p) {
+  p.dp = resolve_seed(p.dp);
+  static_assert(epi_bf16_out(EPI), "bf16 epilogues");
+  constexpr int WN = BN / 4, NREP = WN / 16;
+  constexpr int TA = BM * 64, STAGE = TA + BN * 64;
+  constexpr int GA = 4, GB = BN / 64, G = GA + GB, D0 = 2;
+  constexpr int PB = 2;                                  // 32-row epilogue passes
+  constexpr int STG = 8 * 16 * PB * epi_srow<BN>();      // epilogue staging, elements
+  constexpr int ITER = epi_iter<BN, PB>();
+  constexpr int NST = (8 / PB) * ITER * (epi_two_out(EPI) ? 2 : 1);  // epilogue stores per wave, all rows inside M
+  static_assert(D0 + NST <= 63, "vmcnt field");
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * STAGE + STG];
+  static_assert(sizeof(smem) <= 160 * 1024, "LDS");
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int ntiles = p.ntiles, q8 = ntiles >> 3, r8 = ntiles & 7;
+  const int nt = p.K / BK;
+  HSD_DASSERT(p.K % BK == 0 && nt >= 1 && (gridDim.x == (unsigned)ntiles || gridDim.x % 8 == 0));
+  auto tile_of = [&](int L, int& m0, int& n0) {
+    const int xcd = L & 7;
+    const int v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (L >> 3);
+    m0 = (v / p.tiles_n) * BM;
+    n0 = (v % p.tiles_n) * BN;
+  };
+  const uint32_t smem_lds = (uint32_t)(size_t)(__attribute__((address_space(3))) bf16_t*)smem;
+  uint32_t aoff[G];
+  int m0, n0;
+  auto set_tile = [&](int L) {
+    tile_of(L, m0, n0);
+#pragma unroll
+    for (int q = 0; q < G; ++q)
+      aoff[q] = q < GA ? lane_off<0>(p.lda, m0, p.M, wave * GA + q, lane)
+                       : lane_off<0>(p.ldb, n0, p.N, wave * GB + (q - GA), lane);
+  };
+  auto dma_slot = [&](int q, bf16_t* stage, int k0) {
+    const uint32_t st = smem_lds + (uint32_t)(stage - smem) * 2u;
+    if (q < GA) dma_lds_asm(asm_base<0>(p.A, p.lda, m0, k0), aoff[q], st + (wave * GA + q) * 1024u);
+    else dma_lds_asm(asm_base<0>(p.B, p.ldb, n0, k0), aoff[q], st + (TA + (wave * GB + (q - GA)) * 512) * 2u);
+  };
+  auto prologue = [&]() {
+#pragma unroll
+    for (int q = 0; q < G; ++q) dma_slot(q, smem, 0);
+    if (nt > 1) {
+#pragma unroll
+      for (int q = 0; q < D0; ++q) dma_slot(q, smem + STAGE, BK);
+    }
+  };
+
+  const int arow = wm * 128, bcol = wn * WN;
+  int L = blockIdx.x;
+  set_tile(L);
+  prologue();
+  vmcnt<0>();
+  G2_BARRIER();
+  f32x4 acc[8][NREP];
+  for (;;) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < NREP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    mainloop_staggered<0, 0, BN, 4, G, D0, false>(acc, smem, dma_slot, nt, 0, wm, arow, bcol, lane);
+    const int mw = m0 + arow, nw = n0 + bcol;
+    f32x4 bv[NREP];
+    u32x4 xv0[ITER];
+    epi_bias_regs<EPI, BN>(bv, p, lane, nw);
+    epi_aux_regs<EPI, BN, PB>(xv0, p, lane, mw, nw, 0);
+    L += gridDim.x;
+    const bool more = L < ntiles;
+    if (more) {
+      set_tile(L);
+      prologue();
+    }
+    epilogue_bf16<EPI, BN, 8, PB, true>(acc, p, smem + 2 * STAGE, wave, lane, mw, nw, bv, xv0);
+    if (!more) break;
+    // retire the next tile's K-tile 0 (the oldest G DMAs of this wave) without draining the epilogue's stores:
+    // a wave whose 128 rows are all inside M issued at least NST stores after the DMAs (more with the column-sum
+    // atomics); a wave on the M edge counts none
+    if (mw + 128 <= p.M) {
+      if (nt > 1) vmcnt<D0 + NST>();
+      else vmcnt<NST>();
+    } else {
+      if (nt > 1) vmcnt<D0>();
+      else vmcnt<0>();
+    }
+    G2_BARRIER();
   }
 }
 
@@ -807,6 +927,39 @@ static void g2_launch(const G2Params& p0, int splits, hipStream_t st) {
   HSD_CHECK_LAUNCH();
 }
 
+// Persistent NT kernel (gemm2pk_kernel): for grids of more than one round of workgroups (a one-round grid has no tile
+// seam to hide). Measured on the bert-base B=1024 NT GEMMs (tools/env_ab_gemm.py, profiles/persist_ab_r3.log): 1-6 %
+// faster on every one, bit-identical outputs; the headline step 80.8 -> 79.3 ms. HSD_G2_PERSIST=0 turns it off.
+static int g2_num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return 256;
+    n = prop.multiProcessorCount;
+  }
+  return n;
+}
+
+static bool g2_persist(int tiles) {
+  const char* e = getenv("HSD_G2_PERSIST");  // read per launch: tests flip it in-process
+  if (!(e ? atoi(e) : 1)) return false;
+  return tiles > (g2_num_cus() & ~7);
+}
+
+template <int EPI, int BN>
+static void g2pk_launch(const G2Params& p0, hipStream_t st) {
+  G2Params p = p0;
+  const int tiles_m = (p.M + g2::BM - 1) / g2::BM;
+  p.tiles_n = (p.N + BN - 1) / BN;
+  p.ntiles = tiles_m * p.tiles_n;
+  p.kps = p.K;
+  if (p.K % g2::BK) abort();
+  const int grid = std::min(p.ntiles, g2_num_cus() & ~7);
+  hipLaunchKernelGGL((g2::gemm2pk_kernel<EPI, BN>), dim3(grid), dim3(512), 0, st, p);
+  HSD_CHECK_LAUNCH();
+}
+
 // Tile width for a bf16-output NT GEMM: minimise (rounds of 256 CUs) x (per-tile cost ∝ BN + c).
 int gemm2_pick_bn(int M, int N) {
   const int tm = (M + 255) / 256;
@@ -1011,10 +1164,17 @@ static void launch_nt(const G2Params& p, int epi, int M, int N, int K, int split
       if ((epi != E2_DGELU && epi != E2_MUL) || N % 256) abort();  // fused column sums: 8 columns per lane (BN 256)
       bn = 256;
     }
+    const bool pk = LB == 0 && g2_persist((M + 255) / 256 * (N / bn));
 #define G2_NT(E)                                                     \
   case E:                                                            \
-    if (bn == 256 || LB == 1) g2_launch<0, LB, E, 256>(p, 1, st);    \
-    else g2_launch<0, LB, E, LB == 1 ? 256 : 192>(p, 1, st);         \
+    if (pk) {                                                        \
+      if (bn == 256) g2pk_launch<E, 256>(p, st);                     \
+      else g2pk_launch<E, 192>(p, st);                               \
+    } else if (bn == 256 || LB == 1) {                               \
+      g2_launch<0, LB, E, 256>(p, 1, st);                            \
+    } else {                                                         \
+      g2_launch<0, LB, E, LB == 1 ? 256 : 192>(p, 1, st);            \
+    }                                                                \
     return;
     switch (epi) {
       G2_NT(E2_STORE)

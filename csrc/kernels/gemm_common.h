@@ -148,53 +148,90 @@ __device__ __forceinline__ void colsum_flush(float (&csum)[8], float* dbias, int
 }
 
 // bf16-output epilogue of a 256 x BN tile held as acc[8][BN/64] (acc[i][j] = D[n][m] block: lane l holds
-// m = 16i + (l&15), n = 16j + 4(l>>4) + r), staged through the wave's [64][BN/4 + 8] slice of `smem`.
+// m = 16i + (l&15), n = 16j + 4(l>>4) + r), staged through the wave's [16·PB][SROW] slice of `smem`.
 // MB = 16-row MFMA blocks per wave (8: the 128-row wave tiles of the 256 x BN kernels; 4: the 64-row wave tiles
-// of gemm2s_kernel), one 64-row staging pass per 4 blocks.
-template <int EPI, int BN, int MB = 8>
+// of gemm2s_kernel). PB = 16-row MFMA blocks per staging pass (4: 64-row passes; 2: 32-row passes -- the
+// persistent kernel's staging area beside its two operand stages).
+// PRE: the bias registers (epi_bias_regs) and the first pass's residual chunks (epi_aux_regs, h = 0) were loaded by
+// the caller -- the persistent kernel loads them BEFORE it issues the next tile's LDS-DMA, so waiting for them does
+// not wait for that DMA (vector-memory counters retire loads in order).
+template <int BN, int PB>
+constexpr int epi_iter() { return 16 * PB * (BN / 32) / 64; }
+template <int BN>
+constexpr int epi_srow() { return BN / 4 == 64 ? 64 : BN / 4 + 8; }
+
+template <int EPI, int BN>
+__device__ __forceinline__ void epi_bias_regs(f32x4 (&bv)[BN / 64], const G2Params& p, int lane, int nw) {
+  if constexpr (epi_bias(EPI)) {
+#pragma unroll
+    for (int j = 0; j < BN / 64; ++j) {
+      const int n = min(nw + 16 * j + 4 * (lane >> 4), p.N - 4);
+      const u32x2 b = *reinterpret_cast<const u32x2*>(p.bias + n);
+      bv[j] = f32x4{lo_bf(b.x), hi_bf(b.x), lo_bf(b.y), hi_bf(b.y)};
+    }
+  }
+}
+
+template <int EPI, int BN, int PB, int NIT>
+__device__ __forceinline__ void epi_aux_regs(u32x4 (&xv)[NIT], const G2Params& p, int lane, int mw, int nw, int h) {
+  static_assert(NIT == epi_iter<BN, PB>(), "one chunk per lane per 64 chunks of a pass");
+  constexpr int CPR = BN / 32;
+#pragma unroll
+  for (int it = 0; it < NIT; ++it) {
+    if constexpr (epi_aux(EPI)) {
+      const int idx = lane + 64 * it;
+      const int row = idx / CPR, c8 = idx % CPR;
+      const int m = min(mw + 16 * PB * h + row, p.M - 1);
+      xv[it] = *reinterpret_cast<const u32x4*>(p.aux + (int64_t)m * p.ldaux + nw + c8 * 8);
+    } else {
+      xv[it] = u32x4{0, 0, 0, 0};
+    }
+  }
+}
+
+template <int EPI, int BN, int MB = 8, int PB = 4, bool PRE = false>
 __device__ __forceinline__ void epilogue_bf16(f32x4 (&acc)[MB][BN / 64], const G2Params& p, bf16_t* smem, int wave,
-                                              int lane, int mw, int nw) {
+                                              int lane, int mw, int nw, const f32x4* bv_pre = nullptr,
+                                              const u32x4* xv_pre = nullptr) {
   static_assert(MB == 4 || MB == 8, "64 or 128 rows per wave");
+  static_assert(PB == 2 || PB == 4, "32- or 64-row staging passes");
   constexpr int WN = BN / 4, NREP = WN / 16;
   const int q4 = lane >> 4, lr = lane & 15;
-  // stage bf16(acc [+ bias]) through a wave-private LDS slice ([64 rows][SROW]), then write whole
+  // stage bf16(acc [+ bias]) through a wave-private LDS slice ([16·PB rows][SROW]), then write whole
   // rows with 16-B lanes: each lane owns 8 consecutive n of one m.
   // WN = 64 (BN 256): unpadded 128-B rows whose 8-B slots are XOR-swizzled by (row & 15) -- the 16 lanes of a
   // ds_write_b64 group (16 rows, one slot) then cover all 32 banks, and a ds_read_b128 of chunk c8 finds its
   // two halves in chunk c8 ^ ((row & 15) >> 1), swapped when row is odd (both conflict-free; the padded
   // [64][72] image measured 12 % LDS bank-conflict cycles, tools/pmc_gemm2.sh). Other widths keep the pad.
   constexpr bool kSwz = WN == 64;
-  constexpr int SROW = kSwz ? WN : WN + 8;
+  constexpr int SROW = epi_srow<BN>();
   constexpr int CPR = WN / 8;  // 16-B chunks per row
   constexpr bool kBias = epi_bias(EPI);
-  constexpr bool kAux = epi_aux(EPI);
-  bf16_t* stg = smem + wave * (64 * SROW);
+  constexpr int ITER = epi_iter<BN, PB>();
+  bf16_t* stg = smem + wave * (16 * PB * SROW);
   f32x4 bv[NREP];
-  if constexpr (kBias) {
+  if constexpr (PRE) {
 #pragma unroll
-    for (int j = 0; j < NREP; ++j) {
-      const int n = min(nw + 16 * j + 4 * q4, p.N - 4);
-      const u32x2 b = *reinterpret_cast<const u32x2*>(p.bias + n);
-      bv[j] = f32x4{lo_bf(b.x), hi_bf(b.x), lo_bf(b.y), hi_bf(b.y)};
-    }
+    for (int j = 0; j < NREP; ++j) bv[j] = bv_pre[j];
+  } else {
+    epi_bias_regs<EPI, BN>(bv, p, lane, nw);
   }
   bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
   constexpr bool kColsum = (EPI == E2_DGELU || EPI == E2_MUL) && CPR == 8;
   float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int h = 0; h < MB / 4; ++h) {
+  for (int h = 0; h < MB / PB; ++h) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < PB; ++i)
 #pragma unroll
       for (int j = 0; j < NREP; ++j) {
-        f32x4 v = acc[4 * h + i][j];
+        f32x4 v = acc[PB * h + i][j];
         if constexpr (kBias) v += bv[j];
         const int row = 16 * i + lr;
         const int col = kSwz ? (((4 * j + q4) ^ (row & 15)) << 2) : 16 * j + 4 * q4;
         *reinterpret_cast<u32x2*>(stg + row * SROW + col) = pack4(v);
       }
     __builtin_amdgcn_wave_barrier();
-    constexpr int ITER = 64 * CPR / 64;
     u32x4 sv[ITER], xv[ITER];
 #pragma unroll
     for (int it = 0; it < ITER; ++it) {
@@ -207,18 +244,18 @@ __device__ __forceinline__ void epilogue_bf16(f32x4 (&acc)[MB][BN / 64], const G
       } else {
         sv[it] = *reinterpret_cast<const u32x4*>(stg + row * SROW + c8 * 8);
       }
-      if constexpr (kAux) {
-        const int m = min(mw + 64 * h + row, p.M - 1);
-        xv[it] = *reinterpret_cast<const u32x4*>(p.aux + (int64_t)m * p.ldaux + nw + c8 * 8);
-      } else {
-        xv[it] = u32x4{0, 0, 0, 0};
-      }
+    }
+    if (PRE && h == 0) {
+#pragma unroll
+      for (int it = 0; it < ITER; ++it) xv[it] = xv_pre[it];
+    } else {
+      epi_aux_regs<EPI, BN, PB>(xv, p, lane, mw, nw, h);
     }
 #pragma unroll
     for (int it = 0; it < ITER; ++it) {
       const int idx = lane + 64 * it;
       const int row = idx / CPR, c8 = idx % CPR;
-      const int m = mw + 64 * h + row;
+      const int m = mw + 16 * PB * h + row;
       const int n = nw + c8 * 8;
       if (m >= p.M) continue;
       const int64_t co = (int64_t)m * p.ldc + n;

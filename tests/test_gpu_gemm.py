@@ -325,3 +325,36 @@ def test_gemm2_dgrad_reading_w_directly_matches_stored_wt(gpu, M, N, K, epi):
     ref = dy.float() @ w.float()
     if epi == 0:
         _check(c1, ref)
+
+
+@pytest.mark.parametrize("M,N,K", [(32768, 768, 256), (8292, 3072, 512), (20000, 960, 128), (65536, 2304, 64)])
+@pytest.mark.parametrize("epi", [0, 1, 2, 3, 4, 5, 8, 9])
+def test_gemm2_persistent_matches_one_shot(gpu, monkeypatch, M, N, K, epi):
+    """Persistent NT kernel (gemm2pk: one workgroup per CU walking tiles, next tile's DMA under the epilogue) ==
+    the one-shot gemm2 kernel bit for bit on every bf16 epilogue (same main loop, same dropout sites); fused
+    bias-gradient column sums to fp32 rounding (atomic order). Shapes: >1 round of tiles, BN 256 and 192, M edges."""
+    torch.manual_seed(41 + epi)
+    C_ = _C()
+    A, B = _mk((M, K), gpu), _mk((N, K), gpu, 0.05)
+    bias = _mk((N,), gpu)
+    aux = _mk((M, N), gpu) if epi != 9 else torch.rand(M, N, device=gpu).bfloat16()
+    two = epi in (2, 8)
+    outs = []
+    monkeypatch.setenv("HSD_G2_SPLITK", "1")
+    for persist in ("0", "1"):
+        monkeypatch.setenv("HSD_G2_PERSIST", persist)
+        C = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+        C2 = torch.empty_like(C) if two else None
+        db = torch.zeros(N, device=gpu) if epi in (5, 9) and N % 256 == 0 else None
+        C_.gemm2(A, B, C, 0, 0, epi, bias if epi in (1, 2, 3, 8) else None, aux if epi in (3, 4, 5, 9) else None,
+                 C2, 0.1 if epi == 3 else 0.0, 77, 0, None, db)
+        torch.cuda.synchronize()
+        outs.append((C, C2, db))
+    (c0, c20, d0), (c1, c21, d1) = outs
+    assert torch.equal(c0, c1)
+    if two:
+        assert torch.equal(c20, c21)
+    if d0 is not None:
+        torch.testing.assert_close(d1, d0, rtol=1e-4, atol=1e-4 * float(d0.abs().max()) + 1e-6)
+    if epi == 0:
+        _check(c1, A.float() @ B.float().t())
