@@ -34,8 +34,26 @@ struct G2Params {
   int tiles_n;
   int ntiles;    // tiles_m * tiles_n
   float* dbias;  // E2_DGELU: optional fp32 column sums of the output (the bias gradient), BN 256 only
-  int nt_store;  // non-temporal (streaming) epilogue stores
+  int nt_store;  // bf16 epilogues: non-temporal stores (default; HSD_G2_NT=0 turns them off)
+  int stagger;   // experiment
 };
+
+// Buffer descriptor over `ptr` (wave-uniform: built from readfirstlane'd halves so hipcc keeps it in SGPRs).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const void* ptr) {
+  const uint64_t a = (uint64_t)ptr;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, 0x7FFFFFFF, 0x00020000);
+}
+
+// 16-B non-temporal buffer store (cache policy nt). The bf16 GEMM epilogues store through it: plain stores
+// allocate the output lines in the XCD's 4 MiB L2 and evict the A / B panels the CU's next tiles stream from it;
+// with nt the T x 3072 x 768 GEMM (FFN1 shape) runs 583 -> 494 us and T x 768 x 768 147 -> 125 us
+// (tools/store_policy_probe.py, profiles/store_policy_r3.log). hipcc's __builtin_nontemporal_store emits a plain
+// global_store on gfx950, hence the buffer form.
+__device__ __forceinline__ void st16nt(__amdgpu_buffer_rsrc_t r, uint32_t off, const u32x4& v) {
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 2);
+}
 
 __device__ __forceinline__ void st16(bf16_t* dst, const u32x4& v, int nt) {
   if (nt) __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst));
@@ -217,6 +235,9 @@ __device__ __forceinline__ void epilogue_bf16(f32x4 (&acc)[MB][BN / 64], const G
     epi_bias_regs<EPI, BN>(bv, p, lane, nw);
   }
   bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
+  // stores: non-temporal buffer stores off the wave's first row (st16nt); p.nt_store = 0 (HSD_G2_NT=0): plain
+  const __amdgpu_buffer_rsrc_t rc = wave_rsrc(C + (int64_t)mw * p.ldc);
+  const __amdgpu_buffer_rsrc_t rc2 = wave_rsrc(epi_two_out(EPI) ? p.C2 + (int64_t)mw * p.ldc : C);
   constexpr bool kColsum = (EPI == E2_DGELU || EPI == E2_MUL) && CPR == 8;
   float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -261,8 +282,14 @@ __device__ __forceinline__ void epilogue_bf16(f32x4 (&acc)[MB][BN / 64], const G
       const int64_t co = (int64_t)m * p.ldc + n;
       u32x4 o = sv[it], o2;
       epi_chunk<EPI>(o, o2, xv[it], m, n, p, csum);
-      st16(C + co, o, p.nt_store);
-      if constexpr (epi_two_out(EPI)) st16(p.C2 + co, o2, p.nt_store);
+      if (p.nt_store) {
+        const uint32_t bo = (uint32_t)(((int64_t)(m - mw) * p.ldc + n) * 2);
+        st16nt(rc, bo, o);
+        if constexpr (epi_two_out(EPI)) st16nt(rc2, bo, o2);
+      } else {
+        st16(C + co, o, 0);
+        if constexpr (epi_two_out(EPI)) st16(p.C2 + co, o2, 0);
+      }
     }
     __builtin_amdgcn_wave_barrier();
   }
