@@ -124,8 +124,7 @@ __device__ __forceinline__ bf16x8 frag(const bf16_t* img, int rbase, int ks, int
 // epilogue). Enters with every wave at the same barrier count; leaves the same way.
 template <int LA, int LB, int BN, int SYNC, int G, int D0, bool PRO, class DMA>
 __device__ __forceinline__ void mainloop_staggered(f32x4 (&acc)[8][BN / 64], bf16_t* smem, const DMA& dma_slot,
-                                                   int nt, int kbeg, int wm, int arow, int bcol, int lane,
-                                                   int relax = 0) {
+                                                   int nt, int kbeg, int wm, int arow, int bcol, int lane) {
   constexpr int WN = BN / 4, NREP = WN / 16, NB0 = 2, NB1 = NREP - NB0;
   constexpr int TA = BM * 64, STAGE = TA + BN * 64;
   bf16x8 fa[4][2], fb0[NB0][2], fb1[NB1][2];
@@ -214,8 +213,7 @@ __device__ __forceinline__ void mainloop_staggered(f32x4 (&acc)[8][BN / 64], bf1
     if (n2) {
 #pragma unroll
       for (int q = 0; q < D0; ++q) dma_slot(q, const_cast<bf16_t*>(cA), k2);
-      if (t < relax) vmcnt<63>();
-      else vmcnt<D0>();
+      vmcnt<D0>();
     } else {
       vmcnt<0>();
     }
@@ -653,7 +651,7 @@ __global__ __launch_bounds__(512, 1) void gemm2pk_kernel(G2Params p) {
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < NREP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    mainloop_staggered<0, 0, BN, 4, G, D0, false>(acc, smem, dma_slot, nt, 0, wm, arow, bcol, lane, p.stagger);
+    mainloop_staggered<0, 0, BN, 4, G, D0, false>(acc, smem, dma_slot, nt, 0, wm, arow, bcol, lane);
     const int mw = m0 + arow, nw = n0 + bcol;
     f32x4 bv[NREP];
     u32x4 xv0[ITER];
@@ -957,9 +955,7 @@ static void g2pk_launch(const G2Params& p0, hipStream_t st) {
   p.ntiles = tiles_m * p.tiles_n;
   p.kps = p.K;
   if (p.K % g2::BK) abort();
-  const char* e = getenv("HSD_G2_RELAX");  // EXPERIMENT ONLY (racy): skip the DMA waits of the first K-tiles
-  p.stagger = e ? atoi(e) : 0;
-  const char* gc = getenv("HSD_G2_GRID");  // experiment: cap the persistent grid
+  const char* gc = getenv("HSD_G2_GRID");  // diagnostic (tools/epi_probe2.py): cap the persistent grid (multiple of 8)
   const int grid = std::min(p.ntiles, gc ? atoi(gc) : g2_num_cus() & ~7);
   hipLaunchKernelGGL((g2::gemm2pk_kernel<EPI, BN>), dim3(grid), dim3(512), 0, st, p);
   HSD_CHECK_LAUNCH();

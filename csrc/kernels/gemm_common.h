@@ -35,7 +35,6 @@ struct G2Params {
   int ntiles;    // tiles_m * tiles_n
   float* dbias;  // E2_DGELU: optional fp32 column sums of the output (the bias gradient), BN 256 only
   int nt_store;  // bf16 epilogues: non-temporal stores (default; HSD_G2_NT=0 turns them off)
-  int stagger;   // experiment
 };
 
 // Buffer descriptor over `ptr` (wave-uniform: built from readfirstlane'd halves so hipcc keeps it in SGPRs).
