@@ -492,6 +492,10 @@ void transpose_many(torch::Tensor desc, int64_t total_tiles) {
 
 int64_t gemm2_splits(int64_t M, int64_t N, int64_t K) { return hsd::gemm2_wgrad_splits((int)M, (int)N, (int)K); }
 int64_t gemm2_nt_splits(int64_t M, int64_t N, int64_t K) { return hsd::gemm2_nt_splits((int)M, (int)N, (int)K); }
+void gemm2_set_diag(c10::optional<at::Tensor> buf) {
+  hsd::gemm2_set_diag(buf.has_value() ? buf->data_ptr() : nullptr);
+}
+
 bool gemm2_supported(int64_t la, int64_t lb, int64_t epi, int64_t M, int64_t N, int64_t K) {
   return hsd::gemm2_supported((int)la, (int)lb, (int)epi, (int)M, (int)N, (int)K);
 }
@@ -534,6 +538,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm2_splits", &gemm2_splits);
   m.def("gemm2_nt_splits", &gemm2_nt_splits);
   m.def("gemm2_supported", &gemm2_supported);
+  m.def("gemm2_set_diag", &gemm2_set_diag);
   m.def("transpose_many", &transpose_many);
   m.def("xent", &xent, py::arg("logits"), py::arg("labels"), py::arg("dlogits"), py::arg("stats"),
         py::arg("n_valid"), py::arg("V") = 0);

@@ -652,6 +652,8 @@ __global__ __launch_bounds__(512, 1) void gemm2pk_kernel(G2Params p) {
 #pragma unroll
       for (int j = 0; j < NREP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     mainloop_staggered<0, 0, BN, 4, G, D0, false>(acc, smem, dma_slot, nt, 0, wm, arow, bcol, lane);
+    uint64_t ts0 = 0, ts1 = 0;
+    if (p.diag) ts0 = __builtin_amdgcn_s_memtime();
     const int mw = m0 + arow, nw = n0 + bcol;
     f32x4 bv[NREP];
     u32x4 xv0[ITER];
@@ -664,7 +666,19 @@ __global__ __launch_bounds__(512, 1) void gemm2pk_kernel(G2Params p) {
       prologue();
     }
     epilogue_bf16<EPI, BN, 8, PB, true>(acc, p, smem + 2 * STAGE, wave, lane, mw, nw, bv, xv0);
-    if (!more) break;
+    if (p.diag) ts1 = __builtin_amdgcn_s_memtime();
+    // diagnostic stamps (wave 0): main loop end, epilogue end, seam end, real time -- tools/seam_probe.py
+    auto stamp = [&](uint64_t ts2) {
+      if (p.diag && wave == 0 && lane == 0) {
+        const int it = (L - (int)gridDim.x - (int)blockIdx.x) / (int)gridDim.x;
+        unsigned long long* d = p.diag + ((int64_t)blockIdx.x * 64 + min(it, 63)) * 4;
+        d[0] = ts0; d[1] = ts1; d[2] = ts2; d[3] = __builtin_amdgcn_s_memrealtime();
+      }
+    };
+    if (!more) {
+      stamp(ts1);
+      break;
+    }
     // retire the next tile's K-tile 0 (the oldest G DMAs of this wave) without draining the epilogue's stores:
     // a wave whose 128 rows are all inside M issued at least NST stores after the DMAs (more with the column-sum
     // atomics); a wave on the M edge counts none
@@ -676,6 +690,7 @@ __global__ __launch_bounds__(512, 1) void gemm2pk_kernel(G2Params p) {
       else vmcnt<0>();
     }
     G2_BARRIER();
+    if (p.diag) stamp(__builtin_amdgcn_s_memtime());
   }
 }
 
@@ -1192,11 +1207,15 @@ static void launch_nt(const G2Params& p, int epi, int M, int N, int K, int split
   }
 }
 
+static unsigned long long* g_diag = nullptr;
+void gemm2_set_diag(void* p) { g_diag = (unsigned long long*)p; }
+
 void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, int M, int N,
                   int K, void* C, int64_t ldc, const bf16_t* bias, const bf16_t* aux, int64_t ldaux, bf16_t* C2,
                   double p_drop, uint64_t seed, int splits, float* ws, float* dbias, hipStream_t st) {
   G2Params p{};
   p.dbias = dbias;
+  p.diag = g_diag;
   {
     const char* e = getenv("HSD_G2_NT");
     p.nt_store = e ? atoi(e) : 1;
