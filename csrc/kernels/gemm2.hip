@@ -694,6 +694,192 @@ __global__ __launch_bounds__(512, 1) void gemm2pk_kernel(G2Params p) {
   }
 }
 
+// ------------------------------------------------------------------------------------------------
+// fp8 persistent NT GEMM (gemm8pk): gemm2pk with v_mfma_scale_f32_16x16x128_f8f6f4 (unit block scales, twice the bf16
+// MFMA rate). A K-tile of 128 fp8 values is the same 128-B row as 64 bf16 values, so an fp8 [M][K] operand is handled
+// as a "bf16" [M][K/2] one: same LDS images, DMA slots (inline asm), staggered 4-phase schedule, tile walk, seam and
+// epilogues. Per K-tile a wave issues 32 MFMAs of 32 cycles (bf16: 64 of 16) and reads 24 x 16 B per lane (same).
+typedef __attribute__((ext_vector_type(8))) int i32x8;
+
+// 16x16x128 fragment: lane l holds row rbase + (l&15), k = 32(l>>4) .. +31 (chunks 2(l>>4), 2(l>>4)+1); A and B use
+// the same k assignment, so the product does not depend on the instruction's internal k order
+__device__ __forceinline__ i32x8 frag8(const bf16_t* img, int rbase, int lane) {
+  const int row = rbase + (lane & 15);
+  const int c0 = 2 * (lane >> 4);
+  const bf16_t* r = img + row * 64;
+  const u32x4 lo = *reinterpret_cast<const u32x4*>(r + ((c0 ^ f1(row)) << 3));
+  const u32x4 hi = *reinterpret_cast<const u32x4*>(r + (((c0 + 1) ^ f1(row)) << 3));
+  i32x8 v;
+  v[0] = (int)lo[0]; v[1] = (int)lo[1]; v[2] = (int)lo[2]; v[3] = (int)lo[3];
+  v[4] = (int)hi[0]; v[5] = (int)hi[1]; v[6] = (int)hi[2]; v[7] = (int)hi[3];
+  return v;
+}
+
+// FB / FA: formats of the B / A operands (0 = e4m3, 1 = e5m2); B is the instruction's first operand (D[n][m])
+template <int FB, int FA>
+__device__ __forceinline__ f32x4 mma8(const i32x8& b, const i32x8& a, const f32x4& c) {
+  return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(b, a, c, FB, FA, 0, 0, 0, 0);
+}
+
+// mainloop_staggered (SYNC 4, prologue issued by the caller) with fp8 fragments: one MFMA per (i, j) per K-tile
+template <int BN, int G, int D0, int FA, int FB, class DMA>
+__device__ __forceinline__ void mainloop_staggered8(f32x4 (&acc)[8][BN / 64], bf16_t* smem, const DMA& dma_slot,
+                                                    int nt, int wm, int arow, int bcol, int lane) {
+  constexpr int WN = BN / 4, NREP = WN / 16, NB0 = 2, NB1 = NREP - NB0;
+  constexpr int TA = BM * 64, STAGE = TA + BN * 64;
+  constexpr int E1 = D0 + (G - D0 + 1) / 2;
+  i32x8 fa[4], fb0[NB0], fb1[NB1];
+#define G8_CLUSTER(ACC_I0, FB_, NBX, J0)                                                                     \
+  __builtin_amdgcn_s_setprio(1);                                                                             \
+  _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < NBX; ++j)              \
+      acc[ACC_I0 + i][J0 + j] = mma8<FB, FA>(FB_[j], fa[i], acc[ACC_I0 + i][J0 + j]);                        \
+  __builtin_amdgcn_s_setprio(0);
+  if (wm == 1) G2_BARRIER();
+  for (int t = 0; t < nt; ++t) {
+    const bf16_t* cA = smem + (t & 1) * STAGE;
+    const bf16_t* cB = cA + TA;
+    bf16_t* nS = smem + ((t + 1) & 1) * STAGE;
+    const bool n1 = t + 1 < nt, n2 = t + 2 < nt;
+    const int k1 = (t + 1) * BK, k2 = (t + 2) * BK;
+    // P1: A-sub0 + B-sub0, first part of tile t+1's DMA
+#pragma unroll
+    for (int j = 0; j < NB0; ++j) fb0[j] = frag8(cB, bcol + 16 * j, lane);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fa[i] = frag8(cA, arow + 16 * i, lane);
+    if (n1) {
+#pragma unroll
+      for (int q = D0; q < E1; ++q) dma_slot(q, nS, k1);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    G2_BARRIER();
+    G8_CLUSTER(0, fb0, NB0, 0)
+    G2_BARRIER();
+    // P2: B-sub1, rest of tile t+1's DMA
+#pragma unroll
+    for (int j = 0; j < NB1; ++j) fb1[j] = frag8(cB, bcol + 16 * (NB0 + j), lane);
+    if (n1) {
+#pragma unroll
+      for (int q = E1; q < G; ++q) dma_slot(q, nS, k1);
+    }
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    G2_BARRIER();
+    G8_CLUSTER(0, fb1, NB1, NB0)
+    G2_BARRIER();
+    // P3: A-sub1
+#pragma unroll
+    for (int i = 0; i < 4; ++i) fa[i] = frag8(cA, arow + 64 + 16 * i, lane);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    G2_BARRIER();
+    G8_CLUSTER(4, fb1, NB1, NB0)
+    G2_BARRIER();
+    // P4: no reads; D0 slots of tile t+2 into this stage; retire tile t+1
+    if (n2) {
+#pragma unroll
+      for (int q = 0; q < D0; ++q) dma_slot(q, const_cast<bf16_t*>(cA), k2);
+      vmcnt<D0>();
+    } else {
+      vmcnt<0>();
+    }
+    G2_BARRIER();
+    G8_CLUSTER(4, fb0, NB0, 0)
+    G2_BARRIER();
+  }
+  if (wm == 0) G2_BARRIER();
+#undef G8_CLUSTER
+}
+
+// p.A / p.B: fp8 [M][K] / [N][K] viewed as bf16 [..][K/2] (p.K, p.lda, p.ldb in bf16 units); sa / sb: device
+// dequantisation scalars
+template <int EPI, int BN, int FA, int FB>
+__global__ __launch_bounds__(512, 1) void gemm8pk_kernel(G2Params p, const float* __restrict__ sa,
+                                                         const float* __restrict__ sb) {
+  p.dp = resolve_seed(p.dp);
+  static_assert(epi_bf16_out(EPI), "bf16 epilogues");
+  constexpr int WN = BN / 4, NREP = WN / 16;
+  constexpr int TA = BM * 64, STAGE = TA + BN * 64;
+  constexpr int GA = 4, GB = BN / 64, G = GA + GB, D0 = 2;
+  constexpr int PB = 2;
+  constexpr int STG = 8 * 16 * PB * epi_srow<BN>();
+  constexpr int ITER = epi_iter<BN, PB>();
+  constexpr int NST = (8 / PB) * ITER * (epi_two_out(EPI) ? 2 : 1);
+  static_assert(D0 + NST <= 63, "vmcnt field");
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * STAGE + STG];
+  static_assert(sizeof(smem) <= 160 * 1024, "LDS");
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int ntiles = p.ntiles, q8 = ntiles >> 3, r8 = ntiles & 7;
+  const int nt = p.K / BK;
+  const float dq = sa[0] * sb[0];
+  HSD_DASSERT(p.K % BK == 0 && nt >= 1 && (gridDim.x == (unsigned)ntiles || gridDim.x % 8 == 0));
+  const uint32_t smem_lds = (uint32_t)(size_t)(__attribute__((address_space(3))) bf16_t*)smem;
+  uint32_t aoff[G];
+  int m0, n0;
+  auto set_tile = [&](int L) {
+    const int xcd = L & 7;
+    const int v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (L >> 3);
+    m0 = (v / p.tiles_n) * BM;
+    n0 = (v % p.tiles_n) * BN;
+#pragma unroll
+    for (int q = 0; q < G; ++q)
+      aoff[q] = q < GA ? lane_off<0>(p.lda, m0, p.M, wave * GA + q, lane)
+                       : lane_off<0>(p.ldb, n0, p.N, wave * GB + (q - GA), lane);
+  };
+  auto dma_slot = [&](int q, bf16_t* stage, int k0) {
+    const uint32_t st = smem_lds + (uint32_t)(stage - smem) * 2u;
+    if (q < GA) dma_lds_asm(asm_base<0>(p.A, p.lda, m0, k0), aoff[q], st + (wave * GA + q) * 1024u);
+    else dma_lds_asm(asm_base<0>(p.B, p.ldb, n0, k0), aoff[q], st + (TA + (wave * GB + (q - GA)) * 512) * 2u);
+  };
+  auto prologue = [&]() {
+#pragma unroll
+    for (int q = 0; q < G; ++q) dma_slot(q, smem, 0);
+    if (nt > 1) {
+#pragma unroll
+      for (int q = 0; q < D0; ++q) dma_slot(q, smem + STAGE, BK);
+    }
+  };
+
+  const int arow = wm * 128, bcol = wn * WN;
+  int L = blockIdx.x;
+  set_tile(L);
+  prologue();
+  vmcnt<0>();
+  G2_BARRIER();
+  f32x4 acc[8][NREP];
+  for (;;) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < NREP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    mainloop_staggered8<BN, G, D0, FA, FB>(acc, smem, dma_slot, nt, wm, arow, bcol, lane);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < NREP; ++j) acc[i][j] *= dq;
+    const int mw = m0 + arow, nw = n0 + bcol;
+    f32x4 bv[NREP];
+    u32x4 xv0[ITER];
+    epi_bias_regs<EPI, BN>(bv, p, lane, nw);
+    epi_aux_regs<EPI, BN, PB>(xv0, p, lane, mw, nw, 0);
+    L += gridDim.x;
+    const bool more = L < ntiles;
+    if (more) {
+      set_tile(L);
+      prologue();
+    }
+    epilogue_bf16<EPI, BN, 8, PB, true>(acc, p, smem + 2 * STAGE, wave, lane, mw, nw, bv, xv0);
+    if (!more) break;
+    if (mw + 128 <= p.M) {
+      if (nt > 1) vmcnt<D0 + NST>();
+      else vmcnt<NST>();
+    } else {
+      if (nt > 1) vmcnt<D0>();
+      else vmcnt<0>();
+    }
+    G2_BARRIER();
+  }
+}
+
 // main_grad[i] += Σ_s ws[s][i]   (float4 lanes, grid-stride)
 __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ ws, float* __restrict__ C,
                                                           int64_t ldc, int M, int N, int splits) {
@@ -974,6 +1160,54 @@ static void g2pk_launch(const G2Params& p0, hipStream_t st) {
   const int grid = std::min(p.ntiles, gc ? atoi(gc) : g2_num_cus() & ~7);
   hipLaunchKernelGGL((g2::gemm2pk_kernel<EPI, BN>), dim3(grid), dim3(512), 0, st, p);
   HSD_CHECK_LAUNCH();
+}
+
+template <int EPI, int BN, int FA>
+static void g8pk_launch(const G2Params& p0, const float* sa, const float* sb, hipStream_t st) {
+  G2Params p = p0;
+  const int tiles_m = (p.M + g2::BM - 1) / g2::BM;
+  p.tiles_n = (p.N + BN - 1) / BN;
+  p.ntiles = tiles_m * p.tiles_n;
+  p.kps = p.K;
+  const int grid = p.ntiles > (g2_num_cus() & ~7) ? (g2_num_cus() & ~7) : p.ntiles;
+  hipLaunchKernelGGL((g2::gemm8pk_kernel<EPI, BN, FA, 0>), dim3(grid), dim3(512), 0, st, p, sa, sb);
+  HSD_CHECK_LAUNCH();
+}
+
+// fp8 NT GEMM on the persistent kernel (gemm8.hip's launch_gemm8 routes here): A8 [M][K], B8 [N][K] bytes, K % 128 == 0,
+// even leading dimensions; fa: A format (0 e4m3, 1 e5m2), B e4m3.
+void launch_gemm8pk(int epi, int bn, const G2Params& p0, int fa, const float* sa, const float* sb, hipStream_t st) {
+  G2Params p = p0;
+  p.nt_store = 1;
+  {
+    const char* e = getenv("HSD_G2_NT");
+    if (e) p.nt_store = atoi(e);
+  }
+  p.K /= 2;
+  p.lda /= 2;
+  p.ldb /= 2;
+#define G8PK(E)                                                                   \
+  case E:                                                                         \
+    if (bn == 256) {                                                              \
+      if (fa == 0) g8pk_launch<E, 256, 0>(p, sa, sb, st);                         \
+      else g8pk_launch<E, 256, 1>(p, sa, sb, st);                                 \
+    } else {                                                                      \
+      if (fa == 0) g8pk_launch<E, 192, 0>(p, sa, sb, st);                         \
+      else g8pk_launch<E, 192, 1>(p, sa, sb, st);                                 \
+    }                                                                             \
+    return;
+  switch (epi) {
+    G8PK(E2_STORE)
+    G8PK(E2_BIAS)
+    G8PK(E2_BIAS_GELU)
+    G8PK(E2_BIAS_DROP_RES)
+    G8PK(E2_RES)
+    G8PK(E2_DGELU)
+    G8PK(E2_BIAS_GELU_D)
+    G8PK(E2_MUL)
+    default: abort();
+  }
+#undef G8PK
 }
 
 // Tile width for a bf16-output NT GEMM: minimise (rounds of 256 CUs) x (per-tile cost ∝ BN + c).

@@ -12,6 +12,7 @@
 // independent of the instruction's internal k order.
 // sa / sb are device scalars (1 / quantisation scale of each operand, fp8.hip): no host round trip.
 #include "gemm_common.h"
+#include <stdlib.h>
 
 namespace hsd {
 namespace g8 {
@@ -152,6 +153,7 @@ __global__ __launch_bounds__(512, 1) void gemm8_kernel(G2Params p, const float* 
 }  // namespace g8
 
 int gemm2_pick_bn(int M, int N);
+void launch_gemm8pk(int epi, int bn, const G2Params& p, int fa, const float* sa, const float* sb, hipStream_t st);
 
 bool gemm8_supported(int epi, int M, int N, int K) {
   return K % g8::BK == 0 && M >= 1 && N % 8 == 0 && epi_bf16_out(epi) && gemm2_pick_bn(M, N) != 0;
@@ -188,6 +190,15 @@ void launch_gemm8(int epi, const uint8_t* A, int64_t lda, int fa, const float* s
   }
   // formats: activations / weights e4m3, gradients (dgrad A operand) e4m3 or e5m2
   if (fb != 0) abort();
+  // default: the persistent staggered-schedule kernel (gemm2.hip gemm8pk_kernel); HSD_G8_LEGACY=1: this file's
+  // one-barrier-per-K-tile kernel (A/B reference)
+  {
+    const char* e = getenv("HSD_G8_LEGACY");
+    if (!(e && atoi(e)) && lda % 2 == 0 && ldb % 2 == 0) {
+      launch_gemm8pk(epi, bn, p, fa, sa, sb, st);
+      return;
+    }
+  }
 #define G8_E(E)                                                              \
   case E:                                                                    \
     if (bn == 256) {                                                         \
