@@ -26,18 +26,15 @@ class Compression:  # noqa: N801 - Horovod's ``hvd.Compression`` namespace
     bf16 = "bf16"
 
 
-def DistributedOptimizer(optimizer, store=None, bucket_mb=None, compression=Compression.none):
-    """Horovod-compatible spelling: returns ``(optimizer, bucketer)`` wired to the flat store.
+def DistributedOptimizer(optimizer, store=None, bucket_mb=None, compression=Compression.none,
+                         backward_passes_per_step: int = 1):
+    """``hvd.DistributedOptimizer(opt, compression=..., backward_passes_per_step=...)``: a wrapped optimizer whose
+    ``step()`` applies the rank-averaged gradient (``parallel/dist_optim.py``). ``.bucketer`` is the underlying
+    RCCL bucket engine (None in a single process); the wrapped optimizer's attributes (``lr``, state) pass through."""
+    from .parallel.dist_optim import DistributedOptimizer as _DO
 
-    In this framework gradient averaging lives in :class:`parallel.GradBucketer` (all-reduce overlapped
-    with backward) and the ``1/N`` scale is folded into :class:`optim.FusedAdam`; this helper exists so
-    code written against ``hvd.DistributedOptimizer(opt, compression=hvd.Compression.fp16)`` has a direct
-    equivalent.
-    """
-    from .parallel.ddp import GradBucketer
-
-    store = store or optimizer.store
-    return optimizer, (GradBucketer(store, bucket_mb=bucket_mb, compression=compression) if size() > 1 else None)
+    return _DO(optimizer, store=store, bucket_mb=bucket_mb, compression=compression,
+               backward_passes_per_step=backward_passes_per_step)
 
 
 class callbacks:  # noqa: N801 - the ``hvd.callbacks`` namespace

@@ -488,3 +488,54 @@ def test_fp16_wire_compression_keeps_large_accumulated_gradients_finite():
     """fp16 buckets are pre-scaled by 1/(world x micro-steps) before the cast, so large accumulated
     gradients do not overflow to inf on the wire (gloo world 2, gradient accumulation 2)."""
     mp.spawn(_worker_fp16_range, args=(2, _port()), nprocs=2, join=True)
+
+
+def _worker_hvd_optimizer(rank, world, port, out_path, k):
+    _setenv(rank, world, port)
+    import huggingface_sagemaker_tensorflow_distributed_amd as hvd
+
+    hvd.init(device="cpu")
+    from huggingface_sagemaker_tensorflow_distributed_amd.models import build_model, resolve_config
+    from huggingface_sagemaker_tensorflow_distributed_amd.optim import FusedAdam
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel import FlatParamStore
+
+    cfg = resolve_config("hsd-tiny-bert").replace(hidden_dropout_prob=0.0, attention_probs_dropout_prob=0.0)
+    model = build_model(cfg, seed=100 + rank)
+    store = FlatParamStore(model, torch.device("cpu"))
+    opt = hvd.DistributedOptimizer(FusedAdam(store, lr=1e-3), bucket_mb=0.05, backward_passes_per_step=k)
+    assert opt.bucketer is not None and opt.lr == 1e-3
+    hvd.broadcast_parameters(store)
+    ids, am, lab = _data(8 * world)
+    for step in range(3):
+        model.rng.new_step(step)
+        opt.zero_grad()
+        per = 8 // k
+        for j in range(k):  # plain PyTorch loop: k backward passes, one step
+            s = rank * 8 + j * per
+            loss, _ = model(ids[s:s + per], attention_mask=am[s:s + per], labels=lab[s:s + per])
+            loss.backward()
+        opt.step()
+    assert opt.step_count == 3
+    if rank == 0:
+        torch.save(store.master.clone(), out_path)
+    hvd.shutdown()
+
+
+@pytest.mark.parametrize("k", [1, 2])
+def test_hvd_distributed_optimizer_plain_loop(tmp_path, k):
+    """``hvd.DistributedOptimizer(opt, backward_passes_per_step=k)`` in a plain zero_grad/backward/step loop at world 2
+    equals one process on the global batch (Trainer path, already pinned equal to DP above)."""
+    world = 2
+    out = str(tmp_path / "hvdopt.pt")
+    mp.spawn(_worker_hvd_optimizer, args=(world, _port(), out, k), nprocs=world, join=True)
+    dp_master = torch.load(out)
+    for key in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE"):
+        os.environ.pop(key, None)
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel import backend
+
+    backend.init(device="cpu")
+    model, store, opt, tr = _make(seed_init=100)
+    ids, am, lab = _data(8 * world)
+    for step in range(3):
+        tr.train_step([{"input_ids": ids, "attention_mask": am, "labels": lab}])
+    torch.testing.assert_close(store.master, dp_master, atol=2e-6, rtol=1e-5)
