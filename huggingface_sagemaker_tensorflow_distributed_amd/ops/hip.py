@@ -90,6 +90,29 @@ def _use_side_stream(tokens: int) -> bool:
     return _WGRAD_MODE in ("1", "on", "true") or tokens <= _WGRAD_AUTO_MAX_TOKENS
 
 
+def wgrad_side_stream_for(tokens: int) -> bool:
+    """Whether a step of ``tokens`` tokens runs its weight gradients on the side stream (the batch planner sizes
+    the memory regime with it: the side stream's stash keeps the wgrad operands alive until the end of backward)."""
+    return _use_side_stream(tokens)
+
+
+class wgrad_stream_override:  # noqa: N801 - used as a context manager
+    """Temporarily force HSD_WGRAD_STREAM (``"0"`` / ``"1"`` / ``"auto"``), e.g. for memory probes."""
+
+    def __init__(self, mode: str):
+        self.mode = mode
+
+    def __enter__(self):
+        global _WGRAD_MODE
+        self.prev, _WGRAD_MODE = _WGRAD_MODE, self.mode
+        return self
+
+    def __exit__(self, *exc):
+        global _WGRAD_MODE
+        _WGRAD_MODE = self.prev
+        return False
+
+
 def join_side_streams() -> None:
     """Make the current stream wait for every side stream (call before consuming gradients)."""
     cur = torch.cuda.current_stream() if _SIDE else None

@@ -110,26 +110,53 @@ def _probe_peak(model, store, cfg, batch: int, seq_len: int, device) -> int:
     return peak
 
 
+def _shadow_bytes(store, compression: str) -> float:
+    if compression in (None, "none") or store.grad.dtype != torch.float32:
+        return 0.0
+    return float(store.numel) * 2
+
+
 def plan(model, store, seq_len: int, device, *, headroom: float = 0.9, multiple: int = 8,
          max_tokens: Optional[int] = DEFAULT_MAX_TOKENS, probe_batches=None,
-         fallback_budget_bytes: float = 64 * 2**30) -> BatchPlan:
-    """Largest per-GPU batch whose training step fits ``headroom`` of the device memory (see module doc)."""
+         fallback_budget_bytes: float = 64 * 2**30, compression: str = "none") -> BatchPlan:
+    """Largest per-GPU batch whose training step fits ``headroom`` of the device memory (see module doc).
+
+    The two probes run with the weight-gradient side stream OFF (the large-batch regime the chosen batch usually
+    lands in); when the chosen batch is small enough for the side stream to be on, its peak is re-measured in that
+    regime and the batch shrunk if the stash of wgrad operands pushes it over budget. ``compression`` != ``none``
+    adds the data-parallel engine's 16-bit shadow of the gradient buffer (created after planning) to the fixed
+    bytes."""
     cfg = model.cfg
     device = torch.device(device)
     if device.type == "cuda":
+        from ..ops import hip as _hip
+
         # probes of >= 8192 tokens run the large-batch kernel paths (no small-grid split-K workspaces)
         b1, b2 = probe_batches or (max(8, 8192 // seq_len), 2 * max(8, 8192 // seq_len))
-        p1 = _probe_peak(model, store, cfg, b1, seq_len, device)
-        p2 = _probe_peak(model, store, cfg, b2, seq_len, device)
+        with _hip.wgrad_stream_override("0"):
+            p1 = _probe_peak(model, store, cfg, b1, seq_len, device)
+            p2 = _probe_peak(model, store, cfg, b2, seq_len, device)
         per_seq = max(1.0, (p2 - p1) / float(b2 - b1))
-        fixed = p1 - per_seq * b1
+        fixed = p1 - per_seq * b1 + _shadow_bytes(store, compression)
         free, total = torch.cuda.mem_get_info(device)
         others = max(0, total - free - torch.cuda.memory_reserved(device))  # other processes / runtime pools
         budget = headroom * total - others
         method = "probe"
+        b, capped_by = choose(per_seq, fixed, budget, seq_len, multiple=multiple, max_tokens=max_tokens)
+        if b > 0 and _hip.wgrad_side_stream_for(b * seq_len):
+            peak = _probe_peak(model, store, cfg, b, seq_len, device) + _shadow_bytes(store, compression)
+            method = "probe+side-stream"
+            if peak > budget:
+                # the side-stream stash adds a per-sequence term: rescale the slope to the measured peak
+                per_seq = max(per_seq, (peak - fixed) / float(b))
+                b, capped_by = choose(per_seq, fixed, budget, seq_len, multiple=multiple, max_tokens=max_tokens)
+        return BatchPlan(per_gpu_batch=b, seq_len=seq_len, per_seq_bytes=per_seq, fixed_bytes=fixed,
+                         budget_bytes=budget, total_bytes=float(total), method=method, capped_by=capped_by,
+                         predicted_peak_bytes=fixed + per_seq * b)
     else:
         per_seq = activation_bytes_per_seq(cfg, seq_len, 4 if store.compute_dtype == torch.float32 else 2)
         fixed = float(store.numel) * (4 * 4 + store.compute.element_size())  # master, grad, m, v, compute copy
+        fixed += _shadow_bytes(store, compression)
         total = float(fallback_budget_bytes)
         budget = headroom * total
         method = "analytic"

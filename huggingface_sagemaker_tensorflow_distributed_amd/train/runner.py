@@ -133,7 +133,8 @@ def build(args, mode: str):
     if args.train_batch_size == "auto":
         # sized on the device before any readiness hook / bucketer exists (the probes are plain fwd + bwd)
         batch_plan = batch_planner.plan(model, store, max_len, dev, headroom=args.auto_batch_headroom,
-                                        max_tokens=args.auto_batch_max_tokens or None)
+                                        max_tokens=args.auto_batch_max_tokens or None,
+                                        compression=getattr(args, "grad_compression", "none") if world > 1 else "none")
         per_gpu = batch_planner.agree_min(batch_plan.per_gpu_batch, dev)
         batch_plan.per_gpu_batch = per_gpu
         args.train_batch_size = per_gpu if mode == "train" else per_gpu * world

@@ -55,6 +55,20 @@ def test_auto_batch_end_to_end_cpu(tmp_path, monkeypatch):
     assert out["args"].train_batch_size == 4 and out["global_step"] == 2
 
 
+def test_compression_shadow_counts_in_fixed_bytes():
+    """--grad_compression fp16/bf16 adds the engine's 16-bit shadow of the fp32 gradient buffer (numel x 2 bytes),
+    created after planning, to the planned fixed bytes."""
+    from huggingface_sagemaker_tensorflow_distributed_amd.models import build_model
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel import FlatParamStore
+
+    model = build_model(resolve_config("hsd-tiny-bert"), seed=0)
+    store = FlatParamStore(model, torch.device("cpu"))
+    a = bp.plan(model, store, 16, "cpu", max_tokens=None)
+    b = bp.plan(model, store, 16, "cpu", max_tokens=None, compression="fp16")
+    assert b.fixed_bytes - a.fixed_bytes == store.numel * 2
+    assert b.per_gpu_batch <= a.per_gpu_batch
+
+
 @pytest.mark.gpu
 def test_probe_plan_predicts_the_step_peak_on_gpu():
     """On the MI355X the two-probe linear model predicts the peak memory of a full training step (forward,
@@ -73,7 +87,7 @@ def test_probe_plan_predicts_the_step_peak_on_gpu():
     total = torch.cuda.mem_get_info(dev)[1]
     headroom = (torch.cuda.memory_allocated(dev) + 12 * 2**30) / total
     plan = bp.plan(model, store, S, dev, headroom=headroom, max_tokens=None)
-    assert plan.method == "probe" and plan.capped_by == "memory" and plan.per_gpu_batch >= 64, plan
+    assert plan.method.startswith("probe") and plan.capped_by == "memory" and plan.per_gpu_batch >= 64, plan
     B = plan.per_gpu_batch
     ids = torch.randint(1000, cfg.vocab_size, (B, S), device=dev)
     am = torch.ones(B, S, dtype=torch.long, device=dev)
