@@ -21,7 +21,7 @@ hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
 void adam_step(torch::Tensor p, torch::Tensor m, torch::Tensor v, torch::Tensor g, c10::optional<torch::Tensor> out,
                c10::optional<torch::Tensor> decay, double step, double eps, double b1, double b2, double gscale,
-               double lr_wd) {
+               double lr_wd, c10::optional<torch::Tensor> coef) {
   CHECK_CUDA(p); CHECK_CONTIG(p); CHECK_DTYPE(p, torch::kFloat32);
   CHECK_DTYPE(m, torch::kFloat32); CHECK_DTYPE(v, torch::kFloat32);
   TORCH_CHECK(p.numel() == m.numel() && p.numel() == v.numel() && p.numel() == g.numel(), "size mismatch");
@@ -39,9 +39,15 @@ void adam_step(torch::Tensor p, torch::Tensor m, torch::Tensor v, torch::Tensor 
     TORCH_CHECK(decay->numel() * 64 >= p.numel(), "decay mask too small");
     dm = decay->data_ptr<uint8_t>();
   }
+  const float* dcoef = nullptr;  // fp32 [4] on the device: (step, eps, grad_scale, lr*wd) override the scalars
+  if (coef.has_value()) {
+    CHECK_CUDA(*coef); CHECK_DTYPE(*coef, torch::kFloat32);
+    TORCH_CHECK(coef->numel() >= 4, "coef: fp32 [4]");
+    dcoef = coef->data_ptr<float>();
+  }
   hsd::launch_adam(p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), g.data_ptr(), gbf, o, dm,
                    p.numel(), (float)step, (float)eps, (float)b1, (float)b2, (float)gscale, (float)lr_wd,
-                   cur_stream());
+                   dcoef, cur_stream());
 }
 
 #define OPT_BF(o) ((o).has_value() ? reinterpret_cast<hsd::bf16_t*>((o)->data_ptr()) : nullptr)

@@ -31,7 +31,13 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
                                                    float* __restrict__ v, const void* __restrict__ g_,
                                                    bf16_t* __restrict__ out, const uint8_t* __restrict__ decay,
                                                    int64_t n4, float step, float eps, float b1, float b2,
-                                                   float gscale, float lr_wd) {
+                                                   float gscale, float lr_wd, const float* __restrict__ coef) {
+  if (coef != nullptr) {  // HIP-graph replays: this step's scalars live on the device (train/graph.py)
+    step = coef[0];
+    eps = coef[1];
+    gscale = coef[2];
+    lr_wd = coef[3];
+  }
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i0 = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i0 < n4; i0 += stride * U) {
     f32x4 g[U], pp[U], mm[U], vv[U];
@@ -73,7 +79,7 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
 
 void launch_adam(float* p, float* m, float* v, const void* g, bool grad_bf16, bf16_t* out_bf16,
                  const uint8_t* decay, int64_t n, float step, float eps, float b1, float b2, float gscale,
-                 float lr_wd, hipStream_t stream) {
+                 float lr_wd, const float* coef, hipStream_t stream) {
   int64_t n4 = n / 4;  // n is a multiple of 1024 (FlatParamStore)
   const char* ue = getenv("HSD_ADAM_UNROLL");  // A/B: chunks per thread per trip (1, 2 or 4)
   const int U = ue ? atoi(ue) : 2;
@@ -84,13 +90,13 @@ void launch_adam(float* p, float* m, float* v, const void* g, bool grad_bf16, bf
   do {                                                                                                           \
     if (U >= 4)                                                                                                  \
       hipLaunchKernelGGL((adam_kernel<GB, WB, 4>), dim3((unsigned)blocks), dim3(threads), 0, stream, p, m, v, g, \
-                         out_bf16, decay, n4, step, eps, b1, b2, gscale, lr_wd);                                 \
+                         out_bf16, decay, n4, step, eps, b1, b2, gscale, lr_wd, coef);                                 \
     else if (U == 2)                                                                                             \
       hipLaunchKernelGGL((adam_kernel<GB, WB, 2>), dim3((unsigned)blocks), dim3(threads), 0, stream, p, m, v, g, \
-                         out_bf16, decay, n4, step, eps, b1, b2, gscale, lr_wd);                                 \
+                         out_bf16, decay, n4, step, eps, b1, b2, gscale, lr_wd, coef);                                 \
     else                                                                                                         \
       hipLaunchKernelGGL((adam_kernel<GB, WB, 1>), dim3((unsigned)blocks), dim3(threads), 0, stream, p, m, v, g, \
-                         out_bf16, decay, n4, step, eps, b1, b2, gscale, lr_wd);                                 \
+                         out_bf16, decay, n4, step, eps, b1, b2, gscale, lr_wd, coef);                                 \
   } while (0)
   if (grad_bf16) {
     if (out_bf16) HSD_ADAM(true, true); else HSD_ADAM(true, false);

@@ -11,7 +11,7 @@ struct DropoutParams;
 // adam.hip
 void launch_adam(float* p, float* m, float* v, const void* g, bool grad_bf16, bf16_t* out_bf16,
                  const uint8_t* decay, int64_t n, float step, float eps, float b1, float b2, float gscale,
-                 float lr_wd, hipStream_t stream);
+                 float lr_wd, const float* coef, hipStream_t stream);
 
 }  // namespace hsd
 

@@ -114,7 +114,10 @@ class wgrad_stream_override:  # noqa: N801 - used as a context manager
 
 
 def join_side_streams() -> None:
-    """Make the current stream wait for every side stream (call before consuming gradients)."""
+    """Make the current stream wait for every side stream (call before consuming gradients). A no-op inside a HIP
+    graph capture: captured steps never use the wgrad side stream (``_use_side_stream``)."""
+    if _SIDE and torch.cuda.is_current_stream_capturing():
+        return
     cur = torch.cuda.current_stream() if _SIDE else None
     for s in _SIDE.values():
         if s.device == cur.device:
@@ -160,8 +163,10 @@ def _empty(shape, like, dtype=None):
 
 
 # ------------------------------------------------------------------------------------------ optimizer
-def adam_step(p, m, v, g, out, decay, step, eps, b1, b2, gscale, lr_wd):
-    _C.adam_step(p, m, v, g, out, decay, step, eps, b1, b2, gscale, lr_wd)
+def adam_step(p, m, v, g, out, decay, step, eps, b1, b2, gscale, lr_wd, coef=None):
+    """``coef``: optional fp32 [4] device tensor (step, eps, grad_scale, lr*wd) read by the kernel instead of the
+    host scalars (captured HIP-graph steps, train/graph.py)."""
+    _C.adam_step(p, m, v, g, out, decay, step, eps, b1, b2, gscale, lr_wd, coef)
 
 
 # ------------------------------------------------------------------------------------------ linear

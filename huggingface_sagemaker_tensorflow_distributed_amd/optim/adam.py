@@ -47,6 +47,7 @@ class FusedAdam:
         self.exp_avg = torch.zeros_like(store.master)
         self.exp_avg_sq = torch.zeros_like(store.master)
         self._decay_mask = store.decay_block_mask(ALIGN) if weight_decay else None
+        self.dcoef: Optional[torch.Tensor] = None  # device-side step scalars (HIP-graph replays), see use_device_coef
 
     # --------------------------------------------------------------------------
     def state_tensors(self) -> List[torch.Tensor]:
@@ -69,6 +70,23 @@ class FusedAdam:
         step = self.lr * math.sqrt(bc2) / bc1
         eps_eff = self.eps if self.eps_mode == "keras" else self.eps * math.sqrt(bc2)
         return step, eps_eff
+
+    # -------------------------------------------------------------------------- device-side coefficients
+    def use_device_coef(self) -> torch.Tensor:
+        """From now on every Adam launch reads (step, eps, grad_scale, lr*wd) from an fp32 [4] device tensor instead
+        of kernel arguments, so a captured HIP graph of the whole training step replays with each step's bias
+        correction and learning rate (train/graph.py). :meth:`prepare_device_step` fills it before a replay."""
+        if self.dcoef is None:
+            self.dcoef = torch.zeros(4, dtype=torch.float32, device=self.store.master.device)
+        return self.dcoef
+
+    def prepare_device_step(self, grad_scale: float) -> None:
+        """Advance the step count and write this step's scalars to :attr:`dcoef` (stream-ordered H2D copy of a
+        fresh host tensor: the host may move on at once)."""
+        self.step_count += 1
+        step, eps_eff = self._coeffs()
+        self.dcoef.copy_(torch.tensor([step, eps_eff, float(grad_scale), self.lr * self.weight_decay],
+                                      dtype=torch.float32), non_blocking=True)
 
     # -------------------------------------------------------------------------- overlap with backward
     def enable_overlap(self, ranges: List[Tuple[int, int]], on_ready: Optional[Callable] = None) -> None:
@@ -125,7 +143,7 @@ class FusedAdam:
         out = s.compute[st:e] if s.compute is not s.master else None
         dm = self._decay_mask[st // ALIGN:(e + ALIGN - 1) // ALIGN] if self._decay_mask is not None else None
         hip.adam_step(s.master[st:e], self.exp_avg[st:e], self.exp_avg_sq[st:e], s.grad[st:e], out, dm, step,
-                      eps_eff, self.beta1, self.beta2, gscale, self.lr * self.weight_decay)
+                      eps_eff, self.beta1, self.beta2, gscale, self.lr * self.weight_decay, self.dcoef)
         if self._tsub is not None:
             s.refresh_transposed_subset(self._tsub[b])
         self._done[b] = True
@@ -160,7 +178,7 @@ class FusedAdam:
             hip.join_side_streams()  # weight gradients may still be in flight on the wgrad stream
             hip.adam_step(s.master, self.exp_avg, self.exp_avg_sq, s.grad, s.compute if write_compute else None,
                           self._decay_mask, step, eps_eff, self.beta1, self.beta2, float(grad_scale),
-                          self.lr * self.weight_decay)
+                          self.lr * self.weight_decay, self.dcoef)
             s.refresh_transposed()
             return
         # reference path (CPU): identical math on flat buffers
@@ -221,7 +239,7 @@ class LocalOverlap:
             cur = torch.cuda.current_stream(self.stream.device)
             self.stream.wait_stream(cur)
             side = hip.side_stream(self.stream.device)
-            if side is not None:
+            if side is not None and not torch.cuda.is_current_stream_capturing():  # (no wgrad stream in a capture)
                 self.stream.wait_stream(side)
             with torch.cuda.stream(self.stream):
                 self.opt.step_range(b)

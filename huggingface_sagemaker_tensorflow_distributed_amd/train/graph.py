@@ -84,10 +84,14 @@ class CapturedStep:
         torch.cuda.synchronize(trainer.device)
         store.zero_grad()
         self.graph = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.graph):
-            model.rng.new_step(0)  # per-site seeds fixed; the device step seed varies per replay
-            self.loss, self.logits = trainer._forward_loss(self.static)
-            self.loss.backward()
+        cb, store.ready_callback = store.ready_callback, None  # no optimizer slices inside a fwd+bwd-only graph
+        try:
+            with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
+                model.rng.new_step(0)  # per-site seeds fixed; the device step seed varies per replay
+                self.loss, self.logits = trainer._forward_loss(self.static)
+                self.loss.backward()
+        finally:
+            store.ready_callback = cb
         torch.cuda.synchronize(trainer.device)
         logger.info("captured training step graph for batch shape %s", tuple(example["input_ids"].shape))
 
@@ -95,5 +99,67 @@ class CapturedStep:
         """Copy ``batch`` into the static inputs and replay (gradients ACCUMULATE into main_grad)."""
         for k, v in batch.items():
             self.static[k].copy_(v, non_blocking=True)
+        self.graph.replay()
+        return self.loss, self.logits
+
+
+class CapturedTrainStep:
+    """The WHOLE one-process training step as one graph: gradient zeroing, forward, loss, backward, the optimizer
+    slices stepped under backward (optim/adam.py LocalOverlap: a side-stream branch of the graph per slice, forked
+    when the slice's last gradient is queued), the remaining slices and the Wᵀ / fp8 weight-copy refresh.
+
+    Adam's per-step scalars (bias-corrected step, ε, grad scale, lr·wd) are read from a device tensor
+    (``FusedAdam.use_device_coef``) that :meth:`run` refreshes before each replay, as the dropout step seed is; the
+    Python-side optimizer bookkeeping that ran once during capture is replayed by hand (step count). Capturing
+    runs no kernel, so it changes no weight; the forward + backward warm-up before it (lazy workspaces, first-use
+    allocations) leaves the gradients zeroed."""
+
+    def __init__(self, trainer, example: Dict[str, torch.Tensor], warmup: int = 2):
+        self.trainer = trainer
+        self.static = {k: v.clone() for k, v in example.items()}
+        model, store, opt = trainer.model, trainer.store, trainer.optimizer
+        model.train()
+        s = torch.cuda.Stream(device=trainer.device)
+        s.wait_stream(torch.cuda.current_stream(trainer.device))
+        cb, store.ready_callback = store.ready_callback, None
+        try:
+            with torch.cuda.stream(s):
+                for _ in range(warmup):
+                    model.rng.new_step(0)
+                    store.zero_grad()
+                    loss, _ = trainer._forward_loss(self.static)
+                    loss.backward()
+        finally:
+            store.ready_callback = cb
+        torch.cuda.current_stream(trainer.device).wait_stream(s)
+        torch.cuda.synchronize(trainer.device)
+        store.zero_grad()
+        opt.use_device_coef()
+        ov = trainer._opt_overlap
+        gscale = 1.0 / trainer.world
+        self.graph = torch.cuda.CUDAGraph()
+        step0 = opt.step_count
+        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
+            store.zero_grad()
+            model.rng.new_step(0)
+            if ov is not None:
+                opt.begin_step(grad_scale=gscale)
+                ov.begin()
+            self.loss, self.logits = trainer._forward_loss(self.static)
+            self.loss.backward()
+            if ov is not None:
+                ov.join()
+            opt.step(grad_scale=gscale)
+        opt.step_count = step0  # begin_step / step advanced it once during capture; each replay advances it
+        torch.cuda.synchronize(trainer.device)
+        self.gscale = gscale
+        logger.info("captured whole training step graph (optimizer %s) for batch shape %s",
+                    "overlapped" if ov is not None else "after backward", tuple(example["input_ids"].shape))
+
+    def run(self, batch: Dict[str, torch.Tensor]):
+        """Copy ``batch`` in, set this step's optimizer scalars, replay: one complete optimizer step."""
+        for k, v in batch.items():
+            self.static[k].copy_(v, non_blocking=True)
+        self.trainer.optimizer.prepare_device_step(self.gscale)
         self.graph.replay()
         return self.loss, self.logits

@@ -60,9 +60,12 @@ class _Meter:
             self.t += s[[3, 1, 2]]
             self._pending.clear()
 
-    def update(self, loss: torch.Tensor, logits: torch.Tensor, labels: torch.Tensor) -> None:
+    def update(self, loss: torch.Tensor, logits: torch.Tensor, labels: torch.Tensor, static: bool = False) -> None:
+        """``static``: ``loss`` / ``logits`` are a captured graph's output buffers, overwritten by the next replay."""
         fused_stats = getattr(loss, "_hsd_stats", None)
         if fused_stats is not None:
+            if static:
+                fused_stats = fused_stats.clone()
             # the fused head already counted {loss sum, hits, rows} on the device: keep the tensor, add them up
             # when the metrics are read (no kernels per step)
             self._pending.append(fused_stats)
@@ -125,10 +128,10 @@ class Trainer:
         self.lr_warmup_steps = max(0, int(lr_warmup_steps))
         self.base_lr = float(getattr(optimizer, "lr", 0.0))
         self.total_steps: Optional[int] = None
+        self._full_graph = False
+        self._setup_opt_overlap()
         if hip_graph:
             self.enable_hip_graph()
-        if self._seed is None:
-            self._setup_opt_overlap()
 
     def _setup_opt_overlap(self) -> None:
         """Optimizer slices stepped under backward (optim/adam.py). Off: HSD_OPT_OVERLAP=0, CPU, HIP-graph mode,
@@ -168,9 +171,21 @@ class Trainer:
             return False
         from .graph import DeviceStepSeed
 
-        self._drop_opt_overlap()  # captured steps keep the optimizer outside the graph
+        # whole-step capture (HSD_GRAPH_FULL=1, default) for one-micro-step optimizer steps: forward, backward, the
+        # overlapped optimizer slices and the weight-copy refresh in one graph; accumulation steps replay a
+        # forward + backward graph per micro-step and step the optimizer eagerly
+        self._full_graph = os.environ.get("HSD_GRAPH_FULL", "1") == "1" and hasattr(self.optimizer, "use_device_coef")
         self._seed = DeviceStepSeed(self.device, self.model.rng.base_seed, self.rank)
         return True
+
+    def _full_graph_for(self, mb):
+        key = ("full",) + tuple((k, tuple(v.shape), v.dtype) for k, v in sorted(mb.items()))
+        g = self._graphs.get(key)
+        if g is None:
+            from .graph import CapturedTrainStep
+
+            g = self._graphs[key] = CapturedTrainStep(self, mb)
+        return g
 
     def _graph_for(self, mb):
         key = tuple((k, tuple(v.shape), v.dtype) for k, v in sorted(mb.items()))
@@ -200,6 +215,8 @@ class Trainer:
     def train_step(self, micro_batches: List[Dict[str, torch.Tensor]], meter: Optional[_Meter] = None) -> torch.Tensor:
         """One optimizer step over ``len(micro_batches)`` accumulation micro-steps."""
         self.model.train()
+        if self._seed is not None and self._graph_replay and self._full_graph and len(micro_batches) == 1:
+            return self._graph_step(micro_batches[0], meter)
         if self._seed is not None:
             # graph mode: per-site seeds fixed (step 0), the device step seed carries the step
             self._seed.set_step(self.global_step)
@@ -243,6 +260,24 @@ class Trainer:
                 raise RuntimeError(f"ranks diverged at step {self.global_step} (--check_sync)")
         return loss
 
+    def _graph_step(self, mb, meter):
+        """One optimizer step as one replay of the captured whole-step graph (train/graph.py CapturedTrainStep)."""
+        self._seed.set_step(self.global_step)
+        self.model.rng.new_step(0)
+        if self.lr_schedule != "constant" or self.lr_warmup_steps:
+            self.optimizer.lr = self.lr_at(self.global_step)
+        self._phase = "graph-step"
+        with prange("graph-step"):
+            loss, logits = self._full_graph_for(mb).run(mb)
+        if meter is not None:
+            meter.update(loss, logits, mb["labels"], static=True)
+        self._phase = "idle"
+        self.global_step += 1
+        if self.check_sync and self.global_step % self.check_sync == 0:
+            if not params_in_sync(self.store):
+                raise RuntimeError(f"ranks diverged at step {self.global_step} (--check_sync)")
+        return loss
+
     def _micro_steps(self, micro_batches, meter, ov, k):
         """Forward + backward of every accumulation micro-step (the bucket all-reduces and, with the optimizer
         overlap, the Adam slices start under the last backward)."""
@@ -255,7 +290,7 @@ class Trainer:
                 with prange("graph-replay"):
                     loss, logits = self._graph_for(mb).run(mb)
                 if meter is not None:
-                    meter.update(loss, logits, mb["labels"])
+                    meter.update(loss, logits, mb["labels"], static=True)
                 continue
             ctx = self.bucketer.no_sync() if (self.bucketer is not None and not last) else contextlib.nullcontext()
             with ctx:

@@ -9,7 +9,7 @@ import torch
 pytestmark = pytest.mark.gpu
 
 
-def _trainer(gpu, graph_replay):
+def _trainer(gpu, graph_replay, **kw):
     from huggingface_sagemaker_tensorflow_distributed_amd.models import build_model, resolve_config
     from huggingface_sagemaker_tensorflow_distributed_amd.optim import FusedAdam
     from huggingface_sagemaker_tensorflow_distributed_amd.parallel import FlatParamStore
@@ -19,13 +19,18 @@ def _trainer(gpu, graph_replay):
     model = build_model(cfg, seed=0).to(gpu)
     model.rng.base_seed = 5
     store = FlatParamStore(model, gpu, compute_dtype=torch.bfloat16)
-    opt = FusedAdam(store, lr=1e-4)
-    tr = Trainer(model, store, opt, None, gpu, hip_graph=True)
+    opt = FusedAdam(store, lr=1e-4, weight_decay=kw.pop("weight_decay", 0.0))
+    tr = Trainer(model, store, opt, None, gpu, hip_graph=True, **kw)
     tr._graph_replay = graph_replay
     return tr
 
 
-def test_graph_replay_matches_eager(gpu):
+@pytest.mark.parametrize("full", ["1", "0"])
+def test_graph_replay_matches_eager(gpu, monkeypatch, full):
+    """full=1: the whole step (zeroing, fwd, bwd, overlapped Adam slices, Wᵀ refresh) is one graph replay with
+    device-side Adam scalars; full=0: fwd+bwd graph, eager optimizer. A linear LR schedule with warm-up and AdamW
+    weight decay make every step's scalars differ."""
+    monkeypatch.setenv("HSD_GRAPH_FULL", full)
     g = torch.Generator().manual_seed(0)
     batches = []
     for _ in range(3):
@@ -36,10 +41,13 @@ def test_graph_replay_matches_eager(gpu):
                         "labels": torch.randint(0, 2, (16,), generator=g).to(gpu)})
     res = {}
     for replay in (False, True):
-        tr = _trainer(gpu, replay)
+        tr = _trainer(gpu, replay, weight_decay=0.01, lr_schedule="linear", lr_warmup_steps=2)
+        tr.total_steps = 3
         losses = [float(tr.train_step([b])) for b in batches]
         if replay:
             assert len(tr._graphs) == 1
+            assert tr._full_graph == (full == "1")
+        assert tr.optimizer.step_count == 3
         torch.cuda.synchronize()
         res[replay] = (losses, tr.store.master.clone())
         tr._seed.close()
@@ -50,3 +58,43 @@ def test_graph_replay_matches_eager(gpu):
     assert rel < 1e-4, float(rel)
     # dropout masks move with the step: the three losses are not a replay of one step
     assert len({round(x, 6) for x in l1}) == 3
+
+
+def test_graph_accumulation_and_metrics_match_eager(gpu, monkeypatch):
+    """Two accumulation micro-steps (fwd+bwd graph per micro-step, optimizer slices stepped at the join) and the
+    fused-head metrics of graph replays (static output buffers: every step's stats are kept, not the last one's)."""
+    from huggingface_sagemaker_tensorflow_distributed_amd.train.trainer import _Meter
+
+    g = torch.Generator().manual_seed(1)
+    mbs = []
+    for _ in range(4):
+        ids = torch.randint(1000, 30000, (8, 128), generator=g)
+        mbs.append({"input_ids": ids.to(gpu), "attention_mask": torch.ones(8, 128, dtype=torch.long, device=gpu),
+                    "labels": torch.randint(0, 2, (8,), generator=g).to(gpu)})
+    res = {}
+    for replay in (False, True):
+        tr = _trainer(gpu, replay)
+        meter = _Meter(gpu)
+        tr.train_step(mbs[:2], meter)
+        tr.train_step(mbs[2:], meter)
+        m = meter.result(global_=False)
+        torch.cuda.synchronize()
+        res[replay] = (m, tr.store.master.clone())
+        tr._seed.close()
+    (m0, w0), (m1, w1) = res[False], res[True]
+    assert (w0 - w1).norm() / w0.norm() < 1e-4
+    for k in m0:
+        assert abs(m0[k] - m1[k]) <= 2e-3 * max(1.0, abs(m0[k])), (m0, m1)
+
+    # one-micro-step graph replays: metrics over 2 steps = eager metrics
+    monkeypatch.setenv("HSD_GRAPH_FULL", "1")
+    res = {}
+    for replay in (False, True):
+        tr = _trainer(gpu, replay)
+        meter = _Meter(gpu)
+        tr.train_step(mbs[:1], meter)
+        tr.train_step(mbs[1:2], meter)
+        res[replay] = meter.result(global_=False)
+        tr._seed.close()
+    for k in res[False]:
+        assert abs(res[False][k] - res[True][k]) <= 2e-3 * max(1.0, abs(res[False][k])), res
