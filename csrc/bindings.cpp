@@ -80,6 +80,25 @@ void ln_fwd(torch::Tensor y, c10::optional<torch::Tensor> res, torch::Tensor gam
                      cur_stream());
 }
 
+// LN forward + the output's fp8 e4m3 copy (delayed scaling: amax_in = the site's previous amax, fp32 [1]; sinv fp32 [1]
+// written; amax_track fp32 [1] accumulates this tensor's amax)
+void ln_fwd_q8(torch::Tensor y, torch::Tensor gamma, torch::Tensor beta, torch::Tensor out, torch::Tensor mean,
+               torch::Tensor rstd, double eps, torch::Tensor q8, torch::Tensor amax_in, torch::Tensor sinv,
+               torch::Tensor amax_track) {
+  check_bf16(y, "y"); check_bf16(out, "out"); check_bf16(gamma, "gamma"); check_bf16(beta, "beta");
+  check_f32(mean, "mean"); check_f32(rstd, "rstd");
+  check_f32(amax_in, "amax_in"); check_f32(sinv, "sinv"); check_f32(amax_track, "amax_track");
+  CHECK_CUDA(q8); CHECK_CONTIG(q8); CHECK_DTYPE(q8, torch::kUInt8);
+  const int H = (int)y.size(-1);
+  const int rows = (int)(y.numel() / H);
+  TORCH_CHECK(H % 8 == 0 && H <= 1024, "ln_fwd_q8: H % 8 == 0 and H <= 1024");
+  TORCH_CHECK(gamma.numel() == H && beta.numel() == H && mean.numel() >= rows && rstd.numel() >= rows, "ln shapes");
+  TORCH_CHECK(q8.numel() == y.numel() && out.numel() == y.numel(), "q8 / out shape");
+  hsd::launch_ln_fwd_q8(CBF(y), CBF(gamma), CBF(beta), BF(out), mean.data_ptr<float>(), rstd.data_ptr<float>(), rows,
+                        H, (float)eps, q8.data_ptr<uint8_t>(), amax_in.data_ptr<float>(), sinv.data_ptr<float>(),
+                        amax_track.data_ptr<float>(), cur_stream());
+}
+
 void ln_bwd(torch::Tensor dout, torch::Tensor z, torch::Tensor mean, torch::Tensor rstd, torch::Tensor gamma,
             c10::optional<torch::Tensor> dz, c10::optional<torch::Tensor> dy, c10::optional<torch::Tensor> dres_add,
             torch::Tensor dgamma, torch::Tensor dbeta, c10::optional<torch::Tensor> dbias, double p, int64_t seed) {
@@ -96,6 +115,28 @@ void ln_bwd(torch::Tensor dout, torch::Tensor z, torch::Tensor mean, torch::Tens
   hsd::launch_ln_bwd(CBF(dout), CBF(z), mean.data_ptr<float>(), rstd.data_ptr<float>(), CBF(gamma), OPT_BF(dz),
                      OPT_BF(dy), dres_add.has_value() ? CBF(*dres_add) : nullptr, dgamma.data_ptr<float>(),
                      dbeta.data_ptr<float>(), OPT_F(dbias), rows, H, p, (uint64_t)seed, cur_stream());
+}
+
+// ln_bwd + dy's fp8 copy (qfmt 0 e4m3 / 1 e5m2) for the fp8 dgrad GEMM; dy required
+void ln_bwd_q8(torch::Tensor dout, torch::Tensor z, torch::Tensor mean, torch::Tensor rstd, torch::Tensor gamma,
+               c10::optional<torch::Tensor> dz, torch::Tensor dy, torch::Tensor dgamma, torch::Tensor dbeta,
+               c10::optional<torch::Tensor> dbias, double p, int64_t seed, torch::Tensor q8, torch::Tensor amax_in,
+               torch::Tensor sinv, torch::Tensor amax_track, int64_t qfmt) {
+  check_bf16(dout, "dout"); check_bf16(z, "z"); check_bf16(gamma, "gamma"); check_bf16(dy, "dy");
+  check_f32(mean, "mean"); check_f32(rstd, "rstd"); check_f32(dgamma, "dgamma"); check_f32(dbeta, "dbeta");
+  check_f32(amax_in, "amax_in"); check_f32(sinv, "sinv"); check_f32(amax_track, "amax_track");
+  CHECK_CUDA(q8); CHECK_CONTIG(q8); CHECK_DTYPE(q8, torch::kUInt8);
+  const int H = (int)z.size(-1);
+  const int rows = (int)(z.numel() / H);
+  TORCH_CHECK(dout.numel() == z.numel() && dy.numel() == z.numel() && q8.numel() == z.numel(), "ln_bwd_q8 shapes");
+  TORCH_CHECK(H % 4 == 0 && H <= 1024 && (qfmt == 0 || qfmt == 1), "ln_bwd_q8: H % 4 == 0, H <= 1024, qfmt 0/1");
+  TORCH_CHECK(dgamma.numel() == H && dbeta.numel() == H, "dgamma/dbeta shape");
+  if (dz.has_value()) { check_bf16(*dz, "dz"); TORCH_CHECK(dz->numel() == z.numel(), "dz shape"); }
+  if (dbias.has_value()) { check_f32(*dbias, "dbias"); TORCH_CHECK(dbias->numel() == H, "dbias shape"); }
+  hsd::launch_ln_bwd_q8(CBF(dout), CBF(z), mean.data_ptr<float>(), rstd.data_ptr<float>(), CBF(gamma), OPT_BF(dz),
+                        BF(dy), nullptr, dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), OPT_F(dbias), rows, H, p,
+                        (uint64_t)seed, q8.data_ptr<uint8_t>(), amax_in.data_ptr<float>(), sinv.data_ptr<float>(),
+                        amax_track.data_ptr<float>(), (int)qfmt, cur_stream());
 }
 
 void embed_fwd(torch::Tensor ids, torch::Tensor pos_ids, c10::optional<torch::Tensor> type_ids, torch::Tensor word,
@@ -512,6 +553,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 HIP kernels for huggingface_sagemaker_tensorflow_distributed_amd";
   hsd::register_comm(m);
   m.def("adam_step", &adam_step);
+  m.def("ln_fwd_q8", &ln_fwd_q8);
+  m.def("ln_bwd_q8", &ln_bwd_q8);
   m.def("ln_fwd", &ln_fwd);
   m.def("ln_bwd", &ln_bwd);
   m.def("embed_fwd", &embed_fwd);

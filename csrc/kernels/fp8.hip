@@ -11,18 +11,9 @@
 // site's first use (no history yet) runs the separate amax pass ("current" scaling). The *_many
 // variants batch all weight matrices of the model (W and its stored transpose share one amax) into one
 // launch each after every optimizer step.
-#include "common.h"
+#include "fp8_common.h"
 
 namespace hsd {
-
-constexpr float kE4M3Max = 448.0f, kE5M2Max = 57344.0f;
-
-__device__ __forceinline__ void atomic_max_pos(float* addr, float v) {
-  // non-negative floats order like their bit patterns; skip the (same-address, serialising) atomic when a
-  // larger value is already there — after the first few blocks almost every block skips it
-  if (v > __hip_atomic_load(addr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT))
-    atomicMax(reinterpret_cast<unsigned int*>(addr), __float_as_uint(v));
-}
 
 __device__ __forceinline__ float block_max(float v) {
   __shared__ float red[16];
@@ -37,12 +28,6 @@ __device__ __forceinline__ float block_max(float v) {
   return r;  // valid in thread 0
 }
 
-// |x| max over [beg, end) of x (same access pattern as quant_range)
-__device__ __forceinline__ float absmax8(const u32x4& v, float m) {
-#pragma unroll
-  for (int k = 0; k < 4; ++k) m = fmaxf(m, fmaxf(fabsf(lo_bf(v[k])), fabsf(hi_bf(v[k]))));
-  return m;
-}
 __device__ __forceinline__ float absmax_range(const bf16_t* __restrict__ x, int64_t beg, int64_t end, int64_t stride) {
   float m = 0.f;
   int64_t i = beg;
@@ -61,32 +46,6 @@ __device__ __forceinline__ float absmax_range(const bf16_t* __restrict__ x, int6
     }
   }
   return m;
-}
-
-template <int FMT>
-__device__ __forceinline__ uint32_t cvt4(float a, float b, float c, float d) {
-  constexpr float mx = FMT == 0 ? kE4M3Max : kE5M2Max;
-  a = fminf(fmaxf(a, -mx), mx);
-  b = fminf(fmaxf(b, -mx), mx);
-  c = fminf(fmaxf(c, -mx), mx);
-  d = fminf(fmaxf(d, -mx), mx);
-  int r;
-  if constexpr (FMT == 0) {
-    r = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
-    r = __builtin_amdgcn_cvt_pk_fp8_f32(c, d, r, true);
-  } else {
-    r = __builtin_amdgcn_cvt_pk_bf8_f32(a, b, 0, false);
-    r = __builtin_amdgcn_cvt_pk_bf8_f32(c, d, r, true);
-  }
-  return (uint32_t)r;
-}
-
-template <int FMT>
-__device__ __forceinline__ u32x2 quant8(const u32x4& v, float s) {
-  u32x2 o;
-  o.x = cvt4<FMT>(lo_bf(v[0]) * s, hi_bf(v[0]) * s, lo_bf(v[1]) * s, hi_bf(v[1]) * s);
-  o.y = cvt4<FMT>(lo_bf(v[2]) * s, hi_bf(v[2]) * s, lo_bf(v[3]) * s, hi_bf(v[3]) * s);
-  return o;
 }
 
 // quantise [beg, end) (thread's first element `beg`, `stride` between a thread's vectors); four 16-B
@@ -119,10 +78,6 @@ __device__ __forceinline__ float quant_range(const bf16_t* __restrict__ x, uint8
     }
   }
   return m;
-}
-
-__device__ __forceinline__ float fmt_scale(int fmt, float amax) {
-  return (fmt == 0 ? kE4M3Max : kE5M2Max) / fmaxf(amax, 1e-12f);
 }
 
 // ---- single tensor -----------------------------------------------------------------------------

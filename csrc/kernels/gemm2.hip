@@ -589,15 +589,6 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
 // * the DMA is inline asm (invisible to hipcc), so hipcc's wait for an epilogue LDS store cannot turn into a drain;
 // * after the epilogue, vmcnt<D0 + stores issued since> + barrier retires the next tile's K-tile 0 for every wave
 //   while the epilogue's stores are still in flight (they drain under the next tile's first K-tile).
-// Start stagger: every other CU of each XCD (workgroup bid -> XCD bid & 7, CU slot bid >> 3) idles `ticks` of the
-// 100 MHz real-time counter before its first tile, so half the chip's epilogues (store-bound when all 256 CUs run
-// them at once) fall under the other half's main loops. Read-only scalar timer + s_sleep: no memory traffic.
-__device__ __forceinline__ void stagger_start(int ticks) {
-  if (ticks <= 0 || !((blockIdx.x >> 3) & 1)) return;
-  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
-  while (__builtin_amdgcn_s_memrealtime() - t0 < (uint64_t)ticks) __builtin_amdgcn_s_sleep(4);
-}
-
 template <int EPI, int BN>
 __global__ __launch_bounds__(512, 1) void gemm2pk_kernel(G2Params p) {
   p.dp = resolve_seed(p.dp);
@@ -650,7 +641,6 @@ __global__ __launch_bounds__(512, 1) void gemm2pk_kernel(G2Params p) {
 
   const int arow = wm * 128, bcol = wn * WN;
   int L = blockIdx.x;
-  stagger_start(p.stagger);
   set_tile(L);
   prologue();
   vmcnt<0>();
@@ -851,7 +841,6 @@ __global__ __launch_bounds__(512, 1) void gemm8pk_kernel(G2Params p, const float
 
   const int arow = wm * 128, bcol = wn * WN;
   int L = blockIdx.x;
-  stagger_start(p.stagger);
   set_tile(L);
   prologue();
   vmcnt<0>();
@@ -1159,14 +1148,6 @@ static bool g2_persist(int tiles) {
   return tiles > (g2_num_cus() & ~7);
 }
 
-// start stagger of the persistent kernels (HSD_G2_STAGGER, 10 ns ticks; read per launch): only when every
-// workgroup walks at least 2 tiles, so the delayed half cannot lengthen a one-tile kernel
-static int g2_stagger(int ntiles, int grid) {
-  const char* e = getenv("HSD_G2_STAGGER");
-  const int t = e ? atoi(e) : 0;
-  return ntiles >= 2 * grid ? t : 0;
-}
-
 template <int EPI, int BN>
 static void g2pk_launch(const G2Params& p0, hipStream_t st) {
   G2Params p = p0;
@@ -1177,7 +1158,6 @@ static void g2pk_launch(const G2Params& p0, hipStream_t st) {
   if (p.K % g2::BK) abort();
   const char* gc = getenv("HSD_G2_GRID");  // diagnostic (tools/epi_probe2.py): cap the persistent grid (multiple of 8)
   const int grid = std::min(p.ntiles, gc ? atoi(gc) : g2_num_cus() & ~7);
-  p.stagger = g2_stagger(p.ntiles, grid);
   hipLaunchKernelGGL((g2::gemm2pk_kernel<EPI, BN>), dim3(grid), dim3(512), 0, st, p);
   HSD_CHECK_LAUNCH();
 }
@@ -1190,7 +1170,6 @@ static void g8pk_launch(const G2Params& p0, const float* sa, const float* sb, hi
   p.ntiles = tiles_m * p.tiles_n;
   p.kps = p.K;
   const int grid = p.ntiles > (g2_num_cus() & ~7) ? (g2_num_cus() & ~7) : p.ntiles;
-  p.stagger = g2_stagger(p.ntiles, grid);
   hipLaunchKernelGGL((g2::gemm8pk_kernel<EPI, BN, FA, 0>), dim3(grid), dim3(512), 0, st, p, sa, sb);
   HSD_CHECK_LAUNCH();
 }

@@ -36,7 +36,6 @@ struct G2Params {
   float* dbias;  // E2_DGELU: optional fp32 column sums of the output (the bias gradient), BN 256 only
   int nt_store;  // bf16 epilogues: non-temporal stores (default; HSD_G2_NT=0 turns them off)
   unsigned long long* diag;  // persistent NT kernel, diagnostic: per-workgroup seam timestamps (gemm2_set_diag)
-  int stagger;  // persistent kernels: start delay of every other CU of an XCD, s_memrealtime ticks (10 ns); 0 = none
 };
 
 // Buffer descriptor over `ptr` (wave-uniform: built from readfirstlane'd halves so hipcc keeps it in SGPRs).

@@ -20,6 +20,13 @@ namespace hsd {
 void launch_ln_fwd(const bf16_t* y, const bf16_t* res, const bf16_t* gamma, const bf16_t* beta, bf16_t* z,
                    bf16_t* out, float* mean, float* rstd, int rows, int H, float eps, double p, uint64_t seed,
                    hipStream_t st);
+void launch_ln_fwd_q8(const bf16_t* y, const bf16_t* gamma, const bf16_t* beta, bf16_t* out, float* mean, float* rstd,
+                      int rows, int H, float eps, uint8_t* q8, const float* amax_in, float* sinv, float* amax_track,
+                      hipStream_t st);
+void launch_ln_bwd_q8(const bf16_t* dout, const bf16_t* z, const float* mean, const float* rstd, const bf16_t* gamma,
+                      bf16_t* dz, bf16_t* dy, const bf16_t* dres_add, float* dgamma, float* dbeta, float* dbias,
+                      int rows, int H, double p, uint64_t seed, uint8_t* q8, const float* amax_in, float* sinv,
+                      float* amax_track, int qfmt, hipStream_t st);
 void launch_ln_bwd(const bf16_t* dout, const bf16_t* z, const float* mean, const float* rstd, const bf16_t* gamma,
                    bf16_t* dz, bf16_t* dy, const bf16_t* dres_add, float* dgamma, float* dbeta, float* dbias,
                    int rows, int H, double p, uint64_t seed, hipStream_t st);

@@ -12,6 +12,7 @@
 // partial sums for the weight/bias gradients accumulate in registers across the rows a block
 // walks, with no atomics until the block ends.
 #include "common.h"
+#include "fp8_common.h"
 #include <stdlib.h>
 #include <algorithm>
 
@@ -100,17 +101,23 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
 // epilogue, so no residual / dropout / z here): every wave walks `rpw` consecutive rows with the NEXT row's
 // 16-B loads in flight while the current row reduces. 5.1 TB/s at T = 131072, H = 768 against 3.6 TB/s for the
 // one-row-per-wave kernel above with its 8-B lanes (tools/bench_ln.py, profiles/bench_ln_r2.json). Needs
-// H % 8 == 0.
-template <int NC8>
+// H % 8 == 0. Q8: also the output's fp8 copy (launch_ln_fwd_q8).
+template <int NC8, bool Q8>
 __global__ __launch_bounds__(256) void ln_fwd_plain16_kernel(const bf16_t* __restrict__ y,
                                                              const bf16_t* __restrict__ gamma,
                                                              const bf16_t* __restrict__ beta, bf16_t* __restrict__ out,
                                                              float* __restrict__ mean_out, float* __restrict__ rstd_out,
-                                                             int rows, int H, int rpw, float eps) {
+                                                             int rows, int H, int rpw, float eps, Q8Out q8o) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int n8 = H >> 3;
   const int r0 = (blockIdx.x * kLnWaves + wave) * rpw;
   const int r1 = min(rows, r0 + rpw);
+  // fp8 copy of the output (Q8: e4m3, delayed scaling from q8o.amax_in; this pass's amax into q8o.amax_track)
+  float qs = 0.f, qm = 0.f;
+  if constexpr (Q8) {
+    qs = fmt_scale(0, *q8o.amax_in);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *q8o.sinv = 1.0f / qs;
+  }
   if (r0 >= r1) return;
   u32x4 gw[NC8], bw[NC8];
 #pragma unroll
@@ -160,6 +167,10 @@ __global__ __launch_bounds__(256) void ln_fwd_plain16_kernel(const bf16_t* __res
           o[k] = pack_bf2((lo_bf(yw[i][k]) - mean) * rstd * lo_bf(gw[i][k]) + lo_bf(bw[i][k]),
                           (hi_bf(yw[i][k]) - mean) * rstd * hi_bf(gw[i][k]) + hi_bf(bw[i][k]));
         *reinterpret_cast<u32x4*>(out + (size_t)row * H + 8 * c) = o;
+        if constexpr (Q8) {
+          qm = absmax8(o, qm);
+          *reinterpret_cast<u32x2*>(q8o.q + (size_t)row * H + 8 * c) = quant8<0>(o, qs);
+        }
       }
     }
     if (lane == 0) {
@@ -177,6 +188,7 @@ __global__ __launch_bounds__(256) void ln_fwd_plain16_kernel(const bf16_t* __res
     if (r + 2 < r1) load(r + 2, ya);
     process(r + 1, yb);
   }
+  if constexpr (Q8) wave_amax_track(qm, q8o.amax_track);
 }
 
 // Block = 4 waves; block walks `rows_per_block` rows (wave-strided, TWO rows in flight per wave so the
@@ -199,12 +211,14 @@ __device__ __forceinline__ void ln_bwd_load(const bf16_t* __restrict__ dout, con
   }
 }
 
-template <int NCH>
+// QF >= 0: also dy's fp8 copy (QF = format) into q8 with scale qs, max |dy| into qm
+template <int NCH, int QF = -1>
 __device__ __forceinline__ void ln_bwd_row(const u32x2 (&zw)[NCH], const u32x2 (&dw)[NCH], float mean, float rstd,
                                            const float (&gam)[NCH][4], int row, int H, int lane,
                                            bf16_t* __restrict__ dz_out, bf16_t* __restrict__ dy_out,
                                            const bf16_t* __restrict__ dres_add, const DropoutParams& dp,
-                                           float (&acc_g)[NCH][4], float (&acc_b)[NCH][4], float (&acc_db)[NCH][4]) {
+                                           float (&acc_g)[NCH][4], float (&acc_b)[NCH][4], float (&acc_db)[NCH][4],
+                                           uint8_t* __restrict__ q8 = nullptr, float qs = 0.f, float* qm = nullptr) {
   const int nq = H >> 2;
   float xh[NCH][4], g[NCH][4];
   float s1 = 0.f, s2 = 0.f;
@@ -259,6 +273,11 @@ __device__ __forceinline__ void ln_bwd_row(const u32x2 (&zw)[NCH], const u32x2 (
       // bias grad sums the bf16-rounded dy that the dgrad GEMM consumes
       acc_db[i][0] += lo_bf(yo.x); acc_db[i][1] += hi_bf(yo.x);
       acc_db[i][2] += lo_bf(yo.y); acc_db[i][3] += hi_bf(yo.y);
+      if constexpr (QF >= 0) {
+        const float a0 = lo_bf(yo.x), a1 = hi_bf(yo.x), a2 = lo_bf(yo.y), a3 = hi_bf(yo.y);
+        *qm = fmaxf(*qm, fmaxf(fmaxf(fabsf(a0), fabsf(a1)), fmaxf(fabsf(a2), fabsf(a3))));
+        *reinterpret_cast<uint32_t*>(q8 + off) = cvt4<QF>(a0 * qs, a1 * qs, a2 * qs, a3 * qs);
+      }
     }
   }
 }
@@ -366,7 +385,7 @@ __global__ __launch_bounds__(256) void ln_bwd_cols_kernel(const bf16_t* __restri
 // row reduces), keeps dgamma / dbeta / dbias column partials in registers, and the block reduces its 4
 // waves' partials through LDS into one fp32 atomic per column per block. Reads dout, z once; writes
 // dz, dy once (the split rows + cols passes read dout / z twice).
-template <int NCH>
+template <int NCH, int QF>
 __global__ __launch_bounds__(256) void ln_bwd_fused_kernel(const bf16_t* __restrict__ dout,
                                                            const bf16_t* __restrict__ z,
                                                            const float* __restrict__ mean_in,
@@ -376,8 +395,13 @@ __global__ __launch_bounds__(256) void ln_bwd_fused_kernel(const bf16_t* __restr
                                                            const bf16_t* __restrict__ dres_add,
                                                            float* __restrict__ dgamma, float* __restrict__ dbeta,
                                                            float* __restrict__ dbias, int rows, int H, int rpw,
-                                                           DropoutParams dp) {
+                                                           DropoutParams dp, Q8Out q8o) {
   dp = resolve_seed(dp);
+  float qs = 0.f, qm = 0.f;
+  if constexpr (QF >= 0) {
+    qs = fmt_scale(QF, *q8o.amax_in);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *q8o.sinv = 1.0f / qs;
+  }
   __shared__ float red[kLnWaves][3][NCH * 256];
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
   const int nq = H >> 2;
@@ -406,7 +430,7 @@ __global__ __launch_bounds__(256) void ln_bwd_fused_kernel(const bf16_t* __restr
         mu2 = mean_in[r + 1];
         rs2 = rstd_in[r + 1];
       }
-      ln_bwd_row<NCH>(za, da, mu, rs, gam, r, H, lane, dz_out, dy_out, dres_add, dp, ag, ab, ad);
+      ln_bwd_row<NCH, QF>(za, da, mu, rs, gam, r, H, lane, dz_out, dy_out, dres_add, dp, ag, ab, ad, q8o.q, qs, &qm);
       if (!more) break;
       const bool more2 = r + 2 < r1;
       if (more2) {
@@ -414,9 +438,11 @@ __global__ __launch_bounds__(256) void ln_bwd_fused_kernel(const bf16_t* __restr
         mu = mean_in[r + 2];
         rs = rstd_in[r + 2];
       }
-      ln_bwd_row<NCH>(zb, db, mu2, rs2, gam, r + 1, H, lane, dz_out, dy_out, dres_add, dp, ag, ab, ad);
+      ln_bwd_row<NCH, QF>(zb, db, mu2, rs2, gam, r + 1, H, lane, dz_out, dy_out, dres_add, dp, ag, ab, ad, q8o.q, qs,
+                          &qm);
     }
   }
+  if constexpr (QF >= 0) wave_amax_track(qm, q8o.amax_track);
 #pragma unroll
   for (int i = 0; i < NCH; ++i)
 #pragma unroll
@@ -448,11 +474,11 @@ static void ln_fwd_t(const bf16_t* y, const bf16_t* res, const bf16_t* gamma, co
     const int waves = (rows + rpw - 1) / rpw;
     const int blocks = (waves + kLnWaves - 1) / kLnWaves;
     if (H <= 512)
-      hipLaunchKernelGGL((ln_fwd_plain16_kernel<1>), dim3(blocks), dim3(256), 0, st, y, gamma, beta, out, mean, rstd,
-                         rows, H, rpw, eps);
+      hipLaunchKernelGGL((ln_fwd_plain16_kernel<1, false>), dim3(blocks), dim3(256), 0, st, y, gamma, beta, out, mean,
+                         rstd, rows, H, rpw, eps, Q8Out{});
     else
-      hipLaunchKernelGGL((ln_fwd_plain16_kernel<2>), dim3(blocks), dim3(256), 0, st, y, gamma, beta, out, mean, rstd,
-                         rows, H, rpw, eps);
+      hipLaunchKernelGGL((ln_fwd_plain16_kernel<2, false>), dim3(blocks), dim3(256), 0, st, y, gamma, beta, out, mean,
+                         rstd, rows, H, rpw, eps, Q8Out{});
     return;
   }
   dim3 grid((rows + kLnWaves - 1) / kLnWaves);
@@ -477,8 +503,9 @@ void launch_ln_fwd(const bf16_t* y, const bf16_t* res, const bf16_t* gamma, cons
 template <int NCH>
 static void ln_bwd_t(const bf16_t* dout, const bf16_t* z, const float* mean, const float* rstd, const bf16_t* gamma,
                      bf16_t* dz, bf16_t* dy, const bf16_t* dres_add, float* dgamma, float* dbeta, float* dbias,
-                     int rows, int H, const DropoutParams& dp, hipStream_t st) {
-  if (!getenv("HSD_LN_SPLIT")) {
+                     int rows, int H, const DropoutParams& dp, hipStream_t st, const Q8Out& q8o = Q8Out{},
+                     int qfmt = -1) {
+  if (qfmt >= 0 || !getenv("HSD_LN_SPLIT")) {
     // ~16 rows per wave at the headline's 131072 rows: 2048 waves = 8 per CU, a few thousand column atomics per
     // block; at least 4 rows per wave (a floor of 2 for small row counts, twice the waves and the column atomics,
     // measured 1-2 % slower end to end at bert-large B = 8 and bert-base B = 32: profiles/small_tiles_r2.log;
@@ -492,8 +519,15 @@ static void ln_bwd_t(const bf16_t* dout, const bf16_t* z, const float* mean, con
     const int blocks = (waves + kLnWaves - 1) / kLnWaves;
     // dbias sums the gradient that enters the GEMM: dy (or dz, which equals dy when there is no dropout)
     bf16_t* ysink = dy ? dy : nullptr;
-    hipLaunchKernelGGL((ln_bwd_fused_kernel<NCH>), dim3(blocks), dim3(256), 0, st, dout, z, mean, rstd, gamma, dz,
-                       ysink, dres_add, dgamma, dbeta, dbias, rows, H, rpw, dp);
+    if (qfmt == 0)
+      hipLaunchKernelGGL((ln_bwd_fused_kernel<NCH, 0>), dim3(blocks), dim3(256), 0, st, dout, z, mean, rstd, gamma, dz,
+                         ysink, dres_add, dgamma, dbeta, dbias, rows, H, rpw, dp, q8o);
+    else if (qfmt == 1)
+      hipLaunchKernelGGL((ln_bwd_fused_kernel<NCH, 1>), dim3(blocks), dim3(256), 0, st, dout, z, mean, rstd, gamma, dz,
+                         ysink, dres_add, dgamma, dbeta, dbias, rows, H, rpw, dp, q8o);
+    else
+      hipLaunchKernelGGL((ln_bwd_fused_kernel<NCH, -1>), dim3(blocks), dim3(256), 0, st, dout, z, mean, rstd, gamma, dz,
+                         ysink, dres_add, dgamma, dbeta, dbias, rows, H, rpw, dp, q8o);
     return;
   }
   hipLaunchKernelGGL((ln_bwd_rows_kernel<NCH>), dim3((rows + kLnWaves - 1) / kLnWaves), dim3(256), 0, st, dout, z,
@@ -507,6 +541,41 @@ static void ln_bwd_t(const bf16_t* dout, const bf16_t* z, const float* mean, con
   const bf16_t* ysrc = dy ? dy : dz;
   hipLaunchKernelGGL(ln_bwd_cols_kernel, dim3(gx, gy), dim3(256), 0, st, dout, z, mean, rstd, ysrc, dgamma, dbeta,
                      ysrc ? dbias : nullptr, rows, H, rpb);
+}
+
+// LayerNorm forward (no residual / dropout) that also writes the output's fp8 e4m3 copy for the next fp8 GEMM
+// (ops/hip.py: the LN at the end of a block quantises for the next block's first GEMM), H % 8 == 0, H <= 1024.
+void launch_ln_fwd_q8(const bf16_t* y, const bf16_t* gamma, const bf16_t* beta, bf16_t* out, float* mean, float* rstd,
+                      int rows, int H, float eps, uint8_t* q8, const float* amax_in, float* sinv, float* amax_track,
+                      hipStream_t st) {
+  const int rpw = 2;
+  const int waves = (rows + rpw - 1) / rpw;
+  const int blocks = (waves + kLnWaves - 1) / kLnWaves;
+  const Q8Out q{q8, amax_in, sinv, amax_track};
+  if (H <= 512)
+    hipLaunchKernelGGL((ln_fwd_plain16_kernel<1, true>), dim3(blocks), dim3(256), 0, st, y, gamma, beta, out, mean,
+                       rstd, rows, H, rpw, eps, q);
+  else
+    hipLaunchKernelGGL((ln_fwd_plain16_kernel<2, true>), dim3(blocks), dim3(256), 0, st, y, gamma, beta, out, mean,
+                       rstd, rows, H, rpw, eps, q);
+  HSD_CHECK_LAUNCH();
+}
+
+// LN backward (fused single-pass kernel) that also writes dy's fp8 copy (qfmt 0 = e4m3, 1 = e5m2) for the fp8
+// dgrad GEMM that consumes dy; dy must be materialised (dy != nullptr)
+void launch_ln_bwd_q8(const bf16_t* dout, const bf16_t* z, const float* mean, const float* rstd, const bf16_t* gamma,
+                      bf16_t* dz, bf16_t* dy, const bf16_t* dres_add, float* dgamma, float* dbeta, float* dbias,
+                      int rows, int H, double p, uint64_t seed, uint8_t* q8, const float* amax_in, float* sinv,
+                      float* amax_track, int qfmt, hipStream_t st) {
+  DropoutParams dp = make_dropout(p, seed);
+  const Q8Out q{q8, amax_in, sinv, amax_track};
+  int nch = (H / 4 + 63) / 64;
+  if (nch <= 1) ln_bwd_t<1>(dout, z, mean, rstd, gamma, dz, dy, dres_add, dgamma, dbeta, dbias, rows, H, dp, st, q, qfmt);
+  else if (nch <= 2) ln_bwd_t<2>(dout, z, mean, rstd, gamma, dz, dy, dres_add, dgamma, dbeta, dbias, rows, H, dp, st, q, qfmt);
+  else if (nch <= 3) ln_bwd_t<3>(dout, z, mean, rstd, gamma, dz, dy, dres_add, dgamma, dbeta, dbias, rows, H, dp, st, q, qfmt);
+  else if (nch <= 4) ln_bwd_t<4>(dout, z, mean, rstd, gamma, dz, dy, dres_add, dgamma, dbeta, dbias, rows, H, dp, st, q, qfmt);
+  else abort();
+  HSD_CHECK_LAUNCH();
 }
 
 void launch_ln_bwd(const bf16_t* dout, const bf16_t* z, const float* mean, const float* rstd, const bf16_t* gamma,

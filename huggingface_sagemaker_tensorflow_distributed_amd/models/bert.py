@@ -75,8 +75,9 @@ class Encoder(nn.Module):
         B, S = input_ids.shape
         h = self.embeddings(input_ids, token_type_ids, rng, training).view(B * S, -1)
         mask_bias = ops.key_mask_bias(attention_mask) if attention_mask is not None else None
-        for layer in self.layers:
-            h = layer(h, mask_bias, B, S, rng, training)
+        n = len(self.layers)
+        for i, layer in enumerate(self.layers):
+            h = layer(h, mask_bias, B, S, rng, training, self.layers[i + 1].qkv_weight if i + 1 < n else None)
         return h.view(B, S, -1)
 
 

@@ -47,7 +47,8 @@ class EncoderLayer(nn.Module):
         self.ln2_bias = _param(H)
 
     def forward(self, h: torch.Tensor, mask_bias: Optional[torch.Tensor], batch: int, seq: int,
-                rng: DropoutSeeds, training: bool) -> torch.Tensor:
+                rng: DropoutSeeds, training: bool, next_qkv: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """``next_qkv``: the next layer's QKV weight (fp8 path: this layer's last LayerNorm quantises for it)."""
         c = self.cfg
         p_h = c.hidden_dropout_prob if training else 0.0
         p_a = c.attention_probs_dropout_prob if training else 0.0
@@ -55,10 +56,10 @@ class EncoderLayer(nn.Module):
         seed_h1 = rng.next() if p_h else 0
         h1 = ops.attn_block(h, self.qkv_weight, self.qkv_bias, self.attn_out_weight, self.attn_out_bias,
                             self.ln1_weight, self.ln1_bias, c.layer_norm_eps, mask_bias, batch, seq,
-                            c.num_attention_heads, p_a, seed_a, p_h, seed_h1)
+                            c.num_attention_heads, p_a, seed_a, p_h, seed_h1, q8_next=self.ffn1_weight)
         seed_h2 = rng.next() if p_h else 0
         return ops.ffn_block(h1, self.ffn1_weight, self.ffn1_bias, self.ffn2_weight, self.ffn2_bias,
-                             self.ln2_weight, self.ln2_bias, c.layer_norm_eps, p_h, seed_h2)
+                             self.ln2_weight, self.ln2_bias, c.layer_norm_eps, p_h, seed_h2, q8_next=next_qkv)
 
 
 # name tables: internal name -> list of (hf suffix, row-slice or None)

@@ -82,20 +82,21 @@ def dense_residual_ln(x, w, b, residual, ln_w, ln_b, eps, p, seed):
 
 
 def attn_block(h, qkv_w, qkv_b, out_w, out_b, ln_w, ln_b, eps, mask_bias, batch, seq, heads, p_attn, seed_attn,
-               p_hidden, seed_hidden):
-    """Self-attention sub-block: ``LN(dropout(attn(h Wqkvᵀ + b) Woᵀ + bo) + h)``."""
+               p_hidden, seed_hidden, q8_next=None):
+    """Self-attention sub-block: ``LN(dropout(attn(h Wqkvᵀ + b) Woᵀ + bo) + h)``. ``q8_next``: the weight of the
+    GEMM that consumes the output (HIP fp8 path: the LayerNorm writes its fp8 input copy)."""
     if _hip(h) and h.dtype == torch.bfloat16 and qkv_w.shape[0] == 3 * heads * 64:
         return _hipmod().attn_block(h, qkv_w, qkv_b, out_w, out_b, ln_w, ln_b, eps, mask_bias, batch, seq, heads,
-                                    p_attn, seed_attn, p_hidden, seed_hidden)
+                                    p_attn, seed_attn, p_hidden, seed_hidden, q8_next)
     qkv = linear(h, qkv_w, qkv_b)
     ctx = attention(qkv, mask_bias, batch, seq, heads, p_attn, seed_attn)
     return dense_residual_ln(ctx, out_w, out_b, h, ln_w, ln_b, eps, p_hidden, seed_hidden)
 
 
-def ffn_block(h, w1, b1, w2, b2, ln_w, ln_b, eps, p, seed):
+def ffn_block(h, w1, b1, w2, b2, ln_w, ln_b, eps, p, seed, q8_next=None):
     """Feed-forward sub-block: ``LN(dropout(gelu(h W1ᵀ + b1) W2ᵀ + b2) + h)``."""
     if _hip(h) and h.dtype == torch.bfloat16:
-        return _hipmod().ffn_block(h, w1, b1, w2, b2, ln_w, ln_b, eps, p, seed)
+        return _hipmod().ffn_block(h, w1, b1, w2, b2, ln_w, ln_b, eps, p, seed, q8_next)
     a = linear_gelu(h, w1, b1)
     return dense_residual_ln(a, w2, b2, h, ln_w, ln_b, eps, p, seed)
 

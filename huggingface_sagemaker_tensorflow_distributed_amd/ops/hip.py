@@ -516,13 +516,38 @@ def _fp8_w(w, attr):
     return getattr(w, attr, None)
 
 
-def gemm_fwd(x, w, epi, bias=None, aux=None, out2=None, p=0.0, seed=0):
+# fp8 copies written by the producing LayerNorm (fused quantisation, no standalone quant pass): the LN at the end of
+# a block quantises its output for the NEXT block's first GEMM with that GEMM's delayed-scaling site, and the LN
+# backward quantises dy for the block's own fp8 dgrad. A site is fused only once it is calibrated (its first use
+# runs the standalone amax + quant passes), so fused and standalone paths give the same bytes.
+_Q8_PENDING = {}
+
+
+def _site_ready(w, state_attr: str, wattr: str):
+    """The calibrated delayed-scaling state of ``w``'s fp8 site, or None (fp8 off / no fp8 copy / first use)."""
+    if w is None or not _FP8["on"] or getattr(w, wattr, None) is None:
+        return None
+    st = getattr(w, state_attr, None)
+    return st if st is not None and getattr(st, "_hsd_cal", False) else None
+
+
+def _take_q8(x):
+    """The fp8 copy a LayerNorm wrote for activation ``x`` (popped), or None."""
+    if not _Q8_PENDING:
+        return None
+    e = _Q8_PENDING.pop((x.data_ptr(), x.numel()), None)
+    _Q8_PENDING.clear()  # only the immediately-following GEMM may use a pending copy
+    return e
+
+
+def gemm_fwd(x, w, epi, bias=None, aux=None, out2=None, p=0.0, seed=0, xq=None):
     """y[T, N] = x[T, K] · w[N, K]ᵀ with epilogue (gemm2 8-phase kernel; 128-tile kernel for odd shapes;
-    gemm8 fp8 kernel when fp8 is on and the weight has an fp8 copy)."""
+    gemm8 fp8 kernel when fp8 is on and the weight has an fp8 copy). ``xq``: x's fp8 copy (q, sinv) already
+    written by its producer."""
     y = torch.empty((x.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)
     wq = _fp8_w(w, "_hsd_q")
     if wq is not None and _C.gemm8_supported(epi, x.shape[0], w.shape[0], x.shape[1]):
-        qx, sx = quant_fp8(x, FP8_E4M3, getattr(w, "_hsd_fp8_x", None))
+        qx, sx = xq if xq is not None else quant_fp8(x, FP8_E4M3, getattr(w, "_hsd_fp8_x", None))
         _C.gemm8(qx, FP8_E4M3, sx, wq, FP8_E4M3, w._hsd_qs, y, epi, bias, aux, out2, float(p), _s64(seed), None)
         return y
     if _nt_ok(x.shape[0], w.shape[0], x.shape[1], epi):
@@ -532,7 +557,7 @@ def gemm_fwd(x, w, epi, bias=None, aux=None, out2=None, p=0.0, seed=0):
     return y
 
 
-def gemm_dgrad(dy, w, epi=EPI_STORE, aux=None, dbias=None):
+def gemm_dgrad(dy, w, epi=EPI_STORE, aux=None, dbias=None, dyq=None):
     """dx[T, K] = dy[T, N] · w[N, K]  (NT kernel on the transposed weight wᵀ [K, N]).
 
     ``dbias`` (DGELU only): fp32 [K] buffer that receives the column sums of dx (the bias gradient of
@@ -542,7 +567,7 @@ def gemm_dgrad(dy, w, epi=EPI_STORE, aux=None, dbias=None):
     if wqt is not None and _C.gemm8_supported(epi, dy.shape[0], w.shape[1], dy.shape[1]):
         fuse = dbias is not None and epi in (EPI_DGELU, EPI_MUL) and w.shape[1] % 256 == 0
         fmt = _FP8["grad_fmt"]
-        qdy, sdy = quant_fp8(dy, fmt, getattr(w, "_hsd_fp8_g", None))
+        qdy, sdy = dyq if dyq is not None else quant_fp8(dy, fmt, getattr(w, "_hsd_fp8_g", None))
         _C.gemm8(qdy, fmt, sdy, wqt, FP8_E4M3, w._hsd_qs, dx, epi, None, aux, None, 0.0, 0, dbias if fuse else None)
         if dbias is not None and not fuse:
             _C.colsum(dx, dbias)
@@ -581,13 +606,37 @@ def gemm_wgrad_(g: "_Grad", dy, x):
         _C.gemm(dy, x, g.buf, 1, 1, EPI_F32_ATOMIC, None, None, None, 0.0, 0, splits)
 
 
-def _ln_fwd(z, w, b, eps):
+def _ln_fwd(z, w, b, eps, q8_for=None):
+    """LayerNorm forward; with ``q8_for`` (the next GEMM's weight) on a calibrated fp8 site, the kernel also writes
+    the output's fp8 copy, which the next block's first GEMM picks up (:func:`_take_q8`)."""
     rows, H = z.shape
     out = torch.empty_like(z)
     mean = torch.empty(rows, dtype=torch.float32, device=z.device)
     rstd = torch.empty_like(mean)
-    _C.ln_fwd(z, None, w, b, None, out, mean, rstd, float(eps), 0.0, 0)
+    st = _site_ready(q8_for, "_hsd_fp8_x", "_hsd_q")
+    if st is not None and H % 8 == 0 and H <= 1024 and _C.gemm8_supported(EPI_BIAS, rows, q8_for.shape[0], H):
+        q = torch.empty((rows, H), dtype=torch.uint8, device=z.device)
+        sinv = torch.empty(1, dtype=torch.float32, device=z.device)
+        _C.ln_fwd_q8(z, w, b, out, mean, rstd, float(eps), q, st[0:1], sinv, st[1:2])
+        _Q8_PENDING[(out.data_ptr(), out.numel())] = (q, sinv)
+    else:
+        _C.ln_fwd(z, None, w, b, None, out, mean, rstd, float(eps), 0.0, 0)
     return out, mean, rstd
+
+
+def _ln_bwd(dout2, z, mean, rstd, ln_w, dz, dy, g_lnw, g_lnb, g_b, p, seed, consumer_w):
+    """LN backward into dy (and dz with dropout); returns dy's fp8 copy (q, sinv) when ``consumer_w``'s dgrad runs
+    fp8 on a calibrated site (quantised in the same pass), else None."""
+    st = _site_ready(consumer_w, "_hsd_fp8_g", "_hsd_qt")
+    rows, H = z.shape
+    if st is not None and H <= 1024 and _C.gemm8_supported(EPI_STORE, rows, consumer_w.shape[1], H):
+        q = torch.empty((rows, H), dtype=torch.uint8, device=z.device)
+        sinv = torch.empty(1, dtype=torch.float32, device=z.device)
+        _C.ln_bwd_q8(dout2, z, mean, rstd, ln_w, dz, dy, g_lnw.buf, g_lnb.buf, g_b.buf, p, _s64(seed) if p > 0 else 0,
+                     q, st[0:1], sinv, st[1:2], _FP8["grad_fmt"])
+        return q, sinv
+    _C.ln_bwd(dout2, z, mean, rstd, ln_w, dz, dy, None, g_lnw.buf, g_lnb.buf, g_b.buf, p, _s64(seed) if p > 0 else 0)
+    return None
 
 
 # ------------------------------------------------------------------------------------------ fused blocks
@@ -598,16 +647,16 @@ class _AttnBlock(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, h, qkv_w, qkv_b, out_w, out_b, ln_w, ln_b, eps, mask_bias, B, S, heads, p_a, seed_a, p_h,
-                seed_h):
+                seed_h, q8_next=None):
         h2d = h.reshape(-1, h.shape[-1])
-        qkv = gemm_fwd(h2d, qkv_w, EPI_BIAS, bias=qkv_b)
+        qkv = gemm_fwd(h2d, qkv_w, EPI_BIAS, bias=qkv_b, xq=_take_q8(h2d))
         H = out_w.shape[0]
         actx = torch.empty((h2d.shape[0], H), dtype=h.dtype, device=h.device)
         lse = torch.empty(B * heads * S, dtype=torch.float32, device=h.device)
         mb = mask_bias.contiguous().float() if mask_bias is not None else None
         _C.attn_fwd(qkv, mb, actx, lse, B, S, heads, float(p_a), _s64(seed_a))
         z = gemm_fwd(actx, out_w, EPI_BIAS_DROP_RES, bias=out_b, aux=h2d, p=p_h, seed=seed_h)
-        out, mean, rstd = _ln_fwd(z, ln_w, ln_b, eps)
+        out, mean, rstd = _ln_fwd(z, ln_w, ln_b, eps, q8_for=q8_next)
         ctx.save_for_backward(h2d, qkv_w, qkv_b, out_w, out_b, ln_w, ln_b, qkv, actx, lse, z, mean, rstd,
                               mb if mb is not None else lse)
         ctx.cfg = (B, S, heads, float(p_a), seed_a, float(p_h), seed_h, mb is not None)
@@ -620,15 +669,13 @@ class _AttnBlock(torch.autograd.Function):
         dout2 = dout.reshape(z.shape).contiguous()
         g_lnw, g_lnb, g_ow, g_ob = _Grad(ln_w), _Grad(ln_b), _Grad(out_w), _Grad(out_b)
         dy = torch.empty_like(z)
-        if p_h > 0:
-            dz = torch.empty_like(z)
-            _C.ln_bwd(dout2, z, mean, rstd, ln_w, dz, dy, None, g_lnw.buf, g_lnb.buf, g_ob.buf, p_h, _s64(seed_h))
-        else:
-            _C.ln_bwd(dout2, z, mean, rstd, ln_w, None, dy, None, g_lnw.buf, g_lnb.buf, g_ob.buf, 0.0, 0)
+        dz = torch.empty_like(z) if p_h > 0 else None
+        dyq = _ln_bwd(dout2, z, mean, rstd, ln_w, dz, dy, g_lnw, g_lnb, g_ob, p_h, seed_h, out_w)
+        if dz is None:
             dz = dy
         r_lnw, r_lnb, r_ob = g_lnw.done(), g_lnb.done(), g_ob.done()
         r_ow = wgrad_done(g_ow, dy, actx)
-        dctx = gemm_dgrad(dy, out_w)
+        dctx = gemm_dgrad(dy, out_w, dyq=dyq)
         dqkv = torch.empty_like(qkv)
         dq_acc = _attn_ws(B, S, heads, actx.device)
         g_qw, g_qb = _Grad(qkv_w), _Grad(qkv_b)
@@ -639,12 +686,15 @@ class _AttnBlock(torch.autograd.Function):
         r_qw = wgrad_done(g_qw, dqkv, h2d)
         dh = gemm_dgrad(dqkv, qkv_w, EPI_RES, aux=dz) if ctx.needs_input_grad[0] else None
         return (dh.view(dout.shape) if dh is not None else None, r_qw, r_qb, r_ow, r_ob, r_lnw, r_lnb,
-                None, None, None, None, None, None, None, None, None)
+                None, None, None, None, None, None, None, None, None, None)
 
 
-def attn_block(h, qkv_w, qkv_b, out_w, out_b, ln_w, ln_b, eps, mask_bias, B, S, heads, p_a, seed_a, p_h, seed_h):
+def attn_block(h, qkv_w, qkv_b, out_w, out_b, ln_w, ln_b, eps, mask_bias, B, S, heads, p_a, seed_a, p_h, seed_h,
+               q8_next=None):
+    """``q8_next``: the weight of the GEMM that consumes this block's output (the FFN's W1): its fp8 input copy is
+    written by this block's LayerNorm."""
     return _AttnBlock.apply(h, qkv_w, qkv_b, out_w, out_b, ln_w, ln_b, eps, mask_bias, B, S, heads, p_a, seed_a,
-                            p_h, seed_h)
+                            p_h, seed_h, q8_next)
 
 
 class _FFNBlock(torch.autograd.Function):
@@ -653,16 +703,17 @@ class _FFNBlock(torch.autograd.Function):
     + b2 grad) -> W2 wgrad -> dgrad with gelu' epilogue -> b1 colsum -> W1 wgrad -> dgrad + residual."""
 
     @staticmethod
-    def forward(ctx, h, w1, b1, w2, b2, ln_w, ln_b, eps, p, seed):
+    def forward(ctx, h, w1, b1, w2, b2, ln_w, ln_b, eps, p, seed, q8_next=None):
         h2d = h.reshape(-1, h.shape[-1])
+        xq = _take_q8(h2d)
         act = torch.empty((h2d.shape[0], w1.shape[0]), dtype=h.dtype, device=h.device)
         # keep gelu'(pre) instead of pre when the gemm2 path handles both FFN GEMMs: the FFN2 dgrad
         # epilogue is then a product (no erf/exp per element in backward)
         keep_grad = _nt_ok(h2d.shape[0], w1.shape[0], h2d.shape[1], EPI_BIAS_GELU_D) and \
             _nt_ok(h2d.shape[0], w1.shape[0], w2.shape[0], EPI_MUL)
-        pre = gemm_fwd(h2d, w1, EPI_BIAS_GELU_D if keep_grad else EPI_BIAS_GELU, bias=b1, out2=act)
+        pre = gemm_fwd(h2d, w1, EPI_BIAS_GELU_D if keep_grad else EPI_BIAS_GELU, bias=b1, out2=act, xq=xq)
         z = gemm_fwd(act, w2, EPI_BIAS_DROP_RES, bias=b2, aux=h2d, p=p, seed=seed)
-        out, mean, rstd = _ln_fwd(z, ln_w, ln_b, eps)
+        out, mean, rstd = _ln_fwd(z, ln_w, ln_b, eps, q8_for=q8_next)
         ctx.save_for_backward(h2d, w1, b1, w2, b2, ln_w, ln_b, pre, act, z, mean, rstd)
         ctx.cfg = (float(p), seed, keep_grad)
         return out.view(h.shape)
@@ -674,25 +725,24 @@ class _FFNBlock(torch.autograd.Function):
         dout2 = dout.reshape(z.shape).contiguous()
         g_lnw, g_lnb, g_w2, g_b2 = _Grad(ln_w), _Grad(ln_b), _Grad(w2), _Grad(b2)
         dy = torch.empty_like(z)
-        if p > 0:
-            dz = torch.empty_like(z)
-            _C.ln_bwd(dout2, z, mean, rstd, ln_w, dz, dy, None, g_lnw.buf, g_lnb.buf, g_b2.buf, p, _s64(seed))
-        else:
-            _C.ln_bwd(dout2, z, mean, rstd, ln_w, None, dy, None, g_lnw.buf, g_lnb.buf, g_b2.buf, 0.0, 0)
+        dz = torch.empty_like(z) if p > 0 else None
+        dyq = _ln_bwd(dout2, z, mean, rstd, ln_w, dz, dy, g_lnw, g_lnb, g_b2, p, seed, w2)
+        if dz is None:
             dz = dy
         r_lnw, r_lnb, r_b2 = g_lnw.done(), g_lnb.done(), g_b2.done()
         r_w2 = wgrad_done(g_w2, dy, act)
         g_w1, g_b1 = _Grad(w1), _Grad(b1)
-        da = gemm_dgrad(dy, w2, EPI_MUL if keep_grad else EPI_DGELU, aux=pre, dbias=g_b1.buf)
+        da = gemm_dgrad(dy, w2, EPI_MUL if keep_grad else EPI_DGELU, aux=pre, dbias=g_b1.buf, dyq=dyq)
         r_b1 = g_b1.done()
         r_w1 = wgrad_done(g_w1, da, h2d)
         dh = gemm_dgrad(da, w1, EPI_RES, aux=dz) if ctx.needs_input_grad[0] else None
         return (dh.view(dout.shape) if dh is not None else None, r_w1, r_b1, r_w2, r_b2, r_lnw, r_lnb,
-                None, None, None)
+                None, None, None, None)
 
 
-def ffn_block(h, w1, b1, w2, b2, ln_w, ln_b, eps, p, seed):
-    return _FFNBlock.apply(h, w1, b1, w2, b2, ln_w, ln_b, eps, p, seed)
+def ffn_block(h, w1, b1, w2, b2, ln_w, ln_b, eps, p, seed, q8_next=None):
+    """``q8_next``: the next layer's QKV weight (its fp8 input copy is written by this block's LayerNorm)."""
+    return _FFNBlock.apply(h, w1, b1, w2, b2, ln_w, ln_b, eps, p, seed, q8_next)
 
 
 # ------------------------------------------------------------------------------------------ attention mask

@@ -222,6 +222,11 @@ class LocalOverlap:
         self.opt = opt
         self.stream = torch.cuda.Stream(device=store.device)
         self.sync = True
+        # the stream the backward kernels are queued on, when it is not the hook thread's current stream: a HIP
+        # graph capture (the capture stream; train/graph.py). Post-accumulate hooks of gradients the HIP backward
+        # writes into main_grad itself run on autograd's thread with no producer stream (its current stream is the
+        # device default), so a slice's fork must name the stream the gradients were really queued on.
+        self.parent: Optional[torch.cuda.Stream] = None
         opt.enable_overlap(self.ranges, on_ready=self.mark_ready)
 
     def begin(self) -> None:
@@ -236,10 +241,10 @@ class LocalOverlap:
         if self.pending[b] == 0:
             from ..ops import hip
 
-            cur = torch.cuda.current_stream(self.stream.device)
+            cur = self.parent if self.parent is not None else torch.cuda.current_stream(self.stream.device)
             self.stream.wait_stream(cur)
             side = hip.side_stream(self.stream.device)
-            if side is not None and not torch.cuda.is_current_stream_capturing():  # (no wgrad stream in a capture)
+            if side is not None and self.parent is None:  # (a capture runs no wgrad side stream)
                 self.stream.wait_stream(side)
             with torch.cuda.stream(self.stream):
                 self.opt.step_range(b)

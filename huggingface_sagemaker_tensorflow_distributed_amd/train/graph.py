@@ -139,17 +139,22 @@ class CapturedTrainStep:
         gscale = 1.0 / trainer.world
         self.graph = torch.cuda.CUDAGraph()
         step0 = opt.step_count
-        with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
-            store.zero_grad()
-            model.rng.new_step(0)
+        try:
+            with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
+                store.zero_grad()
+                model.rng.new_step(0)
+                if ov is not None:
+                    ov.parent = torch.cuda.current_stream(trainer.device)  # the capture stream
+                    opt.begin_step(grad_scale=gscale)
+                    ov.begin()
+                self.loss, self.logits = trainer._forward_loss(self.static)
+                self.loss.backward()
+                if ov is not None:
+                    ov.join()
+                opt.step(grad_scale=gscale)
+        finally:
             if ov is not None:
-                opt.begin_step(grad_scale=gscale)
-                ov.begin()
-            self.loss, self.logits = trainer._forward_loss(self.static)
-            self.loss.backward()
-            if ov is not None:
-                ov.join()
-            opt.step(grad_scale=gscale)
+                ov.parent = None
         opt.step_count = step0  # begin_step / step advanced it once during capture; each replay advances it
         torch.cuda.synchronize(trainer.device)
         self.gscale = gscale

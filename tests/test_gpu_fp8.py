@@ -190,3 +190,121 @@ def test_gemm8_persistent_matches_legacy(gpu, monkeypatch, M, N, K, epi, fa):
         assert torch.equal(a2, b2)
     if ad is not None:
         torch.testing.assert_close(bd, ad, rtol=1e-4, atol=1e-4 * float(ad.abs().max()) + 1e-6)
+
+
+@pytest.mark.parametrize("rows,H", [(4096, 768), (1000, 1024), (333, 512)])
+def test_ln_fwd_q8_equals_ln_then_quant(gpu, rows, H):
+    """LN forward writing the output's fp8 copy (delayed-scaling site) == LN, then the standalone quantiser with the
+    same site: identical bf16 output, fp8 bytes, sinv and tracked amax."""
+    hip = _hip()
+    C = hip._C
+    torch.manual_seed(3)
+    z = (torch.randn(rows, H, device=gpu) * 2 + 0.3).bfloat16()
+    w = (1 + 0.1 * torch.randn(H, device=gpu)).bfloat16()
+    b = (0.1 * torch.randn(H, device=gpu)).bfloat16()
+    out_ref, mean_ref, rstd_ref = (torch.empty_like(z), torch.empty(rows, device=gpu), torch.empty(rows, device=gpu))
+    C.ln_fwd(z, None, w, b, None, out_ref, mean_ref, rstd_ref, 1e-12, 0.0, 0)
+    st_ref = torch.tensor([3.0, 0.0], device=gpu)
+    st_ref._hsd_cal = True
+    q_ref, s_ref = hip.quant_fp8(out_ref, 0, st_ref)
+    st = torch.tensor([3.0, 0.0], device=gpu)
+    out, mean, rstd = torch.empty_like(z), torch.empty(rows, device=gpu), torch.empty(rows, device=gpu)
+    q = torch.empty(rows, H, dtype=torch.uint8, device=gpu)
+    sinv = torch.empty(1, device=gpu)
+    C.ln_fwd_q8(z, w, b, out, mean, rstd, 1e-12, q, st[0:1], sinv, st[1:2])
+    torch.cuda.synchronize()
+    assert torch.equal(out, out_ref) and torch.equal(mean, mean_ref) and torch.equal(rstd, rstd_ref)
+    assert torch.equal(q, q_ref)
+    assert torch.equal(sinv, s_ref) and torch.equal(st, st_ref)
+
+
+@pytest.mark.parametrize("rows,H,p,fmt", [(4096, 768, 0.1, 0), (1000, 1024, 0.0, 1), (2048, 1024, 0.1, 1)])
+def test_ln_bwd_q8_equals_ln_bwd_then_quant(gpu, rows, H, p, fmt):
+    """LN backward writing dy's fp8 copy == LN backward, then the standalone quantiser: identical dz / dy / dgamma /
+    dbeta / dbias inputs to the GEMMs, fp8 bytes, sinv and tracked amax."""
+    hip = _hip()
+    C = hip._C
+    torch.manual_seed(4)
+    z = torch.randn(rows, H, device=gpu).bfloat16()
+    dout = torch.randn(rows, H, device=gpu).bfloat16()
+    w = (1 + 0.1 * torch.randn(H, device=gpu)).bfloat16()
+    mean = z.float().mean(1)
+    rstd = torch.rsqrt(z.float().var(1, unbiased=False) + 1e-12)
+    res = {}
+    for fused in (False, True):
+        dz = torch.empty_like(z) if p > 0 else None
+        dy = torch.empty_like(z)
+        dg, db, dbias = (torch.zeros(H, device=gpu) for _ in range(3))
+        st = torch.tensor([5.0, 0.0], device=gpu)
+        if fused:
+            q = torch.empty(rows, H, dtype=torch.uint8, device=gpu)
+            sinv = torch.empty(1, device=gpu)
+            C.ln_bwd_q8(dout, z, mean, rstd, w, dz, dy, dg, db, dbias, p, 11, q, st[0:1], sinv, st[1:2], fmt)
+        else:
+            C.ln_bwd(dout, z, mean, rstd, w, dz, dy, None, dg, db, dbias, p, 11)
+            st._hsd_cal = True
+            q, sinv = hip.quant_fp8(dy, fmt, st)
+        torch.cuda.synchronize()
+        res[fused] = (dz, dy, dg, db, dbias, q, sinv, st)
+    a, b = res[False], res[True]
+    for i, (x, y) in enumerate(zip(a, b)):
+        if x is None:
+            assert y is None
+        elif i in (2, 3, 4):  # column sums: fp32 atomics in a different order
+            torch.testing.assert_close(y, x, rtol=1e-5, atol=1e-4)
+        else:
+            assert torch.equal(x, y), i
+
+
+def test_fp8_fused_ln_quant_in_the_step(gpu):
+    """bert-base (2 layers) fp8 step: after calibration the LayerNorms write the fp8 copies (no standalone quant of
+    LN outputs / LN-bwd dy), and the step matches the same step with fused quantisation switched off."""
+    from huggingface_sagemaker_tensorflow_distributed_amd.models import build_model, resolve_config
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel import FlatParamStore
+
+    hip = _hip()
+    cfg = resolve_config("bert-base-uncased").replace(num_hidden_layers=2, hidden_dropout_prob=0.0,
+                                                      attention_probs_dropout_prob=0.0)
+    g = torch.Generator().manual_seed(0)
+    ids = torch.randint(1000, 30000, (64, 128), generator=g).to(gpu)
+    am = torch.ones(64, 128, dtype=torch.long, device=gpu)
+    labels = torch.randint(0, 2, (64,), generator=g).to(gpu)
+    m = build_model(cfg, seed=0).to(gpu)
+    store = FlatParamStore(m, gpu, compute_dtype=torch.bfloat16, fp8=True)
+    hip.set_fp8(True)
+    calls = {"ln_fwd_q8": 0, "ln_bwd_q8": 0}
+    orig = {k: getattr(hip._C, k) for k in calls}
+
+    class _Count:
+        def __getattr__(self, k):
+            f = getattr(orig_C, k)
+            if k in calls:
+                def w(*a):
+                    calls[k] += 1
+                    return f(*a)
+                return w
+            return f
+
+    orig_C = hip._C
+    try:
+        grads = []
+        for step in range(3):
+            if step == 2:
+                hip._C = _Count()
+            m.train()
+            m.rng.new_step(0)
+            store.zero_grad()
+            loss, _ = m(ids, attention_mask=am, labels=labels)
+            loss.backward()
+            torch.cuda.synchronize()
+            grads.append((float(loss), store.grad.clone()))
+            store.refresh_fp8()
+    finally:
+        hip._C = orig_C
+        hip.set_fp8(False)
+    # per layer: the attention block's LN writes W1's copy (+ the first FFN LN writes layer 2's QKV copy);
+    # every block's LN backward writes dy's copy
+    assert calls["ln_fwd_q8"] == 3 and calls["ln_bwd_q8"] == 4, calls
+    assert torch.isfinite(grads[-1][1]).all()
+    cos = torch.nn.functional.cosine_similarity(grads[1][1], grads[2][1], dim=0)
+    assert cos > 0.999, float(cos)
