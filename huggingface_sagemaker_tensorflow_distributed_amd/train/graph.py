@@ -32,10 +32,10 @@ from ..ops.rng import mix32_int
 logger = logging.getLogger(__name__)
 
 
-def step_seed(base_seed: int, rank: int, step: int):
-    """Two 32-bit words of the device step seed for ``step``."""
+def step_seed(base_seed: int, rank: int, step: int, micro: int = 0):
+    """Two 32-bit words of the device step seed for accumulation micro-step ``micro`` of optimizer step ``step``."""
     a = mix32_int((base_seed ^ 0x2545F491) & 0xFFFFFFFF)
-    b = mix32_int(a ^ ((step * 0x9E3779B9 + rank * 0x7F4A7C15) & 0xFFFFFFFF))
+    b = mix32_int(a ^ ((step * 0x9E3779B9 + rank * 0x7F4A7C15 + micro * 0x85EBCA6B) & 0xFFFFFFFF))
     c = mix32_int(b ^ 0x68E31DA4)
     return b, c
 
@@ -50,8 +50,8 @@ class DeviceStepSeed:
         self.base_seed, self.rank = int(base_seed), int(rank)
         hip._C.set_dropout_device_seed(self.t)
 
-    def set_step(self, step: int) -> None:
-        lo, hi = step_seed(self.base_seed, self.rank, step)
+    def set_step(self, step: int, micro: int = 0) -> None:
+        lo, hi = step_seed(self.base_seed, self.rank, step, micro)
         # stream-ordered fills (the value travels as a kernel argument: no host buffer the GPU could
         # read after the host moved on to the next step); int32 view of the uint32 words
         self.t[0].fill_(lo - (1 << 32) if lo >= 1 << 31 else lo)
@@ -71,18 +71,25 @@ class CapturedStep:
         self.static = {k: v.clone() for k, v in example.items()}
         model, store = trainer.model, trainer.store
         model.train()
-        # warm up on a side stream (kernel/workspace first-use allocations, lazy caches) — not captured
+        # warm up on a side stream (kernel/workspace first-use allocations, lazy caches) — not captured; no
+        # readiness callbacks (an optimizer step may already have begun: its slices must not see warm-up gradients)
+        saved = store.grad.clone()  # earlier micro-steps of this optimizer step (gradient accumulation)
         s = torch.cuda.Stream(device=trainer.device)
         s.wait_stream(torch.cuda.current_stream(trainer.device))
-        with torch.cuda.stream(s):
-            for _ in range(warmup):
-                model.rng.new_step(0)
-                store.zero_grad()
-                loss, _ = trainer._forward_loss(self.static)
-                loss.backward()
+        cb, store.ready_callback = store.ready_callback, None
+        try:
+            with torch.cuda.stream(s):
+                for _ in range(warmup):
+                    model.rng.new_step(0)
+                    store.zero_grad()
+                    loss, _ = trainer._forward_loss(self.static)
+                    loss.backward()
+        finally:
+            store.ready_callback = cb
         torch.cuda.current_stream(trainer.device).wait_stream(s)
         torch.cuda.synchronize(trainer.device)
-        store.zero_grad()
+        store.grad.copy_(saved)  # the warm-up overwrote main_grad
+        del saved
         self.graph = torch.cuda.CUDAGraph()
         cb, store.ready_callback = store.ready_callback, None  # no optimizer slices inside a fwd+bwd-only graph
         try:

@@ -284,6 +284,10 @@ class Trainer:
         loss = None
         for i, mb in enumerate(micro_batches):
             last = i == k - 1
+            if self._seed is not None and i > 0:
+                # graph-mode seeding: every micro-step draws its own dropout masks (replayed graphs included)
+                self._seed.set_step(self.global_step, i)
+                self.model.rng.new_step(0)
             if ov is not None and ov != "engine":
                 ov.sync = last  # accumulation micro-steps: gradients not final
             if self._seed is not None and self._graph_replay:
