@@ -240,6 +240,50 @@ void attn_bwd(torch::Tensor qkv, c10::optional<torch::Tensor> mask, torch::Tenso
                        OPT_F(dbias), (int)B, (int)S, (int)heads, p, (uint64_t)seed, cur_stream());
 }
 
+// attention + fp8 copy of its output (forward: e4m3 of the context; backward: dqkv in format qfmt), S > 128 streaming
+// kernels only (attn_q8_supported); amax_in / sinv / amax_track: fp32 [1] delayed-scaling site slots
+static void check_q8(const torch::Tensor& q8, int64_t numel, const torch::Tensor& a, const torch::Tensor& s,
+                     const torch::Tensor& t) {
+  CHECK_CUDA(q8); CHECK_CONTIG(q8); CHECK_DTYPE(q8, torch::kUInt8);
+  TORCH_CHECK(q8.numel() == numel, "q8 shape");
+  check_f32(a, "amax_in"); check_f32(s, "sinv"); check_f32(t, "amax_track");
+}
+
+void attn_fwd_q8(torch::Tensor qkv, c10::optional<torch::Tensor> mask, torch::Tensor out, torch::Tensor lse2, int64_t B,
+                 int64_t S, int64_t heads, double p, int64_t seed, torch::Tensor q8, torch::Tensor amax_in,
+                 torch::Tensor sinv, torch::Tensor amax_track) {
+  check_bf16(qkv, "qkv"); check_bf16(out, "out"); check_f32(lse2, "lse2");
+  TORCH_CHECK(S > 128 && hsd::attn_streaming((int)S), "attn_fwd_q8: streaming attention (S > 128) only");
+  TORCH_CHECK(qkv.size(-1) == 3 * heads * 64, "attention requires head_dim 64");
+  TORCH_CHECK(qkv.numel() == B * S * 3 * heads * 64 && out.numel() == B * S * heads * 64, "attn shapes");
+  TORCH_CHECK(lse2.numel() == B * heads * S, "lse shape");
+  if (mask.has_value()) { check_f32(*mask, "mask"); TORCH_CHECK(mask->numel() == B * S, "mask shape"); }
+  check_q8(q8, out.numel(), amax_in, sinv, amax_track);
+  hsd::launch_attnS_fwd_q8(CBF(qkv), OPT_F(mask), BF(out), lse2.data_ptr<float>(), (int)B, (int)S, (int)heads, p,
+                           (uint64_t)seed, q8.data_ptr<uint8_t>(), amax_in.data_ptr<float>(), sinv.data_ptr<float>(),
+                           amax_track.data_ptr<float>(), cur_stream());
+}
+
+void attn_bwd_q8(torch::Tensor qkv, c10::optional<torch::Tensor> mask, torch::Tensor o, torch::Tensor dout,
+                 torch::Tensor lse2, torch::Tensor dqkv, torch::Tensor ws, int64_t B, int64_t S, int64_t heads, double p,
+                 int64_t seed, c10::optional<torch::Tensor> dbias, torch::Tensor q8, torch::Tensor amax_in,
+                 torch::Tensor sinv, torch::Tensor amax_track, int64_t qfmt) {
+  check_bf16(qkv, "qkv"); check_bf16(o, "o"); check_bf16(dout, "dout"); check_bf16(dqkv, "dqkv");
+  check_f32(lse2, "lse2"); check_f32(ws, "ws");
+  TORCH_CHECK(S > 128 && hsd::attn_streaming((int)S), "attn_bwd_q8: streaming attention (S > 128) only");
+  TORCH_CHECK(qkv.size(-1) == 3 * heads * 64 && dqkv.numel() == qkv.numel(), "attn_bwd shapes");
+  TORCH_CHECK(o.numel() == B * S * heads * 64 && dout.numel() == o.numel(), "attn_bwd o shapes");
+  TORCH_CHECK(ws.numel() == B * heads * S, "ws size");
+  TORCH_CHECK(qfmt == 0 || qfmt == 1, "qfmt");
+  if (mask.has_value()) { check_f32(*mask, "mask"); TORCH_CHECK(mask->numel() == B * S, "mask shape"); }
+  if (dbias.has_value()) { check_f32(*dbias, "dbias"); TORCH_CHECK(dbias->numel() == 3 * heads * 64, "dbias shape"); }
+  check_q8(q8, dqkv.numel(), amax_in, sinv, amax_track);
+  hsd::launch_attnS_bwd_q8(CBF(qkv), OPT_F(mask), CBF(o), CBF(dout), lse2.data_ptr<float>(), BF(dqkv),
+                           ws.data_ptr<float>(), OPT_F(dbias), (int)B, (int)S, (int)heads, p, (uint64_t)seed,
+                           q8.data_ptr<uint8_t>(), amax_in.data_ptr<float>(), sinv.data_ptr<float>(),
+                           amax_track.data_ptr<float>(), (int)qfmt, cur_stream());
+}
+
 // C[M,N] (+)= A·B with fused epilogue. la=0: A [M,K]; la=1: A [K,M]. lb=0: B [N,K]; lb=1: B [K,N].
 void gemm(torch::Tensor A, torch::Tensor B, torch::Tensor C, int64_t la, int64_t lb, int64_t epi,
           c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> aux, c10::optional<torch::Tensor> C2,
@@ -555,6 +599,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("adam_step", &adam_step);
   m.def("ln_fwd_q8", &ln_fwd_q8);
   m.def("ln_bwd_q8", &ln_bwd_q8);
+  m.def("attn_fwd_q8", &attn_fwd_q8);
+  m.def("attn_bwd_q8", &attn_bwd_q8);
+  m.def("attn_q8_supported", [](int64_t S) { return S > 128 && hsd::attn_streaming((int)S); });
   m.def("ln_fwd", &ln_fwd);
   m.def("ln_bwd", &ln_bwd);
   m.def("embed_fwd", &embed_fwd);

@@ -19,6 +19,7 @@
 // LDS once for dQ. dQ is written directly when one workgroup covers all keys (S <= 128) and
 // accumulated with fp32 atomics otherwise.
 #include "common.h"
+#include "fp8_common.h"
 #include <stdlib.h>
 
 namespace hsd {
@@ -378,10 +379,10 @@ void launch_attn128_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, c
 void launch_colsum(const bf16_t* x, float* dbias, int rows, int N, hipStream_t st);
 bool attnS_supported(int S, int head_dim);
 void launch_attnS_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse2, int B, int S, int heads,
-                      double p, uint64_t seed, hipStream_t st);
+                      double p, uint64_t seed, hipStream_t st, Q8Out q8o);
 void launch_attnS_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
                       bf16_t* dqkv, float* delta_ws, float* dbias, int B, int S, int heads, double p, uint64_t seed,
-                      hipStream_t st);
+                      hipStream_t st, Q8Out q8o, int qfmt);
 
 // S in 256..1024 (multiple of 128) runs the streaming kernels of attentionS.hip; its backward takes
 // an fp32 [B*heads*S] scratch (no zeroing) where the generic kernel takes a zeroed [B*S, H] dq accumulator.
@@ -394,7 +395,7 @@ void launch_attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* l
     return;
   }
   if (attn_streaming(S)) {
-    launch_attnS_fwd(qkv, mask, out, lse2, B, S, heads, p, seed, st);
+    launch_attnS_fwd(qkv, mask, out, lse2, B, S, heads, p, seed, st, Q8Out{});
     return;
   }
   DropoutParams dp = make_dropout(p, seed);
@@ -412,7 +413,7 @@ void launch_attn_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, cons
     return;
   }
   if (attn_streaming(S)) {
-    launch_attnS_bwd(qkv, mask, o, dout, lse2, dqkv, dq_acc, dbias, B, S, heads, p, seed, st);
+    launch_attnS_bwd(qkv, mask, o, dout, lse2, dqkv, dq_acc, dbias, B, S, heads, p, seed, st, Q8Out{}, 0);
     return;
   }
   DropoutParams dp = make_dropout(p, seed);

@@ -76,7 +76,7 @@ template <bool DROP>
 __global__ __launch_bounds__(256, 2) void attnS_fwd_kernel(const bf16_t* __restrict__ qkv,
                                                            const float* __restrict__ mask, bf16_t* __restrict__ out,
                                                            float* __restrict__ lse2, int S, int heads, float sl2,
-                                                           DropoutParams dp) {
+                                                           DropoutParams dp, Q8Out q8o) {
   dp = resolve_seed(dp);
   // [K0 K1 K2 | V0 V1 V2 | mask bias]; after the loop K0|K1 is the output staging
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * NSTG * TILE + 2 * kMaxS];
@@ -191,6 +191,15 @@ __global__ __launch_bounds__(256, 2) void attnS_fwd_kernel(const bf16_t* __restr
   l += __shfl_xor(l, 32, 64);
   if (hf == 0) lse2[(int64_t)bh * S + q] = m + __log2f(l);
   __syncthreads();  // K images no longer read: reuse as staging
+  if (q8o.q != nullptr) {  // fp8 e4m3 copy of the output for the fp8 out-projection GEMM (delayed scaling)
+    const float qs = fmt_scale(0, *q8o.amax_in);
+    if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) *q8o.sinv = 1.0f / qs;
+    float qm = 0.f;
+    const int64_t off = ((int64_t)b * S + q0) * H + hh * D;
+    store_rows(Kb + wave * 32 * D, o0, o1, 1.0f / l, out + off, H, lane, nullptr, q8o.q + off, 0, qs, &qm);
+    wave_amax_track(qm, q8o.amax_track);
+    return;
+  }
   store_rows(Kb + wave * 32 * D, o0, o1, 1.0f / l, out + ((int64_t)b * S + q0) * H + hh * D, H, lane);
 }
 
@@ -229,7 +238,7 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_kv_kernel(const bf16_t* __re
                                                               const float* __restrict__ delta,
                                                               bf16_t* __restrict__ dqkv, float* __restrict__ dbias,
                                                               int S, int heads, float sl2, float scale,
-                                                              DropoutParams dp) {
+                                                              DropoutParams dp, Q8Out q8o, int qfmt) {
   dp = resolve_seed(dp);
   // [Q0 Q1 Q2 | dO0 dO1 dO2 | lse | delta | k/v bias partials]; after the loop Q0|Q1 is the output staging
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * NSTG * TILE + 4 * kMaxS + 2 * 2 * 4 * D];
@@ -339,9 +348,17 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_kv_kernel(const bf16_t* __re
   for (int t = 0, stg = 0; t < nt; ++t, stg = stg == NSTG - 1 ? 0 : stg + 1) tile(stg, t);
   __syncthreads();  // Q images no longer read: reuse as staging
   bf16_t* stg_w = Qb + wave * 32 * D;
-  bf16_t* rowbase = dqkv + ((int64_t)b * S + k0) * ld + hh * D;
-  store_rows(stg_w, dv0, dv1, 1.0f, rowbase + 2 * H, ld, lane, dbias ? bsum + (4 + wave) * D : nullptr);
-  store_rows(stg_w, dk0, dk1, scale, rowbase + H, ld, lane, dbias ? bsum + wave * D : nullptr);
+  const int64_t roff = ((int64_t)b * S + k0) * ld + hh * D;
+  bf16_t* rowbase = dqkv + roff;
+  // fp8 copy of dqkv (the fp8 QKV dgrad's A operand; delayed scaling, format qfmt)
+  uint8_t* q8b = q8o.q != nullptr ? q8o.q + roff : nullptr;
+  float qs = 0.f, qm = 0.f;
+  if (q8b != nullptr) qs = fmt_scale(qfmt, *q8o.amax_in);
+  store_rows(stg_w, dv0, dv1, 1.0f, rowbase + 2 * H, ld, lane, dbias ? bsum + (4 + wave) * D : nullptr,
+             q8b ? q8b + 2 * H : nullptr, qfmt, qs, &qm);
+  store_rows(stg_w, dk0, dk1, scale, rowbase + H, ld, lane, dbias ? bsum + wave * D : nullptr,
+             q8b ? q8b + H : nullptr, qfmt, qs, &qm);
+  if (q8b != nullptr) wave_amax_track(qm, q8o.amax_track);
   if (dbias) {
     __syncthreads();
     if (tid < 2 * D) {
@@ -361,7 +378,7 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_q_kernel(const bf16_t* __res
                                                              const float* __restrict__ delta,
                                                              bf16_t* __restrict__ dqkv, float* __restrict__ dbias,
                                                              int S, int heads, float sl2, float scale,
-                                                             DropoutParams dp) {
+                                                             DropoutParams dp, Q8Out q8o, int qfmt) {
   dp = resolve_seed(dp);
   // [K0 K1 K2 | V0 V1 V2 | mask bias | q bias partials]; after the loop K0|K1 is the output staging
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * NSTG * TILE + 2 * kMaxS + 2 * 4 * D];
@@ -462,8 +479,15 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_q_kernel(const bf16_t* __res
 #pragma unroll 1
   for (int t = 0, stg = 0; t < nt; ++t, stg = stg == NSTG - 1 ? 0 : stg + 1) tile(stg, t);
   __syncthreads();  // K images no longer read: reuse as staging
-  store_rows(Kb + wave * 32 * D, dq0, dq1, scale, dqkv + ((int64_t)b * S + q0) * ld + hh * D, ld, lane,
-             dbias ? bsum + wave * D : nullptr);
+  const int64_t qoff = ((int64_t)b * S + q0) * ld + hh * D;
+  float qs = 0.f, qm = 0.f;
+  if (q8o.q != nullptr) {
+    qs = fmt_scale(qfmt, *q8o.amax_in);
+    if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) *q8o.sinv = 1.0f / qs;
+  }
+  store_rows(Kb + wave * 32 * D, dq0, dq1, scale, dqkv + qoff, ld, lane, dbias ? bsum + wave * D : nullptr,
+             q8o.q != nullptr ? q8o.q + qoff : nullptr, qfmt, qs, &qm);
+  if (q8o.q != nullptr) wave_amax_track(qm, q8o.amax_track);
   if (dbias) {
     __syncthreads();
     if (tid < D) atomicAdd(dbias + hh * D + tid, bsum[tid] + bsum[D + tid] + bsum[2 * D + tid] + bsum[3 * D + tid]);
@@ -477,22 +501,22 @@ bool attnS_supported(int S, int head_dim) {
 }
 
 void launch_attnS_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse2, int B, int S, int heads,
-                      double p, uint64_t seed, hipStream_t st) {
+                      double p, uint64_t seed, hipStream_t st, Q8Out q8o) {
   DropoutParams dp = make_dropout(p, seed);
   const float sl2 = attn::kLog2e / sqrtf((float)attn::D);
   if (dp.enabled)
     hipLaunchKernelGGL(aS::attnS_fwd_kernel<true>, dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, out, lse2, S,
-                       heads, sl2, dp);
+                       heads, sl2, dp, q8o);
   else
     hipLaunchKernelGGL(aS::attnS_fwd_kernel<false>, dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, out, lse2, S,
-                       heads, sl2, dp);
+                       heads, sl2, dp, q8o);
   HSD_CHECK_LAUNCH();
 }
 
 // delta_ws: fp32 [B*heads*S] scratch
 void launch_attnS_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
                       bf16_t* dqkv, float* delta_ws, float* dbias, int B, int S, int heads, double p, uint64_t seed,
-                      hipStream_t st) {
+                      hipStream_t st, Q8Out q8o, int qfmt) {
   DropoutParams dp = make_dropout(p, seed);
   const float sl2 = attn::kLog2e / sqrtf((float)attn::D);
   const float scale = 1.0f / sqrtf((float)attn::D);
@@ -502,18 +526,33 @@ void launch_attnS_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, con
   HSD_CHECK_LAUNCH();
   if (dp.enabled) {
     hipLaunchKernelGGL(aS::attnS_bwd_kv_kernel<true>, dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, dout,
-                       lse2, delta_ws, dqkv, dbias, S, heads, sl2, scale, dp);
+                       lse2, delta_ws, dqkv, dbias, S, heads, sl2, scale, dp, q8o, qfmt);
     HSD_CHECK_LAUNCH();
     hipLaunchKernelGGL(aS::attnS_bwd_q_kernel<true>, dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, dout,
-                       lse2, delta_ws, dqkv, dbias, S, heads, sl2, scale, dp);
+                       lse2, delta_ws, dqkv, dbias, S, heads, sl2, scale, dp, q8o, qfmt);
   } else {
     hipLaunchKernelGGL(aS::attnS_bwd_kv_kernel<false>, dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, dout,
-                       lse2, delta_ws, dqkv, dbias, S, heads, sl2, scale, dp);
+                       lse2, delta_ws, dqkv, dbias, S, heads, sl2, scale, dp, q8o, qfmt);
     HSD_CHECK_LAUNCH();
     hipLaunchKernelGGL(aS::attnS_bwd_q_kernel<false>, dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, dout,
-                       lse2, delta_ws, dqkv, dbias, S, heads, sl2, scale, dp);
+                       lse2, delta_ws, dqkv, dbias, S, heads, sl2, scale, dp, q8o, qfmt);
   }
   HSD_CHECK_LAUNCH();
+}
+
+// fp8 variants for the fp8 GEMM path (ops/hip.py): the forward also writes the output's e4m3 copy (the out-projection
+// GEMM's A operand), the backward dqkv's copy in format qfmt (the QKV dgrad's A operand); delayed-scaling sites
+void launch_attnS_fwd_q8(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse2, int B, int S, int heads,
+                         double p, uint64_t seed, uint8_t* q8, const float* amax_in, float* sinv, float* amax_track,
+                         hipStream_t st) {
+  launch_attnS_fwd(qkv, mask, out, lse2, B, S, heads, p, seed, st, Q8Out{q8, amax_in, sinv, amax_track});
+}
+
+void launch_attnS_bwd_q8(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
+                         bf16_t* dqkv, float* delta_ws, float* dbias, int B, int S, int heads, double p, uint64_t seed,
+                         uint8_t* q8, const float* amax_in, float* sinv, float* amax_track, int qfmt, hipStream_t st) {
+  launch_attnS_bwd(qkv, mask, o, dout, lse2, dqkv, delta_ws, dbias, B, S, heads, p, seed, st,
+                   Q8Out{q8, amax_in, sinv, amax_track}, qfmt);
 }
 
 }  // namespace hsd

@@ -4,6 +4,7 @@
 // the wave-private staging used for 128-B row stores. head_dim is 64.
 #pragma once
 #include "common.h"
+#include "fp8_common.h"
 
 namespace hsd {
 namespace attn {
@@ -71,9 +72,11 @@ __device__ __forceinline__ void dma_img(bf16_t* img, const bf16_t* __restrict__ 
 
 // acc (32 rows on the lane x 64 d in regs: d = 32*blk + (reg&3) + 8(reg>>2) + 4h) * scale -> bf16 rows
 // of `dst` (row stride ld) through the wave-private staging slice `stg` ([32][64]).
+// q8dst (optional): the rows' fp8 copy (format qfmt, scale qs; same element offsets as dst), max |x| into *qm
 __device__ __forceinline__ void store_rows(bf16_t* stg, const f32x16& a0, const f32x16& a1, float scale,
                                            bf16_t* __restrict__ dst, int64_t ld, int lane,
-                                           float* colsum_lds = nullptr) {
+                                           float* colsum_lds = nullptr, uint8_t* __restrict__ q8dst = nullptr,
+                                           int qfmt = 0, float qs = 0.f, float* qm = nullptr) {
   const int r = lane & 31, h = lane >> 5;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -92,6 +95,10 @@ __device__ __forceinline__ void store_rows(bf16_t* stg, const f32x16& a0, const 
     const int row = (lane >> 3) + 8 * it, c = lane & 7;
     const u32x4 v = *reinterpret_cast<const u32x4*>(stg + stoff(row, c * 8));
     *reinterpret_cast<u32x4*>(dst + (int64_t)row * ld + c * 8) = v;
+    if (q8dst != nullptr) {
+      *qm = absmax8(v, *qm);
+      *reinterpret_cast<u32x2*>(q8dst + (int64_t)row * ld + c * 8) = qfmt == 0 ? quant8<0>(v, qs) : quant8<1>(v, qs);
+    }
     if (colsum_lds) {
 #pragma unroll
       for (int k = 0; k < 4; ++k) {

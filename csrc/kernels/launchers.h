@@ -65,6 +65,13 @@ void launch_cls_head_bwd(const bf16_t* t_in, const bf16_t* W2, const bf16_t* log
 bool attn_streaming(int S);
 void launch_attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse2, int B, int S, int heads,
                      double p, uint64_t seed, hipStream_t st);
+// attentionS.hip fp8 variants (S > 128 streaming kernels only: attn_streaming(S) && S > 128)
+void launch_attnS_fwd_q8(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse2, int B, int S, int heads,
+                         double p, uint64_t seed, uint8_t* q8, const float* amax_in, float* sinv, float* amax_track,
+                         hipStream_t st);
+void launch_attnS_bwd_q8(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
+                         bf16_t* dqkv, float* delta_ws, float* dbias, int B, int S, int heads, double p, uint64_t seed,
+                         uint8_t* q8, const float* amax_in, float* sinv, float* amax_track, int qfmt, hipStream_t st);
 // dbias (optional): fp32 [3H] += column sums of dqkv (the fused QKV bias gradient)
 void launch_attn_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
                      bf16_t* dqkv, float* dq_acc, float* dbias, int B, int S, int heads, double p, uint64_t seed,

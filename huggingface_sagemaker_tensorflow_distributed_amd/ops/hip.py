@@ -654,8 +654,17 @@ class _AttnBlock(torch.autograd.Function):
         actx = torch.empty((h2d.shape[0], H), dtype=h.dtype, device=h.device)
         lse = torch.empty(B * heads * S, dtype=torch.float32, device=h.device)
         mb = mask_bias.contiguous().float() if mask_bias is not None else None
-        _C.attn_fwd(qkv, mb, actx, lse, B, S, heads, float(p_a), _s64(seed_a))
-        z = gemm_fwd(actx, out_w, EPI_BIAS_DROP_RES, bias=out_b, aux=h2d, p=p_h, seed=seed_h)
+        xq = None
+        st = _site_ready(out_w, "_hsd_fp8_x", "_hsd_q")
+        if st is not None and _C.attn_q8_supported(S) and _C.gemm8_supported(EPI_BIAS_DROP_RES, h2d.shape[0], H, H):
+            # the attention kernel writes the context's fp8 copy for the fp8 out-projection (no quant pass)
+            q = torch.empty((h2d.shape[0], H), dtype=torch.uint8, device=h.device)
+            sinv = torch.empty(1, dtype=torch.float32, device=h.device)
+            _C.attn_fwd_q8(qkv, mb, actx, lse, B, S, heads, float(p_a), _s64(seed_a), q, st[0:1], sinv, st[1:2])
+            xq = (q, sinv)
+        else:
+            _C.attn_fwd(qkv, mb, actx, lse, B, S, heads, float(p_a), _s64(seed_a))
+        z = gemm_fwd(actx, out_w, EPI_BIAS_DROP_RES, bias=out_b, aux=h2d, p=p_h, seed=seed_h, xq=xq)
         out, mean, rstd = _ln_fwd(z, ln_w, ln_b, eps, q8_for=q8_next)
         ctx.save_for_backward(h2d, qkv_w, qkv_b, out_w, out_b, ln_w, ln_b, qkv, actx, lse, z, mean, rstd,
                               mb if mb is not None else lse)
@@ -680,11 +689,22 @@ class _AttnBlock(torch.autograd.Function):
         dq_acc = _attn_ws(B, S, heads, actx.device)
         g_qw, g_qb = _Grad(qkv_w), _Grad(qkv_b)
         # the QKV bias gradient (column sums of dqkv) comes out of the attention backward itself
-        _C.attn_bwd(qkv, mb if has_mask else None, actx, dctx, lse, dqkv, dq_acc, B, S, heads, p_a, _s64(seed_a),
-                    g_qb.buf)
+        st = _site_ready(qkv_w, "_hsd_fp8_g", "_hsd_qt") if ctx.needs_input_grad[0] else None
+        dqq = None
+        if st is not None and _C.attn_q8_supported(S) and _C.gemm8_supported(EPI_RES, dqkv.shape[0], qkv_w.shape[1],
+                                                                              dqkv.shape[1]):
+            # ... and so does dqkv's fp8 copy for the fp8 QKV dgrad
+            q = torch.empty(dqkv.shape, dtype=torch.uint8, device=dqkv.device)
+            sinv = torch.empty(1, dtype=torch.float32, device=dqkv.device)
+            _C.attn_bwd_q8(qkv, mb if has_mask else None, actx, dctx, lse, dqkv, dq_acc, B, S, heads, p_a,
+                           _s64(seed_a), g_qb.buf, q, st[0:1], sinv, st[1:2], _FP8["grad_fmt"])
+            dqq = (q, sinv)
+        else:
+            _C.attn_bwd(qkv, mb if has_mask else None, actx, dctx, lse, dqkv, dq_acc, B, S, heads, p_a, _s64(seed_a),
+                        g_qb.buf)
         r_qb = g_qb.done()
         r_qw = wgrad_done(g_qw, dqkv, h2d)
-        dh = gemm_dgrad(dqkv, qkv_w, EPI_RES, aux=dz) if ctx.needs_input_grad[0] else None
+        dh = gemm_dgrad(dqkv, qkv_w, EPI_RES, aux=dz, dyq=dqq) if ctx.needs_input_grad[0] else None
         return (dh.view(dout.shape) if dh is not None else None, r_qw, r_qb, r_ow, r_ob, r_lnw, r_lnb,
                 None, None, None, None, None, None, None, None, None, None)
 

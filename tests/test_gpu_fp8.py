@@ -308,3 +308,52 @@ def test_fp8_fused_ln_quant_in_the_step(gpu):
     assert torch.isfinite(grads[-1][1]).all()
     cos = torch.nn.functional.cosine_similarity(grads[1][1], grads[2][1], dim=0)
     assert cos > 0.999, float(cos)
+
+
+@pytest.mark.parametrize("S,p,fmt", [(512, 0.1, 0), (256, 0.0, 1)])
+def test_attention_q8_equals_attention_then_quant(gpu, S, p, fmt):
+    """Streaming attention writing the fp8 copy of its output (forward) / of dqkv (backward) == the bf16 kernels,
+    then the standalone quantiser with the same delayed-scaling site."""
+    hip = _hip()
+    C = hip._C
+    assert C.attn_q8_supported(S) and not C.attn_q8_supported(128)
+    torch.manual_seed(5)
+    B, heads = 2, 16
+    H = heads * 64
+    qkv = (torch.randn(B * S, 3 * H, device=gpu) * 0.5).bfloat16()
+    mb = torch.zeros(B, S, device=gpu)
+    mb[1, S - 37:] = -10000.0
+    res = {}
+    for fused in (False, True):
+        out = torch.empty(B * S, H, device=gpu, dtype=torch.bfloat16)
+        lse = torch.empty(B * heads * S, device=gpu)
+        st = torch.tensor([2.0, 0.0], device=gpu)
+        if fused:
+            q, sinv = torch.empty(B * S, H, dtype=torch.uint8, device=gpu), torch.empty(1, device=gpu)
+            C.attn_fwd_q8(qkv, mb, out, lse, B, S, heads, p, 9, q, st[0:1], sinv, st[1:2])
+        else:
+            C.attn_fwd(qkv, mb, out, lse, B, S, heads, p, 9)
+            st._hsd_cal = True
+            q, sinv = hip.quant_fp8(out, 0, st)
+        dout = torch.randn_like(out)
+        dqkv = torch.empty_like(qkv)
+        ws = hip._attn_ws(B, S, heads, gpu)
+        db = torch.zeros(3 * H, device=gpu)
+        gst = torch.tensor([3.0, 0.0], device=gpu)
+        torch.manual_seed(6)
+        dout = torch.randn_like(out)
+        if fused:
+            gq, gs = torch.empty(B * S, 3 * H, dtype=torch.uint8, device=gpu), torch.empty(1, device=gpu)
+            C.attn_bwd_q8(qkv, mb, out, dout, lse, dqkv, ws, B, S, heads, p, 9, db, gq, gst[0:1], gs, gst[1:2], fmt)
+        else:
+            C.attn_bwd(qkv, mb, out, dout, lse, dqkv, ws, B, S, heads, p, 9, db)
+            gst._hsd_cal = True
+            gq, gs = hip.quant_fp8(dqkv, fmt, gst)
+        torch.cuda.synchronize()
+        res[fused] = (out, lse, q, sinv, st, dqkv, gq, gs, gst, db)
+    a, b = res[False], res[True]
+    for i, (x, y) in enumerate(zip(a, b)):
+        if i == 9:
+            torch.testing.assert_close(y, x, rtol=1e-5, atol=1e-4)
+        else:
+            assert torch.equal(x, y), i
