@@ -355,9 +355,24 @@ void fp8_quant_many(torch::Tensor amax_desc, int64_t amax_blocks, torch::Tensor 
 }
 
 // C = epilogue(sa·sb · A8 · B8ᵀ): A8 [M][K], B8 [N][K] uint8 (fp8 bits), same epilogue codes as gemm2 (bf16 out)
+// q8 (optional): uint8 [M][N] fp8 copy of the bf16 output (C2 for two-output epilogues, else C) in format q8fmt,
+// delayed scaling from q8_amax[0]; q8_sinv[0] = 1/scale; q8_track[0] accumulates the output's amax
 void gemm8(torch::Tensor A, int64_t fa, torch::Tensor sa, torch::Tensor B, int64_t fb, torch::Tensor sb,
            torch::Tensor C, int64_t epi, c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> aux,
-           c10::optional<torch::Tensor> C2, double p, int64_t seed, c10::optional<torch::Tensor> dbias) {
+           c10::optional<torch::Tensor> C2, double p, int64_t seed, c10::optional<torch::Tensor> dbias,
+           c10::optional<torch::Tensor> q8, c10::optional<torch::Tensor> q8_amax, c10::optional<torch::Tensor> q8_sinv,
+           c10::optional<torch::Tensor> q8_track, int64_t q8fmt) {
+  uint8_t* q8p = nullptr;
+  float *q8s = nullptr, *q8t = nullptr;
+  const float* q8a = nullptr;
+  if (q8.has_value()) {
+    TORCH_CHECK(q8_amax.has_value() && q8_sinv.has_value() && q8_track.has_value(), "gemm8 q8: amax / sinv / track");
+    check_q8(*q8, C.numel(), *q8_amax, *q8_sinv, *q8_track);
+    TORCH_CHECK(C.is_contiguous(), "gemm8 q8: contiguous C");
+    TORCH_CHECK(q8fmt == 0 || q8fmt == 1, "gemm8 q8 format");
+    q8p = q8->data_ptr<uint8_t>(); q8a = q8_amax->data_ptr<float>(); q8s = q8_sinv->data_ptr<float>();
+    q8t = q8_track->data_ptr<float>();
+  }
   TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda(), "gemm8 operands must be GPU tensors");
   TORCH_CHECK(A.scalar_type() == torch::kUInt8 && B.scalar_type() == torch::kUInt8, "gemm8 inputs: uint8 fp8 bits");
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "gemm8 operands must be 2-D");
@@ -393,7 +408,7 @@ void gemm8(torch::Tensor A, int64_t fa, torch::Tensor sa, torch::Tensor B, int64
                     B.stride(0), (int)fb, sb.data_ptr<float>(), (int)M, (int)N, (int)K, BF(C), C.stride(0),
                     bias.has_value() ? CBF(*bias) : nullptr, aux.has_value() ? CBF(*aux) : nullptr,
                     aux.has_value() ? aux->stride(0) : 0, C2.has_value() ? BF(*C2) : nullptr, p, (uint64_t)seed, dbp,
-                    cur_stream());
+                    cur_stream(), q8p, q8a, q8s, q8t, (int)q8fmt);
 }
 
 // device step seed for dropout (uint32/int32 [2] GPU tensor, kept alive by the caller), None = off
@@ -617,7 +632,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("fp8_elems_per_block", &hsd::fp8_elems_per_block);
   m.def("gemm8", &gemm8, py::arg("A"), py::arg("fa"), py::arg("sa"), py::arg("B"), py::arg("fb"), py::arg("sb"),
         py::arg("C"), py::arg("epi"), py::arg("bias") = py::none(), py::arg("aux") = py::none(),
-        py::arg("C2") = py::none(), py::arg("p") = 0.0, py::arg("seed") = 0, py::arg("dbias") = py::none());
+        py::arg("C2") = py::none(), py::arg("p") = 0.0, py::arg("seed") = 0, py::arg("dbias") = py::none(),
+        py::arg("q8") = py::none(), py::arg("q8_amax") = py::none(),
+        py::arg("q8_sinv") = py::none(), py::arg("q8_track") = py::none(), py::arg("q8fmt") = 0);
   m.def("gemm8_supported", &hsd::gemm8_supported);
   m.def("attn_fwd", &attn_fwd);
   // backward workspace for S > 128: (numel, must_be_zeroed)

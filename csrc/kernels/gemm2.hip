@@ -790,7 +790,10 @@ __device__ __forceinline__ void mainloop_staggered8(f32x4 (&acc)[8][BN / 64], bf
 
 // p.A / p.B: fp8 [M][K] / [N][K] viewed as bf16 [..][K/2] (p.K, p.lda, p.ldb in bf16 units); sa / sb: device
 // dequantisation scalars
-template <int EPI, int BN, int FA, int FB>
+// Q8: the epilogue also writes the output's fp8 copy (the next fp8 GEMM's operand). Its stores and amax atomics come
+// after the next tile's DMA like the bf16 stores; the seam's counted wait still uses NST (bf16 stores only), which is
+// conservative: fewer outstanding operations allowed than were issued after the DMA.
+template <int EPI, int BN, int FA, int FB, bool Q8 = false>
 __global__ __launch_bounds__(512, 1) void gemm8pk_kernel(G2Params p, const float* __restrict__ sa,
                                                          const float* __restrict__ sb) {
   p.dp = resolve_seed(p.dp);
@@ -867,7 +870,7 @@ __global__ __launch_bounds__(512, 1) void gemm8pk_kernel(G2Params p, const float
       set_tile(L);
       prologue();
     }
-    epilogue_bf16<EPI, BN, 8, PB, true>(acc, p, smem + 2 * STAGE, wave, lane, mw, nw, bv, xv0);
+    epilogue_bf16<EPI, BN, 8, PB, true, Q8>(acc, p, smem + 2 * STAGE, wave, lane, mw, nw, bv, xv0);
     if (!more) break;
     if (mw + 128 <= p.M) {
       if (nt > 1) vmcnt<D0 + NST>();
@@ -1170,7 +1173,16 @@ static void g8pk_launch(const G2Params& p0, const float* sa, const float* sb, hi
   p.ntiles = tiles_m * p.tiles_n;
   p.kps = p.K;
   const int grid = p.ntiles > (g2_num_cus() & ~7) ? (g2_num_cus() & ~7) : p.ntiles;
-  hipLaunchKernelGGL((g2::gemm8pk_kernel<EPI, BN, FA, 0>), dim3(grid), dim3(512), 0, st, p, sa, sb);
+  if (p.q8 != nullptr) {
+    // fp8 output copies: the FFN epilogues whose outputs feed the next fp8 GEMM (GELU -> FFN2 forward, GELU'
+    // product -> FFN1 dgrad)
+    if constexpr (EPI == E2_BIAS_GELU_D || EPI == E2_BIAS_GELU || EPI == E2_MUL || EPI == E2_DGELU)
+      hipLaunchKernelGGL((g2::gemm8pk_kernel<EPI, BN, FA, 0, true>), dim3(grid), dim3(512), 0, st, p, sa, sb);
+    else
+      abort();
+  } else {
+    hipLaunchKernelGGL((g2::gemm8pk_kernel<EPI, BN, FA, 0>), dim3(grid), dim3(512), 0, st, p, sa, sb);
+  }
   HSD_CHECK_LAUNCH();
 }
 

@@ -174,9 +174,10 @@ static void g8_launch(const G2Params& p0, const float* sa, const float* sb, hipS
 void launch_gemm8(int epi, const uint8_t* A, int64_t lda, int fa, const float* sa, const uint8_t* B, int64_t ldb,
                   int fb, const float* sb, int M, int N, int K, bf16_t* C, int64_t ldc, const bf16_t* bias,
                   const bf16_t* aux, int64_t ldaux, bf16_t* C2, double p_drop, uint64_t seed, float* dbias,
-                  hipStream_t st) {
+                  hipStream_t st, uint8_t* q8, const float* q8_amax, float* q8_sinv, float* q8_track, int q8_fmt) {
   if (!gemm8_supported(epi, M, N, K)) abort();
   G2Params p{};
+  p.q8 = q8; p.q8_amax = q8_amax; p.q8_sinv = q8_sinv; p.q8_track = q8_track; p.q8_fmt = q8_fmt;
   p.A = reinterpret_cast<const bf16_t*>(A); p.lda = lda;
   p.B = reinterpret_cast<const bf16_t*>(B); p.ldb = ldb;
   p.M = M; p.N = N; p.K = K; p.C = C; p.ldc = ldc;
@@ -199,6 +200,7 @@ void launch_gemm8(int epi, const uint8_t* A, int64_t lda, int fa, const float* s
       return;
     }
   }
+  if (q8 != nullptr) abort();  // fp8 output copies: persistent kernel only
 #define G8_E(E)                                                              \
   case E:                                                                    \
     if (bn == 256) {                                                         \

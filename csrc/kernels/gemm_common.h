@@ -3,6 +3,7 @@
 // stores, fused bias / GELU / dropout+residual / derivative products / bias-gradient column sums).
 #pragma once
 #include "common.h"
+#include "fp8_common.h"
 
 namespace hsd {
 
@@ -36,6 +37,13 @@ struct G2Params {
   float* dbias;  // E2_DGELU: optional fp32 column sums of the output (the bias gradient), BN 256 only
   int nt_store;  // bf16 epilogues: non-temporal stores (default; HSD_G2_NT=0 turns them off)
   unsigned long long* diag;  // persistent NT kernel, diagnostic: per-workgroup seam timestamps (gemm2_set_diag)
+  // optional fp8 copy of the bf16 output (C2 for two-output epilogues, else C) for the next fp8 GEMM: q8 [M][ldc]
+  // bytes, format q8_fmt, delayed scaling from *q8_amax; 1/scale into *q8_sinv, this output's amax into *q8_track
+  uint8_t* q8;
+  const float* q8_amax;
+  float* q8_sinv;
+  float* q8_track;
+  int q8_fmt;
 };
 
 // Buffer descriptor over `ptr` (wave-uniform: built from readfirstlane'd halves so hipcc keeps it in SGPRs).
@@ -207,7 +215,8 @@ __device__ __forceinline__ void epi_aux_regs(u32x4 (&xv)[NIT], const G2Params& p
   }
 }
 
-template <int EPI, int BN, int MB = 8, int PB = 4, bool PRE = false>
+// Q8: also the output's fp8 copy (G2Params q8 fields; fp8 persistent kernel only)
+template <int EPI, int BN, int MB = 8, int PB = 4, bool PRE = false, bool Q8 = false>
 __device__ __forceinline__ void epilogue_bf16(f32x4 (&acc)[MB][BN / 64], const G2Params& p, bf16_t* smem, int wave,
                                               int lane, int mw, int nw, const f32x4* bv_pre = nullptr,
                                               const u32x4* xv_pre = nullptr) {
@@ -240,6 +249,8 @@ __device__ __forceinline__ void epilogue_bf16(f32x4 (&acc)[MB][BN / 64], const G
   const __amdgpu_buffer_rsrc_t rc2 = wave_rsrc(epi_two_out(EPI) ? p.C2 + (int64_t)mw * p.ldc : C);
   constexpr bool kColsum = (EPI == E2_DGELU || EPI == E2_MUL) && CPR == 8;
   float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float qs = 0.f, qm = 0.f;
+  if constexpr (Q8) qs = fmt_scale(p.q8_fmt, *p.q8_amax);
 #pragma unroll
   for (int h = 0; h < MB / PB; ++h) {
 #pragma unroll
@@ -290,11 +301,20 @@ __device__ __forceinline__ void epilogue_bf16(f32x4 (&acc)[MB][BN / 64], const G
         st16(C + co, o, 0);
         if constexpr (epi_two_out(EPI)) st16(p.C2 + co, o2, 0);
       }
+      if constexpr (Q8) {
+        const u32x4 src = epi_two_out(EPI) ? o2 : o;
+        qm = absmax8(src, qm);
+        *reinterpret_cast<u32x2*>(p.q8 + co) = p.q8_fmt == 0 ? quant8<0>(src, qs) : quant8<1>(src, qs);
+      }
     }
     __builtin_amdgcn_wave_barrier();
   }
   if constexpr (kColsum) {
     if (p.dbias != nullptr) colsum_flush(csum, p.dbias, nw, p.N, lane);
+  }
+  if constexpr (Q8) {
+    wave_amax_track(qm, p.q8_track);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *p.q8_sinv = 1.0f / qs;
   }
 }
 

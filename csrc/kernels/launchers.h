@@ -93,7 +93,8 @@ bool gemm8_supported(int epi, int M, int N, int K);
 void launch_gemm8(int epi, const uint8_t* A, int64_t lda, int fa, const float* sa, const uint8_t* B, int64_t ldb,
                   int fb, const float* sb, int M, int N, int K, bf16_t* C, int64_t ldc, const bf16_t* bias,
                   const bf16_t* aux, int64_t ldaux, bf16_t* C2, double p_drop, uint64_t seed, float* dbias,
-                  hipStream_t st);
+                  hipStream_t st, uint8_t* q8 = nullptr, const float* q8_amax = nullptr, float* q8_sinv = nullptr,
+                  float* q8_track = nullptr, int q8_fmt = 0);
 void launch_fp8_quant(const bf16_t* x, int64_t n, float* amax, uint8_t* q, float* sinv, int fmt, bool compute_amax,
                       float* amax_track, hipStream_t st);
 void launch_fp8_quant_many(const int64_t* amax_desc, int n_amax, int amax_blocks, const int64_t* quant_desc,

@@ -540,15 +540,37 @@ def _take_q8(x):
     return e
 
 
-def gemm_fwd(x, w, epi, bias=None, aux=None, out2=None, p=0.0, seed=0, xq=None):
+def _q8_out(like, w, state_attr: str, wattr: str, fmt: int):
+    """Buffers for a producer-written fp8 copy of ``like`` for ``w``'s calibrated site, or None."""
+    st = _site_ready(w, state_attr, wattr)
+    if st is None:
+        return None
+    q = torch.empty(like.shape, dtype=torch.uint8, device=like.device)
+    return q, torch.empty(1, dtype=torch.float32, device=like.device), st, fmt
+
+
+def _q8_kw(q8):
+    if q8 is None:
+        return {}
+    q, sinv, st, fmt = q8
+    return {"q8": q, "q8_amax": st[0:1], "q8_sinv": sinv, "q8_track": st[1:2], "q8fmt": fmt}
+
+
+def gemm_fwd(x, w, epi, bias=None, aux=None, out2=None, p=0.0, seed=0, xq=None, q8_for=None):
     """y[T, N] = x[T, K] · w[N, K]ᵀ with epilogue (gemm2 8-phase kernel; 128-tile kernel for odd shapes;
     gemm8 fp8 kernel when fp8 is on and the weight has an fp8 copy). ``xq``: x's fp8 copy (q, sinv) already
-    written by its producer."""
+    written by its producer. ``q8_for``: the weight of the fp8 GEMM that consumes the output (``out2`` for the
+    two-output GELU epilogue): on the fp8 path the epilogue writes that GEMM's fp8 input copy too."""
     y = torch.empty((x.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)
     wq = _fp8_w(w, "_hsd_q")
     if wq is not None and _C.gemm8_supported(epi, x.shape[0], w.shape[0], x.shape[1]):
         qx, sx = xq if xq is not None else quant_fp8(x, FP8_E4M3, getattr(w, "_hsd_fp8_x", None))
-        _C.gemm8(qx, FP8_E4M3, sx, wq, FP8_E4M3, w._hsd_qs, y, epi, bias, aux, out2, float(p), _s64(seed), None)
+        q8 = _q8_out(y, q8_for, "_hsd_fp8_x", "_hsd_q", FP8_E4M3) \
+            if q8_for is not None and epi in (EPI_BIAS_GELU, EPI_BIAS_GELU_D) and out2 is not None else None
+        _C.gemm8(qx, FP8_E4M3, sx, wq, FP8_E4M3, w._hsd_qs, y, epi, bias, aux, out2, float(p), _s64(seed), None,
+                 **_q8_kw(q8))
+        if q8 is not None:
+            _Q8_PENDING[(out2.data_ptr(), out2.numel())] = (q8[0], q8[1])
         return y
     if _nt_ok(x.shape[0], w.shape[0], x.shape[1], epi):
         _C.gemm2(x, w, y, 0, 0, epi, bias, aux, out2, float(p), _s64(seed), 0, None, None)  # 0: auto split-K
@@ -557,7 +579,7 @@ def gemm_fwd(x, w, epi, bias=None, aux=None, out2=None, p=0.0, seed=0, xq=None):
     return y
 
 
-def gemm_dgrad(dy, w, epi=EPI_STORE, aux=None, dbias=None, dyq=None):
+def gemm_dgrad(dy, w, epi=EPI_STORE, aux=None, dbias=None, dyq=None, q8_for=None):
     """dx[T, K] = dy[T, N] · w[N, K]  (NT kernel on the transposed weight wᵀ [K, N]).
 
     ``dbias`` (DGELU only): fp32 [K] buffer that receives the column sums of dx (the bias gradient of
@@ -568,9 +590,15 @@ def gemm_dgrad(dy, w, epi=EPI_STORE, aux=None, dbias=None, dyq=None):
         fuse = dbias is not None and epi in (EPI_DGELU, EPI_MUL) and w.shape[1] % 256 == 0
         fmt = _FP8["grad_fmt"]
         qdy, sdy = dyq if dyq is not None else quant_fp8(dy, fmt, getattr(w, "_hsd_fp8_g", None))
-        _C.gemm8(qdy, fmt, sdy, wqt, FP8_E4M3, w._hsd_qs, dx, epi, None, aux, None, 0.0, 0, dbias if fuse else None)
+        # q8_for: the next fp8 dgrad's weight -- the epilogue writes its dy copy (the GELU'-product output)
+        q8 = _q8_out(dx, q8_for, "_hsd_fp8_g", "_hsd_qt", fmt) \
+            if q8_for is not None and epi in (EPI_MUL, EPI_DGELU) else None
+        _C.gemm8(qdy, fmt, sdy, wqt, FP8_E4M3, w._hsd_qs, dx, epi, None, aux, None, 0.0, 0, dbias if fuse else None,
+                 **_q8_kw(q8))
         if dbias is not None and not fuse:
             _C.colsum(dx, dbias)
+        if q8 is not None:
+            _Q8_PENDING[(dx.data_ptr(), dx.numel())] = (q8[0], q8[1])
         return dx
     wt = getattr(w, "_hsd_wt", None)  # FlatParamStore keeps Wᵀ fresh (one batched transpose per step)
     if wt is not None and (wt.shape[0] != w.shape[1] or wt.shape[1] != w.shape[0]):
@@ -731,8 +759,8 @@ class _FFNBlock(torch.autograd.Function):
         # epilogue is then a product (no erf/exp per element in backward)
         keep_grad = _nt_ok(h2d.shape[0], w1.shape[0], h2d.shape[1], EPI_BIAS_GELU_D) and \
             _nt_ok(h2d.shape[0], w1.shape[0], w2.shape[0], EPI_MUL)
-        pre = gemm_fwd(h2d, w1, EPI_BIAS_GELU_D if keep_grad else EPI_BIAS_GELU, bias=b1, out2=act, xq=xq)
-        z = gemm_fwd(act, w2, EPI_BIAS_DROP_RES, bias=b2, aux=h2d, p=p, seed=seed)
+        pre = gemm_fwd(h2d, w1, EPI_BIAS_GELU_D if keep_grad else EPI_BIAS_GELU, bias=b1, out2=act, xq=xq, q8_for=w2)
+        z = gemm_fwd(act, w2, EPI_BIAS_DROP_RES, bias=b2, aux=h2d, p=p, seed=seed, xq=_take_q8(act))
         out, mean, rstd = _ln_fwd(z, ln_w, ln_b, eps, q8_for=q8_next)
         ctx.save_for_backward(h2d, w1, b1, w2, b2, ln_w, ln_b, pre, act, z, mean, rstd)
         ctx.cfg = (float(p), seed, keep_grad)
@@ -752,10 +780,12 @@ class _FFNBlock(torch.autograd.Function):
         r_lnw, r_lnb, r_b2 = g_lnw.done(), g_lnb.done(), g_b2.done()
         r_w2 = wgrad_done(g_w2, dy, act)
         g_w1, g_b1 = _Grad(w1), _Grad(b1)
-        da = gemm_dgrad(dy, w2, EPI_MUL if keep_grad else EPI_DGELU, aux=pre, dbias=g_b1.buf, dyq=dyq)
+        da = gemm_dgrad(dy, w2, EPI_MUL if keep_grad else EPI_DGELU, aux=pre, dbias=g_b1.buf, dyq=dyq,
+                        q8_for=w1 if ctx.needs_input_grad[0] else None)
+        daq = _take_q8(da)
         r_b1 = g_b1.done()
         r_w1 = wgrad_done(g_w1, da, h2d)
-        dh = gemm_dgrad(da, w1, EPI_RES, aux=dz) if ctx.needs_input_grad[0] else None
+        dh = gemm_dgrad(da, w1, EPI_RES, aux=dz, dyq=daq) if ctx.needs_input_grad[0] else None
         return (dh.view(dout.shape) if dh is not None else None, r_w1, r_b1, r_w2, r_b2, r_lnw, r_lnb,
                 None, None, None, None)
 

@@ -357,3 +357,42 @@ def test_attention_q8_equals_attention_then_quant(gpu, S, p, fmt):
             torch.testing.assert_close(y, x, rtol=1e-5, atol=1e-4)
         else:
             assert torch.equal(x, y), i
+
+
+@pytest.mark.parametrize("M,N,K,epi,fmt", [(8192, 4096, 1024, 8, 0), (8192, 1024, 4096, 9, 1), (5000, 3072, 768, 9, 0)])
+def test_gemm8_epilogue_q8_equals_gemm8_then_quant(gpu, M, N, K, epi, fmt):
+    """The fp8 GEMM's epilogue writing the fp8 copy of its output (GELU output for the FFN1 forward, the GELU'-product
+    for the FFN2 dgrad) == the same GEMM, then the standalone quantiser on the same site."""
+    hip = _hip()
+    C = hip._C
+    torch.manual_seed(8)
+    x = torch.randn(M, K, device=gpu).bfloat16()
+    w = (torch.randn(N, K, device=gpu) * 0.05).bfloat16()
+    qx, sx = hip.quant_fp8(x, 0)
+    qw, sw = hip.quant_fp8(w, 0)
+    bias = (torch.randn(N, device=gpu) * 0.1).bfloat16()
+    aux = torch.randn(M, N, device=gpu).bfloat16()
+    res = {}
+    for fused in (False, True):
+        y = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+        y2 = torch.empty_like(y) if epi == 8 else None
+        db = torch.zeros(N, device=gpu) if epi == 9 else None
+        st = torch.tensor([1.5, 0.0], device=gpu)
+        kw = {}
+        if fused:
+            q, sinv = torch.empty(M, N, dtype=torch.uint8, device=gpu), torch.empty(1, device=gpu)
+            kw = dict(q8=q, q8_amax=st[0:1], q8_sinv=sinv, q8_track=st[1:2], q8fmt=fmt)
+        C.gemm8(qx, 0, sx, qw, 0, sw, y, epi, bias if epi == 8 else None, aux if epi == 9 else None, y2, 0.0, 0, db,
+                **kw)
+        if not fused:
+            st._hsd_cal = True
+            q, sinv = hip.quant_fp8(y2 if epi == 8 else y, fmt, st)
+        torch.cuda.synchronize()
+        res[fused] = (y, y2, q, sinv, st, db)
+    a, b = res[False], res[True]
+    assert torch.equal(a[0], b[0])
+    if a[1] is not None:
+        assert torch.equal(a[1], b[1])
+    assert torch.equal(a[2], b[2]) and torch.equal(a[3], b[3]) and torch.equal(a[4], b[4])
+    if a[5] is not None:
+        torch.testing.assert_close(b[5], a[5], rtol=1e-4, atol=1e-3)
