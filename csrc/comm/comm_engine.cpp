@@ -261,6 +261,9 @@ class CommEngine {
     dep_events_.push_back(e);
   }
 
+  // 0 = the current stream (default); otherwise every caller-side event record / wait uses this stream
+  void set_caller_stream(int64_t stream_ptr) { caller_override_ = reinterpret_cast<hipStream_t>(stream_ptr); }
+
   int64_t num_buckets() const { return (int64_t)buckets_.size(); }
   int64_t launched_count() const {
     int64_t n = 0;
@@ -269,7 +272,11 @@ class CommEngine {
   }
 
  private:
-  hipStream_t caller() const { return c10::hip::getCurrentHIPStream(device_).stream(); }
+  // the stream the gradients are produced on: the thread's current stream, or the stream set by set_caller_stream
+  // (a HIP-graph capture: readiness hooks run on autograd's thread, whose current stream is not the capture stream)
+  hipStream_t caller() const {
+    return caller_override_ ? caller_override_ : c10::hip::getCurrentHIPStream(device_).stream();
+  }
 
   void check(const torch::Tensor& t) const {
     if (!t.is_cuda() || t.get_device() != device_) throw std::runtime_error("CommEngine: tensor on the wrong device");
@@ -279,7 +286,9 @@ class CommEngine {
   void order_after_caller() {
     HIP_OK(hipEventRecord(ready_, caller()));
     HIP_OK(hipStreamWaitEvent(stream_, ready_, 0));
-    // gradients may also be produced on registered side streams (the wgrad stream): order after them too
+    // gradients may also be produced on registered side streams (the wgrad stream): order after them too -- not
+    // inside a capture (set_caller_stream), which runs no side stream and must not wait on uncaptured work
+    if (caller_override_) return;
     for (size_t i = 0; i < deps_.size(); ++i) {
       HIP_OK(hipEventRecord(dep_events_[i], deps_[i]));
       HIP_OK(hipStreamWaitEvent(stream_, dep_events_[i], 0));
@@ -335,6 +344,7 @@ class CommEngine {
 
   int rank_, world_, device_;
   hipStream_t stream_ = nullptr;
+  hipStream_t caller_override_ = nullptr;
   ncclComm_t comm_ = nullptr;
   hipEvent_t ready_ = nullptr;
   bool timing_ = false;
@@ -376,6 +386,7 @@ void register_comm(pybind11::module& m) {
       .def("num_buckets", &CommEngine::num_buckets)
       .def("launched_count", &CommEngine::launched_count)
       .def("stream_ptr", &CommEngine::stream_ptr)
+      .def("set_caller_stream", &CommEngine::set_caller_stream)
       .def_property_readonly("rank", &CommEngine::rank)
       .def_property_readonly("world", &CommEngine::world);
 }

@@ -111,9 +111,10 @@ class CapturedStep:
 
 
 class CapturedTrainStep:
-    """The WHOLE one-process training step as one graph: gradient zeroing, forward, loss, backward, the optimizer
-    slices stepped under backward (optim/adam.py LocalOverlap: a side-stream branch of the graph per slice, forked
-    when the slice's last gradient is queued), the remaining slices and the Wᵀ / fp8 weight-copy refresh.
+    """The WHOLE training step as one graph: gradient zeroing, forward, loss, backward, the optimizer slices stepped
+    under backward (one process: optim/adam.py LocalOverlap, a side-stream branch of the graph per slice, forked when
+    the slice's last gradient is queued; data parallel: the native RCCL engine's bucket all-reduces, each followed by
+    its Adam slice on the engine stream), the remaining slices and the Wᵀ / fp8 weight-copy refresh.
 
     Adam's per-step scalars (bias-corrected step, ε, grad scale, lr·wd) are read from a device tensor
     (``FusedAdam.use_device_coef``) that :meth:`run` refreshes before each replay, as the dropout step seed is; the
@@ -143,25 +144,39 @@ class CapturedTrainStep:
         store.zero_grad()
         opt.use_device_coef()
         ov = trainer._opt_overlap
+        buck = trainer.bucketer
+        eng = buck.engine if buck is not None else None
         gscale = 1.0 / trainer.world
         self.graph = torch.cuda.CUDAGraph()
         step0 = opt.step_count
         try:
             with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
+                cap = torch.cuda.current_stream(trainer.device)  # the capture stream
                 store.zero_grad()
                 model.rng.new_step(0)
+                if eng is not None:
+                    # data parallel: the bucket all-reduces (and, with the engine overlap, each bucket's Adam slice
+                    # on the engine stream) are captured too -- the engine forks its stream from the capture stream
+                    eng.set_caller_stream(cap.cuda_stream)
+                    buck.begin(micro_steps=1)
                 if ov is not None:
-                    ov.parent = torch.cuda.current_stream(trainer.device)  # the capture stream
+                    if ov != "engine":
+                        ov.parent = cap
                     opt.begin_step(grad_scale=gscale)
-                    ov.begin()
+                    if ov != "engine":
+                        ov.begin()
                 self.loss, self.logits = trainer._forward_loss(self.static)
                 self.loss.backward()
-                if ov is not None:
+                if buck is not None:
+                    buck.finish()
+                if ov is not None and ov != "engine":
                     ov.join()
                 opt.step(grad_scale=gscale)
         finally:
-            if ov is not None:
+            if ov is not None and ov != "engine":
                 ov.parent = None
+            if eng is not None:
+                eng.set_caller_stream(0)
         opt.step_count = step0  # begin_step / step advanced it once during capture; each replay advances it
         torch.cuda.synchronize(trainer.device)
         self.gscale = gscale

@@ -163,8 +163,15 @@ class Trainer:
     def enable_hip_graph(self) -> bool:
         """Replay forward + backward from captured HIP graphs (train/graph.py). Single-process GPU runs of
         models without data-dependent shapes; otherwise stays eager (returns False)."""
-        if self.device.type != "cuda" or self.bucketer is not None or self.world > 1:
-            logger.warning("--hip_graph: needs one GPU process (data-parallel steps stay eager)")
+        if self.device.type != "cuda":
+            logger.warning("--hip_graph: needs a GPU")
+            return False
+        if (self.bucketer is not None or self.world > 1) and not (
+                self.bucketer is not None and self.bucketer.engine is not None and self.bucketer.overlap
+                and os.environ.get("HSD_GRAPH_FULL", "1") == "1"):
+            # data parallel: only the whole-step graph over the native RCCL engine captures the collectives
+            logger.warning("--hip_graph: data-parallel steps need the native RCCL engine and the whole-step graph; "
+                           "staying eager")
             return False
         if not getattr(self.model, "graph_safe", True):
             logger.warning("--hip_graph: %s has data-dependent shapes; staying eager", type(self.model).__name__)
@@ -217,6 +224,9 @@ class Trainer:
         self.model.train()
         if self._seed is not None and self._graph_replay and self._full_graph and len(micro_batches) == 1:
             return self._graph_step(micro_batches[0], meter)
+        if self._seed is not None and self.bucketer is not None:
+            raise RuntimeError("--hip_graph with data parallelism captures whole one-micro-step optimizer steps only "
+                               "(gradient accumulation: run eagerly)")
         if self._seed is not None:
             # graph mode: per-site seeds fixed (step 0), the device step seed carries the step
             self._seed.set_step(self.global_step)

@@ -165,3 +165,47 @@ def test_comm_engine_wire_compression(gpu, mode, dtype):
     assert torch.equal(flat, ref)
     with pytest.raises(RuntimeError):
         eng.set_compression(3)
+
+
+def test_whole_step_graph_with_native_engine(gpu, monkeypatch):
+    """Data-parallel whole-step HIP graph (train/graph.py CapturedTrainStep): the bucket all-reduces and the Adam slices
+    on the engine stream are captured with forward / backward (world-of-one RCCL communicator). Three replayed steps
+    equal three eager steps of the same engine configuration (same dropout masks via graph-mode seeding)."""
+    from huggingface_sagemaker_tensorflow_distributed_amd import data as hdata
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel import GradBucketer
+    from huggingface_sagemaker_tensorflow_distributed_amd.train.runner import build
+    from huggingface_sagemaker_tensorflow_distributed_amd.train.trainer import Trainer
+    from huggingface_sagemaker_tensorflow_distributed_amd.utils.args import build_parser
+
+    monkeypatch.setenv("HSD_OPT_OVERLAP", "1")
+    monkeypatch.setenv("HSD_GRAPH_FULL", "1")
+    ds = hdata.synthetic_classification(32, 128, 30522, seed=1)
+    batches = [{k: torch.from_numpy(v[16 * i:16 * (i + 1)]).long().to(gpu) for k, v in
+                (("input_ids", ds.input_ids), ("attention_mask", ds.attention_mask), ("labels", ds.labels))}
+               for i in range(2)]
+    res = {}
+    C = _C()
+    for replay in (False, True):
+        args, _ = build_parser("train").parse_known_args(
+            ["--model_name_or_path", "bert-base-uncased", "--train_batch_size", "16", "--dtype", "bf16",
+             "--learning_rate", "1e-4", "--log_every", "0", "--seed", "3"])
+        parts = build(args, "train")
+        model, store, opt = parts["model"], parts["store"], parts["optimizer"]
+        model.cfg  # noqa: B018
+        eng = C.CommEngine(0, 1, C.CommEngine.unique_id(), gpu.index, True)
+        buck = GradBucketer(store, bucket_mb=8, engine=eng)
+        tr = Trainer(model, store, opt, buck, gpu, hip_graph=True)
+        tr._graph_replay = replay
+        assert tr._opt_overlap == "engine" and tr._seed is not None
+        losses = [float(tr.train_step([batches[s % 2]])) for s in range(3)]
+        torch.cuda.synchronize()
+        if replay:
+            assert any(k[0] == "full" for k in tr._graphs)
+        assert opt.step_count == 3
+        res[replay] = (losses, store.master.clone())
+        tr._seed.close()
+        buck.detach()
+    (l0, w0), (l1, w1) = res[False], res[True]
+    for a, b in zip(l0, l1):
+        assert abs(a - b) <= 2e-3 * max(1.0, abs(a)), (l0, l1)
+    assert float((w0 - w1).norm() / w0.norm()) < 1e-4
