@@ -224,7 +224,7 @@ class Trainer:
         self.model.train()
         if self._seed is not None and self._graph_replay and self._full_graph and len(micro_batches) == 1:
             return self._graph_step(micro_batches[0], meter)
-        if self._seed is not None and self.bucketer is not None:
+        if self._seed is not None and self._graph_replay and self.bucketer is not None:
             raise RuntimeError("--hip_graph with data parallelism captures whole one-micro-step optimizer steps only "
                                "(gradient accumulation: run eagerly)")
         if self._seed is not None:
