@@ -1,6 +1,7 @@
 // Python bindings for the gfx950 kernels: argument validation + current-HIP-stream launch.
 // Compiled into huggingface_sagemaker_tensorflow_distributed_amd/_C.so by _build.py (hipcc).
 #include <torch/extension.h>
+#include <c10/hip/HIPGuard.h>
 #include <c10/hip/HIPStream.h>
 
 #include "kernels/launchers.h"
@@ -12,6 +13,27 @@ void register_comm(pybind11::module& m);
 namespace {
 
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
+
+// ---- host-cheap stream ordering (ops/hip.py weight-gradient side stream, optimizer slices): one event from a
+// per-thread ring per fork, no Python stream objects / context managers on the per-layer backward path
+static hipEvent_t ring_event() {
+  constexpr int kRing = 64;
+  thread_local hipEvent_t ring[kRing] = {};
+  thread_local int next = 0;
+  hipEvent_t& e = ring[next];
+  next = (next + 1) % kRing;
+  if (e == nullptr) TORCH_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess, "hipEventCreate");
+  return e;
+}
+
+// dst waits for the work queued on src so far (0 = the current stream)
+void stream_wait(int64_t dst_ptr, int64_t src_ptr) {
+  hipStream_t dst = dst_ptr ? reinterpret_cast<hipStream_t>(dst_ptr) : cur_stream();
+  hipStream_t src = src_ptr ? reinterpret_cast<hipStream_t>(src_ptr) : cur_stream();
+  hipEvent_t e = ring_event();
+  TORCH_CHECK(hipEventRecord(e, src) == hipSuccess, "hipEventRecord");
+  TORCH_CHECK(hipStreamWaitEvent(dst, e, 0) == hipSuccess, "hipStreamWaitEvent");
+}
 
 #define CHECK_CUDA(x) TORCH_CHECK((x).is_cuda(), #x " must be a GPU tensor")
 #define CHECK_CONTIG(x) TORCH_CHECK((x).is_contiguous(), #x " must be contiguous")
@@ -485,6 +507,16 @@ void gemm2(torch::Tensor A, torch::Tensor B, torch::Tensor C, int64_t la, int64_
                     C2.has_value() ? BF(*C2) : nullptr, p, (uint64_t)seed, sp, wsp, dbp, cur_stream());
 }
 
+// gemm2 on an explicit stream (the weight-gradient side stream): no Python stream context per call
+void gemm2_on(int64_t stream_ptr, torch::Tensor A, torch::Tensor B, torch::Tensor C, int64_t la, int64_t lb, int64_t epi,
+              c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> aux, c10::optional<torch::Tensor> C2,
+              double p, int64_t seed, int64_t splits, c10::optional<torch::Tensor> ws,
+              c10::optional<torch::Tensor> dbias) {
+  c10::hip::HIPStreamGuard guard(
+      c10::hip::getStreamFromExternal(reinterpret_cast<hipStream_t>(stream_ptr), A.get_device()));
+  gemm2(A, B, C, la, lb, epi, bias, aux, C2, p, seed, splits, ws, dbias);
+}
+
 // logits [R, V] (bf16 | fp32), labels int64 [R] (-100 = ignore); stats fp32 [2] += {Σ loss, correct};
 // dlogits (optional, same dtype/shape) = (softmax - onehot) / n_valid
 // logits [rows][ld] (unit inner stride), the first V columns scored (V = 0: all); dlogits same shape / strides
@@ -613,6 +645,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   hsd::register_comm(m);
   m.def("adam_step", &adam_step);
   m.def("ln_fwd_q8", &ln_fwd_q8);
+  m.def("stream_wait", &stream_wait);
+  m.def("gemm2_on", &gemm2_on);
   m.def("ln_bwd_q8", &ln_bwd_q8);
   m.def("attn_fwd_q8", &attn_fwd_q8);
   m.def("attn_bwd_q8", &attn_bwd_q8);

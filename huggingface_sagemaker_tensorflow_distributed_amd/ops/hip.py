@@ -67,9 +67,29 @@ _WGRAD_AUTO_MAX_TOKENS = int(_os.environ.get("HSD_WGRAD_STREAM_MAX_TOKENS", "655
 # the compute stream's pool with no cross-stream event bookkeeping in the allocator; record_stream collapsed
 # throughput 7x at B = 256-1024). Costs the operands' memory until the end of the backward.
 _WGRAD_STASH = _os.environ.get("HSD_WGRAD_STASH", "1") == "1"
+# HSD_WGRAD_CXX=0: fork to the side stream through torch's Python stream objects (the round-2 path) instead of the
+# extension's stream_wait + gemm2_on
+_WGRAD_CXX = _os.environ.get("HSD_WGRAD_CXX", "1") == "1"
 _SIDE = {}
 _STASH = []
 _JOIN_QUEUED = [False]
+
+
+# Cross-stream ordering without a new event per call. ``Stream.wait_stream`` creates (and on ROCm lazily
+# hipEventCreate's) a fresh event every time and goes through torch's Python stream plumbing; with ~80 forks / joins
+# per step (weight-gradient side stream, optimizer slices) small-batch steps were host-bound
+# (tools/cpu_profile_step.py). The extension records an event from a per-thread ring instead; a wait takes the
+# event's state at the time of the call, so re-recording it later does not move an earlier wait.
+
+
+def stream_wait(dst, src) -> None:
+    """``dst`` waits for everything queued on ``src`` so far (``dst.wait_stream(src)`` with an event from the
+    extension's per-thread ring). Streams or raw handles; ``None`` / 0 = the current stream."""
+    if not _WGRAD_CXX and hasattr(dst, "wait_stream") and hasattr(src, "cuda_stream"):
+        dst.wait_stream(src)
+        return
+    _C.stream_wait(dst.cuda_stream if hasattr(dst, "cuda_stream") else int(dst or 0),
+                   src.cuda_stream if hasattr(src, "cuda_stream") else int(src or 0))
 
 
 def side_stream(device) -> Optional[torch.cuda.Stream]:
@@ -118,10 +138,12 @@ def join_side_streams() -> None:
     graph capture: captured steps never use the wgrad side stream (``_use_side_stream``)."""
     if _SIDE and torch.cuda.is_current_stream_capturing():
         return
-    cur = torch.cuda.current_stream() if _SIDE else None
-    for s in _SIDE.values():
-        if s.device == cur.device:
-            cur.wait_stream(s)
+    if not _SIDE:
+        return
+    dev = torch.cuda.current_device()
+    for k, s in _SIDE.items():
+        if k == dev:
+            _C.stream_wait(0, s.cuda_stream)
     _STASH.clear()
     _JOIN_QUEUED[0] = False
 
@@ -141,10 +163,24 @@ def wgrad_done(g: "_Grad", dy: torch.Tensor, x: torch.Tensor):
         # join the compute stream to the side stream when this backward pass finishes
         torch.autograd.Variable._execution_engine.queue_callback(_end_of_backward)
         _JOIN_QUEUED[0] = True
-    s.wait_stream(torch.cuda.current_stream())
-    with torch.cuda.stream(s):
-        gemm_wgrad_(g, dy, x)
-        r = g.done()
+    N, K, T = dy.shape[1], x.shape[1], dy.shape[0]
+    if not _WGRAD_CXX:
+        s.wait_stream(torch.cuda.current_stream())
+        with torch.cuda.stream(s):
+            gemm_wgrad_(g, dy, x)
+            r = g.done()
+    elif g.buf is g.mg and _C.gemm2_supported(1, 1, 7, N, K, T):
+        _C.stream_wait(s.cuda_stream, 0)
+        # the common case without any Python stream plumbing: TT GEMM (+ split-K reduce) launched on the side stream
+        sp = _C.gemm2_splits(N, K, T)
+        _C.gemm2_on(s.cuda_stream, dy, x, g.buf, 1, 1, 7, None, None, None, 0.0, 0, sp,
+                    _workspace(sp * N * K, dy.device, s), None)
+        r = None
+    else:
+        _C.stream_wait(s.cuda_stream, 0)
+        with torch.cuda.stream(s):
+            gemm_wgrad_(g, dy, x)
+            r = g.done()
     if _WGRAD_STASH:
         _STASH.append((dy, x))
     else:
@@ -459,12 +495,17 @@ def _wgrad_splits(n_out: int, k_in: int, tokens: int) -> int:
 _WS = {}
 
 
-def _workspace(numel: int, device) -> torch.Tensor:
-    """Split-K slab workspace (fp32), grown on demand, reused stream-ordered across wgrad GEMMs."""
+def _workspace(numel: int, device, stream=None) -> torch.Tensor:
+    """Split-K slab workspace (fp32), grown on demand, reused stream-ordered across wgrad GEMMs. ``stream``: the
+    stream that will use it (a grown buffer is allocated from that stream's pool)."""
     key = (device.type, device.index)
     buf = _WS.get(key)
     if buf is None or buf.numel() < numel:
-        buf = torch.empty(max(numel, 1 << 20), dtype=torch.float32, device=device)
+        if stream is not None:
+            with torch.cuda.stream(stream):
+                buf = torch.empty(max(numel, 1 << 20), dtype=torch.float32, device=device)
+        else:
+            buf = torch.empty(max(numel, 1 << 20), dtype=torch.float32, device=device)
         _WS[key] = buf
     return buf
 

@@ -242,12 +242,14 @@ class LocalOverlap:
             from ..ops import hip
 
             cur = self.parent if self.parent is not None else torch.cuda.current_stream(self.stream.device)
-            self.stream.wait_stream(cur)
+            hip.stream_wait(self.stream, cur)
             side = hip.side_stream(self.stream.device)
             if side is not None and self.parent is None:  # (a capture runs no wgrad side stream)
-                self.stream.wait_stream(side)
+                hip.stream_wait(self.stream, side)
             with torch.cuda.stream(self.stream):
                 self.opt.step_range(b)
 
     def join(self) -> None:
-        torch.cuda.current_stream(self.stream.device).wait_stream(self.stream)
+        from ..ops import hip
+
+        hip.stream_wait(torch.cuda.current_stream(self.stream.device), self.stream)
