@@ -71,6 +71,9 @@ __device__ __forceinline__ void st16(bf16_t* dst, const u32x4& v, int nt) {
 namespace g2 {
 
 constexpr int BM = 256;
+#ifndef G2_AUX_NO_PREFETCH
+#define G2_AUX_NO_PREFETCH 0
+#endif
 
 __device__ __forceinline__ int f1(int row) { return (row >> 1) & 7; }
 
@@ -251,6 +254,11 @@ __device__ __forceinline__ void epilogue_bf16(f32x4 (&acc)[MB][BN / 64], const G
   float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float qs = 0.f, qm = 0.f;
   if constexpr (Q8) qs = fmt_scale(p.q8_fmt, *p.q8_amax);
+  // aux (residual / GELU' operand) chunks of the NEXT pass are loaded right after this pass's staging writes, i.e.
+  // BEFORE this pass's stores: the vector-memory counter retires loads and stores in issue order, so a load issued
+  // after the previous pass's stores made its consumer wait for all of them (s_waitcnt vmcnt(0) per pass)
+  constexpr bool kAuxPf = epi_aux(EPI) && !G2_AUX_NO_PREFETCH;
+  u32x4 xnext[ITER];
 #pragma unroll
   for (int h = 0; h < MB / PB; ++h) {
 #pragma unroll
@@ -265,6 +273,13 @@ __device__ __forceinline__ void epilogue_bf16(f32x4 (&acc)[MB][BN / 64], const G
       }
     __builtin_amdgcn_wave_barrier();
     u32x4 sv[ITER], xv[ITER];
+    if constexpr (kAuxPf) {
+      if (h > 0) {
+#pragma unroll
+        for (int it = 0; it < ITER; ++it) xv[it] = xnext[it];
+      }
+      if (h + 1 < MB / PB) epi_aux_regs<EPI, BN, PB>(xnext, p, lane, mw, nw, h + 1);
+    }
 #pragma unroll
     for (int it = 0; it < ITER; ++it) {
       const int idx = lane + 64 * it;
@@ -280,7 +295,7 @@ __device__ __forceinline__ void epilogue_bf16(f32x4 (&acc)[MB][BN / 64], const G
     if (PRE && h == 0) {
 #pragma unroll
       for (int it = 0; it < ITER; ++it) xv[it] = xv_pre[it];
-    } else {
+    } else if (!kAuxPf || h == 0) {
       epi_aux_regs<EPI, BN, PB>(xv, p, lane, mw, nw, h);
     }
 #pragma unroll
