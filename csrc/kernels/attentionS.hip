@@ -204,17 +204,16 @@ __global__ __launch_bounds__(256, 2) void attnS_fwd_kernel(const bf16_t* __restr
 }
 
 // ------------------------------------------------------------------------------------------------
-// delta[bh*S + s] = Σ_d dO[b*S+s][h*64+d] · O[b*S+s][h*64+d]; 8 threads per (token, head)
+// delta[bh*S + s] = Σ_d dO[b*S+s][h*64+d] · O[b*S+s][h*64+d]. One workgroup per (32 tokens, b·head): 8 threads
+// per token (16 B each of O and dO, one 128-B line per token), so each wave stores 8 consecutive deltas and the
+// workgroup one contiguous 128-B run (the old token-major mapping scattered one 4-B store per head, S·4 B apart).
 __global__ __launch_bounds__(256) void attnS_delta_kernel(const bf16_t* __restrict__ o, const bf16_t* __restrict__ dout,
-                                                          float* __restrict__ delta, int T, int S, int heads) {
-  const int64_t g = (int64_t)blockIdx.x * 256 + threadIdx.x;
-  const int64_t item = g >> 3;
-  const int c = (int)(g & 7);
-  const bool ok = item < (int64_t)T * heads;
-  const int64_t it = ok ? item : 0;
-  const int64_t t = it / heads;
-  const int hh = (int)(it % heads);
-  const int64_t off = t * heads * D + hh * D + c * 8;
+                                                          float* __restrict__ delta, int S, int heads) {
+  const int bh = blockIdx.y;
+  const int b = bh / heads, hh = bh - b * heads;
+  const int s = blockIdx.x * 32 + (threadIdx.x >> 3);  // S % 128 == 0 (attnS_supported)
+  const int c = threadIdx.x & 7;
+  const int64_t off = (((int64_t)b * S + s) * heads + hh) * D + c * 8;
   const u32x4 ov = *reinterpret_cast<const u32x4*>(o + off);
   const u32x4 dv = *reinterpret_cast<const u32x4*>(dout + off);
   float acc = 0.f;
@@ -223,10 +222,7 @@ __global__ __launch_bounds__(256) void attnS_delta_kernel(const bf16_t* __restri
   acc += __shfl_xor(acc, 1, 64);
   acc += __shfl_xor(acc, 2, 64);
   acc += __shfl_xor(acc, 4, 64);
-  if (ok && c == 0) {
-    const int64_t bb = t / S, s = t % S;
-    delta[(bb * heads + hh) * S + s] = acc;
-  }
+  if (c == 0) delta[(int64_t)bh * S + s] = acc;
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -520,9 +516,7 @@ void launch_attnS_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, con
   DropoutParams dp = make_dropout(p, seed);
   const float sl2 = attn::kLog2e / sqrtf((float)attn::D);
   const float scale = 1.0f / sqrtf((float)attn::D);
-  const int64_t threads = (int64_t)B * S * heads * 8;
-  hipLaunchKernelGGL(aS::attnS_delta_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, o, dout,
-                     delta_ws, B * S, S, heads);
+  hipLaunchKernelGGL(aS::attnS_delta_kernel, dim3(S / 32, B * heads), dim3(256), 0, st, o, dout, delta_ws, S, heads);
   HSD_CHECK_LAUNCH();
   if (dp.enabled) {
     hipLaunchKernelGGL(aS::attnS_bwd_kv_kernel<true>, dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, dout,
