@@ -660,6 +660,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("colsum", &colsum);
   m.def("dropout", &dropout);
   m.def("set_dropout_device_seed", &set_dropout_device_seed);
+  m.def("cu_hog", [](int64_t blocks, double usec) { hsd::launch_cu_hog((int)blocks, usec, cur_stream()); },
+        "contention emulation: hold `blocks` whole CUs for `usec` us on the current stream");
+  m.def("refresh_env", &hsd::refresh_env_knobs, "re-read the HSD_* launch knobs (cached per generation)");
   m.def("fp8_quant", &fp8_quant, py::arg("x"), py::arg("amax"), py::arg("q"), py::arg("sinv"), py::arg("fmt"),
         py::arg("compute_amax"), py::arg("amax_track") = py::none());
   m.def("fp8_quant_many", &fp8_quant_many);

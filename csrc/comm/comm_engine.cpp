@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
 
+#include "../kernels/launchers.h"
+
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -177,7 +179,7 @@ class CommEngine {
     }
   }
 
-  // fp16 wire pre-scale for the coming step(s): 1 / (world x gradient-accumulation micro-steps)
+  // fp16 wire pre-scale for the coming step(s): 1 / gradient-accumulation micro-steps
   void set_prescale(double s) { prescale_ = s > 0.0 ? s : 1.0; }
 
   void begin_step() {
@@ -319,20 +321,16 @@ class CommEngine {
     if (timing_) HIP_OK(hipEventRecord(b.t_start, stream_));
     if (n > 0 && comp_ != 0 && flat_.scalar_type() == at::kFloat) {
       // cast -> all-reduce in 16 bits -> cast back, all ordered on the comm stream
-      c10::hip::HIPStreamGuard guard(c10::hip::getStreamFromExternal(stream_, device_));
-      at::Tensor src = flat_.narrow(0, b.start, n);
-      at::Tensor wire = shadow_.narrow(0, b.start, n);
-      if (comp_ == 2 && prescale_ != 1.0) {
-        // fp16 on the wire: pre-scale by 1/(world x micro-steps) so the rank SUM of k accumulated micro-steps stays
-        // inside fp16's range (65504); scaled back in fp32 after the all-reduce (exact for powers of two)
-        wire.copy_(src.mul(prescale_));
-      } else {
-        wire.copy_(src);
-      }
-      NCCL_OK(ncclAllReduce(wire.data_ptr(), wire.data_ptr(), (size_t)n, to_nccl(wire.scalar_type()), ncclSum, comm_,
-                            stream_));
-      src.copy_(wire);
-      if (comp_ == 2 && prescale_ != 1.0) src.mul_(1.0 / prescale_);
+      // one fused HIP pass each way (elementwise.hip launch_wire_cast). fp16 on the wire: pre-scaled by 1/micro-steps
+      // so the rank SUM of k accumulated micro-steps stays inside fp16's range (65504), scaled back in fp32 after
+      // the all-reduce (exact for powers of two); the 1/world average stays in the optimizer's fp32 grad_scale
+      float* src = flat_.data_ptr<float>() + b.start;
+      void* wire = static_cast<char*>(shadow_.data_ptr()) + b.start * shadow_.element_size();
+      const bool half = comp_ == 2;
+      const float pre = half ? (float)prescale_ : 1.0f;
+      launch_wire_cast(src, wire, n, true, half, pre, stream_);
+      NCCL_OK(ncclAllReduce(wire, wire, (size_t)n, to_nccl(shadow_.scalar_type()), ncclSum, comm_, stream_));
+      launch_wire_cast(wire, src, n, false, half, 1.0f / pre, stream_);
     } else if (n > 0) {
       char* base = static_cast<char*>(flat_.data_ptr()) + b.start * flat_.element_size();
       NCCL_OK(ncclAllReduce(base, base, (size_t)n, to_nccl(flat_.scalar_type()), ncclSum, comm_, stream_));

@@ -81,8 +81,7 @@ void launch_adam(float* p, float* m, float* v, const void* g, bool grad_bf16, bf
                  const uint8_t* decay, int64_t n, float step, float eps, float b1, float b2, float gscale,
                  float lr_wd, const float* coef, hipStream_t stream) {
   int64_t n4 = n / 4;  // n is a multiple of 1024 (FlatParamStore)
-  const char* ue = getenv("HSD_ADAM_UNROLL");  // A/B: chunks per thread per trip (1, 2 or 4)
-  const int U = ue ? atoi(ue) : 2;
+  const int U = HSD_KNOB("HSD_ADAM_UNROLL", 2);  // A/B: chunks per thread per trip (1, 2 or 4)
   int threads = 256;
   int64_t blocks = (n4 + threads - 1) / threads;
   if (blocks > 256 * 8) blocks = 256 * 8;  // grid-stride: 8 blocks (32 waves) per CU over 256 CUs

@@ -386,11 +386,11 @@ void launch_attnS_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, con
 
 // S in 256..1024 (multiple of 128) runs the streaming kernels of attentionS.hip; its backward takes
 // an fp32 [B*heads*S] scratch (no zeroing) where the generic kernel takes a zeroed [B*S, H] dq accumulator.
-bool attn_streaming(int S) { return attnS_supported(S, kD) && !getenv("HSD_ATTN_GENERIC"); }
+bool attn_streaming(int S) { return attnS_supported(S, kD) && !HSD_KNOB("HSD_ATTN_GENERIC", 0); }
 
 void launch_attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse2, int B, int S, int heads,
                      double p, uint64_t seed, hipStream_t st) {
-  if (attn128_supported(S, kD) && !getenv("HSD_ATTN_GENERIC")) {
+  if (attn128_supported(S, kD) && !HSD_KNOB("HSD_ATTN_GENERIC", 0)) {
     launch_attn128_fwd(qkv, mask, out, lse2, B, heads, p, seed, st);
     return;
   }
@@ -408,7 +408,7 @@ void launch_attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* l
 void launch_attn_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
                      bf16_t* dqkv, float* dq_acc, float* dbias, int B, int S, int heads, double p, uint64_t seed,
                      hipStream_t st) {
-  if (attn128_supported(S, kD) && !getenv("HSD_ATTN_GENERIC")) {
+  if (attn128_supported(S, kD) && !HSD_KNOB("HSD_ATTN_GENERIC", 0)) {
     launch_attn128_bwd(qkv, mask, o, dout, lse2, dqkv, dbias, B, heads, p, seed, st);
     return;
   }

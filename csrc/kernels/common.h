@@ -11,8 +11,26 @@
 #include <hip/hip_runtime.h>
 #include <hip/hip_bf16.h>
 #include <stdint.h>
+#include <stdlib.h>
 
 namespace hsd {
+
+// ---- host-side A/B knobs (HSD_* environment variables) --------------------------------
+// Read once per knob generation, not per launch: launch paths call HSD_KNOB(name, default) (a cached int; the
+// default when unset). refresh_env_knobs() (bound as _C.refresh_env, called by tests that flip a knob in-process)
+// bumps the generation so every knob is re-read at its next use.
+inline int g_env_gen = 0;
+#define HSD_KNOB(NAME, DFLT)                                 \
+  ([]() -> int {                                             \
+    static int v_ = 0, gen_ = -1;                            \
+    if (gen_ != ::hsd::g_env_gen) {                          \
+      const char* e_ = getenv(NAME);                         \
+      v_ = e_ ? atoi(e_) : (DFLT);                           \
+      gen_ = ::hsd::g_env_gen;                               \
+    }                                                        \
+    return v_;                                               \
+  }())
+constexpr int kKnobUnset = -0x7fffffff;  // HSD_KNOB default meaning "not set"
 
 typedef uint16_t bf16_t;
 typedef __attribute__((ext_vector_type(4))) float f32x4;

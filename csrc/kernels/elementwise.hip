@@ -233,6 +233,88 @@ void launch_transpose_many(const int64_t* desc, int n, int total_tiles, hipStrea
   HSD_CHECK_LAUNCH();
 }
 
+// Gradient wire casts of the RCCL engine's 16-bit compression (comm_engine.cpp; Horovod's hvd.Compression.fp16 /
+// bf16): to16: w = 16-bit(g · scale); from16: g = float(w) · scale. One pass each, 16-B loads and
+// 8-B stores, where the ATen form was a scaled fp32 temporary + a cast copy (and back: a copy + an in-place mul).
+// fp16: round-to-nearest-even via the hardware cvt; bf16: the shared RNE pack.
+template <bool kHalf>
+__global__ __launch_bounds__(256) void wire_to16_kernel(const float* __restrict__ g, uint16_t* __restrict__ w,
+                                                        int64_t n4, float scale) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const f32x4 v = reinterpret_cast<const f32x4*>(g)[i] * scale;
+    u32x2 o;
+    if constexpr (kHalf) {
+      const _Float16 a = (_Float16)v[0], b = (_Float16)v[1], c = (_Float16)v[2], d = (_Float16)v[3];
+      o.x = (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+      o.y = (uint32_t)__builtin_bit_cast(uint16_t, c) | ((uint32_t)__builtin_bit_cast(uint16_t, d) << 16);
+    } else {
+      o.x = pack_bf2(v[0], v[1]);
+      o.y = pack_bf2(v[2], v[3]);
+    }
+    reinterpret_cast<u32x2*>(w)[i] = o;
+  }
+}
+
+template <bool kHalf>
+__global__ __launch_bounds__(256) void wire_from16_kernel(const uint16_t* __restrict__ w, float* __restrict__ g,
+                                                          int64_t n4, float scale) {
+  const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    const u32x2 v = reinterpret_cast<const u32x2*>(w)[i];
+    f32x4 o;
+    if constexpr (kHalf) {
+      o[0] = (float)__builtin_bit_cast(_Float16, (uint16_t)(v.x & 0xFFFF));
+      o[1] = (float)__builtin_bit_cast(_Float16, (uint16_t)(v.x >> 16));
+      o[2] = (float)__builtin_bit_cast(_Float16, (uint16_t)(v.y & 0xFFFF));
+      o[3] = (float)__builtin_bit_cast(_Float16, (uint16_t)(v.y >> 16));
+    } else {
+      o = f32x4{lo_bf(v.x), hi_bf(v.x), lo_bf(v.y), hi_bf(v.y)};
+    }
+    reinterpret_cast<f32x4*>(g)[i] = o * scale;
+  }
+}
+
+static int wire_blocks(int64_t n4) { return (int)std::min<int64_t>(2048, std::max<int64_t>(1, (n4 + 255) / 256)); }
+
+void launch_wire_cast(const void* src, void* dst, int64_t n, bool to16, bool half, float scale, hipStream_t st) {
+  if (n <= 0) return;
+  if (n % 4 != 0) {
+    fprintf(stderr, "launch_wire_cast: n %% 4 != 0 (%lld)\n", (long long)n);
+    abort();
+  }
+  const int64_t n4 = n / 4;
+  if (to16) {
+    if (half) hipLaunchKernelGGL(wire_to16_kernel<true>, dim3(wire_blocks(n4)), dim3(256), 0, st, (const float*)src, (uint16_t*)dst, n4, scale);
+    else hipLaunchKernelGGL(wire_to16_kernel<false>, dim3(wire_blocks(n4)), dim3(256), 0, st, (const float*)src, (uint16_t*)dst, n4, scale);
+  } else {
+    if (half) hipLaunchKernelGGL(wire_from16_kernel<true>, dim3(wire_blocks(n4)), dim3(256), 0, st, (const uint16_t*)src, (float*)dst, n4, scale);
+    else hipLaunchKernelGGL(wire_from16_kernel<false>, dim3(wire_blocks(n4)), dim3(256), 0, st, (const uint16_t*)src, (float*)dst, n4, scale);
+  }
+  HSD_CHECK_LAUNCH();
+}
+
 void set_dropout_dev_seed(const uint32_t* p) { g_dropout_dev_seed = p; }
+
+void refresh_env_knobs() { ++g_env_gen; }
+
+// Contention emulation (tools/contention_ab.py): `blocks` workgroups that each hold a whole CU (all 160 KiB of LDS,
+// so no other 160-KiB workgroup -- the persistent GEMMs -- can share it) for `usec` microseconds, then exit. Stands
+// in for the RCCL all-reduce kernels (one workgroup per channel) that a data-parallel step runs beside its backward
+// GEMMs. Waits on the 100 MHz constant clock (s_memrealtime) with s_sleep between polls; every wave exits.
+__global__ __launch_bounds__(64) void cu_hog_kernel(uint64_t ticks, float* sink) {
+  __shared__ float hog_lds[160 * 1024 / 4];
+  hog_lds[threadIdx.x] = (float)threadIdx.x;
+  const uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(8);
+  __syncthreads();
+  if (sink != nullptr) sink[threadIdx.x] = hog_lds[(threadIdx.x * 37) & 63];
+}
+
+void launch_cu_hog(int blocks, double usec, hipStream_t st) {
+  if (blocks <= 0 || usec <= 0.0) return;
+  hipLaunchKernelGGL(cu_hog_kernel, dim3(blocks), dim3(64), 0, st, (uint64_t)(usec * 100.0), (float*)nullptr);
+  HSD_CHECK_LAUNCH();
+}
 
 }  // namespace hsd

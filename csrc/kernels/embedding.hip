@@ -387,7 +387,7 @@ void launch_embed_bwd(const bf16_t* dout, const int64_t* ids, const int64_t* pos
                       const float* mean, const float* rstd, float* gword, float* gpos, float* gtype, float* ggamma,
                       float* gbeta, int B, int S, int H, int pos_is_arange, double p, uint64_t seed, hipStream_t st) {
   DropoutParams dp = make_dropout(p, seed);
-  if (H % 8 == 0 && H <= 1024 && !getenv("HSD_EMBED_BWD_SCALAR")) {
+  if (H % 8 == 0 && H <= 1024 && !HSD_KNOB("HSD_EMBED_BWD_SCALAR", 0)) {
     int chunks = max(1, min(B, (2048 + S - 1) / S));
     int bpc = (B + chunks - 1) / chunks;
     chunks = (B + bpc - 1) / bpc;

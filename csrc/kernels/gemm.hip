@@ -465,7 +465,7 @@ void launch_gemm(int la, int lb, int epi, const bf16_t* A, int64_t lda, const bf
   p.A = A; p.lda = lda; p.B = B; p.ldb = ldb; p.M = M; p.N = N; p.K = K; p.C = C; p.ldc = ldc;
   p.bias = bias; p.aux = aux; p.ldaux = ldaux; p.C2 = C2;
   p.dp = make_dropout(p_drop, seed);
-  const bool dma = (K % 64 == 0) && (M >= 128) && (N >= 128) && !getenv("HSD_GEMM_V1");
+  const bool dma = (K % 64 == 0) && (M >= 128) && (N >= 128) && !HSD_KNOB("HSD_GEMM_V1", 0);
   if (dma) {
     if (epi == EPI_F32_ATOMIC) {
       if (la == 1 && lb == 1) { gemm_dma_launch<1, 1, EPI_F32_ATOMIC, 256, 128, 4, 2>(p, splits, st); return; }

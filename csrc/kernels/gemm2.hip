@@ -86,8 +86,12 @@ __device__ __forceinline__ const bf16_t* asm_base(const bf16_t* X, int64_t ld, i
   else return X + (int64_t)r0 * ld + k0;
 }
 
-__device__ __forceinline__ void dma_lds_asm(const bf16_t* sbase, uint32_t voff, uint32_t lds_addr) {
+__device__ __forceinline__ void dma_lds_asm(const bf16_t* sbase_in, uint32_t voff, uint32_t lds_addr) {
   const uint32_t lds = (uint32_t)__builtin_amdgcn_readfirstlane((int)lds_addr);
+  // the base is wave-uniform by construction; say so (folded away where the compiler already proves it)
+  const uint64_t ba = (uint64_t)sbase_in;
+  const bf16_t* sbase = (const bf16_t*)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(ba >> 32)) << 32) |
+                                        (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)ba));
   unsigned keep;
   asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %3\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, %2\n\ts_mov_b32 m0, %0"
                : "=&s"(keep)
@@ -640,13 +644,34 @@ __global__ __launch_bounds__(512, 1) void gemm2pk_kernel(G2Params p) {
   };
 
   const int arow = wm * 128, bcol = wn * WN;
+  // tile walk: static (L = blockIdx.x, +gridDim.x, ...) or claimed from the launch's tile queue (p.tq; gemm_common.h
+  // tq_*). The claimed index reaches every wave through one LDS word in stage 1 at byte 2048 (A slot 2 of wave 0):
+  // no DMA is in flight when it is written (before the first prologue / after the last K-tile's vmcnt<0>), and the
+  // next DMA into those bytes is issued in P1 of the next main loop, after the seam barrier every wave passes after
+  // reading it.
+  int* const tq = p.tq;
+  const int xg = tq != nullptr ? tq_xcc() : 0;
+  uint32_t dead = 0;  // wave 0 lane 0: XCD groups seen exhausted
+  int* const bcast = reinterpret_cast<int*>(smem + STAGE + 1024);
   int L = blockIdx.x;
+  if (tq != nullptr) {
+    if (wave == 0 && lane == 0) *bcast = tq_claim(tq, xg, dead, ntiles);
+    __syncthreads();
+    L = __builtin_amdgcn_readfirstlane(*bcast);  // wave-uniform: tile addresses stay scalar
+    if (L >= ntiles) {
+      if (wave == 0 && lane == 0) tq_exit(tq);
+      return;
+    }
+  }
   set_tile(L);
   prologue();
   vmcnt<0>();
   G2_BARRIER();
   f32x4 acc[8][NREP];
-  for (;;) {
+  for (int it = 0;; ++it) {
+    // claim the NEXT tile now (wave 0 lane 0, own XCD group): the atomic returns under this tile's main loop
+    int pre = 0;
+    if (tq != nullptr && wave == 0 && lane == 0 && !(dead & (1u << xg))) pre = tq_fetch(tq, xg);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -654,12 +679,25 @@ __global__ __launch_bounds__(512, 1) void gemm2pk_kernel(G2Params p) {
     mainloop_staggered<0, 0, BN, 4, G, D0, false>(acc, smem, dma_slot, nt, 0, wm, arow, bcol, lane);
     uint64_t ts0 = 0, ts1 = 0;
     if (p.diag) ts0 = __builtin_amdgcn_s_memtime();
+    if (tq != nullptr) {
+      if (wave == 0 && lane == 0) {
+        int Ln = dead & (1u << xg) ? ntiles : xg + 8 * pre;
+        if (Ln >= ntiles) {
+          dead |= 1u << xg;
+          Ln = tq_claim(tq, xg, dead, ntiles);
+        }
+        *bcast = Ln;
+      }
+      __syncthreads();  // nothing in flight here: the main loop ended with vmcnt<0>
+      L = __builtin_amdgcn_readfirstlane(*bcast);  // wave-uniform: tile addresses stay scalar
+    } else {
+      L += gridDim.x;
+    }
     const int mw = m0 + arow, nw = n0 + bcol;
     f32x4 bv[NREP];
     u32x4 xv0[ITER];
     epi_bias_regs<EPI, BN>(bv, p, lane, nw);
     epi_aux_regs<EPI, BN, PB>(xv0, p, lane, mw, nw, 0);
-    L += gridDim.x;
     const bool more = L < ntiles;
     if (more) {
       set_tile(L);
@@ -670,13 +708,13 @@ __global__ __launch_bounds__(512, 1) void gemm2pk_kernel(G2Params p) {
     // diagnostic stamps (wave 0): main loop end, epilogue end, seam end, real time -- tools/seam_probe.py
     auto stamp = [&](uint64_t ts2) {
       if (p.diag && wave == 0 && lane == 0) {
-        const int it = (L - (int)gridDim.x - (int)blockIdx.x) / (int)gridDim.x;
         unsigned long long* d = p.diag + ((int64_t)blockIdx.x * 64 + min(it, 63)) * 4;
         d[0] = ts0; d[1] = ts1; d[2] = ts2; d[3] = __builtin_amdgcn_s_memrealtime();
       }
     };
     if (!more) {
       stamp(ts1);
+      if (tq != nullptr && wave == 0 && lane == 0) tq_exit(tq);
       break;
     }
     // retire the next tile's K-tile 0 (the oldest G DMAs of this wave) without draining the epilogue's stores:
@@ -843,13 +881,29 @@ __global__ __launch_bounds__(512, 1) void gemm8pk_kernel(G2Params p, const float
   };
 
   const int arow = wm * 128, bcol = wn * WN;
+  // tile walk: static or claimed from p.tq, exactly as gemm2pk_kernel (broadcast word in stage 1 at byte 2048)
+  int* const tq = p.tq;
+  const int xg = tq != nullptr ? tq_xcc() : 0;
+  uint32_t dead = 0;
+  int* const bcast = reinterpret_cast<int*>(smem + STAGE + 1024);
   int L = blockIdx.x;
+  if (tq != nullptr) {
+    if (wave == 0 && lane == 0) *bcast = tq_claim(tq, xg, dead, ntiles);
+    __syncthreads();
+    L = __builtin_amdgcn_readfirstlane(*bcast);  // wave-uniform: tile addresses stay scalar
+    if (L >= ntiles) {
+      if (wave == 0 && lane == 0) tq_exit(tq);
+      return;
+    }
+  }
   set_tile(L);
   prologue();
   vmcnt<0>();
   G2_BARRIER();
   f32x4 acc[8][NREP];
   for (;;) {
+    int pre = 0;
+    if (tq != nullptr && wave == 0 && lane == 0 && !(dead & (1u << xg))) pre = tq_fetch(tq, xg);
 #pragma unroll
     for (int i = 0; i < 8; ++i)
 #pragma unroll
@@ -859,19 +913,35 @@ __global__ __launch_bounds__(512, 1) void gemm8pk_kernel(G2Params p, const float
     for (int i = 0; i < 8; ++i)
 #pragma unroll
       for (int j = 0; j < NREP; ++j) acc[i][j] *= dq;
+    if (tq != nullptr) {
+      if (wave == 0 && lane == 0) {
+        int Ln = dead & (1u << xg) ? ntiles : xg + 8 * pre;
+        if (Ln >= ntiles) {
+          dead |= 1u << xg;
+          Ln = tq_claim(tq, xg, dead, ntiles);
+        }
+        *bcast = Ln;
+      }
+      __syncthreads();
+      L = __builtin_amdgcn_readfirstlane(*bcast);  // wave-uniform: tile addresses stay scalar
+    } else {
+      L += gridDim.x;
+    }
     const int mw = m0 + arow, nw = n0 + bcol;
     f32x4 bv[NREP];
     u32x4 xv0[ITER];
     epi_bias_regs<EPI, BN>(bv, p, lane, nw);
     epi_aux_regs<EPI, BN, PB>(xv0, p, lane, mw, nw, 0);
-    L += gridDim.x;
     const bool more = L < ntiles;
     if (more) {
       set_tile(L);
       prologue();
     }
     epilogue_bf16<EPI, BN, 8, PB, true, Q8>(acc, p, smem + 2 * STAGE, wave, lane, mw, nw, bv, xv0);
-    if (!more) break;
+    if (!more) {
+      if (tq != nullptr && wave == 0 && lane == 0) tq_exit(tq);
+      break;
+    }
     if (mw + 128 <= p.M) {
       if (nt > 1) vmcnt<D0 + NST>();
       else vmcnt<NST>();
@@ -1102,10 +1172,9 @@ __global__ __launch_bounds__(256, NSTG <= 2 ? 2 : 1) void gemm2s_kernel(G2Params
 // on the four bert-base weights (tools/tt_probe.py, profiles/tt_probe_r3_sync_splits.json). HSD_G2_SYNC overrides
 // for A/B runs; HSD_G2_NT=0 makes the bf16 epilogue stores plain (default: non-temporal, st16nt).
 static int g2_sync_mode(int la, int K) {
-  const char* e = getenv("HSD_G2_SYNC");
-  if (e) return atoi(e);
+  const int e = HSD_KNOB("HSD_G2_SYNC", kKnobUnset);
   (void)la;
-  return 4;
+  return e != kKnobUnset ? e : 4;
 }
 
 template <int LA, int LB, int EPI, int BN>
@@ -1145,9 +1214,33 @@ static int g2_num_cus() {
   return n;
 }
 
+// Tile-queue ring of the persistent kernels (gemm_common.h tq_*): one 9-counter slot per launch, 256 slots per device,
+// zeroed once; every launch leaves its slot zeroed (the last workgroup resets it). Launches on one stream reuse a slot
+// only 256 launches later; persistent GEMMs run on the compute stream only (the weight-gradient side stream runs the
+// TT kernels), so no two co-running launches share a slot. HSD_G2_DYN=0: static tile walk (A/B).
+static int* g2_tq_slot(hipStream_t st) {
+  if (!HSD_KNOB("HSD_G2_DYN", 1)) return nullptr;
+  constexpr int kSlots = 256;
+  static int* base[64] = {};
+  static unsigned next = 0;
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= 64) abort();
+  if (base[dev] == nullptr) {
+    hipStreamCaptureStatus cs = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(st, &cs) != hipSuccess || cs != hipStreamCaptureStatusNone) {
+      fprintf(stderr, "gemm2: first persistent GEMM launch inside a graph capture (tile queue not allocated)\n");
+      abort();
+    }
+    int* b = nullptr;
+    if (hipMalloc(&b, sizeof(int) * kTqInts * kSlots) != hipSuccess) abort();
+    if (hipMemset(b, 0, sizeof(int) * kTqInts * kSlots) != hipSuccess) abort();
+    base[dev] = b;
+  }
+  return base[dev] + (size_t)(next++ % kSlots) * kTqInts;
+}
+
 static bool g2_persist(int tiles) {
-  const char* e = getenv("HSD_G2_PERSIST");  // read per launch: tests flip it in-process
-  if (!(e ? atoi(e) : 1)) return false;
+  if (!HSD_KNOB("HSD_G2_PERSIST", 1)) return false;
   return tiles > (g2_num_cus() & ~7);
 }
 
@@ -1159,8 +1252,9 @@ static void g2pk_launch(const G2Params& p0, hipStream_t st) {
   p.ntiles = tiles_m * p.tiles_n;
   p.kps = p.K;
   if (p.K % g2::BK) abort();
-  const char* gc = getenv("HSD_G2_GRID");  // diagnostic (tools/epi_probe2.py): cap the persistent grid (multiple of 8)
-  const int grid = std::min(p.ntiles, gc ? atoi(gc) : g2_num_cus() & ~7);
+  // HSD_G2_GRID, diagnostic (tools/epi_probe2.py): cap the persistent grid (multiple of 8)
+  const int grid = std::min(p.ntiles, HSD_KNOB("HSD_G2_GRID", g2_num_cus() & ~7));
+  p.tq = g2_tq_slot(st);
   hipLaunchKernelGGL((g2::gemm2pk_kernel<EPI, BN>), dim3(grid), dim3(512), 0, st, p);
   HSD_CHECK_LAUNCH();
 }
@@ -1173,6 +1267,7 @@ static void g8pk_launch(const G2Params& p0, const float* sa, const float* sb, hi
   p.ntiles = tiles_m * p.tiles_n;
   p.kps = p.K;
   const int grid = p.ntiles > (g2_num_cus() & ~7) ? (g2_num_cus() & ~7) : p.ntiles;
+  p.tq = g2_tq_slot(st);
   if (p.q8 != nullptr) {
     // fp8 output copies: the FFN epilogues whose outputs feed the next fp8 GEMM (GELU -> FFN2 forward, GELU'
     // product -> FFN1 dgrad)
@@ -1190,11 +1285,7 @@ static void g8pk_launch(const G2Params& p0, const float* sa, const float* sb, hi
 // even leading dimensions; fa: A format (0 e4m3, 1 e5m2), B e4m3.
 void launch_gemm8pk(int epi, int bn, const G2Params& p0, int fa, const float* sa, const float* sb, hipStream_t st) {
   G2Params p = p0;
-  p.nt_store = 1;
-  {
-    const char* e = getenv("HSD_G2_NT");
-    if (e) p.nt_store = atoi(e);
-  }
+  p.nt_store = HSD_KNOB("HSD_G2_NT", 1);
   p.K /= 2;
   p.lda /= 2;
   p.ldb /= 2;
@@ -1245,9 +1336,9 @@ constexpr int SBN_HOST = 128;
 bool gemm2s_use(int M, int N, int K);
 
 int gemm2_nt_splits(int M, int N, int K) {
-  const char* e = getenv("HSD_G2_SPLITK");
+  const int e = HSD_KNOB("HSD_G2_SPLITK", kKnobUnset);
   const int kt = K / 64;
-  if (e) return std::max(1, std::min(atoi(e), kt));
+  if (e != kKnobUnset) return std::max(1, std::min(e, kt));
   if (gemm2s_use(M, N, K)) {
     // 128 x 128 tiles: split only grids that leave more than half of the CUs idle (serving batches: B = 1 has 6-24
     // tiles, each a latency-bound chain of 12-48 K-steps), >= 2 K-tiles per split
@@ -1268,8 +1359,8 @@ int gemm2_nt_splits(int M, int N, int K) {
 // =1 forces it for every shape it supports.
 bool gemm2s_use(int M, int N, int K) {
   if (N % SBN_HOST != 0 || K % 64 != 0) return false;
-  const char* e = getenv("HSD_G2_SMALL");
-  if (e) return atoi(e) != 0;
+  const int e = HSD_KNOB("HSD_G2_SMALL", kKnobUnset);
+  if (e != kKnobUnset) return e != 0;
   const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
   return tiles * 2 <= 256;
 }
@@ -1296,12 +1387,10 @@ static double wgrad_cost(int M, int N, int K, int s, bool small) {
 }
 
 static WgradPlan wgrad_plan(int M, int N, int K) {
-  const char* e = getenv("HSD_G2_SMALL_TT");
-  const int force = e ? atoi(e) : -1;
+  const int force = HSD_KNOB("HSD_G2_SMALL_TT", -1);
   const bool can_small = N % SBN_HOST == 0 && M % 8 == 0 && K % 64 == 0 && force != 0;
   const bool can_big = N % 256 == 0 && force != 1;
-  const char* m = getenv("HSD_WGRAD_MIN_KT");
-  const int min_kt = m ? std::max(1, atoi(m)) : 2;
+  const int min_kt = std::max(1, HSD_KNOB("HSD_WGRAD_MIN_KT", 2));
   const int kt_all = K / 64;
   WgradPlan best{can_small && !can_big, 1};
   double best_cost = 1e30;
@@ -1322,8 +1411,8 @@ bool gemm2st_use(int M, int N, int K) { return wgrad_plan(M, N, K).small; }
 // bert-base GEMMs run 19-49 us at 2 stages vs 26-68 us at 3; at <= 256 tiles 3 stages are equal or up to 5 % faster).
 // HSD_G2S_STAGES (2-4) overrides.
 static int g2s_stages(int grid) {
-  const char* e = getenv("HSD_G2S_STAGES");
-  const int v = e ? atoi(e) : (grid <= 256 ? 3 : 2);
+  const int e = HSD_KNOB("HSD_G2S_STAGES", kKnobUnset);
+  const int v = e != kKnobUnset ? e : (grid <= 256 ? 3 : 2);
   return v < 2 ? 2 : (v > 4 ? 4 : v);
 }
 
@@ -1462,10 +1551,7 @@ void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const b
   G2Params p{};
   p.dbias = dbias;
   p.diag = g_diag;
-  {
-    const char* e = getenv("HSD_G2_NT");
-    p.nt_store = e ? atoi(e) : 1;
-  }
+  p.nt_store = HSD_KNOB("HSD_G2_NT", 1);
   p.A = A; p.lda = lda; p.B = B; p.ldb = ldb; p.M = M; p.N = N; p.K = K; p.C = C; p.ldc = ldc;
   p.bias = bias; p.aux = aux; p.ldaux = ldaux; p.C2 = C2;
   p.dp = make_dropout(p_drop, seed);

@@ -194,8 +194,7 @@ void launch_gemm8(int epi, const uint8_t* A, int64_t lda, int fa, const float* s
   // default: the persistent staggered-schedule kernel (gemm2.hip gemm8pk_kernel); HSD_G8_LEGACY=1: this file's
   // one-barrier-per-K-tile kernel (A/B reference)
   {
-    const char* e = getenv("HSD_G8_LEGACY");
-    if (!(e && atoi(e)) && lda % 2 == 0 && ldb % 2 == 0) {
+    if (!HSD_KNOB("HSD_G8_LEGACY", 0) && lda % 2 == 0 && ldb % 2 == 0) {
       launch_gemm8pk(epi, bn, p, fa, sa, sb, st);
       return;
     }

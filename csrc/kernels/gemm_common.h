@@ -44,7 +44,51 @@ struct G2Params {
   float* q8_sinv;
   float* q8_track;
   int q8_fmt;
+  // persistent kernels: dynamic tile queue (tq_* below; one ring slot per launch), nullptr = static tile walk
+  int* tq;
 };
+
+// ---- dynamic tile queue of the persistent NT GEMMs (gemm2pk / gemm8pk) ----------------------------------------------
+// A persistent workgroup that starts late (its CU held by a co-running RCCL kernel or optimizer slice) must not own a
+// fixed share of the tiles, or the GEMM's tail grows by the delay. Tiles are claimed instead: 8 counters, one per XCD
+// group (tile L belongs to group L & 7, which the XCD-aware remap maps to that group's contiguous tile range, so a
+// workgroup claiming from the counter of the XCD it runs on keeps its L2 locality); a workgroup whose own group is
+// exhausted steals from the others. Counters are relaxed agent-scope atomics (they hand out indices, no data: no
+// acquire/release needed). The last workgroup to leave resets the slot for the next launch that uses it (the exit
+// counter reaches gridDim.x only after every claim of the launch has returned), so no memset node per launch.
+// Layout: 9 counters 128 B apart (8 claim counters + the exit counter).
+constexpr int kTqStride = 32;
+constexpr int kTqInts = 9 * kTqStride;
+
+__device__ __forceinline__ int tq_xcc() {
+  int v;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+  return v & 7;
+}
+
+__device__ __forceinline__ int tq_fetch(int* q, int g) {
+  return __hip_atomic_fetch_add(q + g * kTqStride, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// blocking claim: own group first, then the others not yet seen exhausted (`dead` bit mask); ntiles = none left
+__device__ __forceinline__ int tq_claim(int* q, int g, uint32_t& dead, int ntiles) {
+  for (int k = 0; k < 8; ++k) {
+    const int gg = (g + k) & 7;
+    if (dead & (1u << gg)) continue;
+    const int L = gg + 8 * tq_fetch(q, gg);
+    if (L < ntiles) return L;
+    dead |= 1u << gg;
+  }
+  return ntiles;
+}
+
+__device__ __forceinline__ void tq_exit(int* q) {
+  if (__hip_atomic_fetch_add(q + 8 * kTqStride, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+      (int)gridDim.x - 1) {
+#pragma unroll
+    for (int g = 0; g <= 8; ++g) __hip_atomic_store(q + g * kTqStride, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
 
 // Buffer descriptor over `ptr` (wave-uniform: built from readfirstlane'd halves so hipcc keeps it in SGPRs).
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const void* ptr) {

@@ -51,6 +51,9 @@ void launch_small_wgrad(const bf16_t* dy, int64_t ldy, const bf16_t* x, int64_t 
 // xent.hip: fused softmax cross-entropy (+ gradient, + argmax-correct count); stats = {Σloss, correct}
 void launch_xent(const void* logits, bool bf16, const int64_t* labels, void* dlogits, float* stats,
                  const float* n_valid, int rows, int V, int64_t ld, hipStream_t st);
+// gradient wire casts (comm_engine 16-bit compression): to16: dst16 = src32 * scale; else dst32 = src16 * scale.
+// half: fp16, else bf16. n % 4 == 0, 16-B aligned fp32 side.
+void launch_wire_cast(const void* src, void* dst, int64_t n, bool to16, bool half, float scale, hipStream_t st);
 // desc: int64 [n][5] = {src, dst, rows, cols, first_tile}; rows, cols multiples of 4
 void launch_transpose_many(const int64_t* desc, int n, int total_tiles, hipStream_t st);
 // cls_head.hip: fused sequence-classification head after the dense GEMM (act, dropout, classifier, CE, accuracy)
@@ -87,6 +90,10 @@ void launch_gemm(int la, int lb, int epi, const bf16_t* A, int64_t lda, const bf
 // (epi 6 = atomics, 7 = split-K slabs in `ws` [splits][M][N] + reduce into C)
 // device step seed for dropout (common.h g_dropout_dev_seed); nullptr = off
 void set_dropout_dev_seed(const uint32_t* p);
+// HSD_* knobs are cached per generation (common.h HSD_KNOB); this re-reads them at their next use
+void refresh_env_knobs();
+// contention emulation: `blocks` workgroups holding one whole CU each (160 KiB LDS) for `usec` us
+void launch_cu_hog(int blocks, double usec, hipStream_t st);
 
 // fp8 (gemm8.hip / fp8.hip)
 bool gemm8_supported(int epi, int M, int N, int K);

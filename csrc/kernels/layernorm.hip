@@ -464,8 +464,7 @@ template <int NCH>
 static void ln_fwd_t(const bf16_t* y, const bf16_t* res, const bf16_t* gamma, const bf16_t* beta, bf16_t* z,
                      bf16_t* out, float* mean, float* rstd, int rows, int H, float eps, const DropoutParams& dp,
                      hipStream_t st) {
-  const char* env = getenv("HSD_LN_FWD_RPW");  // A/B: 1 = the one-row kernel; > 1 = rows per wave
-  const int mode = env ? atoi(env) : 0;
+  const int mode = HSD_KNOB("HSD_LN_FWD_RPW", 0);  // A/B: 1 = the one-row kernel; > 1 = rows per wave
   if (mode != 1 && res == nullptr && z == nullptr && !dp.enabled && H % 8 == 0 && H <= 1024) {
     // 2 rows per wave (the next row's loads in flight while one reduces): best at the HBM-bound headline shape
     // (131072 x 768: 75 us vs 81 us at 16 rows per wave); every setting is equal once the tensors fit the MALL
@@ -505,15 +504,12 @@ static void ln_bwd_t(const bf16_t* dout, const bf16_t* z, const float* mean, con
                      bf16_t* dz, bf16_t* dy, const bf16_t* dres_add, float* dgamma, float* dbeta, float* dbias,
                      int rows, int H, const DropoutParams& dp, hipStream_t st, const Q8Out& q8o = Q8Out{},
                      int qfmt = -1) {
-  if (qfmt >= 0 || !getenv("HSD_LN_SPLIT")) {
+  if (qfmt >= 0 || !HSD_KNOB("HSD_LN_SPLIT", 0)) {
     // ~16 rows per wave at the headline's 131072 rows: 2048 waves = 8 per CU, a few thousand column atomics per
     // block; at least 4 rows per wave (a floor of 2 for small row counts, twice the waves and the column atomics,
     // measured 1-2 % slower end to end at bert-large B = 8 and bert-base B = 32: profiles/small_tiles_r2.log;
     // HSD_LN_BWD_MIN_RPW overrides the floor)
-    static const int min_rpw = [] {
-      const char* e = getenv("HSD_LN_BWD_MIN_RPW");
-      return e ? std::max(1, atoi(e)) : 4;
-    }();
+    const int min_rpw = std::max(1, HSD_KNOB("HSD_LN_BWD_MIN_RPW", 4));
     const int rpw = std::max(min_rpw, (rows + 2047) / 2048);
     const int waves = (rows + rpw - 1) / rpw;
     const int blocks = (waves + kLnWaves - 1) / kLnWaves;

@@ -22,6 +22,7 @@ at ``step()`` is the join, the slices no gradient reached, and the batched Wᵀ 
 """
 from __future__ import annotations
 
+import contextlib
 import math
 import os
 from typing import Callable, Iterable, List, Optional, Tuple
@@ -48,6 +49,7 @@ class FusedAdam:
         self.exp_avg_sq = torch.zeros_like(store.master)
         self._decay_mask = store.decay_block_mask(ALIGN) if weight_decay else None
         self.dcoef: Optional[torch.Tensor] = None  # device-side step scalars (HIP-graph replays), see use_device_coef
+        self._capturing = False  # dcoef is handed to the kernel only while a whole-step graph is being captured
 
     # --------------------------------------------------------------------------
     def state_tensors(self) -> List[torch.Tensor]:
@@ -73,12 +75,26 @@ class FusedAdam:
 
     # -------------------------------------------------------------------------- device-side coefficients
     def use_device_coef(self) -> torch.Tensor:
-        """From now on every Adam launch reads (step, eps, grad_scale, lr*wd) from an fp32 [4] device tensor instead
-        of kernel arguments, so a captured HIP graph of the whole training step replays with each step's bias
-        correction and learning rate (train/graph.py). :meth:`prepare_device_step` fills it before a replay."""
+        """The fp32 [4] device tensor (step, eps, grad_scale, lr*wd) that Adam launches CAPTURED into a HIP graph of
+        the whole training step read instead of kernel arguments, so replays run with each step's bias correction
+        and learning rate (train/graph.py). :meth:`prepare_device_step` fills it before a replay. Only launches
+        issued inside :meth:`capturing` read it; eager steps always pass their own scalars."""
         if self.dcoef is None:
             self.dcoef = torch.zeros(4, dtype=torch.float32, device=self.store.master.device)
         return self.dcoef
+
+    @contextlib.contextmanager
+    def capturing(self):
+        """Scope of a whole-step graph capture: Adam launches inside it take their scalars from :attr:`dcoef`."""
+        self.use_device_coef()
+        self._capturing = True
+        try:
+            yield
+        finally:
+            self._capturing = False
+
+    def _kernel_coef(self) -> Optional[torch.Tensor]:
+        return self.dcoef if self._capturing else None
 
     def prepare_device_step(self, grad_scale: float) -> None:
         """Advance the step count and write this step's scalars to :attr:`dcoef` (stream-ordered H2D copy of a
@@ -143,7 +159,7 @@ class FusedAdam:
         out = s.compute[st:e] if s.compute is not s.master else None
         dm = self._decay_mask[st // ALIGN:(e + ALIGN - 1) // ALIGN] if self._decay_mask is not None else None
         hip.adam_step(s.master[st:e], self.exp_avg[st:e], self.exp_avg_sq[st:e], s.grad[st:e], out, dm, step,
-                      eps_eff, self.beta1, self.beta2, gscale, self.lr * self.weight_decay, self.dcoef)
+                      eps_eff, self.beta1, self.beta2, gscale, self.lr * self.weight_decay, self._kernel_coef())
         if self._tsub is not None:
             s.refresh_transposed_subset(self._tsub[b])
         self._done[b] = True
@@ -178,7 +194,7 @@ class FusedAdam:
             hip.join_side_streams()  # weight gradients may still be in flight on the wgrad stream
             hip.adam_step(s.master, self.exp_avg, self.exp_avg_sq, s.grad, s.compute if write_compute else None,
                           self._decay_mask, step, eps_eff, self.beta1, self.beta2, float(grad_scale),
-                          self.lr * self.weight_decay, self.dcoef)
+                          self.lr * self.weight_decay, self._kernel_coef())
             s.refresh_transposed()
             return
         # reference path (CPU): identical math on flat buffers
@@ -227,11 +243,18 @@ class LocalOverlap:
         # writes into main_grad itself run on autograd's thread with no producer stream (its current stream is the
         # device default), so a slice's fork must name the stream the gradients were really queued on.
         self.parent: Optional[torch.cuda.Stream] = None
+        # contention emulation (tools/contention_ab.py): before each of the first HSD_HOG_POINTS slices of a step,
+        # hold HSD_HOG_CUS whole CUs for HSD_HOG_US us on the slice stream -- what a data-parallel rank's RCCL
+        # all-reduce kernels do beside its backward GEMMs -- so one GPU measures the persistent GEMMs under it
+        self._hog = (int(os.environ.get("HSD_HOG_CUS", "0")), float(os.environ.get("HSD_HOG_US", "400")),
+                     int(os.environ.get("HSD_HOG_POINTS", "7")))
+        self._hogs = 0
         opt.enable_overlap(self.ranges, on_ready=self.mark_ready)
 
     def begin(self) -> None:
         self.pending = list(self.count)
         self.sync = True
+        self._hogs = 0
 
     def mark_ready(self, i: int) -> None:
         if not self.sync:  # accumulation micro-step: gradients are not final yet
@@ -247,6 +270,9 @@ class LocalOverlap:
             if side is not None and self.parent is None:  # (a capture runs no wgrad side stream)
                 hip.stream_wait(self.stream, side)
             with torch.cuda.stream(self.stream):
+                if self._hog[0] > 0 and self._hogs < self._hog[2]:
+                    self._hogs += 1
+                    hip._C.cu_hog(self._hog[0], self._hog[1])
                 self.opt.step_range(b)
 
     def join(self) -> None:

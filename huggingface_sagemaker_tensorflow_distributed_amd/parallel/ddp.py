@@ -154,8 +154,10 @@ class GradBucketer:
             _hip.join_side_streams()  # gradients of this bucket may come from the wgrad stream
         wire_dtype = COMPRESSION[self.compression][1]
         if wire_dtype is not None and view.dtype == torch.float32:
-            # fp16: pre-scaled by 1/(world x micro-steps) so the rank sum stays inside fp16's range (undone in
-            # finish); bf16 has fp32's range and travels unscaled
+            # fp16: pre-scaled by 1/micro-steps (the accumulated micro-step sum back to one step's magnitude, undone
+            # in finish); the 1/world average stays in fp32 (optimizer grad_scale), as Horovod's fp16 compression
+            # sums first and averages after: a 1/world pre-scale would push small gradients log2(world) binades
+            # closer to fp16's subnormal range. bf16 has fp32's range and travels unscaled
             b.wire = (view * self._prescale).to(wire_dtype) if self._prescale != 1.0 else view.to(wire_dtype)
             b.handle = dist.all_reduce(b.wire, op=dist.ReduceOp.SUM, group=self.group, async_op=True)
         else:
@@ -167,7 +169,7 @@ class GradBucketer:
     # ---------------------------------------------------------------- step API
     def begin(self, micro_steps: int = 1) -> None:
         self.last_launched = None
-        self._prescale = 1.0 / (self.world * max(1, int(micro_steps))) if self.compression == "fp16" else 1.0
+        self._prescale = 1.0 / max(1, int(micro_steps)) if self.compression == "fp16" else 1.0
         if self.engine is not None:
             if self.compression == "fp16":
                 self.engine.set_prescale(self._prescale)

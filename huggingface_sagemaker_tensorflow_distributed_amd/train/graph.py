@@ -150,7 +150,7 @@ class CapturedTrainStep:
         self.graph = torch.cuda.CUDAGraph()
         step0 = opt.step_count
         try:
-            with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
+            with opt.capturing(), torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
                 cap = torch.cuda.current_stream(trainer.device)  # the capture stream
                 store.zero_grad()
                 model.rng.new_step(0)

@@ -166,13 +166,20 @@ class Trainer:
         if self.device.type != "cuda":
             logger.warning("--hip_graph: needs a GPU")
             return False
-        if (self.bucketer is not None or self.world > 1) and not (
-                self.bucketer is not None and self.bucketer.engine is not None and self.bucketer.overlap
-                and os.environ.get("HSD_GRAPH_FULL", "1") == "1"):
-            # data parallel: only the whole-step graph over the native RCCL engine captures the collectives
-            logger.warning("--hip_graph: data-parallel steps need the native RCCL engine and the whole-step graph; "
-                           "staying eager")
-            return False
+        if self.bucketer is not None or self.world > 1:
+            # data parallel: only the whole-step graph over the native RCCL engine captures the collectives. It is
+            # OPT-IN (HSD_GRAPH_DP=1): captured all-reduces + engine-stream Adam slices have been checked against
+            # eager with a world-of-one communicator only (tests/test_gpu_graph.py), not on a multi-GPU node
+            if not (self.bucketer is not None and self.bucketer.engine is not None and self.bucketer.overlap
+                    and os.environ.get("HSD_GRAPH_FULL", "1") == "1"
+                    and os.environ.get("HSD_GRAPH_DP", "0") == "1"):
+                logger.warning("--hip_graph: data-parallel whole-step capture is opt-in (HSD_GRAPH_DP=1, native RCCL "
+                               "engine with overlap); staying eager")
+                return False
+            if self.grad_accum > 1:
+                logger.warning("--hip_graph: data-parallel capture covers one-micro-step optimizer steps only "
+                               "(--gradient_accumulation_steps %d); staying eager", self.grad_accum)
+                return False
         if not getattr(self.model, "graph_safe", True):
             logger.warning("--hip_graph: %s has data-dependent shapes; staying eager", type(self.model).__name__)
             return False

@@ -36,3 +36,31 @@ def gpu():
     if not torch.cuda.is_available():
         pytest.skip("no GPU")
     return torch.device("cuda", 0)
+
+
+def _refresh_native_knobs():
+    """The native launchers cache their HSD_* knobs (csrc/kernels/common.h HSD_KNOB); re-read them when a test changes
+    the environment. No-op unless the extension is already loaded (CPU tier)."""
+    mod = sys.modules.get("huggingface_sagemaker_tensorflow_distributed_amd._C") or sys.modules.get(
+        "huggingface_sagemaker_tensorflow_distributed_amd._C_debug")
+    if mod is not None and hasattr(mod, "refresh_env"):
+        mod.refresh_env()
+
+
+@pytest.fixture(autouse=True)
+def _native_knobs(monkeypatch):
+    # every test starts from the (already undone) environment of the previous one; knob flips inside the test go
+    # through monkeypatch.setenv / delenv, which re-read the cache at once
+    _refresh_native_knobs()
+    set0, del0 = monkeypatch.setenv, monkeypatch.delenv
+
+    def setenv(name, value, prepend=None):
+        set0(name, value, prepend)
+        _refresh_native_knobs()
+
+    def delenv(name, raising=True):
+        del0(name, raising)
+        _refresh_native_knobs()
+
+    monkeypatch.setenv, monkeypatch.delenv = setenv, delenv
+    yield

@@ -179,6 +179,7 @@ def test_whole_step_graph_with_native_engine(gpu, monkeypatch):
 
     monkeypatch.setenv("HSD_OPT_OVERLAP", "1")
     monkeypatch.setenv("HSD_GRAPH_FULL", "1")
+    monkeypatch.setenv("HSD_GRAPH_DP", "1")  # data-parallel whole-step capture is opt-in
     ds = hdata.synthetic_classification(32, 128, 30522, seed=1)
     batches = [{k: torch.from_numpy(v[16 * i:16 * (i + 1)]).long().to(gpu) for k, v in
                 (("input_ids", ds.input_ids), ("attention_mask", ds.attention_mask), ("labels", ds.labels))}

@@ -70,6 +70,7 @@ for k, (fl, fn) in cases.items():
     snaps = []
     for v in variants:
         os.environ[AB_VAR] = str(v)
+        hip._C.refresh_env()  # launch knobs are cached (common.h HSD_KNOB)
         for t in list(bufs[k]):
             t.zero_()
         fn()
@@ -86,6 +87,7 @@ for rnd in range(3):
     for k, (fl, fn) in cases.items():
         for v in variants:
             os.environ[AB_VAR] = str(v)
+            hip._C.refresh_env()  # launch knobs are cached (common.h HSD_KNOB)
             res[k][v].append(fl / timeit(fn) / 1e12)
 for k in cases:
     print(k, "  ".join(f"v{v}: {max(res[k][v]):7.1f} (med {sorted(res[k][v])[1]:7.1f})" for v in variants), flush=True)

@@ -17,6 +17,7 @@ p0, m0, v0 = torch.randn(n, device=dev), torch.randn(n, device=dev) * 1e-3, torc
 
 def run(u, iters):
     os.environ["HSD_ADAM_UNROLL"] = str(u)
+    hip._C.refresh_env()  # launch knobs are cached (common.h HSD_KNOB)
     p, m, v, out = p0.clone(), m0.clone(), v0.clone(), torch.empty(n, device=dev, dtype=torch.bfloat16)
     hip.adam_step(p, m, v, g0, out, None, 1e-4, 1e-7, 0.9, 0.999, 1.0, 0.0)
     torch.cuda.synchronize()

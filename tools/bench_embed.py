@@ -45,8 +45,10 @@ grads = {}
 for mode in ("scalar", "vec16"):
     if mode == "scalar":
         os.environ["HSD_EMBED_BWD_SCALAR"] = "1"
+        hip._C.refresh_env()  # launch knobs are cached (common.h HSD_KNOB)
     else:
         os.environ.pop("HSD_EMBED_BWD_SCALAR", None)
+        hip._C.refresh_env()  # launch knobs are cached (common.h HSD_KNOB)
     gw, gp, gt = torch.zeros(V, H, device=dev), torch.zeros(512, H, device=dev), torch.zeros(2, H, device=dev)
     gg, gb = torch.zeros(H, device=dev), torch.zeros(H, device=dev)
     fn = lambda: C_.embed_bwd(dout, ids, pos, tt, word, pw, tw, g, mean, rstd, gw, gp, gt, gg, gb, B, S, True, 0.1, 5)  # noqa: E731

@@ -34,6 +34,7 @@ res = {}
 outs = {}
 for mode in ["1", "8", "16", "0"]:
     os.environ["HSD_LN_FWD_RPW"] = mode
+    hip._C.refresh_env()  # launch knobs are cached (common.h HSD_KNOB)
     for p in (0.0, 0.1):
         for with_res in (False, True):
             z = torch.empty_like(y) if with_res else None

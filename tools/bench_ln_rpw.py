@@ -42,6 +42,7 @@ t = {m: [] for m in modes}
 for _ in range(4):
     for m in modes:
         os.environ["HSD_LN_FWD_RPW"] = m
+        hip._C.refresh_env()  # launch knobs are cached (common.h HSD_KNOB)
         t[m].append(timeit())
 res = {f"rpw{m}_us": round(min(v), 1) for m, v in t.items()}
 res.update({f"rpw{m}_TBs": round(2 * T * H * 2 / (min(v) * 1e-6) / 1e12, 2) for m, v in t.items()})

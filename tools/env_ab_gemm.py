@@ -43,6 +43,7 @@ for name, lay, M, N, K, epi in GEMMS:
     for rnd_i in range(3):
         for v in VALS:
             os.environ[VAR] = v
+            hip._C.refresh_env()  # launch knobs are cached (common.h HSD_KNOB)
             c = torch.empty(M, N, device=dev, dtype=torch.bfloat16)
             c2 = torch.empty_like(c) if epi in (2, 8) else None
             db = torch.zeros(N, device=dev) if epi in (5, 9) else None
@@ -57,6 +58,7 @@ for name, lay, M, N, K, epi in GEMMS:
                 outs[v] = c.clone()
             t[v].append(timeit(fn))
     os.environ.pop(VAR, None)
+    hip._C.refresh_env()  # launch knobs are cached (common.h HSD_KNOB)
     same = all(torch.equal(outs[VALS[0]], outs[v]) for v in VALS[1:])
     print(json.dumps({"gemm": name, "epi": epi, "same": same, **{f"{VAR}={v}": round(min(t[v]), 1) for v in VALS}}),
           flush=True)

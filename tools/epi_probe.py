@@ -53,8 +53,10 @@ for r in range(3):
     for k, (fl, fn) in cases.items():
         for v in VARS:
             os.environ["HSD_G2_SYNC"] = str(v)
+            hip._C.refresh_env()  # launch knobs are cached (common.h HSD_KNOB)
             res_t[k].setdefault(f"s{v}", []).append(fl / timeit(fn) / 1e12)
         os.environ.pop("HSD_G2_SYNC", None)
+        hip._C.refresh_env()  # launch knobs are cached (common.h HSD_KNOB)
 out = {k: {kk: round(sorted(vv)[1], 1) for kk, vv in v.items()} for k, v in res_t.items()}
 for k, v in out.items():
     print(k, v, flush=True)

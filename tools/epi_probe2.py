@@ -44,6 +44,8 @@ for K in (64, 768):
         r = {}
         for g in ("256", "128", "64"):
             os.environ["HSD_G2_GRID"] = g
+            hip._C.refresh_env()  # launch knobs are cached (common.h HSD_KNOB)
             r[g] = round(min(timeit(fn) for _ in range(2)), 1)
         os.environ.pop("HSD_G2_GRID")
+        hip._C.refresh_env()  # launch knobs are cached (common.h HSD_KNOB)
         print(json.dumps({"K": K, "epi": epi, "us_by_grid": r}), flush=True)

@@ -40,10 +40,12 @@ def timeit(fn, iters=10):
 
 def with_sync(v, fn):
     os.environ["HSD_G2_SYNC"] = str(v)
+    hip._C.refresh_env()  # launch knobs are cached (common.h HSD_KNOB)
     try:
         return fn()
     finally:
         os.environ.pop("HSD_G2_SYNC", None)
+        hip._C.refresh_env()  # launch knobs are cached (common.h HSD_KNOB)
 
 
 torch.manual_seed(0)

@@ -42,6 +42,7 @@ for (N, K, epi) in [(3072, 64, 0), (3072, 64, 8), (3072, 768, 0), (3072, 768, 8)
     for rnd_i in range(3):
         for pol in POLS:
             os.environ["HSD_G2_NT"] = pol
+            hip._C.refresh_env()  # launch knobs are cached (common.h HSD_KNOB)
             if rnd_i == 0:
                 fn()
                 torch.cuda.synchronize()
@@ -51,5 +52,6 @@ for (N, K, epi) in [(3072, 64, 0), (3072, 64, 8), (3072, 768, 0), (3072, 768, 8)
                     same = same and torch.equal(ref, c)
             r[pol].append(timeit(fn))
     os.environ.pop("HSD_G2_NT")
+    hip._C.refresh_env()  # launch knobs are cached (common.h HSD_KNOB)
     print(json.dumps({"N": N, "K": K, "epi": epi, "same": same, **{f"pol{p}": round(min(v), 1) for p, v in r.items()}}),
           flush=True)

@@ -49,6 +49,7 @@ def main():
         for rnd in range(3):
             for v in variants:
                 os.environ["HSD_G2_SYNC"] = str(v[0])
+                hip._C.refresh_env()  # launch knobs are cached (common.h HSD_KNOB)
                 g = torch.zeros(N, K, device=dev)
 
                 def run():
@@ -63,6 +64,7 @@ def main():
                         assert err < 1e-4, (name, v, err)
                 times[v].append(timeit(run))
         os.environ.pop("HSD_G2_SYNC", None)
+        hip._C.refresh_env()  # launch knobs are cached (common.h HSD_KNOB)
         r = {}
         for v, ts in times.items():
             t = min(ts)

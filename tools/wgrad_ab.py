@@ -21,11 +21,13 @@ def apply(setting):
     for kv in setting.split():
         k, v = kv.split("=")
         os.environ[k] = v
+        hip._C.refresh_env()  # launch knobs are cached (common.h HSD_KNOB)
 
 
 def clear(setting):
     for kv in setting.split():
         os.environ.pop(kv.split("=")[0], None)
+        hip._C.refresh_env()  # launch knobs are cached (common.h HSD_KNOB)
 
 
 def timeit(fn, iters=10):
