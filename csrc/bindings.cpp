@@ -507,6 +507,144 @@ void gemm2(torch::Tensor A, torch::Tensor B, torch::Tensor C, int64_t la, int64_
                     C2.has_value() ? BF(*C2) : nullptr, p, (uint64_t)seed, sp, wsp, dbp, cur_stream());
 }
 
+// ---- fp32 step (fp32.hip, ops/hip32.py) ---------------------------------------------------------------------------
+// C [M][N] fp32 = A [M][K] · Bᵀ (lb 0: B [N][K]; lb 1: B [K][N]), bf16 operands (the split-product concatenations)
+void gemm2_f32nt(torch::Tensor A, torch::Tensor B, torch::Tensor C, int64_t lb) {
+  check_bf16(A, "A"); check_bf16(B, "B"); check_f32(C, "C");
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2 && (lb == 0 || lb == 1), "gemm2_f32nt: 2-D operands");
+  const int64_t M = A.size(0), K = A.size(1);
+  const int64_t N = lb == 0 ? B.size(0) : B.size(1), KB = lb == 0 ? B.size(1) : B.size(0);
+  TORCH_CHECK(K == KB && C.size(0) == M && C.size(1) == N, "gemm2_f32nt shapes");
+  TORCH_CHECK(hsd::gemm2_supported(0, (int)lb, 7, (int)M, (int)N, (int)K), "gemm2_f32nt: unsupported shape");
+  hsd::launch_gemm2(0, (int)lb, 7, CBF(A), A.stride(0), CBF(B), B.stride(0), (int)M, (int)N, (int)K, C.data_ptr(),
+                    C.stride(0), nullptr, nullptr, 0, nullptr, 0.0, 0, 1, nullptr, nullptr, cur_stream());
+}
+
+void split3(torch::Tensor x, torch::Tensor out, int64_t pat, bool rows) {
+  check_f32(x, "x"); check_bf16(out, "out");
+  TORCH_CHECK(x.dim() == 2 && x.size(1) % 4 == 0 && out.numel() == 3 * x.numel(), "split3 shapes");
+  TORCH_CHECK(rows ? (out.size(0) == 3 * x.size(0) && out.size(1) == x.size(1))
+                   : (out.size(0) == x.size(0) && out.size(1) == 3 * x.size(1)), "split3 out shape");
+  hsd::launch_split3(x.data_ptr<float>(), BF(out), x.size(0), x.size(1), (int)pat, rows, cur_stream());
+}
+
+void epi32(torch::Tensor y, c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> aux, torch::Tensor out,
+           int64_t kind, double p, int64_t seed) {
+  check_f32(y, "y"); check_f32(out, "out");
+  TORCH_CHECK(y.dim() == 2 && y.sizes() == out.sizes() && y.size(1) % 4 == 0, "epi32 shapes");
+  if (bias.has_value()) { check_f32(*bias, "bias"); TORCH_CHECK(bias->numel() == y.size(1), "epi32 bias"); }
+  if (kind >= 2) { TORCH_CHECK(aux.has_value(), "epi32 aux"); check_f32(*aux, "aux"); TORCH_CHECK(aux->sizes() == y.sizes(), "aux"); }
+  hsd::launch_epi32(y.data_ptr<float>(), OPT_F(bias), OPT_F(aux), out.data_ptr<float>(), y.size(0), (int)y.size(1),
+                    (int)kind, p, (uint64_t)seed, cur_stream());
+}
+
+void dropout32(torch::Tensor x, torch::Tensor out, double p, int64_t seed) {
+  check_f32(x, "x"); check_f32(out, "out");
+  TORCH_CHECK(x.numel() == out.numel() && x.numel() % 4 == 0, "dropout32 sizes");
+  hsd::launch_dropout32(x.data_ptr<float>(), out.data_ptr<float>(), x.numel(), p, (uint64_t)seed, cur_stream());
+}
+
+void colsum32(torch::Tensor x, torch::Tensor dbias) {
+  check_f32(x, "x"); check_f32(dbias, "dbias");
+  TORCH_CHECK(x.dim() == 2 && dbias.numel() == x.size(1), "colsum32 shapes");
+  hsd::launch_colsum32(x.data_ptr<float>(), dbias.data_ptr<float>(), (int)x.size(0), (int)x.size(1), cur_stream());
+}
+
+void ln32_fwd(torch::Tensor x, torch::Tensor g, torch::Tensor b, torch::Tensor out, torch::Tensor mean,
+              torch::Tensor rstd, double eps) {
+  check_f32(x, "x"); check_f32(g, "g"); check_f32(b, "b"); check_f32(out, "out"); check_f32(mean, "mean");
+  check_f32(rstd, "rstd");
+  const int64_t R = x.size(0), H = x.size(1);
+  TORCH_CHECK(x.dim() == 2 && H % 4 == 0 && H <= 1024 && g.numel() == H && b.numel() == H && mean.numel() == R &&
+              rstd.numel() == R && out.sizes() == x.sizes(), "ln32_fwd shapes");
+  hsd::launch_ln32_fwd(x.data_ptr<float>(), g.data_ptr<float>(), b.data_ptr<float>(), out.data_ptr<float>(),
+                       mean.data_ptr<float>(), rstd.data_ptr<float>(), (int)R, (int)H, (float)eps, cur_stream());
+}
+
+void ln32_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor mean, torch::Tensor rstd, torch::Tensor g,
+              torch::Tensor dx, torch::Tensor dg, torch::Tensor db) {
+  check_f32(dy, "dy"); check_f32(x, "x"); check_f32(mean, "mean"); check_f32(rstd, "rstd"); check_f32(g, "g");
+  check_f32(dx, "dx"); check_f32(dg, "dg"); check_f32(db, "db");
+  const int64_t R = x.size(0), H = x.size(1);
+  TORCH_CHECK(dy.sizes() == x.sizes() && dx.sizes() == x.sizes() && H % 4 == 0 && H <= 1024 && dg.numel() == H &&
+              db.numel() == H && mean.numel() == R, "ln32_bwd shapes");
+  hsd::launch_ln32_bwd(dy.data_ptr<float>(), x.data_ptr<float>(), mean.data_ptr<float>(), rstd.data_ptr<float>(),
+                       g.data_ptr<float>(), dx.data_ptr<float>(), dg.data_ptr<float>(), db.data_ptr<float>(), (int)R,
+                       (int)H, cur_stream());
+}
+
+void embed32_gather(torch::Tensor ids, torch::Tensor pids, c10::optional<torch::Tensor> tids, torch::Tensor word,
+                    torch::Tensor pos, c10::optional<torch::Tensor> type, torch::Tensor x) {
+  CHECK_DTYPE(ids, torch::kInt64); CHECK_DTYPE(pids, torch::kInt64); CHECK_CONTIG(ids); CHECK_CONTIG(pids);
+  check_f32(word, "word"); check_f32(pos, "pos"); check_f32(x, "x");
+  const int64_t R = ids.numel(), H = word.size(1);
+  TORCH_CHECK(pids.numel() == R && x.size(0) == R && x.size(1) == H && pos.size(1) == H && H % 4 == 0, "embed32 shapes");
+  if (tids.has_value()) { CHECK_DTYPE(*tids, torch::kInt64); CHECK_CONTIG(*tids); TORCH_CHECK(tids->numel() == R, "tids"); }
+  if (type.has_value()) check_f32(*type, "type");
+  hsd::launch_embed32_gather(ids.data_ptr<int64_t>(), pids.data_ptr<int64_t>(), OPT_I64(tids), word.data_ptr<float>(),
+                             pos.data_ptr<float>(), OPT_F(type), x.data_ptr<float>(), (int)R, (int)H, cur_stream());
+}
+
+void embed32_scatter(torch::Tensor dx, torch::Tensor ids, torch::Tensor pids, c10::optional<torch::Tensor> tids,
+                     torch::Tensor gword, c10::optional<torch::Tensor> gpos, c10::optional<torch::Tensor> gtype) {
+  check_f32(dx, "dx"); check_f32(gword, "gword");
+  CHECK_DTYPE(ids, torch::kInt64); CHECK_DTYPE(pids, torch::kInt64);
+  const int64_t R = ids.numel(), H = dx.size(1);
+  TORCH_CHECK(dx.size(0) == R && gword.size(1) == H, "embed32_scatter shapes");
+  if (gpos.has_value()) check_f32(*gpos, "gpos");
+  if (gtype.has_value()) check_f32(*gtype, "gtype");
+  hsd::launch_embed32_scatter(dx.data_ptr<float>(), ids.data_ptr<int64_t>(), pids.data_ptr<int64_t>(), OPT_I64(tids),
+                              gword.data_ptr<float>(), OPT_F(gpos), OPT_F(gtype), (int)R, (int)H, cur_stream());
+}
+
+void attn32_fwd(torch::Tensor qkv, c10::optional<torch::Tensor> mask, torch::Tensor out, torch::Tensor lse, int64_t B,
+                int64_t S, int64_t heads, double p, int64_t seed) {
+  check_f32(qkv, "qkv"); check_f32(out, "out"); check_f32(lse, "lse");
+  TORCH_CHECK(qkv.size(0) == B * S && qkv.size(1) == 3 * heads * 64 && out.size(0) == B * S &&
+              out.size(1) == heads * 64 && lse.numel() == B * heads * S && S % 2 == 0, "attn32_fwd shapes (head dim 64)");
+  if (mask.has_value()) { check_f32(*mask, "mask"); TORCH_CHECK(mask->numel() == B * S, "mask"); }
+  hsd::launch_attn32_fwd(qkv.data_ptr<float>(), OPT_F(mask), out.data_ptr<float>(), lse.data_ptr<float>(), (int)B,
+                         (int)S, (int)heads, p, (uint64_t)seed, cur_stream());
+}
+
+void attn32_bwd(torch::Tensor qkv, c10::optional<torch::Tensor> mask, torch::Tensor o, torch::Tensor dout,
+                torch::Tensor lse, torch::Tensor dqkv, torch::Tensor delta, int64_t B, int64_t S, int64_t heads, double p,
+                int64_t seed) {
+  check_f32(qkv, "qkv"); check_f32(o, "o"); check_f32(dout, "dout"); check_f32(lse, "lse"); check_f32(dqkv, "dqkv");
+  check_f32(delta, "delta");
+  TORCH_CHECK(qkv.sizes() == dqkv.sizes() && o.sizes() == dout.sizes() && o.size(0) == B * S &&
+              o.size(1) == heads * 64 && lse.numel() == B * heads * S && delta.numel() >= B * heads * S, "attn32_bwd shapes");
+  if (mask.has_value()) { check_f32(*mask, "mask"); TORCH_CHECK(mask->numel() == B * S, "mask"); }
+  hsd::launch_attn32_bwd(qkv.data_ptr<float>(), OPT_F(mask), o.data_ptr<float>(), dout.data_ptr<float>(),
+                         lse.data_ptr<float>(), dqkv.data_ptr<float>(), delta.data_ptr<float>(), (int)B, (int)S,
+                         (int)heads, p, (uint64_t)seed, cur_stream());
+}
+
+void cls32_fwd(torch::Tensor pre, torch::Tensor W2, torch::Tensor b2, torch::Tensor labels, torch::Tensor t_out,
+               torch::Tensor logits, torch::Tensor stats, int64_t act, double p, int64_t seed) {
+  check_f32(pre, "pre"); check_f32(W2, "W2"); check_f32(b2, "b2"); check_f32(t_out, "t_out"); check_f32(logits, "logits");
+  check_f32(stats, "stats"); CHECK_DTYPE(labels, torch::kInt64); CHECK_CONTIG(labels);
+  const int64_t R = pre.size(0), H = pre.size(1), C = W2.size(0);
+  TORCH_CHECK(W2.size(1) == H && b2.numel() == C && C <= 8 && labels.numel() == R && t_out.sizes() == pre.sizes() &&
+              logits.size(0) == R && logits.size(1) == C && stats.numel() >= 2 && H % 2 == 0, "cls32_fwd shapes");
+  hsd::launch_cls32_fwd(pre.data_ptr<float>(), W2.data_ptr<float>(), b2.data_ptr<float>(), labels.data_ptr<int64_t>(),
+                        t_out.data_ptr<float>(), logits.data_ptr<float>(), stats.data_ptr<float>(), (int)R, (int)H,
+                        (int)C, (int)act, p, (uint64_t)seed, cur_stream());
+}
+
+void cls32_bwd(torch::Tensor pre, torch::Tensor t, torch::Tensor W2, torch::Tensor logits, torch::Tensor labels,
+               torch::Tensor dloss, torch::Tensor dpre, torch::Tensor dW2, torch::Tensor db2, int64_t act, double p,
+               int64_t seed) {
+  check_f32(pre, "pre"); check_f32(t, "t"); check_f32(W2, "W2"); check_f32(logits, "logits"); check_f32(dloss, "dloss");
+  check_f32(dpre, "dpre"); check_f32(dW2, "dW2"); check_f32(db2, "db2");
+  const int64_t R = pre.size(0), H = pre.size(1), C = W2.size(0);
+  TORCH_CHECK(dpre.sizes() == pre.sizes() && dW2.sizes() == W2.sizes() && db2.numel() == C && C <= 8, "cls32_bwd shapes");
+  hsd::launch_cls32_bwd(pre.data_ptr<float>(), t.data_ptr<float>(), W2.data_ptr<float>(), logits.data_ptr<float>(),
+                        labels.data_ptr<int64_t>(), dloss.data_ptr<float>(), dpre.data_ptr<float>(),
+                        dW2.data_ptr<float>(), db2.data_ptr<float>(), (int)R, (int)H, (int)C, (int)act, p,
+                        (uint64_t)seed, cur_stream());
+}
+
 // gemm2 on an explicit stream (the weight-gradient side stream): no Python stream context per call
 void gemm2_on(int64_t stream_ptr, torch::Tensor A, torch::Tensor B, torch::Tensor C, int64_t la, int64_t lb, int64_t epi,
               c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> aux, c10::optional<torch::Tensor> C2,
@@ -662,6 +800,19 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("set_dropout_device_seed", &set_dropout_device_seed);
   m.def("cu_hog", [](int64_t blocks, double usec) { hsd::launch_cu_hog((int)blocks, usec, cur_stream()); },
         "contention emulation: hold `blocks` whole CUs for `usec` us on the current stream");
+  m.def("gemm2_f32nt", &gemm2_f32nt);
+  m.def("split3", &split3);
+  m.def("epi32", &epi32);
+  m.def("dropout32", &dropout32);
+  m.def("colsum32", &colsum32);
+  m.def("ln32_fwd", &ln32_fwd);
+  m.def("ln32_bwd", &ln32_bwd);
+  m.def("embed32_gather", &embed32_gather);
+  m.def("embed32_scatter", &embed32_scatter);
+  m.def("attn32_fwd", &attn32_fwd);
+  m.def("attn32_bwd", &attn32_bwd);
+  m.def("cls32_fwd", &cls32_fwd);
+  m.def("cls32_bwd", &cls32_bwd);
   m.def("refresh_env", &hsd::refresh_env_knobs, "re-read the HSD_* launch knobs (cached per generation)");
   m.def("fp8_quant", &fp8_quant, py::arg("x"), py::arg("amax"), py::arg("q"), py::arg("sinv"), py::arg("fmt"),
         py::arg("compute_amax"), py::arg("amax_track") = py::none());

@@ -1427,6 +1427,7 @@ static void g2s_launch(const G2Params& q, int grid, hipStream_t st) {
 
 bool gemm2_supported(int la, int lb, int epi, int M, int N, int K) {
   if (K % 64 || M < 1 || N % 8) return false;
+  if (la == 0 && epi == E2_F32_SLAB) return N % 256 == 0;  // fp32-output NT, one pass (launch_gemm2)
   if (la == 0 && lb == 0) return epi_bf16_out(epi) && gemm2_pick_bn(M, N) != 0;
   if (la == 0 && lb == 1) return epi_bf16_out(epi) && (N % 256 == 0 || gemm2s_use(M, N, K));
   if (la == 1 && lb == 1)
@@ -1555,6 +1556,13 @@ void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const b
   p.A = A; p.lda = lda; p.B = B; p.ldb = ldb; p.M = M; p.N = N; p.K = K; p.C = C; p.ldc = ldc;
   p.bias = bias; p.aux = aux; p.ldaux = ldaux; p.C2 = C2;
   p.dp = make_dropout(p_drop, seed);
+  if (la == 0 && epi == E2_F32_SLAB) {
+    // fp32 output [M][N] (ldc == N), one pass: the split-product GEMMs of the fp32 step (fp32.hip, ops/hip32.py)
+    if (ldc != N || splits > 1) abort();
+    if (lb == 0) g2_launch<0, 0, E2_F32_SLAB, 256>(p, 1, st);
+    else g2_launch<0, 1, E2_F32_SLAB, 256>(p, 1, st);
+    return;
+  }
   if (la == 0 && lb == 0) {
     launch_nt<0>(p, epi, M, N, K, splits, ws, dbias, st);
   } else if (la == 1 && lb == 1) {

@@ -92,6 +92,31 @@ void launch_gemm(int la, int lb, int epi, const bf16_t* A, int64_t lda, const bf
 void set_dropout_dev_seed(const uint32_t* p);
 // HSD_* knobs are cached per generation (common.h HSD_KNOB); this re-reads them at their next use
 void refresh_env_knobs();
+// fp32.hip: the fp32 (reference precision) step -- split-product operands for the bf16 MFMA GEMMs, fp32 epilogues,
+// LayerNorm, embeddings, streaming attention, classification head (ops/hip32.py)
+void launch_split3(const float* x, bf16_t* out, int64_t R, int64_t C, int pat, bool rows, hipStream_t st);
+void launch_epi32(float* y, const float* bias, const float* aux, float* out, int64_t M, int N, int kind, double p,
+                  uint64_t seed, hipStream_t st);
+void launch_dropout32(const float* x, float* out, int64_t n, double p, uint64_t seed, hipStream_t st);
+void launch_colsum32(const float* x, float* dbias, int M, int N, hipStream_t st);
+void launch_ln32_fwd(const float* x, const float* g, const float* b, float* out, float* mean, float* rstd, int R,
+                     int H, float eps, hipStream_t st);
+void launch_ln32_bwd(const float* dy, const float* x, const float* mean, const float* rstd, const float* g, float* dx,
+                     float* dg, float* db, int R, int H, hipStream_t st);
+void launch_embed32_gather(const int64_t* ids, const int64_t* pids, const int64_t* tids, const float* word,
+                           const float* pos, const float* type, float* x, int R, int H, hipStream_t st);
+void launch_embed32_scatter(const float* dx, const int64_t* ids, const int64_t* pids, const int64_t* tids,
+                            float* gword, float* gpos, float* gtype, int R, int H, hipStream_t st);
+void launch_attn32_fwd(const float* qkv, const float* mask, float* out, float* lse, int B, int S, int heads, double p,
+                       uint64_t seed, hipStream_t st);
+void launch_attn32_bwd(const float* qkv, const float* mask, const float* o, const float* dout, const float* lse,
+                       float* dqkv, float* delta, int B, int S, int heads, double p, uint64_t seed, hipStream_t st);
+void launch_cls32_fwd(const float* pre, const float* W2, const float* b2, const int64_t* labels, float* t_out,
+                      float* logits, float* stats, int R, int H, int C, int act, double p, uint64_t seed,
+                      hipStream_t st);
+void launch_cls32_bwd(const float* pre, const float* t_in, const float* W2, const float* logits,
+                      const int64_t* labels, const float* dloss, float* dpre, float* dW2, float* db2, int R, int H,
+                      int C, int act, double p, uint64_t seed, hipStream_t st);
 // contention emulation: `blocks` workgroups holding one whole CU each (160 KiB LDS) for `usec` us
 void launch_cu_hog(int blocks, double usec, hipStream_t st);
 

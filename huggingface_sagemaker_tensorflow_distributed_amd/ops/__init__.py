@@ -3,10 +3,12 @@
 * CUDA (=HIP on ROCm) tensors -> hand-written gfx950 kernels in ``csrc/kernels`` via
   :mod:`.hip` (custom autograd Functions). If the compiled extension is missing on a GPU box this
   raises — there is no silent eager fallback.
-* CPU tensors, and fp32 GPU tensors (``--dtype fp32``) -> :mod:`.reference` (plain torch; also the numerics oracle
-  for the kernel tests).
+* fp32 GPU tensors (``--dtype fp32``, the reference's own precision) -> :mod:`.hip32` (fp32 kernels in
+  ``csrc/kernels/fp32.hip`` + split-product MFMA GEMMs).
+* CPU tensors -> :mod:`.reference` (plain torch; also the numerics oracle for the kernel tests).
 
-``HSD_OPS=torch`` forces the reference path on GPU (only for A/B measurements of the kernels).
+``HSD_OPS=torch`` forces the reference path on GPU (only for A/B measurements of the kernels); ``HSD_FP32_OPS=torch``
+does so for fp32 tensors only.
 """
 from __future__ import annotations
 
@@ -18,18 +20,30 @@ import torch
 from . import reference as _ref
 
 _FORCE_TORCH = os.environ.get("HSD_OPS", "").lower() == "torch"
+_FP32_TORCH = os.environ.get("HSD_FP32_OPS", "").lower() == "torch"
 
 
 def _hip(x: torch.Tensor) -> bool:
-    # fp32 tensors (``--dtype fp32``, the reference's own precision: scripts/train.py:113-123 has no mixed-precision
-    # policy) run the fp32 reference ops on the GPU (hipBLASLt / rocBLAS fp32 GEMMs); the HIP kernels are bf16 / fp8
+    # bf16 / fp8 steps: the HIP kernels of ops/hip.py
     return x.is_cuda and not _FORCE_TORCH and x.dtype != torch.float32
+
+
+def _hip32(x: torch.Tensor) -> bool:
+    # fp32 steps (``--dtype fp32``, the reference's own precision: scripts/train.py:113-123 has no mixed-precision
+    # policy): the fp32 kernels of ops/hip32.py
+    return x.is_cuda and not _FORCE_TORCH and not _FP32_TORCH and x.dtype == torch.float32
 
 
 def _hipmod():
     from . import hip  # noqa: WPS433 (lazy: imports the compiled extension)
 
     return hip
+
+
+def _hip32mod():
+    from . import hip32  # noqa: WPS433
+
+    return hip32
 
 
 def key_mask_bias(attention_mask: Optional[torch.Tensor]):
@@ -44,6 +58,8 @@ def dropout(x: torch.Tensor, p: float, seed: int):
         return x
     if _hip(x):
         return _hipmod().dropout(x, p, seed)
+    if _hip32(x):
+        return _hip32mod().dropout(x, p, seed)
     return _ref.dropout(x, p, seed, True)
 
 
@@ -52,6 +68,9 @@ def embed_ln(input_ids, position_ids, token_type_ids, word_w, pos_w, type_w, ln_
     if _hip(word_w):
         return _hipmod().embed_ln(input_ids, position_ids, token_type_ids, word_w, pos_w, type_w, ln_w, ln_b,
                                   eps, p, seed, pos_is_arange)
+    if _hip32(word_w) and word_w.shape[1] % 4 == 0 and word_w.shape[1] <= 1024:
+        return _hip32mod().embed_ln(input_ids, position_ids, token_type_ids, word_w, pos_w, type_w, ln_w, ln_b,
+                                    eps, p, seed)
     return _ref.embed_ln(input_ids, position_ids, token_type_ids, word_w, pos_w, type_w, ln_w, ln_b, eps, p, seed,
                          p > 0)
 
@@ -59,18 +78,24 @@ def embed_ln(input_ids, position_ids, token_type_ids, word_w, pos_w, type_w, ln_
 def linear(x, w, b):
     if _hip(x):
         return _hipmod().linear(x, w, b)
+    if _hip32(x):
+        return _hip32mod().linear(x, w, b)
     return _ref.linear(x, w, b)
 
 
 def linear_gelu(x, w, b):
     if _hip(x):
         return _hipmod().linear_gelu(x, w, b)
+    if _hip32(x):
+        return _hip32mod().linear_gelu(x, w, b)
     return _ref.linear_gelu(x, w, b)
 
 
 def layer_norm(x, w, b, eps):
     if _hip(x):
         return _hipmod().layer_norm(x, w, b, eps)
+    if _hip32(x) and x.shape[-1] % 4 == 0 and x.shape[-1] <= 1024:
+        return _hip32mod().layer_norm(x, w, b, eps)
     return _ref.layer_norm(x, w, b, eps)
 
 
@@ -78,6 +103,8 @@ def dense_residual_ln(x, w, b, residual, ln_w, ln_b, eps, p, seed):
     """``LN(dropout(x Wᵀ + b) + residual)`` — the post-LN block tail."""
     if _hip(x):
         return _hipmod().dense_residual_ln(x, w, b, residual, ln_w, ln_b, eps, p, seed)
+    if _hip32(x) and w.shape[0] % 4 == 0 and w.shape[0] <= 1024:
+        return _hip32mod().dense_residual_ln(x, w, b, residual, ln_w, ln_b, eps, p, seed)
     return _ref.layer_norm(_ref.linear_dropout_residual(x, w, b, residual, p, seed, p > 0), ln_w, ln_b, eps)
 
 
@@ -104,6 +131,8 @@ def ffn_block(h, w1, b1, w2, b2, ln_w, ln_b, eps, p, seed, q8_next=None):
 def attention(qkv, mask_bias, batch, seq, heads, p, seed):
     if _hip(qkv):
         return _hipmod().attention(qkv, mask_bias, batch, seq, heads, p, seed)
+    if _hip32(qkv):
+        return _hip32mod().attention(qkv, mask_bias, batch, seq, heads, p, seed)
     return _ref.attention(qkv, mask_bias, batch, seq, heads, p, seed, p > 0)
 
 
@@ -146,8 +175,13 @@ def cls_head(h, w1, b1, w2, b2, labels, act: str, p_in: float, seed_in: int, p: 
         loss._hsd_correct = stats[1]
         loss._hsd_stats = stats  # {mean loss, hits, rows, loss sum}: the metric meter folds these lazily
         return loss, logits
+    if _hip32(h) and labels is not None and _hip32mod().cls_head_ok(h, w1, w2):
+        loss, logits, stats = _hip32mod().cls_head(h, w1, b1, w2, b2, labels, act, p_in, seed_in, p, seed)
+        loss._hsd_correct = stats[1]
+        loss._hsd_stats = stats
+        return loss, logits
     x = h[:, 0].contiguous()
-    if _hip(h):
+    if _hip(h) or _hip32(h):
         x = dropout(x, p_in, seed_in)
         y = linear(x, w1, b1)
         y = torch.tanh(y) if act == "tanh" else torch.relu(y)

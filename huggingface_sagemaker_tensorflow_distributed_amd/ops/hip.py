@@ -12,6 +12,8 @@ from __future__ import annotations
 
 from typing import Optional
 
+import weakref
+
 import torch
 
 from ._ext import load
@@ -561,7 +563,36 @@ def _fp8_w(w, attr):
 # a block quantises its output for the NEXT block's first GEMM with that GEMM's delayed-scaling site, and the LN
 # backward quantises dy for the block's own fp8 dgrad. A site is fused only once it is calibrated (its first use
 # runs the standalone amax + quant passes), so fused and standalone paths give the same bytes.
-_Q8_PENDING = {}
+class _Q8Handoff:
+    """One producer-written fp8 copy waiting for the GEMM that consumes the producer's output.
+
+    The producer (LayerNorm fwd / bwd, a GEMM epilogue) calls :meth:`put` with its bf16 output; the next GEMM calls
+    :meth:`take` with its input. The copy is handed over only if that input IS the producer's output (same memory,
+    same size) and the output is still alive and unmodified: a weak reference to the producer's tensor (a view keeps
+    its base alive, so a dead reference means the memory may have been reused by another tensor) and the tensor's
+    version counter (bumped by any in-place write). One slot: only the immediately following GEMM may take it."""
+
+    def __init__(self):
+        self._slot = None
+
+    def put(self, out: torch.Tensor, q: torch.Tensor, sinv: torch.Tensor) -> None:
+        self._slot = (weakref.ref(out), out.data_ptr(), out.numel(), out._version, q, sinv)
+
+    def take(self, x: torch.Tensor):
+        s, self._slot = self._slot, None
+        if s is None:
+            return None
+        ref, ptr, numel, ver, q, sinv = s
+        out = ref()
+        if out is None or out._version != ver or x.data_ptr() != ptr or x.numel() != numel:
+            return None
+        return q, sinv
+
+    def clear(self) -> None:
+        self._slot = None
+
+
+_Q8_HANDOFF = _Q8Handoff()
 
 
 def _site_ready(w, state_attr: str, wattr: str):
@@ -573,12 +604,8 @@ def _site_ready(w, state_attr: str, wattr: str):
 
 
 def _take_q8(x):
-    """The fp8 copy a LayerNorm wrote for activation ``x`` (popped), or None."""
-    if not _Q8_PENDING:
-        return None
-    e = _Q8_PENDING.pop((x.data_ptr(), x.numel()), None)
-    _Q8_PENDING.clear()  # only the immediately-following GEMM may use a pending copy
-    return e
+    """The fp8 copy a producer wrote for activation ``x`` (:class:`_Q8Handoff`), or None."""
+    return _Q8_HANDOFF.take(x)
 
 
 def _q8_out(like, w, state_attr: str, wattr: str, fmt: int):
@@ -611,7 +638,7 @@ def gemm_fwd(x, w, epi, bias=None, aux=None, out2=None, p=0.0, seed=0, xq=None, 
         _C.gemm8(qx, FP8_E4M3, sx, wq, FP8_E4M3, w._hsd_qs, y, epi, bias, aux, out2, float(p), _s64(seed), None,
                  **_q8_kw(q8))
         if q8 is not None:
-            _Q8_PENDING[(out2.data_ptr(), out2.numel())] = (q8[0], q8[1])
+            _Q8_HANDOFF.put(out2, q8[0], q8[1])
         return y
     if _nt_ok(x.shape[0], w.shape[0], x.shape[1], epi):
         _C.gemm2(x, w, y, 0, 0, epi, bias, aux, out2, float(p), _s64(seed), 0, None, None)  # 0: auto split-K
@@ -639,7 +666,7 @@ def gemm_dgrad(dy, w, epi=EPI_STORE, aux=None, dbias=None, dyq=None, q8_for=None
         if dbias is not None and not fuse:
             _C.colsum(dx, dbias)
         if q8 is not None:
-            _Q8_PENDING[(dx.data_ptr(), dx.numel())] = (q8[0], q8[1])
+            _Q8_HANDOFF.put(dx, q8[0], q8[1])
         return dx
     wt = getattr(w, "_hsd_wt", None)  # FlatParamStore keeps Wᵀ fresh (one batched transpose per step)
     if wt is not None and (wt.shape[0] != w.shape[1] or wt.shape[1] != w.shape[0]):
@@ -687,7 +714,7 @@ def _ln_fwd(z, w, b, eps, q8_for=None):
         q = torch.empty((rows, H), dtype=torch.uint8, device=z.device)
         sinv = torch.empty(1, dtype=torch.float32, device=z.device)
         _C.ln_fwd_q8(z, w, b, out, mean, rstd, float(eps), q, st[0:1], sinv, st[1:2])
-        _Q8_PENDING[(out.data_ptr(), out.numel())] = (q, sinv)
+        _Q8_HANDOFF.put(out, q, sinv)
     else:
         _C.ln_fwd(z, None, w, b, None, out, mean, rstd, float(eps), 0.0, 0)
     return out, mean, rstd

@@ -110,9 +110,9 @@ def build(args, mode: str):
     # --dtype fp8: bf16 activations / master-weight copies plus fp8 (e4m3) weight copies and per-tensor
     # quantised fp8 forward + dgrad GEMMs on the HIP path (ops/hip.py set_fp8); CPU runs stay bf16.
     if dtype_name == "fp32" and on_gpu:
-        logger.warning("--dtype fp32 on the GPU: the reference's precision, computed by the fp32 PyTorch ops "
-                       "(hipBLASLt / rocBLAS fp32 GEMMs) with the fused fp32 Adam; the hand-written HIP kernels are "
-                       "bf16 / fp8 (use --dtype bf16 for speed)")
+        logger.info("--dtype fp32 on the GPU: the reference's precision on the fp32 kernels (ops/hip32.py: split-product "
+                    "MFMA GEMMs, fp32 LayerNorm / embeddings / streaming attention / head, fused fp32 Adam); "
+                    "--dtype bf16 is the fast path")
     fp8 = dtype_name == "fp8" and on_gpu and ops.hip_active(dev)
     if dtype_name == "fp8" and not fp8:
         logger.warning("--dtype fp8 needs the HIP path on a GPU; computing in bf16")

@@ -1,0 +1,160 @@
+"""fp32 step on hand-written kernels (ops/hip32.py, csrc/kernels/fp32.hip; VERDICT r3 'missing 2'): each kernel vs a
+plain fp32/fp64 torch reference of the same op, then a bert-base-shaped 2-layer training step on the GPU vs the same
+step on the CPU reference ops, with a kernel trace that must hold no library GEMM / softmax / bmm kernel."""
+import copy
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _h32():
+    from huggingface_sagemaker_tensorflow_distributed_amd.ops import hip32
+
+    return hip32
+
+
+def _rel(a, b):
+    return float((a.double() - b.double()).norm() / (b.double().norm() + 1e-30))
+
+
+@pytest.mark.parametrize("M,K,N", [(300, 768, 768), (1024, 768, 3072), (256, 3072, 768), (64, 768, 2304)])
+def test_split_product_gemms(gpu, M, K, N):
+    """x·wᵀ, dy·w and the weight gradient on the split-product MFMA GEMM: per element within 2^-14 of Σ|products|
+    (the three-term split's bound is ~2^-15), and ~1e-6 relative overall against fp64."""
+    h = _h32()
+    torch.manual_seed(M + N)
+    x, w = torch.randn(M, K, device=gpu), torch.randn(N, K, device=gpu) * 0.05
+    y = h.mm_nt(x, w)
+    ref = x.double() @ w.double().t()
+    mag = x.abs().double() @ w.abs().double().t()
+    assert bool(((y.double() - ref).abs() <= 2.0 ** -14 * mag + 1e-30).all())
+    assert _rel(y, ref) < 1e-5
+    dy = torch.randn(M, N, device=gpu)
+    dx = h.mm_dgrad(dy, w)
+    ref = dy.double() @ w.double()
+    assert bool(((dx.double() - ref).abs() <= 2.0 ** -14 * (dy.abs().double() @ w.abs().double()) + 1e-30).all())
+    from huggingface_sagemaker_tensorflow_distributed_amd.ops.hip import _Grad
+
+    g0 = torch.randn(N, K, device=gpu)
+    p = torch.nn.Parameter(torch.zeros(N, K, device=gpu))
+    p.main_grad = g0.clone()
+    gw = _Grad(p)
+    h.wgrad_(gw, dy, x)
+    ref = g0.double() + dy.double().t() @ x.double()
+    mag = g0.abs().double() + dy.abs().double().t() @ x.abs().double()
+    assert bool(((p.main_grad.double() - ref).abs() <= 2.0 ** -14 * mag + 1e-30).all())
+
+
+def _grads(fn, *args):
+    """Run fn(*args) -> scalar, backward, return (value, [grad of each arg that requires grad])."""
+    out = fn(*args)
+    out.backward()
+    return out.detach(), [a.grad.detach().clone() for a in args if isinstance(a, torch.Tensor) and a.requires_grad]
+
+
+@pytest.mark.parametrize("p", [0.0, 0.1])
+@pytest.mark.parametrize("S", [128, 512])
+def test_attention32_fwd_bwd(gpu, p, S):
+    """Streaming fp32 attention forward + three-pass backward == the reference ops (same dropout masks), fp32."""
+    from huggingface_sagemaker_tensorflow_distributed_amd.ops import reference as R
+
+    B, heads = 2, 4
+    H = heads * 64
+    torch.manual_seed(S)
+    qkv = torch.randn(B * S, 3 * H, device=gpu)
+    am = torch.ones(B, S, device=gpu)
+    am[1, S - 37:] = 0
+    mb = R.key_mask_bias(am)
+    g = torch.randn(B * S, H, device=gpu)
+    a = qkv.clone().requires_grad_()
+    out = _h32().attention(a, mb, B, S, heads, p, 1234)
+    (out * g).sum().backward()
+    b = qkv.clone().double().requires_grad_()
+    ref = R.attention(b, mb.double(), B, S, heads, p, 1234, p > 0)  # runs in fp32 internally
+    (ref * g.double()).sum().backward()
+    assert _rel(out, ref) < 2e-5
+    assert _rel(a.grad, b.grad) < 2e-4
+
+
+def test_layernorm_embedding_dropout32(gpu):
+    from huggingface_sagemaker_tensorflow_distributed_amd.ops import reference as R
+
+    h = _h32()
+    torch.manual_seed(3)
+    Bn, S, H, V = 4, 64, 768, 1000
+    word = torch.randn(V, H, device=gpu) * 0.02
+    pos, typ = torch.randn(512, H, device=gpu) * 0.02, torch.randn(2, H, device=gpu) * 0.02
+    lw, lb = 1 + 0.1 * torch.randn(H, device=gpu), 0.1 * torch.randn(H, device=gpu)
+    ids = torch.randint(0, V, (Bn, S), device=gpu)
+    pids = torch.arange(S, device=gpu).expand(Bn, S)
+    tids = torch.zeros_like(ids)
+    g = torch.randn(Bn, S, H, device=gpu)
+    ps = [t.clone().requires_grad_() for t in (word, pos, typ, lw, lb)]
+    out = h.embed_ln(ids, pids, tids, *ps, 1e-12, 0.1, 99)
+    (out * g).sum().backward()
+    qs = [t.clone().requires_grad_() for t in (word, pos, typ, lw, lb)]
+    ref = R.embed_ln(ids, pids, tids, *qs, 1e-12, 0.1, 99, True)
+    (ref * g).sum().backward()
+    assert _rel(out, ref) < 1e-5
+    for a, b in zip(ps, qs):
+        assert _rel(a.grad, b.grad) < 1e-4
+    x = torch.randn(257, H, device=gpu, requires_grad=True)
+    y = h.layer_norm(x, lw, lb, 1e-5)
+    gy = torch.randn_like(y)
+    (y * gy).sum().backward()
+    x2 = x.detach().clone().requires_grad_()
+    y2 = torch.nn.functional.layer_norm(x2, (H,), lw, lb, 1e-5)
+    (y2 * gy).sum().backward()
+    assert _rel(y, y2) < 1e-6 and _rel(x.grad, x2.grad) < 1e-5
+
+
+def _bert2(seed=0):
+    from huggingface_sagemaker_tensorflow_distributed_amd.models import build_model, resolve_config
+
+    cfg = resolve_config("bert-base-uncased").replace(num_hidden_layers=2)
+    return build_model(cfg, seed=seed)
+
+
+def test_fp32_bert_step_on_kernels_matches_cpu(gpu):
+    """A bert-base-shaped 2-layer training step (dropout on, padded batch) with --dtype fp32 semantics: the GPU step on
+    the fp32 kernels reproduces the CPU fp32 reference step -- loss within 1e-4 relative, every parameter gradient
+    within 1e-3 relative -- and its kernel trace holds no library GEMM (Cijk) and no ATen softmax / bmm kernel."""
+    torch.manual_seed(0)
+    cpu = _bert2()
+    dev = copy.deepcopy(cpu).to(gpu)
+    B, S = 4, 128
+    g = torch.Generator().manual_seed(1)
+    ids = torch.randint(1000, 30000, (B, S), generator=g)
+    am = torch.ones(B, S, dtype=torch.long)
+    am[2, 90:] = 0
+    am[3, 40:] = 0
+    labels = torch.randint(0, 2, (B,), generator=g)
+    res = {}
+    for name, model, d in (("cpu", cpu, "cpu"), ("gpu", dev, gpu)):
+        model.train()
+        model.rng.new_step(0)
+        model.zero_grad(set_to_none=True)
+        prof = None
+        if name == "gpu":
+            prof = torch.profiler.profile(activities=[torch.profiler.ProfilerActivity.CUDA])
+            prof.__enter__()
+        loss, logits = model(ids.to(d), attention_mask=am.to(d), labels=labels.to(d))
+        loss.backward()
+        if prof is not None:
+            torch.cuda.synchronize()
+            prof.__exit__(None, None, None)
+            names = {e.name for e in prof.events() if e.device_type == torch.autograd.DeviceType.CUDA}
+            bad = [n for n in names if "hsd::" not in n and ("Cijk" in n or "softmax" in n.lower() or "bmm" in n.lower()
+                                                             or "gemm" in n.lower())]
+            assert not bad, bad
+            assert any("hsd::f32k::attn32" in n for n in names), sorted(names)[:40]
+            assert any("gemm2_kernel" in n for n in names), sorted(names)[:40]
+        res[name] = (float(loss), {k: p.grad.detach().float().cpu() for k, p in model.named_parameters()
+                                   if p.grad is not None})
+    (lc, gc), (lg, gg) = res["cpu"], res["gpu"]
+    assert abs(lg - lc) <= 1e-4 * abs(lc), (lg, lc)
+    assert set(gc) == set(gg)
+    worst = max((_rel(gg[k], gc[k]), k) for k in gc if gc[k].norm() > 0)
+    assert worst[0] < 1e-3, worst

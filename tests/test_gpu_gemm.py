@@ -23,10 +23,33 @@ def _ref(A, B, la, lb):
     return a @ b  # [M, N]
 
 
-def _check(out, ref, tol=2e-2):
-    err = (out.float() - ref).abs().max().item()
-    scale = ref.abs().max().item() + 1e-6
-    assert err <= tol * scale, f"max err {err:.4g} vs scale {scale:.4g}"
+def _check(out, ref, mag=None, acc=None, fp32=False):
+    """Per-element bound (a max-relative 2 % bound let a wrong edge tile at 1 % of the max pass):
+
+        |out - ref| <= rel * mag + 2^-16 * acc + 1e-30
+
+    * rel = 2^-7 for bf16 outputs: one bf16 ulp of each rounded intermediate (the kernel and the reference may round
+      values that differ in the last fp32 bits to neighbouring bf16 values); 2^-20 for fp32 outputs.
+    * mag: elementwise magnitude of the rounded intermediates (default |ref|; epilogues pass |pre-activation| etc.).
+    * acc: elementwise sum of |products| (|A| @ |B|), which bounds fp32 accumulation-order differences from torch's
+      GEMM (~sqrt(K) * 2^-24 * acc typical, 2^-16 * acc is 2^8 above that)."""
+    out = out.float()
+    mag = ref.abs() if mag is None else mag
+    bound = (2.0 ** -20 if fp32 else 2.0 ** -7) * mag + 1e-30
+    if acc is not None:
+        bound = bound + 2.0 ** -16 * acc
+    err = (out - ref).abs()
+    bad = err > bound
+    if bad.any():
+        i = int(bad.flatten().nonzero()[0])
+        raise AssertionError(f"{int(bad.sum())} of {bad.numel()} elements out of bound; first at flat index {i}: "
+                             f"out {out.flatten()[i].item():.6g} ref {ref.flatten()[i].item():.6g} "
+                             f"bound {bound.flatten()[i].item():.3g} (max err {err.max().item():.4g})")
+
+
+def _absmm(A, B, la, lb):
+    """|A| @ |B| in the layout of _ref: the accumulation magnitude of every output element."""
+    return _ref(A.abs(), B.abs(), la, lb)
 
 
 SHAPES = [(256, 256, 128), (200, 136, 72), (1024, 768, 768), (512, 2304, 64), (96, 64, 3072)]
@@ -40,7 +63,7 @@ def test_gemm_store(gpu, M, N, K, la, lb):
     B = _mk((N, K) if lb == 0 else (K, N), gpu)
     C = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
     _C().gemm(A, B, C, la, lb, EPI_STORE, None, None, None, 0.0, 0, 1)
-    _check(C, _ref(A, B, la, lb))
+    _check(C, _ref(A, B, la, lb), acc=_absmm(A, B, la, lb))
 
 
 @pytest.mark.parametrize("M,N,K", SHAPES)
@@ -53,7 +76,7 @@ def test_gemm_f32_atomic_accumulates(gpu, M, N, K, la, lb, splits):
     C0 = torch.randn(M, N, device=gpu)
     C = C0.clone()
     _C().gemm(A, B, C, la, lb, EPI_F32_ATOMIC, None, None, None, 0.0, 0, splits)
-    _check(C, C0 + _ref(A, B, la, lb), 1e-3)
+    _check(C, C0 + _ref(A, B, la, lb), acc=_absmm(A, B, la, lb) + C0.abs(), fp32=True)
 
 
 def test_gemm_bias_epilogues(gpu):
@@ -63,12 +86,14 @@ def test_gemm_bias_epilogues(gpu):
     bias = _mk((N,), gpu)
     ref = _ref(A, B, 0, 0) + bias.float()
     C = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    acc = _absmm(A, B, 0, 0)
     _C().gemm(A, B, C, 0, 0, EPI_BIAS, bias, None, None, 0.0, 0, 1)
-    _check(C, ref)
+    _check(C, ref, acc=acc)
     C2 = torch.empty_like(C)
     _C().gemm(A, B, C, 0, 0, EPI_BIAS_GELU, bias, None, C2, 0.0, 0, 1)
-    _check(C, ref)
-    _check(C2, torch.nn.functional.gelu(ref))
+    _check(C, ref, acc=acc)
+    g = torch.nn.functional.gelu(ref)
+    _check(C2, g, mag=2 * ref.abs() + g.abs(), acc=2 * acc)
 
 
 @pytest.mark.parametrize("p", [0.0, 0.1])
@@ -83,7 +108,7 @@ def test_gemm_bias_dropout_residual(gpu, p):
     ref = dropout(y, p, 4242, True).float() + res.float()
     C = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
     _C().gemm(A, B, C, 0, 0, EPI_BIAS_DROP_RES, bias, res, None, p, 4242, 1)
-    _check(C, ref)
+    _check(C, ref, mag=2 * y.float().abs() + res.float().abs() + ref.abs(), acc=2 * _absmm(A, B, 0, 0))
 
 
 def test_gemm_dgrad_epilogues(gpu):
@@ -93,12 +118,14 @@ def test_gemm_dgrad_epilogues(gpu):
     aux = _mk((M, N), gpu)
     ref = _ref(A, B, 0, 1)
     C = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+    acc = _absmm(A, B, 0, 1)
     _C().gemm(A, B, C, 0, 1, EPI_RES, None, aux, None, 0.0, 0, 1)
-    _check(C, ref + aux.float())
+    _check(C, ref + aux.float(), mag=ref.abs() + aux.float().abs() + (ref + aux.float()).abs(), acc=acc)
     _C().gemm(A, B, C, 0, 1, EPI_DGELU, None, aux, None, 0.0, 0, 1)
     x = aux.float().requires_grad_()
     torch.nn.functional.gelu(x).backward(torch.ones_like(x))
-    _check(C, ref.bfloat16().float() * x.grad, 3e-2)
+    r = ref.bfloat16().float() * x.grad
+    _check(C, r, mag=ref.abs() * x.grad.abs() * 2 + r.abs(), acc=acc * 2)
 
 
 # ---------------------------------------------------------------- gemm2 (8-phase 256-row tiles)
@@ -126,21 +153,28 @@ def test_gemm2_nt_epilogues(gpu, M, N, K, epi):
     C_.gemm2(A, B, C, 0, 0, epi, bias if epi in (1, 2, 3) else None, aux if epi in (3, 4, 5) else None,
              C2 if epi == 2 else None, p, 99, 1, None, None)
     acc = A.float() @ B.float().t()
+    am = _absmm(A, B, 0, 0)
     if epi in (1, 2, 3):
         acc = acc + bias.float()
     if epi == 2:
-        _check(C, acc)
-        _check(C2, torch.nn.functional.gelu(C.float()))
+        _check(C, acc, acc=am)
+        g = torch.nn.functional.gelu(C.float())
+        _check(C2, g, mag=2 * C.float().abs() + g.abs())
         return
+    mag = acc.abs()
     if epi == 3:
         y = acc.bfloat16().float()
         keep = ref.dropout(torch.ones(M, N, device=gpu), p, 99, True)
         acc = (y * keep).bfloat16().float() + aux.float()
+        mag = 2 * (y * keep).abs() + aux.float().abs() + acc.abs()
     elif epi == 4:
         acc = acc.bfloat16().float() + aux.float()
+        mag = mag + aux.float().abs() + acc.abs()
     elif epi == 5:
-        acc = acc.bfloat16().float() * _gelu_grad(aux.float())
-    _check(C, acc)
+        gg = _gelu_grad(aux.float())
+        acc = acc.bfloat16().float() * gg
+        mag = 2 * mag * gg.abs() + acc.abs()
+    _check(C, acc, mag=mag, acc=2 * am)
 
 
 @pytest.mark.parametrize("M,N,K", [(768, 768, 256), (2304, 768, 512), (256, 1024, 4096)])
@@ -154,7 +188,7 @@ def test_gemm2_tt_wgrad(gpu, M, N, K, epi):
     sp = C_.gemm2_splits(M, N, K)
     ws = torch.empty(sp * M * N, device=gpu) if epi == 7 else None
     C_.gemm2(A, B, C, 1, 1, epi, None, None, None, 0.0, 0, sp, ws, None)
-    _check(C, C0 + A.float().t() @ B.float(), 1e-3)
+    _check(C, C0 + A.float().t() @ B.float(), acc=A.float().abs().t() @ B.float().abs() + C0.abs(), fp32=True)
 
 
 @pytest.mark.parametrize("sync", [0, 1, 4, 5, 6, 7])
@@ -168,7 +202,7 @@ def test_gemm2_schedules(gpu, monkeypatch, sync, M, N, K):
     A, B, bias = _mk((M, K), gpu), _mk((N, K), gpu, 0.1), _mk((N,), gpu)
     C = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
     C_.gemm2(A, B, C, 0, 0, 1, bias, None, None, 0.0, 0, 1, None, None)
-    _check(C, A.float() @ B.float().t() + bias.float())
+    _check(C, A.float() @ B.float().t() + bias.float(), acc=_absmm(A, B, 0, 0))
     if K % 256 == 0 and M % 64 == 0:
         dy = _mk((M, N), gpu)
         G0 = torch.randn(N, K, device=gpu)
@@ -176,7 +210,7 @@ def test_gemm2_schedules(gpu, monkeypatch, sync, M, N, K):
         sp = C_.gemm2_splits(N, K, M)
         ws = torch.empty(sp * N * K, device=gpu)
         C_.gemm2(dy, A, G, 1, 1, 7, None, None, None, 0.0, 0, sp, ws, None)
-        _check(G, G0 + dy.float().t() @ A.float(), 1e-3)
+        _check(G, G0 + dy.float().t() @ A.float(), acc=dy.float().abs().t() @ A.float().abs() + G0.abs(), fp32=True)
 
 
 def test_gemm2_dgelu_fused_dbias(gpu):
@@ -187,8 +221,10 @@ def test_gemm2_dgelu_fused_dbias(gpu):
     C = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
     db = torch.full((N,), 0.5, device=gpu)
     C_.gemm2(A, B, C, 0, 0, 5, None, pre, None, 0.0, 0, 1, None, db)
-    _check(C, (A.float() @ B.float().t()).bfloat16().float() * _gelu_grad(pre.float()))
-    _check(db, 0.5 + C.float().sum(0), 1e-3)
+    a32, gg = A.float() @ B.float().t(), _gelu_grad(pre.float())
+    r = a32.bfloat16().float() * gg
+    _check(C, r, mag=2 * a32.abs() * gg.abs() + r.abs(), acc=2 * _absmm(A, B, 0, 0))
+    _check(db, 0.5 + C.float().sum(0), acc=0.5 + C.float().abs().sum(0), fp32=True)
 
 
 def test_gemm2_gelu_derivative_and_mul_epilogues(gpu):
@@ -201,14 +237,17 @@ def test_gemm2_gelu_derivative_and_mul_epilogues(gpu):
     G = torch.empty_like(D)
     C_.gemm2(A, B, D, 0, 0, 8, bias, None, G, 0.0, 0, 1, None, None)
     y = (A.float() @ B.float().t() + bias.float()).bfloat16().float()
-    _check(G, torch.nn.functional.gelu(y))
-    _check(D, _gelu_grad(y))
+    g, d = torch.nn.functional.gelu(y), _gelu_grad(y)
+    _check(G, g, mag=2 * y.abs() + g.abs())
+    _check(D, d, mag=y.abs() + d.abs())
     dy, W = _mk((M, 768), gpu), _mk((N, 768), gpu, 0.1)
     out = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
     db = torch.zeros(N, device=gpu)
     C_.gemm2(dy, W, out, 0, 0, 9, None, D, None, 0.0, 0, 1, None, db)
-    _check(out, (dy.float() @ W.float().t()).bfloat16().float() * D.float())
-    _check(db, out.float().sum(0), 1e-3)
+    a32 = dy.float() @ W.float().t()
+    r = a32.bfloat16().float() * D.float()
+    _check(out, r, mag=2 * a32.abs() * D.float().abs() + r.abs(), acc=2 * _absmm(dy, W, 0, 0))
+    _check(db, out.float().sum(0), acc=out.float().abs().sum(0), fp32=True)
 
 
 @pytest.mark.parametrize("small", ["0", "1"])
@@ -238,9 +277,13 @@ def test_gemm2_nt_splitk_matches_one_pass(gpu, monkeypatch, M, N, K, splits, epi
                  C2, p, 77, sp, None, db)
         outs.append((C.float(), C2.float() if two else None, db))
     (c1, c21, d1), (cs, c2s, ds) = outs
-    _check(cs, c1)
+    # the split sums differ from the one-pass sum in fp32 order only: one ulp of every rounded intermediate
+    y = (A.float() @ B.float().t() + (bias.float() if epi in (1, 2, 3, 8) else 0.0)).abs()
+    ax = aux.float().abs()
+    mag = 2 * y * (1 + ax) + ax + c1.abs()
+    _check(cs, c1, mag=mag, acc=2 * _absmm(A, B, 0, 0))
     if two:
-        _check(c2s, c21)
+        _check(c2s, c21, mag=mag + c21.abs())
     if d1 is not None:
         torch.testing.assert_close(ds, d1, rtol=2e-2, atol=1e-2 * float(d1.abs().max()) + 1e-3)
 
@@ -293,7 +336,7 @@ def test_gemm2_small_tt_wgrad(gpu, monkeypatch, M, N, K, splits, stages):
     sp = splits or C_.gemm2_splits(M, N, K)
     ws = torch.empty(sp * M * N, device=gpu)
     C_.gemm2(A, B, C, 1, 1, 7, None, None, None, 0.0, 0, sp, ws, None)
-    _check(C, C0 + A.float().t() @ B.float(), 1e-3)
+    _check(C, C0 + A.float().t() @ B.float(), acc=A.float().abs().t() @ B.float().abs() + C0.abs(), fp32=True)
 
 
 
@@ -324,7 +367,7 @@ def test_gemm2_dgrad_reading_w_directly_matches_stored_wt(gpu, M, N, K, epi):
         torch.testing.assert_close(d1, d0, rtol=1e-4, atol=1e-4 * float(d0.abs().max()) + 1e-6)
     ref = dy.float() @ w.float()
     if epi == 0:
-        _check(c1, ref)
+        _check(c1, ref, acc=dy.float().abs() @ w.float().abs())
 
 
 @pytest.mark.parametrize("M,N,K", [(32768, 768, 256), (8292, 3072, 512), (20000, 960, 128), (65536, 2304, 64)])
@@ -357,4 +400,4 @@ def test_gemm2_persistent_matches_one_shot(gpu, monkeypatch, M, N, K, epi):
     if d0 is not None:
         torch.testing.assert_close(d1, d0, rtol=1e-4, atol=1e-4 * float(d0.abs().max()) + 1e-6)
     if epi == 0:
-        _check(c1, A.float() @ B.float().t())
+        _check(c1, A.float() @ B.float().t(), acc=_absmm(A, B, 0, 0))
