@@ -159,17 +159,27 @@ __global__ __launch_bounds__(256, 2) void attn128_bwd_kernel(const bf16_t* __res
     vf[s] = *reinterpret_cast<const bf16x8*>(base + (int64_t)key * ld + 2 * H + 16 * s + 8 * hf);
   }
   const float kb2 = mask ? fmaxf(mask[(int64_t)b * S + key] * kLog2e, -1e30f) : 0.f;
-  // delta[q] = Σ_d dO[q][d]·O[q][d]: thread handles rows (tid>>3) + 32i, chunk tid&7
+  // delta[q] = Σ_d dO[q][d]·O[q][d]: thread handles rows (tid>>3) + 32i, chunk tid&7. O comes from global memory
+  // (loads issued here, under the DMA); dO from its LDS image once the DMA has landed -- dO is read from HBM once
+  // (it used to be read a second time for this pre-pass: 16 of the 144 KiB a (batch, head) moves)
+  u32x4 ov[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int row = (tid >> 3) + 32 * i, c = tid & 7;
+    ov[i] = *reinterpret_cast<const u32x4*>(obase + (int64_t)row * H + c * 8);
+  }
+  if (tid < S) lse_s[tid] = lse2[(int64_t)bh * S + tid];
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
   {
     float part[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int row = (tid >> 3) + 32 * i, c = tid & 7;
-      const u32x4 ov = *reinterpret_cast<const u32x4*>(obase + (int64_t)row * H + c * 8);
-      const u32x4 dv = *reinterpret_cast<const u32x4*>(dobase + (int64_t)row * H + c * 8);
+      const u32x4 dv = *reinterpret_cast<const u32x4*>(dOs + toff(row, c * 8));
       float acc = 0.f;
 #pragma unroll
-      for (int k = 0; k < 4; ++k) acc += lo_bf(dv[k]) * lo_bf(ov[k]) + hi_bf(dv[k]) * hi_bf(ov[k]);
+      for (int k = 0; k < 4; ++k) acc += lo_bf(dv[k]) * lo_bf(ov[i][k]) + hi_bf(dv[k]) * hi_bf(ov[i][k]);
       acc += __shfl_xor(acc, 1, 64);
       acc += __shfl_xor(acc, 2, 64);
       acc += __shfl_xor(acc, 4, 64);
@@ -179,9 +189,7 @@ __global__ __launch_bounds__(256, 2) void attn128_bwd_kernel(const bf16_t* __res
 #pragma unroll
       for (int i = 0; i < 4; ++i) del_s[(tid >> 3) + 32 * i] = part[i];
     }
-    if (tid < S) lse_s[tid] = lse2[(int64_t)bh * S + tid];
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
   f32x16 dk0 = {}, dk1 = {}, dv0 = {}, dv1 = {};
