@@ -97,5 +97,20 @@ __device__ __forceinline__ bf16x8 frag(const bf16_t* img, int rbase, int ks, int
   }
 }
 
+// run-time count for the counted waits (a wave-uniform switch over immediates)
+__device__ __forceinline__ void vmcnt_rt(int n) {
+  switch (n) {
+#define G2_VMC(N) \
+  case N:         \
+    vmcnt<N>();   \
+    break;
+    G2_VMC(0) G2_VMC(1) G2_VMC(2) G2_VMC(3) G2_VMC(4) G2_VMC(5) G2_VMC(6) G2_VMC(7) G2_VMC(8) G2_VMC(9) G2_VMC(10)
+    G2_VMC(11) G2_VMC(12) G2_VMC(13) G2_VMC(14) G2_VMC(15) G2_VMC(16) G2_VMC(17) G2_VMC(18) G2_VMC(19) G2_VMC(20)
+    G2_VMC(21) G2_VMC(22) G2_VMC(23) G2_VMC(24) G2_VMC(25) G2_VMC(26) G2_VMC(27) G2_VMC(28) G2_VMC(29) G2_VMC(30)
+#undef G2_VMC
+    default: vmcnt<0>(); break;  // (never: counts stay <= 30) the strictest wait
+  }
+}
+
 }  // namespace g2
 }  // namespace hsd

@@ -19,7 +19,8 @@
 // * every vector-memory op in the loop is counted by hand: DMA slots (inline asm), the pieces' stores (always issued;
 //   rows past M go to an out-of-range buffer offset that the hardware drops), and one wait per K-tile,
 //   vmcnt(S(s-1) + G + S(s)), retires K-tile s + 1 without waiting for any store.
-// * bias: 128 B per wave per tile by two scalar loads at the tile boundary (lgkm counter, not vm).
+// * bias: 8 B per lane per tile, loaded at the tile's start, used at its end (the wait hipcc puts there counts the
+//   pieces' stores issued since, so the load has long landed).
 // Outputs are bit-identical to gemm2pk / gemm2 (same fragments, same K order per element, same epilogue math):
 // tests/test_gpu_gemm.py::test_gemm2_deferred_epilogue_matches_persistent.
 #include "gemm2_dev.h"
@@ -34,27 +35,10 @@ constexpr int GA = 2, GB = 4, G = GA + GB, G1 = 3;              // DMA slots per
 constexpr int SROWS = 16;
 constexpr int STG = 8 * SROWS * 64;  // staging elements (8 waves x one 16-row pass)
 constexpr int NPIECE = 8;            // pieces per deferred tile: 64 rows x 8 chunks / 64 lanes
-
-typedef __attribute__((ext_vector_type(16))) uint32_t u32x16;
+constexpr int BIAS_KT = NPIECE;      // K-tile of the bias DMA; retired by K-tile BIAS_KT + 2's wait -> nt >= 11
 
 template <int EPI>
 constexpr int stores_per_piece() { return epi_two_out(EPI) ? 2 : 1; }
-
-__device__ __forceinline__ void vmcnt_rt(int n) {
-  switch (n) {
-    case 0: vmcnt<0>(); break;
-    case 1: vmcnt<1>(); break;
-    case 2: vmcnt<2>(); break;
-    case 3: vmcnt<3>(); break;
-    case 4: vmcnt<4>(); break;
-    case 5: vmcnt<5>(); break;
-    case 6: vmcnt<6>(); break;
-    case 7: vmcnt<7>(); break;
-    case 8: vmcnt<8>(); break;
-    case 9: vmcnt<9>(); break;
-    default: vmcnt<10>(); break;
-  }
-}
 
 template <int EPI>
 __global__ __launch_bounds__(512, 1) void gemm2pd_kernel(G2Params p) {
@@ -72,13 +56,29 @@ __global__ __launch_bounds__(512, 1) void gemm2pd_kernel(G2Params p) {
   const int grid = gridDim.x, bid = blockIdx.x;
   const int my_tiles = (ntiles - bid + grid - 1) / grid;
   const int total = my_tiles * nt;  // K-tiles of this workgroup's stream
-  HSD_DASSERT(p.K % BK == 0 && nt >= NPIECE && bid < ntiles && grid % 8 == 0);
+  HSD_DASSERT(p.K % BK == 0 && nt >= BIAS_KT + 3 && bid < ntiles && grid % 8 == 0);
+  // tile order: the XCD-aware remap gives each XCD's 32 workgroups 32 consecutive indices v per round; in groups of
+  // group_m row tiles those are group_m rows x 32/group_m columns (8 x 4: 8 A panels + 4 B panels = 3.1 MB, inside
+  // the XCD's 4 MB L2; row-major: ~3 A panels + all 12 B panels of the FFN weight = 5 MB)
+  const int tiles_m = ntiles / p.tiles_n;
   auto tile_of = [&](int j, int& m0, int& n0) {
     const int L = bid + j * grid;
     const int xcd = L & 7;
     const int v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (L >> 3);
-    m0 = (v / p.tiles_n) * BMD;
-    n0 = (v % p.tiles_n) * BND;
+    int tm, tn;
+    if (p.group_m > 0) {
+      const int per = p.group_m * p.tiles_n;
+      const int g = v / per, first = g * p.group_m;
+      const int gs = min(tiles_m - first, p.group_m);
+      const int w = v - g * per;
+      tm = first + w % gs;
+      tn = w / gs;
+    } else {
+      tm = v / p.tiles_n;
+      tn = v % p.tiles_n;
+    }
+    m0 = tm * BMD;
+    n0 = tn * BND;
   };
   const uint32_t smem_lds = (uint32_t)(size_t)(__attribute__((address_space(3))) bf16_t*)smem;
 
@@ -119,16 +119,18 @@ __global__ __launch_bounds__(512, 1) void gemm2pd_kernel(G2Params p) {
   auto piece = [&](int k) {
     const int pass = k >> 1, half = k & 1;
     if (half == 0) {
-      // the pass's 16 rows (accumulator block `pass`) into the wave's staging slice, 8-B slots XOR-swizzled by row
+      // the pass's 16 rows into the wave's staging slice, 8-B slots XOR-swizzled by row. The passes leave y[0] in
+      // order and the blocks rotate down (register moves): y is never indexed at run time (a run-time index sends
+      // the array to scratch, and a scratch load's vmcnt(0) would drain the operand DMA every piece)
 #pragma unroll
-      for (int ps = 0; ps < 4; ++ps) {
-        if (ps != pass) continue;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int col = ((4 * j + q4) ^ lr) << 2;
-          *reinterpret_cast<u32x2*>(stg + lr * 64 + col) = y[ps][j];
-        }
+      for (int j = 0; j < 4; ++j) {
+        const int col = ((4 * j + q4) ^ lr) << 2;
+        *reinterpret_cast<u32x2*>(stg + lr * 64 + col) = y[0][j];
       }
+#pragma unroll
+      for (int i = 0; i < 3; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) y[i][j] = y[i + 1][j];
       __builtin_amdgcn_wave_barrier();
     }
     const int idx = lane + 64 * half;
@@ -139,12 +141,15 @@ __global__ __launch_bounds__(512, 1) void gemm2pd_kernel(G2Params p) {
     const int m = mw + pass * 16 + row, n = yn0 + wn * 64 + c8 * 8;
     float csum[8];
     epi_chunk<EPI>(o, o2, u32x4{0, 0, 0, 0}, m, n, p, csum);
-    // rows past M: an offset past the buffer's range, which the hardware drops (the store is still issued, so the
-    // vm counter sees exactly SP stores per piece)
-    const uint32_t bo = m < p.M ? (uint32_t)(((int64_t)(m - mw) * p.ldc + n) * 2) : 0x7FFFFFF0u;
+    // rows past M: the buffer range ends at row M, so the hardware drops those stores whole while they are still
+    // issued (the vm counter sees exactly SP stores per piece). Range = (M - mw) rows of ldc elements (0 when the
+    // wave's 64 rows all lie past M); the row offset of an in-range store is < 64 rows.
+    const int vrows = max(0, min(64, p.M - mw));
+    const uint32_t nb = (uint32_t)((int64_t)(vrows > 0 ? vrows - 1 : 0) * p.ldc * 2 + (vrows > 0 ? (int64_t)p.N * 2 : 0));
+    const uint32_t bo = (uint32_t)(((int64_t)(m - mw) * p.ldc + n) * 2);
     bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
-    st16nt(wave_rsrc(C + (int64_t)mw * p.ldc), bo, o);
-    if constexpr (SP == 2) st16nt(wave_rsrc(p.C2 + (int64_t)mw * p.ldc), bo, o2);
+    st16nt(wave_rsrc_n(C + (int64_t)mw * p.ldc, nb), bo, o);
+    if constexpr (SP == 2) st16nt(wave_rsrc_n(p.C2 + (int64_t)mw * p.ldc, nb), bo, o2);
   };
 
   // ---- compute stream
@@ -156,6 +161,11 @@ __global__ __launch_bounds__(512, 1) void gemm2pd_kernel(G2Params p) {
   int cj = 0, ck = 0;  // compute tile / K-tile
   int cm0, cn0;
   tile_of(0, cm0, cn0);
+  // the compute tile's bias: the wave's 64 columns (128 B) LDS-DMA'd by lanes 0..7 into the start of its staging
+  // slice in K-tile BIAS_KT, when no piece uses the slice; counted like the pieces' stores, retired by the waits of
+  // the K-tiles after it and read at the tile's end. (A vector load into registers made hipcc, which cannot count
+  // K-tiles across the loop back-edge, wait vmcnt(0) at the tile boundary and drain the operand DMA.)
+  const uint32_t stg_lds = smem_lds + (uint32_t)(NSTG * STAGE + wave * (SROWS * 64)) * 2u;
   dma_tile();
   // prologue: stream K-tiles 0 and 1 (my_tiles >= 1 and nt >= 8, so both exist)
   dma_part(0, 0, G);
@@ -172,7 +182,8 @@ __global__ __launch_bounds__(512, 1) void gemm2pd_kernel(G2Params p) {
     const bf16_t* cB = cA + TA;
     const bool dma_on = s + 2 < total;
     const bool has_piece = cj > 0 && ck < NPIECE;
-    const int s_cur = has_piece ? SP : 0;
+    const bool bias_dma = epi_bias(EPI) && ck == BIAS_KT;
+    const int s_cur = has_piece ? SP : (bias_dma ? 1 : 0);
     bf16x8 fa[4][2], fb[2][2];
     // P1: A (all four row blocks) + B cols 0..31, first DMA slots of stream K-tile s + 2
 #pragma unroll
@@ -206,6 +217,14 @@ __global__ __launch_bounds__(512, 1) void gemm2pd_kernel(G2Params p) {
       dma_advance();
     }
     if (has_piece) piece(ck);
+    if (bias_dma) {
+      if (lane < 8) {
+        const uint64_t ba = (uint64_t)(p.bias + cn0 + bcol);
+        const bf16_t* bp = (const bf16_t*)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(ba >> 32)) << 32) |
+                                           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)ba));
+        dma_lds_asm(bp, (uint32_t)lane * 16u, stg_lds);
+      }
+    }
     vmcnt_rt(s_prev + (dma_on ? G : 0) + s_cur);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     G2_BARRIER();
@@ -223,30 +242,14 @@ __global__ __launch_bounds__(512, 1) void gemm2pd_kernel(G2Params p) {
     if (++ck == nt) {
       // tile boundary: bf16(acc + bias) -> the deferred registers (its pieces of the previous tile all ran in K-tiles
       // 0..7 of this one), next tile
-      f32x4 bv[4] = {{0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}, {0.f, 0.f, 0.f, 0.f}};
-      if constexpr (epi_bias(EPI)) {
-        // 64 bias values of the wave's columns: two scalar loads (lgkm counter), then each lane picks its columns
-        // 16j + 4(lane>>4) .. +3 = dwords 8j + 2(lane>>4), +1
-        const uint64_t ba = (uint64_t)(p.bias + cn0 + bcol);
-        const bf16_t* bp = (const bf16_t*)(((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(ba >> 32)) << 32) |
-                                           (uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)ba));
-        u32x16 b0, b1;
-        asm volatile("s_load_dwordx16 %0, %2, 0x0\n\ts_load_dwordx16 %1, %2, 0x40\n\ts_waitcnt lgkmcnt(0)"
-                     : "=s"(b0), "=s"(b1)
-                     : "s"(bp)
-                     : "memory");
+      f32x4 bv[4];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          uint32_t w0, w1;
-          if (j < 2) {
-            w0 = q4 == 0 ? b0[8 * j] : q4 == 1 ? b0[8 * j + 2] : q4 == 2 ? b0[8 * j + 4] : b0[8 * j + 6];
-            w1 = q4 == 0 ? b0[8 * j + 1] : q4 == 1 ? b0[8 * j + 3] : q4 == 2 ? b0[8 * j + 5] : b0[8 * j + 7];
-          } else {
-            const int jj = j - 2;
-            w0 = q4 == 0 ? b1[8 * jj] : q4 == 1 ? b1[8 * jj + 2] : q4 == 2 ? b1[8 * jj + 4] : b1[8 * jj + 6];
-            w1 = q4 == 0 ? b1[8 * jj + 1] : q4 == 1 ? b1[8 * jj + 3] : q4 == 2 ? b1[8 * jj + 5] : b1[8 * jj + 7];
-          }
-          bv[j] = f32x4{lo_bf(w0), hi_bf(w0), lo_bf(w1), hi_bf(w1)};
+      for (int j = 0; j < 4; ++j) {
+        if constexpr (epi_bias(EPI)) {
+          const u32x2 b = *reinterpret_cast<const u32x2*>(stg + 16 * j + 4 * q4);
+          bv[j] = f32x4{lo_bf(b.x), hi_bf(b.x), lo_bf(b.y), hi_bf(b.y)};
+        } else {
+          bv[j] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
       }
 #pragma unroll
@@ -276,7 +279,7 @@ __global__ __launch_bounds__(512, 1) void gemm2pd_kernel(G2Params p) {
 
 bool gemm2pd_supported(int epi, int M, int N, int K) {
   return (epi == E2_STORE || epi == E2_BIAS || epi == E2_BIAS_GELU || epi == E2_BIAS_GELU_D) && N % 256 == 0 &&
-         K % 64 == 0 && K / 64 >= g2::pd::NPIECE && M >= 1;
+         K % 64 == 0 && K / 64 >= g2::pd::BIAS_KT + 3 && M >= 1;
 }
 
 // grid: one workgroup per CU (multiple of 8), at most one per tile. bias is read by 128-B scalar loads per wave
@@ -287,6 +290,7 @@ void launch_gemm2pd(int epi, const G2Params& p0, int num_cus, hipStream_t st) {
   p.tiles_n = p.N / g2::pd::BND;
   p.ntiles = tiles_m * p.tiles_n;
   p.kps = p.K;
+  p.group_m = HSD_KNOB("HSD_G2_GROUP", 8);
   int grid = num_cus & ~7;
   if (p.ntiles < grid) grid = p.ntiles & ~7;
   if (grid < 8) abort();  // tiny grids: the caller keeps gemm2pk / gemm2
