@@ -642,306 +642,6 @@ __global__ __launch_bounds__(512, 1) void gemm2pk_kernel(G2Params p) {
 }
 
 // ------------------------------------------------------------------------------------------------
-// gemm2pk2: gemm2pk with HALF of each tile's epilogue deferred under the next tile's main loop (BN 256, epilogues
-// without an aux operand: plain store, bias, bias + GELU [+ GELU']).
-//
-// All 256 CUs run their epilogues at the same moment, and stores from every CU at once drain at the chip's ~5.9 TB/s
-// write rate = 23 GB/s per CU, against ~130 GB/s for one CU alone (tools/store_probe.cpp,
-// profiles/store_probe_r4.jsonl): the FFN1 forward's 256 KiB of stores per tile take ~20k cycles + a ~10k seam
-// against a 33k-cycle main loop. A whole 256 x 256 tile cannot wait in registers or LDS while the next one
-// accumulates, half of it can: rows 64..127 of each wave tile leave the accumulators as bf16(acc + bias) in 32
-// registers, and the next tile's main loop runs their epilogue in 8 pieces in P4 of K-tiles 0..7 (P4 issues no LDS
-// reads: the piece's VALU work runs beside the partner wave group's MFMA cluster). Rows 0..63 take the normal
-// epilogue. (A 128 x 256-tile kernel that deferred the whole epilogue was 1.5x slower: its main loop needs 1.5x the
-// operand bytes per FLOP; profiles/gemm2pd_rejected_r4.jsonl.)
-// Counted waits (hipcc sees none of the DMA): K-tile 1 of the next tile is prefetched WHOLE before the epilogue, so
-// the main loop's first wait (P4 of K-tile 0) does not wait for the epilogue's stores; they have until P4 of K-tile 1.
-// Piece stores are always issued (rows past M dropped by the buffer range) and counted in P4's wait.
-template <int EPI>
-__global__ __launch_bounds__(512, 1) void gemm2pk2_kernel(G2Params p) {
-  static_assert(EPI == E2_STORE || EPI == E2_BIAS || EPI == E2_BIAS_GELU || EPI == E2_BIAS_GELU_D, "no aux");
-  constexpr int BN = 256, WN = 64, NREP = 4, NB0 = 2, NB1 = 2;
-  constexpr int TA = BM * 64, STAGE = TA + BN * 64;
-  constexpr int GA = 4, GB = 4, G = GA + GB, D0 = 2, E1 = D0 + (G - D0 + 1) / 2;
-  constexpr int PB = 2;
-  constexpr int STG = 8 * 16 * PB * epi_srow<BN>();
-  constexpr int ITER = epi_iter<BN, PB>();
-  constexpr int SP = epi_two_out(EPI) ? 2 : 1;    // stores per piece
-  constexpr int NSTH = (4 / PB) * ITER * SP;       // stores of the immediate half epilogue per wave
-  constexpr int NPIECE = 8;                        // 64 rows x 8 chunks / 64 lanes
-  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * STAGE + STG];
-  static_assert(sizeof(smem) <= 160 * 1024, "LDS");
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 2, wn = wave & 3;
-  const int ntiles = p.ntiles, q8 = ntiles >> 3, r8 = ntiles & 7;
-  const int nt = p.K / BK;
-  HSD_DASSERT(p.K % BK == 0 && nt > NPIECE && (gridDim.x == (unsigned)ntiles || gridDim.x % 8 == 0));
-  auto tile_of = [&](int L, int& m0, int& n0) {
-    const int xcd = L & 7;
-    const int v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (L >> 3);
-    m0 = (v / p.tiles_n) * BM;
-    n0 = (v % p.tiles_n) * BN;
-  };
-  const uint32_t smem_lds = (uint32_t)(size_t)(__attribute__((address_space(3))) bf16_t*)smem;
-  uint32_t aoff[G];
-  int m0, n0;
-  auto set_tile = [&](int L) {
-    tile_of(L, m0, n0);
-#pragma unroll
-    for (int q = 0; q < G; ++q)
-      aoff[q] = q < GA ? lane_off<0>(p.lda, m0, p.M, wave * GA + q, lane)
-                       : lane_off<0>(p.ldb, n0, p.N, wave * GB + (q - GA), lane);
-  };
-  auto dma_slot = [&](int q, bf16_t* stage, int k0) {
-    const uint32_t st = smem_lds + (uint32_t)(stage - smem) * 2u;
-    if (q < GA) dma_lds_asm(asm_base<0>(p.A, p.lda, m0, k0), aoff[q], st + (wave * GA + q) * 1024u);
-    else dma_lds_asm(asm_base<0>(p.B, p.ldb, n0, k0), aoff[q], st + (TA + (wave * GB + (q - GA)) * 512) * 2u);
-  };
-  // K-tiles 0 AND 1 whole (nt > 8)
-  auto prologue = [&]() {
-#pragma unroll
-    for (int q = 0; q < G; ++q) dma_slot(q, smem, 0);
-#pragma unroll
-    for (int q = 0; q < G; ++q) dma_slot(q, smem + STAGE, BK);
-  };
-
-  // ---- deferred half: rows 64..127 of the previous tile's wave tile, bf16(acc + bias). Rows 64..95 wait in the
-  // wave's staging slice (written at the seam), rows 96..127 in 16 registers until piece 4 stages them.
-  u32x2 y[2][NREP];
-  int ym0 = 0, yn0 = 0;
-  bf16_t* const stg = smem + 2 * STAGE + wave * (16 * PB * epi_srow<BN>());
-  const int q4 = lane >> 4, lr = lane & 15;
-  const int arow = wm * 128, bcol = wn * WN;
-  auto stage_y = [&](const u32x2 (&v)[2][NREP]) {
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int j = 0; j < NREP; ++j) {
-        const int row = 16 * i + lr;
-        *reinterpret_cast<u32x2*>(stg + row * 64 + (((4 * j + q4) ^ (row & 15)) << 2)) = v[i][j];
-      }
-    __builtin_amdgcn_wave_barrier();
-  };
-  auto piece = [&](int k) {
-    const int pass = k >> 2, it = k & 3;
-    if (it == 0 && pass == 1) stage_y(y);
-    // the lane's addresses are recomputed here from an opaque copy of the lane id: hoisted out of the main loop they
-    // would hold ~20 more registers across it (spilled: a scratch reload's wait drains the DMA in flight)
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
-    const int idx = ln + 64 * it;
-    const int row = idx >> 3, c8 = idx & 7, hs = row & 15;
-    const u32x4 t = *reinterpret_cast<const u32x4*>(stg + row * 64 + ((c8 ^ (hs >> 1)) << 3));
-    u32x4 o = (hs & 1) ? u32x4{t.z, t.w, t.x, t.y} : t, o2;
-    const int mw = ym0 + arow + 64;  // the deferred rows
-    const int m = mw + 32 * pass + row, n = yn0 + bcol + c8 * 8;
-    float csum[8];
-    epi_chunk<EPI>(o, o2, u32x4{0, 0, 0, 0}, m, n, p, csum);
-    // always issued (the vm count needs exactly SP stores): rows past M fall outside the buffer range and are dropped
-    const int vrows = max(0, min(64, p.M - mw));
-    const uint32_t nb = vrows > 0 ? (uint32_t)(((int64_t)(vrows - 1) * p.ldc + p.N) * 2) : 0u;
-    const uint32_t bo = (uint32_t)(((int64_t)(m - mw) * p.ldc + n) * 2);
-    st16nt(wave_rsrc_n(reinterpret_cast<bf16_t*>(p.C) + (int64_t)mw * p.ldc, nb), bo, o);
-    if constexpr (SP == 2) st16nt(wave_rsrc_n(p.C2 + (int64_t)mw * p.ldc, nb), bo, o2);
-    if (it == 3) __builtin_amdgcn_wave_barrier();  // the pass's reads before piece 4 restages
-  };
-
-  // ---- tile walk (static, or the dynamic queue as gemm2pk)
-  int* const tq = p.tq;
-  const int xg = tq != nullptr ? tq_xcc() : 0;
-  uint32_t dead = 0;
-  int* const bcast = reinterpret_cast<int*>(smem + STAGE + 1024);
-  int L = blockIdx.x;
-  if (tq != nullptr) {
-    if (wave == 0 && lane == 0) *bcast = tq_claim(tq, xg, dead, ntiles);
-    __syncthreads();
-    L = __builtin_amdgcn_readfirstlane(*bcast);
-    if (L >= ntiles) {
-      if (wave == 0 && lane == 0) tq_exit(tq);
-      return;
-    }
-  }
-  set_tile(L);
-  prologue();
-  vmcnt<0>();
-  G2_BARRIER();
-  f32x4 acc[8][NREP];
-  bool has_def = false;
-  int nst_prev = 0;  // immediate-epilogue stores this wave issued after the current tile's prologue
-  for (;;) {
-    int pre = 0;
-    const bool claim = tq != nullptr && !(__builtin_amdgcn_readfirstlane(dead) & (1u << xg));
-    if (claim && wave == 0 && lane == 0) pre = tq_fetch(tq, xg);
-    const int extra = claim && wave == 0 ? 1 : 0;  // the claim atomic counts on wave 0's vm counter
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < NREP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-    // ---- main loop (gemm2pk's staggered SYNC 4 schedule; K-tile 1 prefetched by the prologue; pieces in P4)
-    bf16x8 fa[4][2], fb0[NB0][2], fb1[NB1][2];
-    // K-tile 0 issues no DMA of K-tile 1 (the prologue did) and its wait also counts the ops issued after K-tile 1's
-    // slots: the seam's stores and wave 0's claim (loop-carried, so K-tile 0 is not peeled off the loop)
-    int c0 = nst_prev + extra, d1 = 0;
-    if (wm == 1) G2_BARRIER();
-    for (int t = 0; t < nt; ++t) {
-      const bf16_t* cA = smem + (t & 1) * STAGE;
-      const bf16_t* cB = cA + TA;
-      bf16_t* nS = smem + ((t + 1) & 1) * STAGE;
-      const bool n1 = t + 1 < nt && d1 != 0, n2 = t + 2 < nt;
-      const int k1 = (t + 1) * BK, k2 = (t + 2) * BK;
-#pragma unroll
-      for (int j = 0; j < NB0; ++j)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) fb0[j][ks] = frag<0>(cB, bcol + 16 * j, ks, lane);
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<0>(cA, arow + 16 * i, ks, lane);
-      if (n1) {
-#pragma unroll
-        for (int q = D0; q < E1; ++q) dma_slot(q, nS, k1);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      G2_BARRIER();
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < NB0; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][ks], fa[i][ks], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-      G2_BARRIER();
-#pragma unroll
-      for (int j = 0; j < NB1; ++j)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) fb1[j][ks] = frag<0>(cB, bcol + 16 * (NB0 + j), ks, lane);
-      if (n1) {
-#pragma unroll
-        for (int q = E1; q < G; ++q) dma_slot(q, nS, k1);
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      G2_BARRIER();
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < NB1; ++j)
-            acc[i][NB0 + j] =
-                __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][ks], fa[i][ks], acc[i][NB0 + j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-      G2_BARRIER();
-#pragma unroll
-      for (int i = 0; i < 4; ++i)
-#pragma unroll
-        for (int ks = 0; ks < 2; ++ks) fa[i][ks] = frag<0>(cA, arow + 64 + 16 * i, ks, lane);
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      G2_BARRIER();
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < NB1; ++j)
-            acc[4 + i][NB0 + j] =
-                __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb1[j][ks], fa[i][ks], acc[4 + i][NB0 + j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-      G2_BARRIER();
-      // P4: D0 slots of K-tile t+2 into this stage, one deferred piece, retire K-tile t+1: every op issued after
-      // K-tile t+1's last slot may stay in flight -- the D0 slots, the piece's stores, and at t = 0 (K-tile 1 came
-      // with the prologue) the previous tile's immediate-epilogue stores and wave 0's claim atomic
-      if (n2) {
-#pragma unroll
-        for (int q = 0; q < D0; ++q) dma_slot(q, const_cast<bf16_t*>(cA), k2);
-      }
-      const bool pc = has_def && t < NPIECE;
-      if (pc) piece(t);
-      vmcnt_rt((n2 ? D0 : 0) + (pc ? SP : 0) + c0);
-      c0 = 0;
-      d1 = 1;
-      asm volatile("" : "+s"(c0), "+s"(d1));  // opaque: hipcc would peel K-tile 0 off the loop
-      G2_BARRIER();
-      __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-      for (int ks = 0; ks < 2; ++ks)
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < NB0; ++j)
-            acc[4 + i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fb0[j][ks], fa[i][ks], acc[4 + i][j], 0, 0, 0);
-      __builtin_amdgcn_s_setprio(0);
-      G2_BARRIER();
-    }
-    if (wm == 0) G2_BARRIER();
-    // ---- next tile
-    if (tq != nullptr) {
-      if (wave == 0 && lane == 0) {
-        int Ln = dead & (1u << xg) ? ntiles : xg + 8 * pre;
-        if (Ln >= ntiles) {
-          dead |= 1u << xg;
-          Ln = tq_claim(tq, xg, dead, ntiles);
-        }
-        *bcast = Ln;
-      }
-      __syncthreads();  // nothing in flight: the last K-tile retired everything (nt > 8: no piece there)
-      L = __builtin_amdgcn_readfirstlane(*bcast);
-    } else {
-      L += gridDim.x;
-    }
-    const int mw = m0 + arow, nw = n0 + bcol;
-    const int cm0 = m0, cn0 = n0;
-    f32x4 bv[NREP];
-    u32x4 xv0[ITER];
-    epi_bias_regs<EPI, BN>(bv, p, lane, nw);
-    epi_aux_regs<EPI, BN, PB>(xv0, p, lane, mw, nw, 0);
-    const bool more = L < ntiles;
-    if (!more) {
-      epilogue_bf16<EPI, BN, 8, PB, true>(acc, p, smem + 2 * STAGE, wave, lane, mw, nw, bv, xv0);
-      if (tq != nullptr && wave == 0 && lane == 0) tq_exit(tq);
-      break;
-    }
-    set_tile(L);
-    prologue();
-    // rows 0..63 now; rows 64..127 deferred (64..95 staged at once, 96..127 in registers)
-    epilogue_bf16<EPI, BN, 4, PB, true>(reinterpret_cast<f32x4(&)[4][NREP]>(acc), p, smem + 2 * STAGE, wave, lane,
-                                        mw, nw, bv, xv0);
-    {
-      u32x2 y0[2][NREP];
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < NREP; ++j) {
-          f32x4 v = acc[4 + i][j], w = acc[6 + i][j];
-          if constexpr (epi_bias(EPI)) {
-            v += bv[j];
-            w += bv[j];
-          }
-          y0[i][j] = pack4(v);
-          y[i][j] = pack4(w);
-        }
-      stage_y(y0);
-    }
-    ym0 = cm0;
-    yn0 = cn0;
-    has_def = true;
-    // a wave whose first 64 rows are all inside M issued exactly NSTH stores after the prologue; an edge wave may
-    // have issued fewer, so it counts none (a stricter wait)
-    nst_prev = mw + 64 <= p.M ? NSTH : 0;
-    // retire K-tile 0 of the next tile (its G slots are the oldest of the prologue's 2G)
-    if (nst_prev == NSTH) vmcnt<G + NSTH>();
-    else vmcnt<G>();
-    G2_BARRIER();
-  }
-  // the last tile's epilogue ran whole; its predecessor's deferred half ran in its main loop
-  vmcnt<0>();
-}
-
-// ------------------------------------------------------------------------------------------------
 // fp8 persistent NT GEMM (gemm8pk): gemm2pk with v_mfma_scale_f32_16x16x128_f8f6f4 (unit block scales, twice the bf16
 // MFMA rate). A K-tile of 128 fp8 values is the same 128-B row as 64 bf16 values, so an fp8 [M][K] operand is handled
 // as a "bf16" [M][K/2] one: same LDS images, DMA slots (inline asm), staggered 4-phase schedule, tile walk, seam and
@@ -1448,15 +1148,6 @@ static int* g2_tq_slot(hipStream_t st) {
   return base[dev] + (size_t)(next++ % kSlots) * kTqInts;
 }
 
-// gemm2pd (gemm2pd.hip): persistent 128 x 256 tiles with the epilogue under the next tile's main loop, for the
-// epilogues without an aux operand. HSD_G2_PD=1 selects it where supported (A/B: tools/env_ab_gemm.py).
-bool gemm2pd_supported(int epi, int M, int N, int K);
-void launch_gemm2pd(int epi, const G2Params& p0, int num_cus, hipStream_t st);
-static bool g2_pd_use(int epi, int M, int N, int K) {
-  if (!HSD_KNOB("HSD_G2_PD", 0) || !gemm2pd_supported(epi, M, N, K)) return false;
-  return ((M + 127) / 128) * (N / 256) >= 256;
-}
-
 static bool g2_persist(int tiles) {
   if (!HSD_KNOB("HSD_G2_PERSIST", 1)) return false;
   return tiles > (g2_num_cus() & ~7);
@@ -1474,28 +1165,6 @@ static void g2pk_launch(const G2Params& p0, hipStream_t st) {
   const int grid = std::min(p.ntiles, HSD_KNOB("HSD_G2_GRID", g2_num_cus() & ~7));
   p.tq = g2_tq_slot(st);
   hipLaunchKernelGGL((g2::gemm2pk_kernel<EPI, BN>), dim3(grid), dim3(512), 0, st, p);
-  HSD_CHECK_LAUNCH();
-}
-
-// gemm2pk2_kernel (half the epilogue deferred under the next tile's main loop): HSD_G2_PK2=1 (A/B:
-// tools/env_ab_gemm.py), BN 256, epilogues without an aux operand, more than 8 K-tiles.
-static bool g2_pk2_use(int epi, int K) {
-  if (!HSD_KNOB("HSD_G2_PK2", 0)) return false;
-  return (epi == E2_STORE || epi == E2_BIAS || epi == E2_BIAS_GELU || epi == E2_BIAS_GELU_D) && K % g2::BK == 0 &&
-         K / g2::BK > 8;
-}
-
-template <int EPI>
-static void g2pk2_launch(const G2Params& p0, hipStream_t st) {
-  G2Params p = p0;
-  const int tiles_m = (p.M + g2::BM - 1) / g2::BM;
-  p.tiles_n = p.N / 256;
-  p.ntiles = tiles_m * p.tiles_n;
-  p.kps = p.K;
-  if (p.K % g2::BK || p.K / g2::BK <= 8 || p.N % 256 || p.ldc < p.N) abort();
-  const int grid = std::min(p.ntiles, HSD_KNOB("HSD_G2_GRID", g2_num_cus() & ~7));
-  p.tq = g2_tq_slot(st);
-  hipLaunchKernelGGL((g2::gemm2pk2_kernel<EPI>), dim3(grid), dim3(512), 0, st, p);
   HSD_CHECK_LAUNCH();
 }
 
@@ -1757,19 +1426,6 @@ static void launch_nt(const G2Params& p, int epi, int M, int N, int K, int split
       bn = 256;
     }
     const bool pk = LB == 0 && g2_persist((M + 255) / 256 * (N / bn));
-    if (pk && bn == 256 && dbias == nullptr && g2_pd_use(epi, M, N, K)) {
-      launch_gemm2pd(epi, p, g2_num_cus(), st);
-      return;
-    }
-    if (pk && bn == 256 && dbias == nullptr && g2_pk2_use(epi, K)) {
-      switch (epi) {
-        case E2_STORE: g2pk2_launch<E2_STORE>(p, st); return;
-        case E2_BIAS: g2pk2_launch<E2_BIAS>(p, st); return;
-        case E2_BIAS_GELU: g2pk2_launch<E2_BIAS_GELU>(p, st); return;
-        case E2_BIAS_GELU_D: g2pk2_launch<E2_BIAS_GELU_D>(p, st); return;
-        default: abort();
-      }
-    }
 #define G2_NT(E)                                                     \
   case E:                                                            \
     if (pk) {                                                        \

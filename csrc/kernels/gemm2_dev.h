@@ -1,4 +1,4 @@
-// Device helpers shared by the bf16 MFMA GEMM kernels (gemm2.hip, gemm2pd.hip): LDS-DMA slots of the operand tile
+// Device helpers shared by the bf16 MFMA GEMM kernels (gemm2.hip): LDS-DMA slots of the operand tile
 // images (builtin and inline-asm forms) and the 16x16x32 fragment reads. Image layouts: gemm2.hip header.
 #pragma once
 #include "gemm_common.h"
@@ -94,21 +94,6 @@ __device__ __forceinline__ bf16x8 frag(const bf16_t* img, int rbase, int ks, int
     r[0] = lo[0]; r[1] = lo[1]; r[2] = lo[2]; r[3] = lo[3];
     r[4] = hi[0]; r[5] = hi[1]; r[6] = hi[2]; r[7] = hi[3];
     return r;
-  }
-}
-
-// run-time count for the counted waits (a wave-uniform switch over immediates)
-__device__ __forceinline__ void vmcnt_rt(int n) {
-  switch (n) {
-#define G2_VMC(N) \
-  case N:         \
-    vmcnt<N>();   \
-    break;
-    G2_VMC(0) G2_VMC(1) G2_VMC(2) G2_VMC(3) G2_VMC(4) G2_VMC(5) G2_VMC(6) G2_VMC(7) G2_VMC(8) G2_VMC(9) G2_VMC(10)
-    G2_VMC(11) G2_VMC(12) G2_VMC(13) G2_VMC(14) G2_VMC(15) G2_VMC(16) G2_VMC(17) G2_VMC(18) G2_VMC(19) G2_VMC(20)
-    G2_VMC(21) G2_VMC(22) G2_VMC(23) G2_VMC(24) G2_VMC(25) G2_VMC(26) G2_VMC(27) G2_VMC(28) G2_VMC(29) G2_VMC(30)
-#undef G2_VMC
-    default: vmcnt<0>(); break;  // (never: counts stay <= 30) the strictest wait
   }
 }
 

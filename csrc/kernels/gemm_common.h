@@ -46,8 +46,6 @@ struct G2Params {
   int q8_fmt;
   // persistent kernels: dynamic tile queue (tq_* below; one ring slot per launch), nullptr = static tile walk
   int* tq;
-  // gemm2pd: tile order in groups of group_m row tiles (0 = row-major)
-  int group_m;
 };
 
 // ---- dynamic tile queue of the persistent NT GEMMs (gemm2pk / gemm8pk) ----------------------------------------------
@@ -98,16 +96,6 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc(const void* ptr) {
   const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
   const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
   return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0, 0x7FFFFFFF, 0x00020000);
-}
-
-// Same with an explicit range: every access at byte offset >= nbytes from `ptr` is dropped by the hardware (all of a
-// 16-B access must lie past the range: the check is per dword, so a store straddling the end writes its first dwords).
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t wave_rsrc_n(const void* ptr, uint32_t nbytes) {
-  const uint64_t a = (uint64_t)ptr;
-  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-  return __builtin_amdgcn_make_buffer_rsrc((void*)(((uint64_t)hi << 32) | lo), 0,
-                                           (int)__builtin_amdgcn_readfirstlane(nbytes), 0x00020000);
 }
 
 // 16-B non-temporal buffer store (cache policy nt). The bf16 GEMM epilogues store through it: plain stores
@@ -282,9 +270,6 @@ __device__ __forceinline__ void epilogue_bf16(f32x4 (&acc)[MB][BN / 64], const G
   static_assert(MB == 4 || MB == 8, "64 or 128 rows per wave");
   static_assert(PB == 2 || PB == 4, "32- or 64-row staging passes");
   constexpr int WN = BN / 4, NREP = WN / 16;
-  // lane-derived addresses come from an opaque copy of the lane id, so a persistent kernel cannot hoist them out of
-  // its tile loop (they would be held, or spilled, across the main loop; a spill reload's wait drains the DMA)
-  asm volatile("" : "+v"(lane));
   const int q4 = lane >> 4, lr = lane & 15;
   // stage bf16(acc [+ bias]) through a wave-private LDS slice ([16·PB rows][SROW]), then write whole
   // rows with 16-B lanes: each lane owns 8 consecutive n of one m.

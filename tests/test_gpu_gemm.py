@@ -402,61 +402,3 @@ def test_gemm2_persistent_matches_one_shot(gpu, monkeypatch, M, N, K, epi):
         torch.testing.assert_close(d1, d0, rtol=1e-4, atol=1e-4 * float(d0.abs().max()) + 1e-6)
     if epi == 0:
         _check(c1, A.float() @ B.float().t(), acc=_absmm(A, B, 0, 0))
-
-
-@pytest.mark.parametrize("M,N,K,dyn", [(16384, 3072, 768, "1"), (12040, 2304, 768, "1"), (12100, 2304, 768, "0"),
-                                       (32768, 768, 3072, "1"), (33000, 768, 1024, "0")])
-@pytest.mark.parametrize("epi", [0, 1, 2, 8])
-def test_gemm2_half_deferred_epilogue_matches_persistent(gpu, monkeypatch, M, N, K, dyn, epi):
-    """gemm2pk2 (256 x 256 persistent tiles, rows 64..127 of each wave tile finished under the next tile's main loop,
-    HSD_G2_PK2=1) == gemm2pk bit for bit, static and dynamic tile walks. M = 12040 / 12100 / 33000 put the M edge in
-    the first half (no immediate stores counted), in the deferred half, and past a whole wave tile."""
-    torch.manual_seed(61 + epi)
-    C_ = _C()
-    A, B = _mk((M, K), gpu), _mk((N, K), gpu, 0.05)
-    bias = _mk((N,), gpu)
-    two = epi in (2, 8)
-    outs = []
-    monkeypatch.setenv("HSD_G2_SPLITK", "1")
-    monkeypatch.setenv("HSD_G2_DYN", dyn)
-    for v in ("0", "1"):
-        monkeypatch.setenv("HSD_G2_PK2", v)
-        C = torch.full((M, N), 7.0, device=gpu, dtype=torch.bfloat16)
-        C2 = torch.full_like(C, 7.0) if two else None
-        C_.gemm2(A, B, C, 0, 0, epi, bias if epi in (1, 2, 8) else None, None, C2, 0.0, 0, 0, None, None)
-        torch.cuda.synchronize()
-        outs.append((C, C2))
-    (c0, c20), (c1, c21) = outs
-    assert torch.equal(c0, c1)
-    if two:
-        assert torch.equal(c20, c21)
-    if epi == 0:
-        _check(c1, A.float() @ B.float().t(), acc=_absmm(A, B, 0, 0))
-
-
-@pytest.mark.parametrize("M,N,K", [(16384, 3072, 768), (12000, 2304, 768), (32768, 768, 3072), (33000, 256, 512)])
-@pytest.mark.parametrize("epi", [0, 1, 2, 8])
-def test_gemm2_deferred_epilogue_matches_persistent(gpu, monkeypatch, M, N, K, epi):
-    """gemm2pd (128 x 256 persistent tiles, each tile's epilogue run in pieces under the next tile's main loop,
-    HSD_G2_PD=1) == the 256 x 256 persistent kernel bit for bit: same fragments and K order per element, same
-    epilogue math; rows past M (M = 12000, 33000) are dropped by the buffer range check."""
-    torch.manual_seed(51 + epi)
-    C_ = _C()
-    A, B = _mk((M, K), gpu), _mk((N, K), gpu, 0.05)
-    bias = _mk((N,), gpu)
-    two = epi in (2, 8)
-    outs = []
-    monkeypatch.setenv("HSD_G2_SPLITK", "1")
-    for pd in ("0", "1"):
-        monkeypatch.setenv("HSD_G2_PD", pd)
-        C = torch.full((M, N), 7.0, device=gpu, dtype=torch.bfloat16)
-        C2 = torch.full_like(C, 7.0) if two else None
-        C_.gemm2(A, B, C, 0, 0, epi, bias if epi in (1, 2, 8) else None, None, C2, 0.0, 0, 0, None, None)
-        torch.cuda.synchronize()
-        outs.append((C, C2))
-    (c0, c20), (c1, c21) = outs
-    assert torch.equal(c0, c1)
-    if two:
-        assert torch.equal(c20, c21)
-    if epi == 0:
-        _check(c1, A.float() @ B.float().t(), acc=_absmm(A, B, 0, 0))
