@@ -75,6 +75,30 @@ _WGRAD_CXX = _os.environ.get("HSD_WGRAD_CXX", "1") == "1"
 _SIDE = {}
 _STASH = []
 _JOIN_QUEUED = [False]
+# HIP-graph capture (train/graph.py): the capture stream the side stream forks from and joins back to (autograd's
+# end-of-backward callback runs with the device's default stream current, not the capture stream), and whether this
+# capture forked it. HSD_GRAPH_SIDE=0: captured steps keep every weight gradient on the capture stream (round 3).
+_CAPTURE = {"parent": None, "forked": False}
+_GRAPH_SIDE = _os.environ.get("HSD_GRAPH_SIDE", "1") == "1"
+
+
+def begin_capture(parent) -> None:
+    """Called by a graph capture before its forward: the wgrad side stream becomes a branch of the capture."""
+    _CAPTURE["parent"], _CAPTURE["forked"] = parent, False
+
+
+CAPTURES_WITH_SIDE_STREAM = [0]  # captures that branched the side stream (tests/test_gpu_graph.py)
+
+
+def end_capture() -> None:
+    if _CAPTURE["forked"]:
+        CAPTURES_WITH_SIDE_STREAM[0] += 1
+    _CAPTURE["parent"], _CAPTURE["forked"] = None, False
+
+
+def side_stream_in_capture() -> bool:
+    """Whether the running capture has forked the wgrad side stream (waits on it are then capture edges)."""
+    return _CAPTURE["forked"]
 
 
 # Cross-stream ordering without a new event per call. ``Stream.wait_stream`` creates (and on ROCm lazily
@@ -107,7 +131,9 @@ def side_stream(device) -> Optional[torch.cuda.Stream]:
 
 
 def _use_side_stream(tokens: int) -> bool:
-    if _WGRAD_MODE in ("0", "off", "false") or torch.cuda.is_current_stream_capturing():
+    if _WGRAD_MODE in ("0", "off", "false"):
+        return False
+    if torch.cuda.is_current_stream_capturing() and (_CAPTURE["parent"] is None or not _GRAPH_SIDE):
         return False
     return _WGRAD_MODE in ("1", "on", "true") or tokens <= _WGRAD_AUTO_MAX_TOKENS
 
@@ -136,11 +162,20 @@ class wgrad_stream_override:  # noqa: N801 - used as a context manager
 
 
 def join_side_streams() -> None:
-    """Make the current stream wait for every side stream (call before consuming gradients). A no-op inside a HIP
-    graph capture: captured steps never use the wgrad side stream (``_use_side_stream``)."""
-    if _SIDE and torch.cuda.is_current_stream_capturing():
-        return
+    """Make the current stream wait for every side stream (call before consuming gradients). Inside a HIP graph
+    capture the capture stream joins the side stream, if this capture forked it (else nothing to join)."""
     if not _SIDE:
+        return
+    parent = _CAPTURE["parent"]
+    if parent is not None:
+        if _CAPTURE["forked"]:
+            for s in _SIDE.values():
+                if s.device == parent.device:
+                    _C.stream_wait(parent.cuda_stream, s.cuda_stream)
+        _STASH.clear()
+        _JOIN_QUEUED[0] = False
+        return
+    if torch.cuda.is_current_stream_capturing():
         return
     dev = torch.cuda.current_device()
     for k, s in _SIDE.items():
@@ -166,20 +201,24 @@ def wgrad_done(g: "_Grad", dy: torch.Tensor, x: torch.Tensor):
         torch.autograd.Variable._execution_engine.queue_callback(_end_of_backward)
         _JOIN_QUEUED[0] = True
     N, K, T = dy.shape[1], x.shape[1], dy.shape[0]
-    if not _WGRAD_CXX:
+    parent = _CAPTURE["parent"]
+    if parent is not None:
+        _CAPTURE["forked"] = True  # a branch of the graph capture, forked from the capture stream itself
+    src = parent.cuda_stream if parent is not None else 0
+    if not _WGRAD_CXX and parent is None:
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
             gemm_wgrad_(g, dy, x)
             r = g.done()
     elif g.buf is g.mg and _C.gemm2_supported(1, 1, 7, N, K, T):
-        _C.stream_wait(s.cuda_stream, 0)
+        _C.stream_wait(s.cuda_stream, src)
         # the common case without any Python stream plumbing: TT GEMM (+ split-K reduce) launched on the side stream
         sp = _C.gemm2_splits(N, K, T)
         _C.gemm2_on(s.cuda_stream, dy, x, g.buf, 1, 1, 7, None, None, None, 0.0, 0, sp,
                     _workspace(sp * N * K, dy.device, s), None)
         r = None
     else:
-        _C.stream_wait(s.cuda_stream, 0)
+        _C.stream_wait(s.cuda_stream, src)
         with torch.cuda.stream(s):
             gemm_wgrad_(g, dy, x)
             r = g.done()

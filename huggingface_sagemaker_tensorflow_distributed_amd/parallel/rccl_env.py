@@ -12,12 +12,16 @@ Why these values (8 GPUs, every pair joined by one xGMI link, 7 links per GPU, ~
   collective only spans all 7 links of a GPU when at least 7 rings run (the directed complete graph on 8 GPUs
   splits into exactly 7 link-disjoint Hamiltonian rings), and two channels per link keep each link busy while the
   other channel's chunk is in the reduce step.
-* ``NCCL_MAX_NCHANNELS`` = 7 x 4. Every channel is one RCCL workgroup that holds a CU for the collective's duration.
-  The gradient all-reduces here overlap the backward GEMMs (one 512-thread workgroup per CU that needs the whole
-  CU), so channels beyond what saturates the links only take CUs away from backward. bert-base sends 418 MiB of
-  fp32 gradients per step; at the 7-link ring bound (7 x 153 GB/s) that is ~0.5 ms of an ~83 ms step, so the
-  collective has ample slack under backward and the cap costs the exposed tail (the last bucket, dominated by the
-  94 MB word-embedding gradient) at most a fraction of a millisecond.
+* ``NCCL_MAX_NCHANNELS`` = 7 x 4. Every channel is one RCCL workgroup that holds a CU for the collective's duration,
+  while the gradient all-reduces overlap the backward GEMMs (persistent, one 512-thread workgroup per CU). What a
+  held CU costs those GEMMs was measured, not estimated (``tools/contention_ab.py``,
+  ``profiles/contention_ab_r4.jsonl``): k whole CUs held for 400 us by a side-stream kernel (``cu_hog``, the RCCL
+  stand-in) during one bert-base GEMM at T = 131072. With the dynamic tile queue (``gemm_common.h`` tq_*, default)
+  a late workgroup takes fewer tiles, and k = 14 / 28 / 56 cost qkv_fwd +1.9 / +4.9 / +10.9 % (proportional CU loss:
+  +5.4 / +10.8 / +21.6 %), while ffn1_fwd and ffn2_dgrad, whose epilogues are bound by the chip's store rate rather
+  than by CUs, ran 3-7 % FASTER with CUs held. With the old static tile walk the same holds cost +71-78 % on qkv_fwd
+  and +26-28 % on ffn2_dgrad. So the cap is set by link saturation (4 channels per link), not by CU pressure: 28 channels
+  held through a bucket's all-reduce cost the overlapped GEMM at most ~5 %, and only for the bucket's ~0.1-0.2 ms.
 * At N = 2 / 4 a GPU reaches 1 / 3 peers; the same floors and caps apply (RCCL lays several channels per link).
 
 Bucket size (``--bucket_mb``, default 64 MiB, ``parallel/ddp.py``): bert-base's 418 MiB of fp32 gradients form 7

@@ -92,12 +92,17 @@ class CapturedStep:
         del saved
         self.graph = torch.cuda.CUDAGraph()
         cb, store.ready_callback = store.ready_callback, None  # no optimizer slices inside a fwd+bwd-only graph
+        from ..ops import hip
+
         try:
             with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
+                hip.begin_capture(torch.cuda.current_stream(trainer.device))
                 model.rng.new_step(0)  # per-site seeds fixed; the device step seed varies per replay
                 self.loss, self.logits = trainer._forward_loss(self.static)
                 self.loss.backward()
+                hip.join_side_streams()
         finally:
+            hip.end_capture()
             store.ready_callback = cb
         torch.cuda.synchronize(trainer.device)
         logger.info("captured training step graph for batch shape %s", tuple(example["input_ids"].shape))
@@ -147,11 +152,16 @@ class CapturedTrainStep:
         buck = trainer.bucketer
         eng = buck.engine if buck is not None else None
         gscale = 1.0 / trainer.world
+        from ..ops import hip
+
         self.graph = torch.cuda.CUDAGraph()
         step0 = opt.step_count
         try:
             with opt.capturing(), torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
                 cap = torch.cuda.current_stream(trainer.device)  # the capture stream
+                # the weight-gradient side stream runs as a branch of the graph (ops/hip.py begin_capture), as in
+                # eager steps: captured sequentially it made the replay slower than eager (round 3)
+                hip.begin_capture(cap)
                 store.zero_grad()
                 model.rng.new_step(0)
                 if eng is not None:
@@ -167,12 +177,14 @@ class CapturedTrainStep:
                         ov.begin()
                 self.loss, self.logits = trainer._forward_loss(self.static)
                 self.loss.backward()
+                hip.join_side_streams()
                 if buck is not None:
                     buck.finish()
                 if ov is not None and ov != "engine":
                     ov.join()
                 opt.step(grad_scale=gscale)
         finally:
+            hip.end_capture()
             if ov is not None and ov != "engine":
                 ov.parent = None
             if eng is not None:

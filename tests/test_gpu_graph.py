@@ -28,7 +28,8 @@ def _trainer(gpu, graph_replay, **kw):
 @pytest.mark.parametrize("full", ["1", "0"])
 def test_graph_replay_matches_eager(gpu, monkeypatch, full):
     """full=1: the whole step (zeroing, fwd, bwd, overlapped Adam slices, Wᵀ refresh) is one graph replay with
-    device-side Adam scalars; full=0: fwd+bwd graph, eager optimizer. A linear LR schedule with warm-up and AdamW
+    device-side Adam scalars; full=0: fwd+bwd graph, eager optimizer. Both with the weight-gradient side stream as a
+    branch of the graph. A linear LR schedule with warm-up and AdamW
     weight decay make every step's scalars differ."""
     monkeypatch.setenv("HSD_GRAPH_FULL", full)
     g = torch.Generator().manual_seed(0)
@@ -39,14 +40,19 @@ def test_graph_replay_matches_eager(gpu, monkeypatch, full):
         am[3, 70:] = 0
         batches.append({"input_ids": ids.to(gpu), "attention_mask": am.to(gpu),
                         "labels": torch.randint(0, 2, (16,), generator=g).to(gpu)})
+    from huggingface_sagemaker_tensorflow_distributed_amd.ops import hip
+
     res = {}
     for replay in (False, True):
         tr = _trainer(gpu, replay, weight_decay=0.01, lr_schedule="linear", lr_warmup_steps=2)
         tr.total_steps = 3
+        side0 = hip.CAPTURES_WITH_SIDE_STREAM[0]
         losses = [float(tr.train_step([b])) for b in batches]
         if replay:
             assert len(tr._graphs) == 1
             assert tr._full_graph == (full == "1")
+            # 2048-token steps run their weight gradients on the side stream: a branch of the captured graph
+            assert hip.CAPTURES_WITH_SIDE_STREAM[0] == side0 + 1
         assert tr.optimizer.step_count == 3
         torch.cuda.synchronize()
         res[replay] = (losses, tr.store.master.clone())
