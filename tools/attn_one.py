@@ -26,19 +26,23 @@ mask = torch.zeros(B, S, device=dev)
 dbias = torch.zeros(3 * H, device=dev)
 ws = torch.empty(B * heads * S, device=dev) if S > 128 else None  # delta workspace of the streaming kernels
 st, en = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+# the production path: the S = 128 forward writes its dropout keep bits for the backward (ops/hip.py _keep_mask);
+# ATTN_KMASK=0 times the re-hashing backward instead
+use_km = os.environ.get("ATTN_KMASK", "1") == "1"
 for pp in sorted({0.0, p}):
-    C_.attn_fwd(qkv, mask, out, lse, B, S, heads, pp, 123)
+    km = hip._keep_mask(B, S, heads, pp, dev) if use_km else None
+    C_.attn_fwd(qkv, mask, out, lse, B, S, heads, pp, 123, km)
     torch.cuda.synchronize()
     st.record()
     for _ in range(iters):
-        C_.attn_fwd(qkv, mask, out, lse, B, S, heads, pp, 123)
+        C_.attn_fwd(qkv, mask, out, lse, B, S, heads, pp, 123, km)
     en.record()
     torch.cuda.synchronize()
     f = st.elapsed_time(en) / iters * 1e3
     st.record()
     for _ in range(iters):
-        C_.attn_bwd(qkv, mask, out, dout, lse, dqkv, ws, B, S, heads, pp, 123, dbias)
+        C_.attn_bwd(qkv, mask, out, dout, lse, dqkv, ws, B, S, heads, pp, 123, dbias, km)
     en.record()
     torch.cuda.synchronize()
     b = st.elapsed_time(en) / iters * 1e3
-    print(f"p={pp}: fwd {f:.1f} us  bwd {b:.1f} us", flush=True)
+    print(f"p={pp} kmask={km is not None}: fwd {f:.1f} us  bwd {b:.1f} us", flush=True)
