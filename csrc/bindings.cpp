@@ -163,7 +163,9 @@ void ln_bwd_q8(torch::Tensor dout, torch::Tensor z, torch::Tensor mean, torch::T
 
 void embed_fwd(torch::Tensor ids, torch::Tensor pos_ids, c10::optional<torch::Tensor> type_ids, torch::Tensor word,
                torch::Tensor pos, c10::optional<torch::Tensor> type, torch::Tensor gamma, torch::Tensor beta,
-               torch::Tensor out, torch::Tensor mean, torch::Tensor rstd, double eps, double p, int64_t seed) {
+               torch::Tensor out, torch::Tensor mean, torch::Tensor rstd, double eps, double p, int64_t seed,
+               c10::optional<torch::Tensor> q8, c10::optional<torch::Tensor> amax_in, c10::optional<torch::Tensor> sinv,
+               c10::optional<torch::Tensor> amax_track) {
   TORCH_CHECK(ids.scalar_type() == torch::kInt64 && pos_ids.scalar_type() == torch::kInt64, "ids must be int64");
   TORCH_CHECK(ids.is_contiguous() && pos_ids.is_contiguous(), "ids contiguous");
   check_bf16(word, "word"); check_bf16(pos, "pos"); check_bf16(out, "out");
@@ -180,10 +182,17 @@ void embed_fwd(torch::Tensor ids, torch::Tensor pos_ids, c10::optional<torch::Te
   TORCH_CHECK(in_range(pos_ids, pos.size(0)), "HSD_DEBUG: position id out of range");
   if (type_ids.has_value()) TORCH_CHECK(in_range(*type_ids, type->size(0)), "HSD_DEBUG: token type id out of range");
 #endif
+  if (q8.has_value()) {  // the output's fp8 copy (the first layer's fp8 QKV GEMM): as ln_fwd_q8
+    CHECK_CUDA(*q8); CHECK_CONTIG(*q8); CHECK_DTYPE(*q8, torch::kUInt8);
+    TORCH_CHECK(q8->numel() == out.numel() && amax_in.has_value() && sinv.has_value() && amax_track.has_value(),
+                "embed_fwd q8 arguments");
+    check_f32(*amax_in, "amax_in"); check_f32(*sinv, "sinv"); check_f32(*amax_track, "amax_track");
+  }
   hsd::launch_embed_fwd(ids.data_ptr<int64_t>(), pos_ids.data_ptr<int64_t>(), OPT_I64(type_ids), CBF(word),
                         CBF(pos), type.has_value() ? CBF(*type) : nullptr, CBF(gamma), CBF(beta), BF(out),
                         mean.data_ptr<float>(), rstd.data_ptr<float>(), rows, H, (float)eps, p, (uint64_t)seed,
-                        cur_stream());
+                        cur_stream(), q8.has_value() ? q8->data_ptr<uint8_t>() : nullptr, OPT_F(amax_in), OPT_F(sinv),
+                        OPT_F(amax_track));
 }
 
 void embed_bwd(torch::Tensor dout, torch::Tensor ids, torch::Tensor pos_ids, c10::optional<torch::Tensor> type_ids,
@@ -232,8 +241,16 @@ void dropout(torch::Tensor x, torch::Tensor out, double p, int64_t seed) {
   hsd::launch_dropout(CBF(x), BF(out), x.numel(), p, (uint64_t)seed, cur_stream());
 }
 
+static uint32_t* keep_mask_ptr(const c10::optional<torch::Tensor>& km, int64_t B, int64_t S, int64_t heads) {
+  if (!km.has_value()) return nullptr;
+  CHECK_CUDA(*km); CHECK_CONTIG(*km); CHECK_DTYPE(*km, torch::kInt32);
+  TORCH_CHECK(km->numel() > 0 && km->numel() == hsd::attn_keep_mask_numel((int)B, (int)S, (int)heads),
+              "attention keep mask (attn_keep_mask_numel)");
+  return reinterpret_cast<uint32_t*>(km->data_ptr<int32_t>());
+}
+
 void attn_fwd(torch::Tensor qkv, c10::optional<torch::Tensor> mask, torch::Tensor out, torch::Tensor lse2, int64_t B,
-              int64_t S, int64_t heads, double p, int64_t seed) {
+              int64_t S, int64_t heads, double p, int64_t seed, c10::optional<torch::Tensor> kmask) {
   check_bf16(qkv, "qkv"); check_bf16(out, "out"); check_f32(lse2, "lse2");
   TORCH_CHECK(qkv.size(-1) == 3 * heads * 64, "attention requires head_dim 64");
   TORCH_CHECK(qkv.numel() == B * S * 3 * heads * 64 && out.numel() == B * S * heads * 64, "attn shapes");
@@ -241,12 +258,13 @@ void attn_fwd(torch::Tensor qkv, c10::optional<torch::Tensor> mask, torch::Tenso
   TORCH_CHECK(S % 2 == 0, "sequence length must be even");
   if (mask.has_value()) { check_f32(*mask, "mask"); TORCH_CHECK(mask->numel() == B * S, "mask shape"); }
   hsd::launch_attn_fwd(CBF(qkv), OPT_F(mask), BF(out), lse2.data_ptr<float>(), (int)B, (int)S, (int)heads, p,
-                       (uint64_t)seed, cur_stream());
+                       (uint64_t)seed, cur_stream(), keep_mask_ptr(kmask, B, S, heads));
 }
 
 void attn_bwd(torch::Tensor qkv, c10::optional<torch::Tensor> mask, torch::Tensor o, torch::Tensor dout,
               torch::Tensor lse2, torch::Tensor dqkv, c10::optional<torch::Tensor> dq_acc, int64_t B, int64_t S,
-              int64_t heads, double p, int64_t seed, c10::optional<torch::Tensor> dbias) {
+              int64_t heads, double p, int64_t seed, c10::optional<torch::Tensor> dbias,
+              c10::optional<torch::Tensor> kmask) {
   check_bf16(qkv, "qkv"); check_bf16(o, "o"); check_bf16(dout, "dout"); check_bf16(dqkv, "dqkv");
   check_f32(lse2, "lse2");
   TORCH_CHECK(qkv.size(-1) == 3 * heads * 64 && dqkv.numel() == qkv.numel(), "attn_bwd shapes");
@@ -259,7 +277,8 @@ void attn_bwd(torch::Tensor qkv, c10::optional<torch::Tensor> mask, torch::Tenso
   if (mask.has_value()) { check_f32(*mask, "mask"); TORCH_CHECK(mask->numel() == B * S, "mask shape"); }
   if (dbias.has_value()) { check_f32(*dbias, "dbias"); TORCH_CHECK(dbias->numel() == 3 * heads * 64, "dbias shape"); }
   hsd::launch_attn_bwd(CBF(qkv), OPT_F(mask), CBF(o), CBF(dout), lse2.data_ptr<float>(), BF(dqkv), OPT_F(dq_acc),
-                       OPT_F(dbias), (int)B, (int)S, (int)heads, p, (uint64_t)seed, cur_stream());
+                       OPT_F(dbias), (int)B, (int)S, (int)heads, p, (uint64_t)seed, cur_stream(),
+                       keep_mask_ptr(kmask, B, S, heads));
 }
 
 // attention + fp8 copy of its output (forward: e4m3 of the context; backward: dqkv in format qfmt), S > 128 streaming
@@ -768,6 +787,9 @@ void transpose_many(torch::Tensor desc, int64_t total_tiles) {
 
 int64_t gemm2_splits(int64_t M, int64_t N, int64_t K) { return hsd::gemm2_wgrad_splits((int)M, (int)N, (int)K); }
 int64_t gemm2_nt_splits(int64_t M, int64_t N, int64_t K) { return hsd::gemm2_nt_splits((int)M, (int)N, (int)K); }
+void attn128_set_diag(c10::optional<at::Tensor> buf) {
+  hsd::attn128_set_diag(buf.has_value() ? buf->data_ptr() : nullptr);
+}
 void gemm2_set_diag(c10::optional<at::Tensor> buf) {
   hsd::gemm2_set_diag(buf.has_value() ? buf->data_ptr() : nullptr);
 }
@@ -791,7 +813,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("attn_q8_supported", [](int64_t S) { return S > 128 && hsd::attn_streaming((int)S); });
   m.def("ln_fwd", &ln_fwd);
   m.def("ln_bwd", &ln_bwd);
-  m.def("embed_fwd", &embed_fwd);
+  m.def("embed_fwd", &embed_fwd, py::arg("ids"), py::arg("pos_ids"), py::arg("type_ids"), py::arg("word"),
+        py::arg("pos"), py::arg("type"), py::arg("gamma"), py::arg("beta"), py::arg("out"), py::arg("mean"),
+        py::arg("rstd"), py::arg("eps"), py::arg("p"), py::arg("seed"), py::arg("q8") = py::none(),
+        py::arg("amax_in") = py::none(), py::arg("sinv") = py::none(), py::arg("amax_track") = py::none());
   m.def("embed_bwd", &embed_bwd);
   m.def("gelu_fwd", &gelu_fwd);
   m.def("gelu_bwd_colsum", &gelu_bwd_colsum);
@@ -824,7 +849,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("q8") = py::none(), py::arg("q8_amax") = py::none(),
         py::arg("q8_sinv") = py::none(), py::arg("q8_track") = py::none(), py::arg("q8fmt") = 0);
   m.def("gemm8_supported", &hsd::gemm8_supported);
-  m.def("attn_fwd", &attn_fwd);
+  m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("mask"), py::arg("out"), py::arg("lse2"), py::arg("B"),
+        py::arg("S"), py::arg("heads"), py::arg("p"), py::arg("seed"), py::arg("kmask") = py::none());
+  m.def("attn_keep_mask_supported", &hsd::attn_keep_mask_supported);
+  m.def("attn_keep_mask_numel", &hsd::attn_keep_mask_numel);
   // backward workspace for S > 128: (numel, must_be_zeroed)
   m.def("attn_bwd_ws", [](int64_t B, int64_t S, int64_t heads) {
     if (S <= 128) return std::make_pair<int64_t, bool>(0, false);
@@ -833,13 +861,14 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   });
   m.def("attn_bwd", &attn_bwd, py::arg("qkv"), py::arg("mask"), py::arg("o"), py::arg("dout"), py::arg("lse2"),
         py::arg("dqkv"), py::arg("dq_acc"), py::arg("B"), py::arg("S"), py::arg("heads"), py::arg("p"), py::arg("seed"),
-        py::arg("dbias") = py::none());
+        py::arg("dbias") = py::none(), py::arg("kmask") = py::none());
   m.def("gemm", &gemm);
   m.def("gemm2", &gemm2);
   m.def("gemm2_splits", &gemm2_splits);
   m.def("gemm2_nt_splits", &gemm2_nt_splits);
   m.def("gemm2_supported", &gemm2_supported);
   m.def("gemm2_set_diag", &gemm2_set_diag);
+  m.def("attn128_set_diag", &attn128_set_diag);
   m.def("transpose_many", &transpose_many);
   m.def("xent", &xent, py::arg("logits"), py::arg("labels"), py::arg("dlogits"), py::arg("stats"),
         py::arg("n_valid"), py::arg("V") = 0);

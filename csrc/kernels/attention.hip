@@ -128,7 +128,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
         st[kb][reg] = x;
         mx = fmaxf(mx, x);
       }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = max_xor32(mx);
     const float mn = fmaxf(m, mx);
     const float alpha = exp2f(m - mn);  // m = -inf on the first tile -> 0
     float ls = 0.f;
@@ -140,7 +140,7 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
         ls += p;
         st[kb][reg] = p;
       }
-    ls += __shfl_xor(ls, 32, 64);
+    ls = sum_xor32(ls);
     l = l * alpha + ls;
     m = mn;
     o0 *= alpha;
@@ -246,9 +246,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const bf16_t* __restrict_
       float part = 0.f;
 #pragma unroll
       for (int k = 0; k < 4; ++k) part += lo_bf(dv[k]) * lo_bf(ov[k]) + hi_bf(dv[k]) * hi_bf(ov[k]);
-      part += __shfl_xor(part, 1, 64);
-      part += __shfl_xor(part, 2, 64);
-      part += __shfl_xor(part, 4, 64);
+      part = sum8_dpp(part);
       if (ch == 0) {
         del_s[row] = part;
         lse_s[row] = qq < S ? lse2[(size_t)bh * S + qq] : 0.f;
@@ -379,23 +377,32 @@ void launch_attn128_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, c
 void launch_colsum(const bf16_t* x, float* dbias, int rows, int N, hipStream_t st);
 bool attnS_supported(int S, int head_dim);
 void launch_attnS_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse2, int B, int S, int heads,
-                      double p, uint64_t seed, hipStream_t st, Q8Out q8o);
+                      double p, uint64_t seed, hipStream_t st, Q8Out q8o, uint32_t* kmask);
 void launch_attnS_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
                       bf16_t* dqkv, float* delta_ws, float* dbias, int B, int S, int heads, double p, uint64_t seed,
-                      hipStream_t st, Q8Out q8o, int qfmt);
+                      hipStream_t st, Q8Out q8o, int qfmt, const uint32_t* kmask);
 
 // S in 256..1024 (multiple of 128) runs the streaming kernels of attentionS.hip; its backward takes
 // an fp32 [B*heads*S] scratch (no zeroing) where the generic kernel takes a zeroed [B*S, H] dq accumulator.
 bool attn_streaming(int S) { return attnS_supported(S, kD) && !HSD_KNOB("HSD_ATTN_GENERIC", 0); }
 
+// the streaming (S > 128) kernels only: at S = 128 the one-workgroup forward is memory-bound with four workgroups per
+// CU, and writing the bits cost it more (+27 us at bert-base B = 1024, plus a lost workgroup per CU) than the
+// backward saved (-26 us; profiles/attn_keep_mask_ab_r4.log)
+bool attn_keep_mask_supported(int S) { return attn_streaming(S); }
+// words of the keep mask per launch: [B*heads][S/32 query blocks][S keys]
+int64_t attn_keep_mask_numel(int B, int S, int heads) {
+  return attn_keep_mask_supported(S) ? (int64_t)B * heads * (S / 32) * S : 0;
+}
+
 void launch_attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse2, int B, int S, int heads,
-                     double p, uint64_t seed, hipStream_t st) {
+                     double p, uint64_t seed, hipStream_t st, uint32_t* kmask) {
   if (attn128_supported(S, kD) && !HSD_KNOB("HSD_ATTN_GENERIC", 0)) {
     launch_attn128_fwd(qkv, mask, out, lse2, B, heads, p, seed, st);
     return;
   }
   if (attn_streaming(S)) {
-    launch_attnS_fwd(qkv, mask, out, lse2, B, S, heads, p, seed, st, Q8Out{});
+    launch_attnS_fwd(qkv, mask, out, lse2, B, S, heads, p, seed, st, Q8Out{}, kmask);
     return;
   }
   DropoutParams dp = make_dropout(p, seed);
@@ -407,13 +414,13 @@ void launch_attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* l
 
 void launch_attn_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
                      bf16_t* dqkv, float* dq_acc, float* dbias, int B, int S, int heads, double p, uint64_t seed,
-                     hipStream_t st) {
+                     hipStream_t st, const uint32_t* kmask) {
   if (attn128_supported(S, kD) && !HSD_KNOB("HSD_ATTN_GENERIC", 0)) {
     launch_attn128_bwd(qkv, mask, o, dout, lse2, dqkv, dbias, B, heads, p, seed, st);
     return;
   }
   if (attn_streaming(S)) {
-    launch_attnS_bwd(qkv, mask, o, dout, lse2, dqkv, dq_acc, dbias, B, S, heads, p, seed, st, Q8Out{}, 0);
+    launch_attnS_bwd(qkv, mask, o, dout, lse2, dqkv, dq_acc, dbias, B, S, heads, p, seed, st, Q8Out{}, 0, kmask);
     return;
   }
   DropoutParams dp = make_dropout(p, seed);

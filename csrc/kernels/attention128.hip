@@ -81,7 +81,7 @@ __global__ __launch_bounds__(256, 4) void attn128_fwd_kernel(const bf16_t* __res
         mx = fmaxf(mx, x);
       }
     }
-  mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+  mx = max_xor32(mx);
   float l = 0.f;
 #pragma unroll
   for (int kb = 0; kb < 4; ++kb)
@@ -91,7 +91,7 @@ __global__ __launch_bounds__(256, 4) void attn128_fwd_kernel(const bf16_t* __res
       l += p;
       st[kb][reg] = p;
     }
-  l += __shfl_xor(l, 32, 64);
+  l = sum_xor32(l);
   if (dp.enabled) {
     const uint32_t rowbase = (uint32_t)(((int64_t)bh * S + q) * S);
 #pragma unroll
@@ -129,8 +129,16 @@ __global__ __launch_bounds__(256, 2) void attn128_bwd_kernel(const bf16_t* __res
                                                              const bf16_t* __restrict__ dout,
                                                              const float* __restrict__ lse2,
                                                              bf16_t* __restrict__ dqkv, float* __restrict__ dbias,
-                                                             int heads, float sl2, float scale, DropoutParams dp) {
+                                                             int heads, float sl2, float scale, DropoutParams dp,
+                                                             unsigned long long* __restrict__ diag) {
   dp = resolve_seed(dp);
+  // diagnostic phase stamps (attn128_set_diag, tools/attn_phase_probe.py): start, operands landed, delta done, loop
+  // done, dK / dV stored, end, and the real-time clock at start / end
+  unsigned long long ts[6] = {0, 0, 0, 0, 0, 0}, rt0 = 0;
+  if (diag) {
+    ts[0] = __builtin_amdgcn_s_memtime();
+    rt0 = __builtin_amdgcn_s_memrealtime();
+  }
   // [Q | dO | dS | lse | delta | bias-grad partials]; after the main loop Q's slot holds K, dO's slot the
   // output staging
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * S * D + S * S + 4 * S + 2 * 3 * 4 * D];
@@ -171,6 +179,7 @@ __global__ __launch_bounds__(256, 2) void attn128_bwd_kernel(const bf16_t* __res
   if (tid < S) lse_s[tid] = lse2[(int64_t)bh * S + tid];
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+  if (diag) ts[1] = __builtin_amdgcn_s_memtime();
   {
     float part[4];
 #pragma unroll
@@ -180,10 +189,7 @@ __global__ __launch_bounds__(256, 2) void attn128_bwd_kernel(const bf16_t* __res
       float acc = 0.f;
 #pragma unroll
       for (int k = 0; k < 4; ++k) acc += lo_bf(dv[k]) * lo_bf(ov[i][k]) + hi_bf(dv[k]) * hi_bf(ov[i][k]);
-      acc += __shfl_xor(acc, 1, 64);
-      acc += __shfl_xor(acc, 2, 64);
-      acc += __shfl_xor(acc, 4, 64);
-      part[i] = acc;
+      part[i] = sum8_dpp(acc);
     }
     if ((tid & 7) == 0) {
 #pragma unroll
@@ -191,6 +197,7 @@ __global__ __launch_bounds__(256, 2) void attn128_bwd_kernel(const bf16_t* __res
     }
   }
   __syncthreads();
+  if (diag) ts[2] = __builtin_amdgcn_s_memtime();
 
   f32x16 dk0 = {}, dk1 = {}, dv0 = {}, dv1 = {};
   const bool odd = (lane & 1) != 0;
@@ -237,9 +244,9 @@ __global__ __launch_bounds__(256, 2) void attn128_bwd_kernel(const bf16_t* __res
       float k0 = 1.f, k1 = 1.f;
       if constexpr (DROP) {
         // element ((bh*S + q)*S + key): keys 2j, 2j+1 (lanes l, l^1) share one hash per query row.
-        // even lane hashes row qi0, odd lane row qi0+1, then they swap.
+        // even lane hashes row qi0, odd lane row qi0+1, then they swap (a DPP lane move, no LDS round trip)
         const uint32_t bits = dropout_bits(pair_qb + (uint32_t)((reg & 3) + 8 * (reg >> 2)) * (S / 2), dp);
-        const uint32_t other = (uint32_t)__shfl_xor((int)bits, 1, 64);
+        const uint32_t other = dpp_xor1(bits);
         const uint32_t b0 = odd ? other : bits;   // hash of row qi0
         const uint32_t b1 = odd ? bits : other;   // hash of row qi0 + 1
         k0 = keep_factor(b0, key & 1, dp);
@@ -273,6 +280,7 @@ __global__ __launch_bounds__(256, 2) void attn128_bwd_kernel(const bf16_t* __res
     }
   }
   __syncthreads();  // every dS written; Q / dO no longer read
+  if (diag) ts[3] = __builtin_amdgcn_s_memtime();
   // K -> Q's slot for dQ, from the K fragments this wave already holds (keys 32w..32w+31, 8 consecutive d
   // per lane and s): LDS writes instead of a second HBM/L2 read, and no s_waitcnt vmcnt before the dQ phase
   // (a vmcnt would also wait for the dK / dV stores below, which count on the same counter).
@@ -287,6 +295,7 @@ __global__ __launch_bounds__(256, 2) void attn128_bwd_kernel(const bf16_t* __res
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
+  if (diag) ts[4] = __builtin_amdgcn_s_memtime();
   // dQᵀ[d][q] = Σ_key Kᵀ[d][key] dSᵀ[key][q], wave w: queries 32w..32w+31
   f32x16 dq0 = {}, dq1 = {};
 #pragma unroll
@@ -307,11 +316,25 @@ __global__ __launch_bounds__(256, 2) void attn128_bwd_kernel(const bf16_t* __res
       atomicAdd(dbias + which * H + hh * D + c, b[0] + b[D] + b[2 * D] + b[3 * D]);
     }
   }
+  if (diag) {
+    ts[5] = __builtin_amdgcn_s_memtime();
+    const unsigned long long rt1 = __builtin_amdgcn_s_memrealtime();
+    if (tid == 0) {
+      unsigned long long* d = diag + (int64_t)blockIdx.x * 8;
+#pragma unroll
+      for (int i = 0; i < 6; ++i) d[i] = ts[i];
+      d[6] = rt0;
+      d[7] = rt1;
+    }
+  }
 }
 
 }  // namespace a128
 
 bool attn128_supported(int S, int head_dim) { return S == a128::S && head_dim == a128::D; }
+
+static unsigned long long* g_a128_diag = nullptr;
+void attn128_set_diag(void* p) { g_a128_diag = (unsigned long long*)p; }
 
 void launch_attn128_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse2, int B, int heads, double p,
                         uint64_t seed, hipStream_t st) {
@@ -328,10 +351,10 @@ void launch_attn128_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, c
   const float scale = 1.0f / sqrtf((float)a128::D);
   if (dp.enabled)
     hipLaunchKernelGGL(a128::attn128_bwd_kernel<true>, dim3(B * heads), dim3(256), 0, st, qkv, mask, o, dout, lse2,
-                       dqkv, dbias, heads, sl2, scale, dp);
+                       dqkv, dbias, heads, sl2, scale, dp, g_a128_diag);
   else
     hipLaunchKernelGGL(a128::attn128_bwd_kernel<false>, dim3(B * heads), dim3(256), 0, st, qkv, mask, o, dout, lse2,
-                       dqkv, dbias, heads, sl2, scale, dp);
+                       dqkv, dbias, heads, sl2, scale, dp, g_a128_diag);
   HSD_CHECK_LAUNCH();
 }
 

@@ -16,6 +16,10 @@
 //   written exactly once and deterministic, at the price of recomputing S and dP (7 instead of 5
 //   GEMM-equivalents) — the MFMA work is cheap next to the atomics traffic it replaces.
 // * delta[q] = Σ_d dO·O is a separate bandwidth kernel (every key block needs all of it).
+// * keep mask (optional, kmask): the forward writes its dropout keep bits, [S/32][S] words per (batch, head), bit i
+//   of word (qb, key) = keep(query 32 qb + i, key) (one wave ballot per key register), and both backward passes read
+//   them (preloaded into LDS) instead of re-hashing every (query, key) pair: the dK/dV pass (keys on lanes) takes
+//   its key's word of each query block, the dQ pass (queries on lanes) bit (q mod 32) of the words of its keys.
 // Dropout / mask / lse conventions are identical to attention.hip / attention128.hip.
 #include "attn_common.h"
 
@@ -64,9 +68,10 @@ __device__ __forceinline__ void settle(const T& v) {
   asm volatile("" ::"v"(v));
 }
 
-template <int INFLIGHT>
+template <int INFLIGHT, int EXTRA = 0>
 __device__ __forceinline__ void tile_barrier() {
-  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(4 * INFLIGHT) : "memory");
+  // EXTRA: younger vector-memory ops issued since the in-flight tiles' DMA (the forward's keep-mask stores)
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)" ::"n"(4 * INFLIGHT + EXTRA) : "memory");
   __builtin_amdgcn_s_barrier();
   asm volatile("" ::: "memory");
 }
@@ -76,7 +81,7 @@ template <bool DROP>
 __global__ __launch_bounds__(256, 2) void attnS_fwd_kernel(const bf16_t* __restrict__ qkv,
                                                            const float* __restrict__ mask, bf16_t* __restrict__ out,
                                                            float* __restrict__ lse2, int S, int heads, float sl2,
-                                                           DropoutParams dp, Q8Out q8o) {
+                                                           DropoutParams dp, Q8Out q8o, uint32_t* __restrict__ kmask) {
   dp = resolve_seed(dp);
   // [K0 K1 K2 | V0 V1 V2 | mask bias]; after the loop K0|K1 is the output staging
   __shared__ __attribute__((aligned(16))) bf16_t lds[2 * NSTG * TILE + 2 * kMaxS];
@@ -111,10 +116,18 @@ __global__ __launch_bounds__(256, 2) void attnS_fwd_kernel(const bf16_t* __restr
   float m = -INFINITY, l = 0.f;
   // dropout pair of (q, key): ((bh S + q) S + key) >> 1 = pair_q + key / 2 (key even in every hashed pair)
   const uint32_t pair_q = (uint32_t)(((int64_t)bh * S + q) * (S / 2)) + 2 * hf;
+  const bool km_on = DROP && kmask != nullptr;
+  // keep-mask words of this wave: key-major [bh][q0 / 32][key], query-major [bh][kt][q][hf] (header)
+  uint32_t* const km_k = km_on ? kmask + ((int64_t)bh * (S / 32) + q0 / 32) * S : nullptr;
   auto tile = [&](const int stg, const int kt) {
-
-    if (kt + 1 < nt) tile_barrier<1>();
-    else tile_barrier<0>();
+    // the previous tile's keep-mask store is younger than tile kt + 1's DMA: counted, not waited for
+    if (kt + 1 < nt) {
+      if (km_on && kt > 0) tile_barrier<1, 1>();
+      else tile_barrier<1>();
+    } else {
+      if (km_on && kt > 0) tile_barrier<0, 1>();
+      else tile_barrier<0>();
+    }
     const bf16_t* Ks = Kb + stg * TILE;
     const bf16_t* Vs = Vb + stg * TILE;
     if (kt + 2 < nt) {
@@ -147,7 +160,7 @@ __global__ __launch_bounds__(256, 2) void attnS_fwd_kernel(const bf16_t* __restr
           mx = fmaxf(mx, x);
         }
       }
-    mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+    mx = max_xor32(mx);
     const float alpha = __builtin_amdgcn_exp2f(m - mx);
     m = mx;
     float ls = 0.f;
@@ -167,15 +180,27 @@ __global__ __launch_bounds__(256, 2) void attnS_fwd_kernel(const bf16_t* __restr
     }
     if constexpr (DROP) {
       const uint32_t pair_t = pair_q + (uint32_t)kt * 32;
+      uint32_t wk = 0;  // keep-mask word of key 64 kt + lane (the wave's 32 queries)
+      auto put = [&](int k, uint32_t v) { wk = lane == k ? v : wk; };  // lane k <- the wave-uniform v
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int reg = 0; reg < 16; reg += 2) {
           // key = kt*64 + kb*32 + (reg & 3) + 8 (reg >> 2) + 4 hf
           const uint32_t bits = dropout_bits(pair_t + (uint32_t)(kb * 16 + ((reg & 3) >> 1) + 4 * (reg >> 2)), dp);
-          st[kb][reg] *= keep_factor(bits, 0, dp);
-          st[kb][reg + 1] *= keep_factor(bits, 1, dp);
+          const float f0 = keep_factor(bits, 0, dp), f1 = keep_factor(bits, 1, dp);
+          st[kb][reg] *= f0;
+          st[kb][reg + 1] *= f1;
+          if (km_on) {
+            const unsigned long long m0 = __ballot(f0 != 0.f), m1 = __ballot(f1 != 0.f);
+            const int kl = kb * 32 + (reg & 3) + 8 * (reg >> 2);  // tile key of `reg` on lanes 0-31
+            put(kl, (uint32_t)m0);
+            put(kl + 4, (uint32_t)(m0 >> 32));
+            put(kl + 1, (uint32_t)m1);
+            put(kl + 5, (uint32_t)(m1 >> 32));
+          }
         }
+      if (km_on) km_k[kt * 64 + lane] = wk;
     }
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
@@ -188,7 +213,7 @@ __global__ __launch_bounds__(256, 2) void attnS_fwd_kernel(const bf16_t* __restr
   };
 #pragma unroll 1
   for (int t = 0, stg = 0; t < nt; ++t, stg = stg == NSTG - 1 ? 0 : stg + 1) tile(stg, t);
-  l += __shfl_xor(l, 32, 64);
+  l = sum_xor32(l);
   if (hf == 0) lse2[(int64_t)bh * S + q] = m + __log2f(l);
   __syncthreads();  // K images no longer read: reuse as staging
   if (q8o.q != nullptr) {  // fp8 e4m3 copy of the output for the fp8 out-projection GEMM (delayed scaling)
@@ -219,9 +244,7 @@ __global__ __launch_bounds__(256) void attnS_delta_kernel(const bf16_t* __restri
   float acc = 0.f;
 #pragma unroll
   for (int k = 0; k < 4; ++k) acc += lo_bf(dv[k]) * lo_bf(ov[k]) + hi_bf(dv[k]) * hi_bf(ov[k]);
-  acc += __shfl_xor(acc, 1, 64);
-  acc += __shfl_xor(acc, 2, 64);
-  acc += __shfl_xor(acc, 4, 64);
+  acc = sum8_dpp(acc);
   if (c == 0) delta[(int64_t)bh * S + s] = acc;
 }
 
@@ -234,15 +257,18 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_kv_kernel(const bf16_t* __re
                                                               const float* __restrict__ delta,
                                                               bf16_t* __restrict__ dqkv, float* __restrict__ dbias,
                                                               int S, int heads, float sl2, float scale,
-                                                              DropoutParams dp, Q8Out q8o, int qfmt) {
+                                                              DropoutParams dp, Q8Out q8o, int qfmt,
+                                                              const uint32_t* __restrict__ kmask) {
   dp = resolve_seed(dp);
-  // [Q0 Q1 Q2 | dO0 dO1 dO2 | lse | delta | k/v bias partials]; after the loop Q0|Q1 is the output staging
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * NSTG * TILE + 4 * kMaxS + 2 * 2 * 4 * D];
+  // [Q0 Q1 Q2 | dO0 dO1 dO2 | lse | delta | k/v bias partials | keep-mask words]; after the loop Q0|Q1 is the output
+  // staging
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * NSTG * TILE + 4 * kMaxS + 2 * 2 * 4 * D + 2 * (kMaxS / 32) * 128];
   bf16_t* Qb = lds;
   bf16_t* dOb = lds + NSTG * TILE;
   float* lse_s = reinterpret_cast<float*>(lds + 2 * NSTG * TILE);
   float* del_s = lse_s + kMaxS;
   float* bsum = del_s + kMaxS;  // [2 (k,v)][4 waves][64]
+  uint32_t* km_s = reinterpret_cast<uint32_t*>(bsum + 2 * 4 * D);  // [S/32 query blocks][this block's 128 keys]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hf = lane >> 5;
@@ -267,6 +293,11 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_kv_kernel(const bf16_t* __re
   for (int i = tid; i < S; i += 256) {
     lse_s[i] = lse2[(int64_t)bh * S + i];
     del_s[i] = delta[(int64_t)bh * S + i];
+  }
+  const bool km_on = DROP && kmask != nullptr;
+  if (km_on) {
+    const uint32_t* src = kmask + (int64_t)bh * (S / 32) * S + blockIdx.x * 128;
+    for (int i = tid; i < (S / 32) * 128; i += 256) km_s[i] = src[(int64_t)(i >> 7) * S + (i & 127)];
   }
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
@@ -308,6 +339,8 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_kv_kernel(const bf16_t* __re
       // rows: query qi = (reg&3) + 8(reg>>2) + 4hf of the sub-block; col (lane): key
       f32x16 pd, ds;
       const uint32_t pair_qs = pair_lane + (uint32_t)(qt * 64 + qs * 32) * (S / 2);
+      // this query block's keep bits of the lane's key, shifted to the lane's rows (4 hf)
+      const uint32_t kmw = km_on ? km_s[(qt * 2 + qs) * 128 + wave * 32 + r] >> (4 * hf) : 0u;
 #pragma unroll
       for (int reg = 0; reg < 16; reg += 2) {
         const int qi0 = qt * 64 + qs * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * hf;  // rows qi0, qi0 + 1
@@ -317,12 +350,18 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_kv_kernel(const bf16_t* __re
         const float p1 = __builtin_amdgcn_exp2f(fmaf(sacc[reg + 1], sl2, kb2) - lse[1]);
         float f0 = 1.f, f1 = 1.f;
         if constexpr (DROP) {
-          // keys 2j, 2j+1 (lanes l, l^1) share one hash per query row: the even lane hashes row qi0,
-          // the odd lane row qi0 + 1, then they swap
-          const uint32_t bits = dropout_bits(pair_qs + (uint32_t)((reg & 3) + 8 * (reg >> 2)) * (S / 2), dp);
-          const uint32_t other = (uint32_t)__shfl_xor((int)bits, 1, 64);
-          f0 = keep_factor(odd ? other : bits, key & 1, dp);
-          f1 = keep_factor(odd ? bits : other, key & 1, dp);
+          if (km_on) {
+            const int pos = (reg & 3) + 8 * (reg >> 2);
+            f0 = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)kmw, pos, 1) & __float_as_uint(dp.scale));
+            f1 = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)kmw, pos + 1, 1) & __float_as_uint(dp.scale));
+          } else {
+            // keys 2j, 2j+1 (lanes l, l^1) share one hash per query row: the even lane hashes row qi0,
+            // the odd lane row qi0 + 1, then they swap
+            const uint32_t bits = dropout_bits(pair_qs + (uint32_t)((reg & 3) + 8 * (reg >> 2)) * (S / 2), dp);
+            const uint32_t other = dpp_xor1(bits);
+            f0 = keep_factor(odd ? other : bits, key & 1, dp);
+            f1 = keep_factor(odd ? bits : other, key & 1, dp);
+          }
         }
         pd[reg] = p0 * f0;
         pd[reg + 1] = p1 * f1;
@@ -374,14 +413,16 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_q_kernel(const bf16_t* __res
                                                              const float* __restrict__ delta,
                                                              bf16_t* __restrict__ dqkv, float* __restrict__ dbias,
                                                              int S, int heads, float sl2, float scale,
-                                                             DropoutParams dp, Q8Out q8o, int qfmt) {
+                                                             DropoutParams dp, Q8Out q8o, int qfmt,
+                                                             const uint32_t* __restrict__ kmask) {
   dp = resolve_seed(dp);
-  // [K0 K1 K2 | V0 V1 V2 | mask bias | q bias partials]; after the loop K0|K1 is the output staging
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * NSTG * TILE + 2 * kMaxS + 2 * 4 * D];
+  // [K0 K1 K2 | V0 V1 V2 | mask bias | q bias partials | keep-mask words]; after the loop K0|K1 is the output staging
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * NSTG * TILE + 2 * kMaxS + 2 * 4 * D + 2 * 4 * kMaxS];
   bf16_t* Kb = lds;
   bf16_t* Vb = lds + NSTG * TILE;
   float* mb_s = reinterpret_cast<float*>(lds + 2 * NSTG * TILE);
   float* bsum = mb_s + kMaxS;  // [4 waves][64]
+  uint32_t* km_s = reinterpret_cast<uint32_t*>(bsum + 4 * D);  // [4 waves' query blocks][S keys]
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hf = lane >> 5;
@@ -404,6 +445,11 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_q_kernel(const bf16_t* __res
   const float lse_q = lse2[(int64_t)bh * S + q];
   const float del_q = delta[(int64_t)bh * S + q];
   for (int k = tid; k < S; k += 256) mb_s[k] = mask ? fmaxf(mask[(int64_t)b * S + k] * kLog2e, -1e30f) : 0.f;
+  const bool km_on = DROP && kmask != nullptr;
+  if (km_on) {
+    const uint32_t* src = kmask + ((int64_t)bh * (S / 32) + blockIdx.x * 4) * S;  // the 4 query blocks, contiguous
+    for (int i = tid; i < 4 * S; i += 256) km_s[i] = src[i];
+  }
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
     settle(qf[s]);
@@ -448,6 +494,8 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_q_kernel(const bf16_t* __res
       for (int g4 = 0; g4 < 4; ++g4) {
         const int kk = kt * 64 + kb * 32 + 8 * g4 + 4 * hf;  // keys kk .. kk+3 in regs 4g4 .. 4g4+3
         const f32x4 mb = *reinterpret_cast<const f32x4*>(mb_s + kk);
+        // keep-mask words of keys kk .. kk+3 for this wave's query block: bit r = this lane's query
+        const u32x4 kw4 = km_on ? *reinterpret_cast<const u32x4*>(km_s + wave * S + kk) : u32x4{0, 0, 0, 0};
 #pragma unroll
         for (int e = 0; e < 4; e += 2) {
           const int reg = 4 * g4 + e;
@@ -455,9 +503,14 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_q_kernel(const bf16_t* __res
           const float p1 = __builtin_amdgcn_exp2f(fmaf(sacc[reg + 1], sl2, mb[e + 1]) - lse_q);
           float f0 = 1.f, f1 = 1.f;
           if constexpr (DROP) {
-            const uint32_t bits = dropout_bits(pair_kb + (uint32_t)(4 * g4 + (e >> 1)), dp);
-            f0 = keep_factor(bits, 0, dp);
-            f1 = keep_factor(bits, 1, dp);
+            if (km_on) {
+              f0 = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)kw4[e], r, 1) & __float_as_uint(dp.scale));
+              f1 = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)kw4[e + 1], r, 1) & __float_as_uint(dp.scale));
+            } else {
+              const uint32_t bits = dropout_bits(pair_kb + (uint32_t)(4 * g4 + (e >> 1)), dp);
+              f0 = keep_factor(bits, 0, dp);
+              f1 = keep_factor(bits, 1, dp);
+            }
           }
           ds[reg] = p0 * fmaf(dpacc[reg], f0, -del_q);
           ds[reg + 1] = p1 * fmaf(dpacc[reg + 1], f1, -del_q);
@@ -497,22 +550,22 @@ bool attnS_supported(int S, int head_dim) {
 }
 
 void launch_attnS_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse2, int B, int S, int heads,
-                      double p, uint64_t seed, hipStream_t st, Q8Out q8o) {
+                      double p, uint64_t seed, hipStream_t st, Q8Out q8o, uint32_t* kmask) {
   DropoutParams dp = make_dropout(p, seed);
   const float sl2 = attn::kLog2e / sqrtf((float)attn::D);
   if (dp.enabled)
     hipLaunchKernelGGL(aS::attnS_fwd_kernel<true>, dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, out, lse2, S,
-                       heads, sl2, dp, q8o);
+                       heads, sl2, dp, q8o, kmask);
   else
     hipLaunchKernelGGL(aS::attnS_fwd_kernel<false>, dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, out, lse2, S,
-                       heads, sl2, dp, q8o);
+                       heads, sl2, dp, q8o, (uint32_t*)nullptr);
   HSD_CHECK_LAUNCH();
 }
 
 // delta_ws: fp32 [B*heads*S] scratch
 void launch_attnS_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
                       bf16_t* dqkv, float* delta_ws, float* dbias, int B, int S, int heads, double p, uint64_t seed,
-                      hipStream_t st, Q8Out q8o, int qfmt) {
+                      hipStream_t st, Q8Out q8o, int qfmt, const uint32_t* kmask) {
   DropoutParams dp = make_dropout(p, seed);
   const float sl2 = attn::kLog2e / sqrtf((float)attn::D);
   const float scale = 1.0f / sqrtf((float)attn::D);
@@ -520,16 +573,16 @@ void launch_attnS_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, con
   HSD_CHECK_LAUNCH();
   if (dp.enabled) {
     hipLaunchKernelGGL(aS::attnS_bwd_kv_kernel<true>, dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, dout,
-                       lse2, delta_ws, dqkv, dbias, S, heads, sl2, scale, dp, q8o, qfmt);
+                       lse2, delta_ws, dqkv, dbias, S, heads, sl2, scale, dp, q8o, qfmt, kmask);
     HSD_CHECK_LAUNCH();
     hipLaunchKernelGGL(aS::attnS_bwd_q_kernel<true>, dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, dout,
-                       lse2, delta_ws, dqkv, dbias, S, heads, sl2, scale, dp, q8o, qfmt);
+                       lse2, delta_ws, dqkv, dbias, S, heads, sl2, scale, dp, q8o, qfmt, kmask);
   } else {
     hipLaunchKernelGGL(aS::attnS_bwd_kv_kernel<false>, dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, dout,
-                       lse2, delta_ws, dqkv, dbias, S, heads, sl2, scale, dp, q8o, qfmt);
+                       lse2, delta_ws, dqkv, dbias, S, heads, sl2, scale, dp, q8o, qfmt, nullptr);
     HSD_CHECK_LAUNCH();
     hipLaunchKernelGGL(aS::attnS_bwd_q_kernel<false>, dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, dout,
-                       lse2, delta_ws, dqkv, dbias, S, heads, sl2, scale, dp, q8o, qfmt);
+                       lse2, delta_ws, dqkv, dbias, S, heads, sl2, scale, dp, q8o, qfmt, nullptr);
   }
   HSD_CHECK_LAUNCH();
 }
@@ -539,14 +592,14 @@ void launch_attnS_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, con
 void launch_attnS_fwd_q8(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse2, int B, int S, int heads,
                          double p, uint64_t seed, uint8_t* q8, const float* amax_in, float* sinv, float* amax_track,
                          hipStream_t st) {
-  launch_attnS_fwd(qkv, mask, out, lse2, B, S, heads, p, seed, st, Q8Out{q8, amax_in, sinv, amax_track});
+  launch_attnS_fwd(qkv, mask, out, lse2, B, S, heads, p, seed, st, Q8Out{q8, amax_in, sinv, amax_track}, nullptr);
 }
 
 void launch_attnS_bwd_q8(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
                          bf16_t* dqkv, float* delta_ws, float* dbias, int B, int S, int heads, double p, uint64_t seed,
                          uint8_t* q8, const float* amax_in, float* sinv, float* amax_track, int qfmt, hipStream_t st) {
   launch_attnS_bwd(qkv, mask, o, dout, lse2, dqkv, delta_ws, dbias, B, S, heads, p, seed, st,
-                   Q8Out{q8, amax_in, sinv, amax_track}, qfmt);
+                   Q8Out{q8, amax_in, sinv, amax_track}, qfmt, nullptr);
 }
 
 }  // namespace hsd

@@ -111,11 +111,7 @@ __device__ __forceinline__ void store_rows(bf16_t* stg, const f32x16& a0, const 
     // lanes with equal (lane & 7) hold the same 8 columns: reduce over lane bits 3..5
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
-      float x = cs[e];
-      x += __shfl_xor(x, 8, 64);
-      x += __shfl_xor(x, 16, 64);
-      x += __shfl_xor(x, 32, 64);
-      cs[e] = x;
+      cs[e] = sum_stride8(cs[e]);
     }
     if (lane < 8) {
 #pragma unroll

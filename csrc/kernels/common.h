@@ -57,6 +57,47 @@ __device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
 __device__ __forceinline__ float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float hi_bf(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
 
+// ---- lane exchanges inside 8-lane groups on DPP (one VALU op each; __shfl_xor is a ds_bpermute: an LDS round trip
+// whose lgkmcnt wait serialises dependent chains, e.g. the attention backward's per-key-pair dropout hash exchange)
+__device__ __forceinline__ uint32_t dpp_xor1(uint32_t v) {  // lane l <- lane l^1 (quad_perm [1,0,3,2])
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)v, 0xB1, 0xF, 0xF, false);
+}
+__device__ __forceinline__ float dpp_xor1(float v) { return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false)); }
+__device__ __forceinline__ float dpp_xor2(float v) {  // lane l <- lane l^2 (quad_perm [2,3,0,1])
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x4E, 0xF, 0xF, false));
+}
+__device__ __forceinline__ float dpp_half_mirror(float v) {  // lane l <- lane 7-l within each 8-lane group
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x141, 0xF, 0xF, false));
+}
+// sum over each aligned group of 8 lanes, every lane gets its group's total (same value in all 8 lanes, and the same
+// additions pairwise as the xor-1/2/4 butterfly: bit-identical to it)
+__device__ __forceinline__ float sum8_dpp(float v) {
+  v += dpp_xor1(v);
+  v += dpp_xor2(v);
+  return v + dpp_half_mirror(v);
+}
+
+// sum over the 8 lanes {l & 7 + 8 j}: lane-bit 3 by DPP row_ror:8, bits 4 and 5 by the gfx950 permlane swaps (each swap
+// of v with itself returns both halves of the xor-16 / xor-32 pair); the same pairwise additions as the xor-8/16/32
+// butterfly, so bit-identical to it, with no LDS round trip
+__device__ __forceinline__ float sum_stride8(float v) {
+  v += __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x128, 0xF, 0xF, false));
+  auto p16 = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(p16[0]) + __uint_as_float(p16[1]);
+  auto p32 = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(p32[0]) + __uint_as_float(p32[1]);
+}
+
+// pair reductions across the two 32-lane halves (lane l with l ^ 32) on one permlane32 swap
+__device__ __forceinline__ float sum_xor32(float v) {
+  auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(p[0]) + __uint_as_float(p[1]);
+}
+__device__ __forceinline__ float max_xor32(float v) {
+  auto p = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(p[0]), __uint_as_float(p[1]));
+}
+
 // ---- wave64 reductions ---------------------------------------------------------------
 __device__ __forceinline__ float wave_sum(float v) {
 #pragma unroll

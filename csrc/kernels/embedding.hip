@@ -10,6 +10,7 @@
 //                                     one-row contention is 14x slower)
 //           dgamma / dbeta           (register partials, one atomic per column per block)
 #include "common.h"
+#include "fp8_common.h"
 
 #include <stdlib.h>
 
@@ -47,10 +48,17 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
                                                         const bf16_t* __restrict__ gamma, const bf16_t* __restrict__ beta,
                                                         bf16_t* __restrict__ out, float* __restrict__ mean_out,
                                                         float* __restrict__ rstd_out, int rows, int H, float eps,
-                                                        DropoutParams dp) {
+                                                        DropoutParams dp, Q8Out q8o) {
   dp = resolve_seed(dp);
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  // q8o.q: the output's fp8 e4m3 copy for the first encoder layer's fp8 QKV GEMM (delayed scaling, as the LayerNorm
+  // forward's q8 path: scale from q8o.amax_in, this pass's max |x| into q8o.amax_track)
+  float qs = 0.f, qm = 0.f;
+  if (q8o.q != nullptr) {
+    qs = fmt_scale(0, *q8o.amax_in);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *q8o.sinv = 1.0f / qs;
+  }
   if (row >= rows) return;
   const int nq = H >> 2;
   float e[NCH][4];
@@ -89,8 +97,14 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
       w.x = pack_bf2(o[0], o[1]);
       w.y = pack_bf2(o[2], o[3]);
       *reinterpret_cast<u32x2*>(out + off) = w;
+      if (q8o.q != nullptr) {  // from the stored bf16 values: the same bytes as the standalone quantiser
+        const float v0 = lo_bf(w.x), v1 = hi_bf(w.x), v2 = lo_bf(w.y), v3 = hi_bf(w.y);
+        qm = fmaxf(qm, fmaxf(fmaxf(fabsf(v0), fabsf(v1)), fmaxf(fabsf(v2), fabsf(v3))));
+        *reinterpret_cast<uint32_t*>(q8o.q + off) = cvt4<0>(v0 * qs, v1 * qs, v2 * qs, v3 * qs);
+      }
     }
   }
+  if (q8o.q != nullptr) wave_amax_track(qm, q8o.amax_track);
   if (lane == 0) {
     mean_out[row] = mean;
     rstd_out[row] = rstd;
@@ -351,20 +365,23 @@ __global__ __launch_bounds__(256, 2) void embed_bwd16_kernel(const bf16_t* __res
 template <int NCH>
 static void embed_fwd_t(const int64_t* ids, const int64_t* pos_ids, const int64_t* type_ids, const bf16_t* word,
                         const bf16_t* pos, const bf16_t* type, const bf16_t* gamma, const bf16_t* beta, bf16_t* out,
-                        float* mean, float* rstd, int rows, int H, float eps, const DropoutParams& dp, hipStream_t st) {
+                        float* mean, float* rstd, int rows, int H, float eps, const DropoutParams& dp, hipStream_t st,
+                        const Q8Out& q8o) {
   hipLaunchKernelGGL((embed_fwd_kernel<NCH>), dim3((rows + 3) / 4), dim3(256), 0, st, ids, pos_ids, type_ids, word, pos,
-                     type, gamma, beta, out, mean, rstd, rows, H, eps, dp);
+                     type, gamma, beta, out, mean, rstd, rows, H, eps, dp, q8o);
 }
 
 void launch_embed_fwd(const int64_t* ids, const int64_t* pos_ids, const int64_t* type_ids, const bf16_t* word,
                       const bf16_t* pos, const bf16_t* type, const bf16_t* gamma, const bf16_t* beta, bf16_t* out,
-                      float* mean, float* rstd, int rows, int H, float eps, double p, uint64_t seed, hipStream_t st) {
+                      float* mean, float* rstd, int rows, int H, float eps, double p, uint64_t seed, hipStream_t st,
+                      uint8_t* q8, const float* amax_in, float* sinv, float* amax_track) {
   DropoutParams dp = make_dropout(p, seed);
+  const Q8Out q8o{q8, amax_in, sinv, amax_track};
   int nch = (H / 4 + 63) / 64;
-  if (nch <= 1) embed_fwd_t<1>(ids, pos_ids, type_ids, word, pos, type, gamma, beta, out, mean, rstd, rows, H, eps, dp, st);
-  else if (nch <= 2) embed_fwd_t<2>(ids, pos_ids, type_ids, word, pos, type, gamma, beta, out, mean, rstd, rows, H, eps, dp, st);
-  else if (nch <= 3) embed_fwd_t<3>(ids, pos_ids, type_ids, word, pos, type, gamma, beta, out, mean, rstd, rows, H, eps, dp, st);
-  else if (nch <= 4) embed_fwd_t<4>(ids, pos_ids, type_ids, word, pos, type, gamma, beta, out, mean, rstd, rows, H, eps, dp, st);
+  if (nch <= 1) embed_fwd_t<1>(ids, pos_ids, type_ids, word, pos, type, gamma, beta, out, mean, rstd, rows, H, eps, dp, st, q8o);
+  else if (nch <= 2) embed_fwd_t<2>(ids, pos_ids, type_ids, word, pos, type, gamma, beta, out, mean, rstd, rows, H, eps, dp, st, q8o);
+  else if (nch <= 3) embed_fwd_t<3>(ids, pos_ids, type_ids, word, pos, type, gamma, beta, out, mean, rstd, rows, H, eps, dp, st, q8o);
+  else if (nch <= 4) embed_fwd_t<4>(ids, pos_ids, type_ids, word, pos, type, gamma, beta, out, mean, rstd, rows, H, eps, dp, st, q8o);
   else abort();
   HSD_CHECK_LAUNCH();
 }

@@ -206,11 +206,7 @@ __device__ __forceinline__ void epi_chunk(u32x4& o, u32x4& o2, const u32x4& x, i
 __device__ __forceinline__ void colsum_flush(float (&csum)[8], float* dbias, int nw, int N, int lane) {
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
-    float v = csum[e];
-    v += __shfl_xor(v, 8, 64);
-    v += __shfl_xor(v, 16, 64);
-    v += __shfl_xor(v, 32, 64);
-    csum[e] = v;
+    csum[e] = sum_stride8(csum[e]);
   }
   if (lane < 8 && nw + lane * 8 < N) {
 #pragma unroll

@@ -33,7 +33,9 @@ void launch_ln_bwd(const bf16_t* dout, const bf16_t* z, const float* mean, const
 // embedding.hip
 void launch_embed_fwd(const int64_t* ids, const int64_t* pos_ids, const int64_t* type_ids, const bf16_t* word,
                       const bf16_t* pos, const bf16_t* type, const bf16_t* gamma, const bf16_t* beta, bf16_t* out,
-                      float* mean, float* rstd, int rows, int H, float eps, double p, uint64_t seed, hipStream_t st);
+                      float* mean, float* rstd, int rows, int H, float eps, double p, uint64_t seed, hipStream_t st,
+                      uint8_t* q8 = nullptr, const float* amax_in = nullptr, float* sinv = nullptr,
+                      float* amax_track = nullptr);  // q8: the output's fp8 copy (as launch_ln_fwd_q8)
 void launch_embed_bwd(const bf16_t* dout, const int64_t* ids, const int64_t* pos_ids, const int64_t* type_ids,
                       const bf16_t* word, const bf16_t* pos, const bf16_t* type, const bf16_t* gamma,
                       const float* mean, const float* rstd, float* gword, float* gpos, float* gtype, float* ggamma,
@@ -66,8 +68,12 @@ void launch_cls_head_bwd(const bf16_t* t_in, const bf16_t* W2, const bf16_t* log
                          int C, int act, double p, uint64_t seed, hipStream_t st);
 // attention.hip
 bool attn_streaming(int S);
+// kmask (optional, streaming S > 128 kernels: attn_keep_mask_supported): the forward writes its dropout keep bits
+// ([B*heads][S/32][S] u32, attentionS.hip header), the backward reads them instead of re-hashing every (query, key) pair
+bool attn_keep_mask_supported(int S);
+int64_t attn_keep_mask_numel(int B, int S, int heads);
 void launch_attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse2, int B, int S, int heads,
-                     double p, uint64_t seed, hipStream_t st);
+                     double p, uint64_t seed, hipStream_t st, uint32_t* kmask = nullptr);
 // attentionS.hip fp8 variants (S > 128 streaming kernels only: attn_streaming(S) && S > 128)
 void launch_attnS_fwd_q8(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse2, int B, int S, int heads,
                          double p, uint64_t seed, uint8_t* q8, const float* amax_in, float* sinv, float* amax_track,
@@ -78,7 +84,7 @@ void launch_attnS_bwd_q8(const bf16_t* qkv, const float* mask, const bf16_t* o, 
 // dbias (optional): fp32 [3H] += column sums of dqkv (the fused QKV bias gradient)
 void launch_attn_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
                      bf16_t* dqkv, float* dq_acc, float* dbias, int B, int S, int heads, double p, uint64_t seed,
-                     hipStream_t st);
+                     hipStream_t st, const uint32_t* kmask = nullptr);
 }  // namespace hsd
 
 namespace hsd {
@@ -132,6 +138,7 @@ void launch_fp8_quant(const bf16_t* x, int64_t n, float* amax, uint8_t* q, float
 void launch_fp8_quant_many(const int64_t* amax_desc, int n_amax, int amax_blocks, const int64_t* quant_desc,
                            int n_quant, int quant_blocks_total, float* amax, float* sinv, int fmt, hipStream_t st);
 int fp8_elems_per_block();
+void attn128_set_diag(void* p);  // diagnostic phase stamps of the S=128 attention backward ([B*heads][8] u64)
 void gemm2_set_diag(void* p);  // diagnostic timestamps of the persistent NT kernel ([grid][64][4] u64), nullptr = off
 void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, int M, int N,
                   int K, void* C, int64_t ldc, const bf16_t* bias, const bf16_t* aux, int64_t ldaux, bf16_t* C2,

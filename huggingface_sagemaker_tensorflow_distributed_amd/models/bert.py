@@ -53,7 +53,9 @@ class Embeddings(nn.Module):
             t = cache[key] = make()
         return t
 
-    def forward(self, input_ids, token_type_ids, rng: DropoutSeeds, training: bool) -> torch.Tensor:
+    def forward(self, input_ids, token_type_ids, rng: DropoutSeeds, training: bool,
+                q8_for: Optional[torch.Tensor] = None) -> torch.Tensor:
+        """``q8_for``: the first encoder layer's QKV weight (fp8 path: the embedding kernel writes its fp8 operand)."""
         c = self.cfg
         pos = self.position_ids(input_ids)
         if token_type_ids is None and self.token_type_embeddings is not None:
@@ -61,7 +63,7 @@ class Embeddings(nn.Module):
         p = c.hidden_dropout_prob if training else 0.0
         return ops.embed_ln(input_ids, pos, token_type_ids, self.word_embeddings, self.position_embeddings,
                             self.token_type_embeddings, self.ln_weight, self.ln_bias, c.layer_norm_eps,
-                            p, rng.next() if p else 0, pos_is_arange=c.model_type != "roberta")
+                            p, rng.next() if p else 0, pos_is_arange=c.model_type != "roberta", q8_for=q8_for)
 
 
 class Encoder(nn.Module):
@@ -73,7 +75,8 @@ class Encoder(nn.Module):
 
     def forward(self, input_ids, attention_mask, token_type_ids, rng, training) -> torch.Tensor:
         B, S = input_ids.shape
-        h = self.embeddings(input_ids, token_type_ids, rng, training).view(B * S, -1)
+        first_qkv = self.layers[0].qkv_weight if len(self.layers) else None
+        h = self.embeddings(input_ids, token_type_ids, rng, training, q8_for=first_qkv).view(B * S, -1)
         mask_bias = ops.key_mask_bias(attention_mask) if attention_mask is not None else None
         n = len(self.layers)
         for i, layer in enumerate(self.layers):

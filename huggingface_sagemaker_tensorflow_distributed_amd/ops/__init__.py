@@ -64,10 +64,10 @@ def dropout(x: torch.Tensor, p: float, seed: int):
 
 
 def embed_ln(input_ids, position_ids, token_type_ids, word_w, pos_w, type_w, ln_w, ln_b, eps, p, seed,
-             pos_is_arange=False):
+             pos_is_arange=False, q8_for=None):
     if _hip(word_w):
         return _hipmod().embed_ln(input_ids, position_ids, token_type_ids, word_w, pos_w, type_w, ln_w, ln_b,
-                                  eps, p, seed, pos_is_arange)
+                                  eps, p, seed, pos_is_arange, q8_for)
     if _hip32(word_w) and word_w.shape[1] % 4 == 0 and word_w.shape[1] <= 1024:
         return _hip32mod().embed_ln(input_ids, position_ids, token_type_ids, word_w, pos_w, type_w, ln_w, ln_b,
                                     eps, p, seed)

@@ -101,6 +101,12 @@ def side_stream_in_capture() -> bool:
     return _CAPTURE["forked"]
 
 
+def side_stream_waitable() -> bool:
+    """Whether work may wait on the wgrad side stream now: always outside a capture; inside one only once the capture
+    has forked it (an event of a stream outside the capture is no capture edge)."""
+    return _CAPTURE["parent"] is None or _CAPTURE["forked"]
+
+
 # Cross-stream ordering without a new event per call. ``Stream.wait_stream`` creates (and on ROCm lazily
 # hipEventCreate's) a fresh event every time and goes through torch's Python stream plumbing; with ~80 forks / joins
 # per step (weight-gradient side stream, optimizer slices) small-batch steps were host-bound
@@ -432,7 +438,7 @@ def dropout(x, p, seed):
 # ------------------------------------------------------------------------------------------ embeddings
 class _EmbedLN(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, ids, pos_ids, type_ids, word, pos, typ, ln_w, ln_b, eps, p, seed, pos_is_arange):
+    def forward(ctx, ids, pos_ids, type_ids, word, pos, typ, ln_w, ln_b, eps, p, seed, pos_is_arange, q8_for):
         B, S = ids.shape
         H = word.shape[1]
         ids_c = ids.contiguous().long()
@@ -441,7 +447,17 @@ class _EmbedLN(torch.autograd.Function):
         out = torch.empty((B * S, H), dtype=word.dtype, device=word.device)
         mean = torch.empty(B * S, dtype=torch.float32, device=word.device)
         rstd = torch.empty_like(mean)
-        _C.embed_fwd(ids_c, pos_c, tt_c, word, pos, typ, ln_w, ln_b, out, mean, rstd, float(eps), float(p), _s64(seed))
+        # fp8: the first layer's QKV GEMM takes its operand's fp8 copy from this kernel (no separate quantise pass)
+        st = _site_ready(q8_for, "_hsd_fp8_x", "_hsd_q")
+        if st is not None and H % 8 == 0 and _C.gemm8_supported(EPI_BIAS, B * S, q8_for.shape[0], H):
+            q = torch.empty((B * S, H), dtype=torch.uint8, device=word.device)
+            sinv = torch.empty(1, dtype=torch.float32, device=word.device)
+            _C.embed_fwd(ids_c, pos_c, tt_c, word, pos, typ, ln_w, ln_b, out, mean, rstd, float(eps), float(p),
+                         _s64(seed), q, st[0:1], sinv, st[1:2])
+            _Q8_HANDOFF.put(out, q, sinv)
+        else:
+            _C.embed_fwd(ids_c, pos_c, tt_c, word, pos, typ, ln_w, ln_b, out, mean, rstd, float(eps), float(p),
+                         _s64(seed))
         ctx.save_for_backward(ids_c, pos_c, tt_c if tt_c is not None else ids_c, word, pos,
                               typ if typ is not None else word, ln_w, ln_b, mean, rstd)
         ctx.has_type = typ is not None
@@ -457,18 +473,31 @@ class _EmbedLN(torch.autograd.Function):
                      typ if ctx.has_type else None, ln_w, mean, rstd, gwd.buf, gp.buf, gt.buf if gt else None,
                      gg.buf, gbe.buf, ctx.B, ctx.S, ctx.arange, ctx.p, _s64(ctx.seed))
         return (None, None, None, gwd.done(), gp.done(), gt.done() if gt else None, gg.done(), gbe.done(),
-                None, None, None, None)
+                None, None, None, None, None)
 
 
 def embed_ln(input_ids, position_ids, token_type_ids, word_w, pos_w, type_w, ln_w, ln_b, eps, p, seed,
-             pos_is_arange=False):
+             pos_is_arange=False, q8_for=None):
     """``pos_is_arange``: position ids are ``arange(S)`` for every row (BERT/DistilBERT) — enables the
-    per-block position-gradient reduction instead of per-token atomics."""
+    per-block position-gradient reduction instead of per-token atomics. ``q8_for``: the first encoder layer's QKV
+    weight (fp8 path: the kernel also writes the output's fp8 copy for it)."""
     return _EmbedLN.apply(input_ids, position_ids, token_type_ids, word_w, pos_w, type_w, ln_w, ln_b, eps, p, seed,
-                          pos_is_arange)
+                          pos_is_arange, q8_for)
 
 
 # ------------------------------------------------------------------------------------------ attention
+def _keep_mask(B, S, heads, p, device):
+    """Dropout keep bits the attention forward writes for its backward, which reads them instead of re-hashing every
+    (query, key) pair (attention128.hip, attentionS.hip headers): S^2/8 B per (batch, head) (25 MB per bert-base
+    layer at B = 1024, S = 128; 4 MB per bert-large layer at B = 8, S = 512). None without dropout or where the
+    kernels do not support it."""
+    if p > 0 and _os.environ.get("HSD_ATTN_KMASK", "1") != "0":  # HSD_ATTN_KMASK=0: re-hash in the backward (A/B)
+        n = _C.attn_keep_mask_numel(B, S, heads)
+        if n > 0:
+            return torch.empty(n, dtype=torch.int32, device=device)
+    return None
+
+
 class _Attention(torch.autograd.Function):
     @staticmethod
     def forward(ctx, qkv, mask_bias, B, S, heads, p, seed):
@@ -477,19 +506,20 @@ class _Attention(torch.autograd.Function):
         out = torch.empty((B * S, H), dtype=qkv.dtype, device=qkv.device)
         lse = torch.empty(B * heads * S, dtype=torch.float32, device=qkv.device)
         mb = mask_bias.contiguous().float() if mask_bias is not None else None
-        _C.attn_fwd(qkv, mb, out, lse, B, S, heads, float(p), _s64(seed))
-        ctx.save_for_backward(qkv, out, lse, mb if mb is not None else lse)
-        ctx.has_mask = mb is not None
+        km = _keep_mask(B, S, heads, p, qkv.device)
+        _C.attn_fwd(qkv, mb, out, lse, B, S, heads, float(p), _s64(seed), km)
+        ctx.save_for_backward(qkv, out, lse, mb if mb is not None else lse, km if km is not None else lse)
+        ctx.has_mask, ctx.has_km = mb is not None, km is not None
         ctx.B, ctx.S, ctx.heads, ctx.p, ctx.seed = B, S, heads, float(p), seed
         return out
 
     @staticmethod
     def backward(ctx, dout):
-        qkv, out, lse, mb = ctx.saved_tensors
+        qkv, out, lse, mb, km = ctx.saved_tensors
         dqkv = torch.empty_like(qkv)
         dq_acc = _attn_ws(ctx.B, ctx.S, ctx.heads, out.device)
         _C.attn_bwd(qkv, mb if ctx.has_mask else None, out, dout.contiguous(), lse, dqkv, dq_acc, ctx.B, ctx.S,
-                    ctx.heads, ctx.p, _s64(ctx.seed))
+                    ctx.heads, ctx.p, _s64(ctx.seed), None, km if ctx.has_km else None)
         return dqkv, None, None, None, None, None, None
 
 
@@ -797,18 +827,21 @@ class _AttnBlock(torch.autograd.Function):
             sinv = torch.empty(1, dtype=torch.float32, device=h.device)
             _C.attn_fwd_q8(qkv, mb, actx, lse, B, S, heads, float(p_a), _s64(seed_a), q, st[0:1], sinv, st[1:2])
             xq = (q, sinv)
+            km = None
         else:
-            _C.attn_fwd(qkv, mb, actx, lse, B, S, heads, float(p_a), _s64(seed_a))
+            km = _keep_mask(B, S, heads, p_a, h.device)
+            _C.attn_fwd(qkv, mb, actx, lse, B, S, heads, float(p_a), _s64(seed_a), km)
         z = gemm_fwd(actx, out_w, EPI_BIAS_DROP_RES, bias=out_b, aux=h2d, p=p_h, seed=seed_h, xq=xq)
         out, mean, rstd = _ln_fwd(z, ln_w, ln_b, eps, q8_for=q8_next)
         ctx.save_for_backward(h2d, qkv_w, qkv_b, out_w, out_b, ln_w, ln_b, qkv, actx, lse, z, mean, rstd,
-                              mb if mb is not None else lse)
+                              mb if mb is not None else lse, km if km is not None else lse)
         ctx.cfg = (B, S, heads, float(p_a), seed_a, float(p_h), seed_h, mb is not None)
+        ctx.has_km = km is not None
         return out.view(h.shape)
 
     @staticmethod
     def backward(ctx, dout):
-        (h2d, qkv_w, qkv_b, out_w, out_b, ln_w, ln_b, qkv, actx, lse, z, mean, rstd, mb) = ctx.saved_tensors
+        (h2d, qkv_w, qkv_b, out_w, out_b, ln_w, ln_b, qkv, actx, lse, z, mean, rstd, mb, km) = ctx.saved_tensors
         B, S, heads, p_a, seed_a, p_h, seed_h, has_mask = ctx.cfg
         dout2 = dout.reshape(z.shape).contiguous()
         g_lnw, g_lnb, g_ow, g_ob = _Grad(ln_w), _Grad(ln_b), _Grad(out_w), _Grad(out_b)
@@ -836,7 +869,7 @@ class _AttnBlock(torch.autograd.Function):
             dqq = (q, sinv)
         else:
             _C.attn_bwd(qkv, mb if has_mask else None, actx, dctx, lse, dqkv, dq_acc, B, S, heads, p_a, _s64(seed_a),
-                        g_qb.buf)
+                        g_qb.buf, km if ctx.has_km else None)
         r_qb = g_qb.done()
         r_qw = wgrad_done(g_qw, dqkv, h2d)
         dh = gemm_dgrad(dqkv, qkv_w, EPI_RES, aux=dz, dyq=dqq) if ctx.needs_input_grad[0] else None

@@ -267,7 +267,7 @@ class LocalOverlap:
             cur = self.parent if self.parent is not None else torch.cuda.current_stream(self.stream.device)
             hip.stream_wait(self.stream, cur)
             side = hip.side_stream(self.stream.device)
-            if side is not None and (self.parent is None or hip.side_stream_in_capture()):
+            if side is not None and hip.side_stream_waitable():
                 hip.stream_wait(self.stream, side)
             with torch.cuda.stream(self.stream):
                 if self._hog[0] > 0 and self._hogs < self._hog[2]:

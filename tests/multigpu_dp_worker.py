@@ -32,8 +32,11 @@ def main(out):
     model = build_model(cfg, seed=0).to(dev)
     store = FlatParamStore(model, dev, compute_dtype=torch.bfloat16)
     opt = FusedAdam(store, lr=1e-3)
-    buck = GradBucketer(store, bucket_mb=1.0) if world > 1 else None
-    tr = Trainer(model, store, opt, buck, dev)
+    # HSD_MGPU_COMPRESSION=fp16|bf16: 16-bit gradient wire (Horovod's Compression.fp16); HSD_MGPU_GRAPH=1: the whole
+    # step captured once and replayed (train/graph.py; data parallel needs HSD_GRAPH_DP=1)
+    comp = os.environ.get("HSD_MGPU_COMPRESSION", "none")
+    buck = GradBucketer(store, bucket_mb=1.0, compression=comp) if world > 1 else None
+    tr = Trainer(model, store, opt, buck, dev, hip_graph=os.environ.get("HSD_MGPU_GRAPH", "0") == "1")
     if world > 1:
         broadcast_parameters(store, opt)
     g = torch.Generator().manual_seed(1234)
@@ -54,6 +57,7 @@ def main(out):
     engine = getattr(buck, "engine", None)
     if rank == 0:
         torch.save({"grad0": first_grad, "master": store.master.float().cpu(), "in_sync": in_sync, "world": world,
+                    "graphs": len(getattr(tr, "_graphs", {}) or {}), "compression": comp,
                     "rccl_world": int(engine.world) if engine is not None else None,
                     "n_buckets": len(buck.buckets) if buck is not None else 0}, out)
     backend.shutdown()

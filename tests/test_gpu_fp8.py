@@ -256,9 +256,45 @@ def test_ln_bwd_q8_equals_ln_bwd_then_quant(gpu, rows, H, p, fmt):
             assert torch.equal(x, y), i
 
 
+@pytest.mark.parametrize("B,S,H,p", [(32, 128, 768, 0.1), (8, 512, 1024, 0.0)])
+def test_embed_fwd_q8_equals_embed_then_quant(gpu, B, S, H, p):
+    """The embedding forward (gather + LayerNorm + dropout) writing its output's fp8 copy == the same kernel, then the
+    standalone quantiser with the same delayed-scaling site: identical bf16 output, fp8 bytes, sinv and tracked amax."""
+    hip = _hip()
+    C = hip._C
+    torch.manual_seed(5)
+    V = 1000
+    word = (torch.randn(V, H, device=gpu) * 0.05).bfloat16()
+    pos = (torch.randn(S, H, device=gpu) * 0.05).bfloat16()
+    typ = (torch.randn(2, H, device=gpu) * 0.05).bfloat16()
+    w = (1 + 0.1 * torch.randn(H, device=gpu)).bfloat16()
+    b = (0.1 * torch.randn(H, device=gpu)).bfloat16()
+    ids = torch.randint(0, V, (B, S), device=gpu)
+    pids = torch.arange(S, device=gpu).expand(B, S).contiguous()
+    tids = torch.zeros_like(ids)
+    res = {}
+    for fused in (False, True):
+        out = torch.empty(B * S, H, device=gpu, dtype=torch.bfloat16)
+        mean, rstd = torch.empty(B * S, device=gpu), torch.empty(B * S, device=gpu)
+        st = torch.tensor([2.0, 0.0], device=gpu)
+        if fused:
+            q = torch.empty(B * S, H, dtype=torch.uint8, device=gpu)
+            sinv = torch.empty(1, device=gpu)
+            C.embed_fwd(ids, pids, tids, word, pos, typ, w, b, out, mean, rstd, 1e-12, p, 21, q, st[0:1], sinv, st[1:2])
+        else:
+            C.embed_fwd(ids, pids, tids, word, pos, typ, w, b, out, mean, rstd, 1e-12, p, 21)
+            st._hsd_cal = True
+            q, sinv = hip.quant_fp8(out, 0, st)
+        torch.cuda.synchronize()
+        res[fused] = (out, mean, rstd, q, sinv, st)
+    for i, (x, y) in enumerate(zip(res[False], res[True])):
+        assert torch.equal(x, y), i
+
+
 def test_fp8_fused_ln_quant_in_the_step(gpu):
-    """bert-base (2 layers) fp8 step: after calibration the LayerNorms write the fp8 copies (no standalone quant of
-    LN outputs / LN-bwd dy), and the step matches the same step with fused quantisation switched off."""
+    """bert-base (2 layers, S = 256) fp8 step: after calibration every fp8 GEMM operand comes from its producer (the
+    embedding, the LayerNorms forward and backward, attention, the FFN epilogues): the calibrated step runs no
+    standalone activation / gradient quantiser, and its gradient tracks the previous step's."""
     from huggingface_sagemaker_tensorflow_distributed_amd.models import build_model, resolve_config
     from huggingface_sagemaker_tensorflow_distributed_amd.parallel import FlatParamStore
 
@@ -266,13 +302,15 @@ def test_fp8_fused_ln_quant_in_the_step(gpu):
     cfg = resolve_config("bert-base-uncased").replace(num_hidden_layers=2, hidden_dropout_prob=0.0,
                                                       attention_probs_dropout_prob=0.0)
     g = torch.Generator().manual_seed(0)
-    ids = torch.randint(1000, 30000, (64, 128), generator=g).to(gpu)
-    am = torch.ones(64, 128, dtype=torch.long, device=gpu)
-    labels = torch.randint(0, 2, (64,), generator=g).to(gpu)
+    # S = 256: the streaming attention kernels write their fp8 copies too (the S = 128 kernels do not: there the
+    # context and dqkv would add 2 standalone quantisations per layer)
+    ids = torch.randint(1000, 30000, (32, 256), generator=g).to(gpu)
+    am = torch.ones(32, 256, dtype=torch.long, device=gpu)
+    labels = torch.randint(0, 2, (32,), generator=g).to(gpu)
     m = build_model(cfg, seed=0).to(gpu)
     store = FlatParamStore(m, gpu, compute_dtype=torch.bfloat16, fp8=True)
     hip.set_fp8(True)
-    calls = {"ln_fwd_q8": 0, "ln_bwd_q8": 0}
+    calls = {"ln_fwd_q8": 0, "ln_bwd_q8": 0, "fp8_quant": 0, "embed_fwd": 0}
     orig = {k: getattr(hip._C, k) for k in calls}
 
     class _Count:
@@ -305,6 +343,8 @@ def test_fp8_fused_ln_quant_in_the_step(gpu):
     # per layer: the attention block's LN writes W1's copy (+ the first FFN LN writes layer 2's QKV copy);
     # every block's LN backward writes dy's copy
     assert calls["ln_fwd_q8"] == 3 and calls["ln_bwd_q8"] == 4, calls
+    # ... and the embedding writes the first layer's: a calibrated step runs no standalone activation quantiser
+    assert calls["embed_fwd"] == 1 and calls["fp8_quant"] == 0, calls
     assert torch.isfinite(grads[-1][1]).all()
     cos = torch.nn.functional.cosine_similarity(grads[1][1], grads[2][1], dim=0)
     assert cos > 0.999, float(cos)

@@ -275,6 +275,48 @@ def test_attention_fast_paths_match_generic_kernel(gpu, p, S, monkeypatch):
     _close(outs[0][1], outs[1][1], 2e-2, 2e-2, "bwd")
 
 
+@pytest.mark.parametrize("S", [256, 512])
+@pytest.mark.parametrize("masked", [False, True])
+def test_attention_keep_mask_matches_rehash(gpu, masked, S):
+    """The forward's dropout keep bits (ballot words, _keep_mask) read by the backward == the backward that re-hashes
+    every (query, key) pair (the streaming dK/dV and dQ passes, attentionS.hip): identical output and dqkv, bit for bit
+    (the atomically summed bias gradient to fp32 rounding)."""
+    hip = _hip()
+    C_ = hip._C
+    torch.manual_seed(11 + S)
+    B, heads, p = 3, 12, 0.1
+    H = heads * 64
+    qkv = torch.randn(B * S, 3 * H, device=gpu, dtype=torch.bfloat16)
+    mb = None
+    if masked:
+        am = torch.ones(B, S, dtype=torch.long, device=gpu)
+        am[2, 50:] = 0
+        am[0, S - 70:] = 0
+        mb = ref.key_mask_bias(am).float().contiguous()
+    dout = torch.randn(B * S, H, device=gpu, dtype=torch.bfloat16)
+    res = []
+    for use_km in (False, True):
+        out = torch.empty(B * S, H, device=gpu, dtype=torch.bfloat16)
+        lse = torch.empty(B * heads * S, device=gpu)
+        km = hip._keep_mask(B, S, heads, p, gpu) if use_km else None
+        assert (km is not None) == use_km
+        C_.attn_fwd(qkv, mb, out, lse, B, S, heads, p, 99, km)
+        dqkv = torch.empty_like(qkv)
+        db = torch.zeros(3 * H, device=gpu)
+        ws = hip._attn_ws(B, S, heads, gpu)
+        C_.attn_bwd(qkv, mb, out, dout, lse, dqkv, ws, B, S, heads, p, 99, db, km)
+        torch.cuda.synchronize()
+        res.append((out, dqkv, db, km))
+    assert torch.equal(res[0][0], res[1][0])
+    assert torch.equal(res[0][1], res[1][1])
+    # the bias gradient is summed by fp32 atomics across workgroups: equal up to the order of those additions
+    torch.testing.assert_close(res[1][2], res[0][2], rtol=1e-5, atol=1e-5 * float(res[0][2].abs().max()))
+    # ~90 % of the bits set (p = 0.1)
+    km = res[1][3]
+    ones = sum(bin(int(w) & 0xFFFFFFFF).count("1") for w in km[:4096].cpu().tolist())
+    assert 0.88 < ones / (4096 * 32) < 0.92
+
+
 @pytest.mark.parametrize("R,V,dtype", [(64, 2, torch.float32), (300, 2, torch.bfloat16), (97, 50265, torch.bfloat16),
                                        (33, 1003, torch.float32)])
 def test_fused_cross_entropy(gpu, R, V, dtype):

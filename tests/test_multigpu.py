@@ -27,19 +27,30 @@ def _port() -> int:
         return s.getsockname()[1]
 
 
-def test_two_rank_native_dp_matches_one_process(tmp_path):
+@pytest.mark.parametrize("mode", ["eager", "graph", "fp16_wire"])
+def test_two_rank_native_dp_matches_one_process(tmp_path, mode):
+    """eager: the bucketed RCCL all-reduce overlapped with backward; graph: the same step captured once (all-reduces
+    and engine-stream Adam slices inside the graph, HSD_GRAPH_DP=1) and replayed; fp16_wire: gradients travel in fp16
+    (pre-scaled, fused wire casts in the engine)."""
     rehearse = torch.cuda.device_count() == 1 and os.environ.get("HSD_MULTIGPU_REHEARSE") == "1"
     if torch.cuda.device_count() < 2 and not rehearse:
         pytest.skip("needs >= 2 GPUs")
+    if rehearse and mode != "eager":
+        pytest.skip("graph capture and the wire compression need the native RCCL engine (>= 2 GPUs)")
     env = dict(os.environ)
     if rehearse:
         env["HSD_DIST_BACKEND"] = "gloo"
+    if mode == "graph":
+        env.update(HSD_MGPU_GRAPH="1", HSD_GRAPH_DP="1")
+    elif mode == "fp16_wire":
+        env["HSD_MGPU_COMPRESSION"] = "fp16"
     dp_out, one_out = str(tmp_path / "dp.pt"), str(tmp_path / "one.pt")
     r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
                         "--master-addr", "127.0.0.1", "--master-port", str(_port()), WORKER, dp_out],
                        env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
-    r = subprocess.run([sys.executable, WORKER, one_out], env=env, capture_output=True, text=True, timeout=300)
+    one_env = {k: v for k, v in env.items() if not k.startswith("HSD_MGPU_")}  # the reference: one eager process
+    r = subprocess.run([sys.executable, WORKER, one_out], env=one_env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     dp = torch.load(dp_out, weights_only=True)
     one = torch.load(one_out, weights_only=True)
@@ -47,6 +58,8 @@ def test_two_rank_native_dp_matches_one_process(tmp_path):
     if not rehearse:
         assert dp["rccl_world"] == 2
     assert dp["in_sync"] is True
+    if mode == "graph":
+        assert dp["graphs"] == 1, dp["graphs"]
     g_dp, g_one = dp["grad0"], one["grad0"]
     rel = float((g_dp - g_one).norm() / g_one.norm())
     cos = float(torch.nn.functional.cosine_similarity(g_dp, g_one, dim=0))

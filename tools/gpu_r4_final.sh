@@ -1,0 +1,15 @@
+#!/bin/bash
+# Round-4 HEAD evidence: full GPU tier, smoke, headline bench + kernel stats (each step time-limited, chained).
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread > gpurun_out/r4_gpu_suite.log 2>&1
+rc=$?; tail -4 gpurun_out/r4_gpu_suite.log; [ $rc -eq 0 ] || exit $rc
+timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > gpurun_out/r4_smoke.log 2>&1 || { tail -20 gpurun_out/r4_smoke.log; exit 1; }
+tail -1 gpurun_out/r4_smoke.log
+for i in 1 2; do
+  timeout -k 10 300 python bench.py > gpurun_out/r4_bench_$i.log 2>&1 || { tail -20 gpurun_out/r4_bench_$i.log; exit 1; }
+  tail -1 gpurun_out/r4_bench_$i.log | cut -c1-220
+done
+PROF_NAME=r4_head bash tools/prof_r4.sh --steps 8 --warmup 3
