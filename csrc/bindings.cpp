@@ -452,6 +452,29 @@ void gemm8(torch::Tensor A, int64_t fa, torch::Tensor sa, torch::Tensor B, int64
                     cur_stream(), q8p, q8a, q8s, q8t, (int)q8fmt);
 }
 
+// C[M][N] fp32 += sdy·sx · dY8ᵀ · X8 (fp8 TT weight gradient): dY8 uint8 [T][M] (format fdy), X8 uint8 [T][N] (e4m3),
+// ws fp32 >= gemm8_wgrad_ws_numel; stream_ptr 0 = the current stream (else e.g. the weight-gradient side stream)
+void gemm8_wgrad(int64_t stream_ptr, torch::Tensor dy, int64_t fdy, torch::Tensor sdy, torch::Tensor x, int64_t fx,
+                 torch::Tensor sx, torch::Tensor C, int64_t splits, torch::Tensor ws) {
+  TORCH_CHECK(dy.is_cuda() && x.is_cuda() && C.is_cuda() && ws.is_cuda(), "gemm8_wgrad: GPU tensors");
+  TORCH_CHECK(dy.scalar_type() == torch::kUInt8 && x.scalar_type() == torch::kUInt8, "gemm8_wgrad: uint8 fp8 bits");
+  TORCH_CHECK(dy.dim() == 2 && x.dim() == 2 && C.dim() == 2, "gemm8_wgrad: 2-D operands");
+  TORCH_CHECK(dy.stride(1) == 1 && x.stride(1) == 1 && C.stride(1) == 1, "gemm8_wgrad: unit inner stride");
+  const int64_t T = dy.size(0), M = dy.size(1), N = x.size(1);
+  TORCH_CHECK(x.size(0) == T, "gemm8_wgrad: token count mismatch");
+  TORCH_CHECK(C.size(0) == M && C.size(1) == N && C.scalar_type() == torch::kFloat32, "gemm8_wgrad: C fp32 [M][N]");
+  TORCH_CHECK(hsd::gemm8_wgrad_supported((int)M, (int)N, (int)T), "gemm8_wgrad: unsupported shape");
+  TORCH_CHECK(dy.stride(0) % 16 == 0 && x.stride(0) % 16 == 0 && C.stride(0) % 4 == 0, "gemm8_wgrad: leading dims");
+  TORCH_CHECK(fdy == 0 || fdy == 1, "gemm8_wgrad: fdy");
+  TORCH_CHECK(fx == 0, "gemm8_wgrad: activations (X8) are e4m3");
+  check_f32(sdy, "sdy"); check_f32(sx, "sx"); check_f32(ws, "ws");
+  TORCH_CHECK(ws.numel() >= hsd::gemm8_wgrad_ws_numel((int)M, (int)N, (int)T, (int)splits), "gemm8_wgrad: workspace");
+  hipStream_t st = stream_ptr ? reinterpret_cast<hipStream_t>(stream_ptr) : cur_stream();
+  hsd::launch_gemm8_wgrad(dy.data_ptr<uint8_t>(), dy.stride(0), (int)fdy, sdy.data_ptr<float>(), x.data_ptr<uint8_t>(),
+                          x.stride(0), (int)fx, sx.data_ptr<float>(), (int)M, (int)N, (int)T, C.data_ptr<float>(),
+                          C.stride(0), (int)splits, ws.data_ptr<float>(), st);
+}
+
 // device step seed for dropout (uint32/int32 [2] GPU tensor, kept alive by the caller), None = off
 void set_dropout_device_seed(c10::optional<torch::Tensor> t) {
   if (!t.has_value()) {
@@ -865,6 +888,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm", &gemm);
   m.def("gemm2", &gemm2);
   m.def("gemm2_splits", &gemm2_splits);
+  m.def("gemm8_wgrad", &gemm8_wgrad);
+  m.def("gemm8_wgrad_supported", [](int64_t M, int64_t N, int64_t T) {
+    return hsd::gemm8_wgrad_supported((int)M, (int)N, (int)T);
+  });
+  m.def("gemm8_wgrad_ws_numel", [](int64_t M, int64_t N, int64_t T, int64_t splits) {
+    return hsd::gemm8_wgrad_ws_numel((int)M, (int)N, (int)T, (int)splits);
+  });
   m.def("gemm2_nt_splits", &gemm2_nt_splits);
   m.def("gemm2_supported", &gemm2_supported);
   m.def("gemm2_set_diag", &gemm2_set_diag);

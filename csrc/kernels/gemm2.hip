@@ -662,14 +662,54 @@ __device__ __forceinline__ i32x8 frag8(const bf16_t* img, int rbase, int lane) {
   return v;
 }
 
+// fp8 k-strided operand image (the TT weight gradient reads dY8 [T][M] and X8 [T][N] as written, tokens = k):
+// [128 tokens][256 B] per operand per stage (the same 32 KiB as a k-contiguous image), 16-B chunk c of token row k
+// stored at chunk c ^ s8t(k). A 16x16x128 fragment is four transposing reads (ds_read_b64_tr_b8): in 16-lane group g,
+// lane i addresses token row 32g + 8r + (i>>1), bytes 8(i&1) .. +7 of the fragment's 16 columns, and receives column
+// i's 8 tokens, so lane l holds column rbase + (l&15), tokens 32(l>>4) .. +31 (in some fixed order that is the same
+// for A and B: the product does not depend on it). s8t: the 16 rows a half-wave reads (groups g, g+1: rows k0..k0+7
+// and k0+32..k0+39) land in 16 distinct chunks = all 64 banks; s8t(k + 8r) = s8t(k) for the four reads of a lane.
+__device__ __forceinline__ int s8t(int k) { return (k & 7) | (((k >> 5) & 1) << 3); }
+
+typedef __attribute__((ext_vector_type(2))) int i32x2;
+typedef __attribute__((address_space(3))) i32x2 lds_i32x2_t;
+
+__device__ __forceinline__ i32x8 frag8t(const bf16_t* img, int rbase, int lane) {
+  const int g = lane >> 4, i = lane & 15;
+  const int k = 32 * g + (i >> 1);
+  const char* a = reinterpret_cast<const char*>(img) + k * 256 + ((((rbase >> 4) ^ s8t(k))) << 4) + 8 * (i & 1);
+  i32x8 v;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    const i32x2 t = __builtin_amdgcn_ds_read_tr8_b64_v2i32((lds_i32x2_t*)(a + r * 8 * 256));
+    v[2 * r] = t[0];
+    v[2 * r + 1] = t[1];
+  }
+  return v;
+}
+
+// per-lane byte offset of DMA slot gs (0..31) of an fp8 k-strided image: token rows 4gs .. 4gs+3, the lane's LDS
+// chunk (lane & 15) holds logical chunk (lane & 15) ^ s8t(row)
+__device__ __forceinline__ uint32_t lane_off8t(int64_t ld, int gs, int lane) {
+  const int row = 4 * gs + (lane >> 4);
+  return (uint32_t)((int64_t)row * ld + 16 * ((lane & 15) ^ s8t(row)));
+}
+
+template <int LT>
+__device__ __forceinline__ i32x8 frag8x(const bf16_t* img, int rbase, int lane) {
+  if constexpr (LT == 0) return frag8(img, rbase, lane);
+  else return frag8t(img, rbase, lane);
+}
+
 // FB / FA: formats of the B / A operands (0 = e4m3, 1 = e5m2); B is the instruction's first operand (D[n][m])
 template <int FB, int FA>
 __device__ __forceinline__ f32x4 mma8(const i32x8& b, const i32x8& a, const f32x4& c) {
   return __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(b, a, c, FB, FA, 0, 0, 0, 0);
 }
 
-// mainloop_staggered (SYNC 4, prologue issued by the caller) with fp8 fragments: one MFMA per (i, j) per K-tile
-template <int BN, int G, int D0, int FA, int FB, class DMA>
+// mainloop_staggered (SYNC 4, prologue issued by the caller) with fp8 fragments: one MFMA per (i, j) per K-tile.
+// LT 0: k-contiguous images (NT), 1: k-strided images (TT, frag8t)
+template <int BN, int G, int D0, int FA, int FB, int LT = 0, class DMA>
 __device__ __forceinline__ void mainloop_staggered8(f32x4 (&acc)[8][BN / 64], bf16_t* smem, const DMA& dma_slot,
                                                     int nt, int wm, int arow, int bcol, int lane) {
   constexpr int WN = BN / 4, NREP = WN / 16, NB0 = 2, NB1 = NREP - NB0;
@@ -690,9 +730,9 @@ __device__ __forceinline__ void mainloop_staggered8(f32x4 (&acc)[8][BN / 64], bf
     const int k1 = (t + 1) * BK, k2 = (t + 2) * BK;
     // P1: A-sub0 + B-sub0, first part of tile t+1's DMA
 #pragma unroll
-    for (int j = 0; j < NB0; ++j) fb0[j] = frag8(cB, bcol + 16 * j, lane);
+    for (int j = 0; j < NB0; ++j) fb0[j] = frag8x<LT>(cB, bcol + 16 * j, lane);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) fa[i] = frag8(cA, arow + 16 * i, lane);
+    for (int i = 0; i < 4; ++i) fa[i] = frag8x<LT>(cA, arow + 16 * i, lane);
     if (n1) {
 #pragma unroll
       for (int q = D0; q < E1; ++q) dma_slot(q, nS, k1);
@@ -703,7 +743,7 @@ __device__ __forceinline__ void mainloop_staggered8(f32x4 (&acc)[8][BN / 64], bf
     G2_BARRIER();
     // P2: B-sub1, rest of tile t+1's DMA
 #pragma unroll
-    for (int j = 0; j < NB1; ++j) fb1[j] = frag8(cB, bcol + 16 * (NB0 + j), lane);
+    for (int j = 0; j < NB1; ++j) fb1[j] = frag8x<LT>(cB, bcol + 16 * (NB0 + j), lane);
     if (n1) {
 #pragma unroll
       for (int q = E1; q < G; ++q) dma_slot(q, nS, k1);
@@ -714,7 +754,7 @@ __device__ __forceinline__ void mainloop_staggered8(f32x4 (&acc)[8][BN / 64], bf
     G2_BARRIER();
     // P3: A-sub1
 #pragma unroll
-    for (int i = 0; i < 4; ++i) fa[i] = frag8(cA, arow + 64 + 16 * i, lane);
+    for (int i = 0; i < 4; ++i) fa[i] = frag8x<LT>(cA, arow + 64 + 16 * i, lane);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     G2_BARRIER();
     G8_CLUSTER(4, fb1, NB1, NB0)
@@ -859,6 +899,77 @@ __global__ __launch_bounds__(512, 1) void gemm8pk_kernel(G2Params p, const float
       else vmcnt<0>();
     }
     G2_BARRIER();
+  }
+}
+
+// fp8 TT weight gradient (gemm8tt): dW[M][N] += sa·sb · Σ_t dY8[t][M] · X8[t][N], the fp8 copies the producers
+// already write for the fp8 forward / dgrad GEMMs (no transposed copies: both operands are staged as written, tokens
+// as the k rows of fp8 k-strided images, and transposed on the way out of LDS by ds_read_b64_tr_b8). One-shot grid over
+// (K-split, tile) with gemm2_kernel's XCD-aware remap, 256 x 256 tiles of 8 waves, K-tiles of 128 tokens, the
+// staggered 4-phase schedule of gemm8pk; fp32 partials [split][M][N] (dequantised) summed into dW by
+// slab_reduce_kernel. M, N multiples of 256, token splits multiples of 128.
+template <int FA, int FB>
+__global__ __launch_bounds__(512, 1) void gemm8tt_kernel(G2Params p, const float* __restrict__ sa,
+                                                         const float* __restrict__ sb) {
+  constexpr int BN = 256, NREP = 4;
+  constexpr int TA = BM * 64, STAGE = TA + BN * 64;
+  constexpr int GA = 4, GB = 4, G = GA + GB, D0 = 2;
+  __shared__ __attribute__((aligned(16))) bf16_t smem[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave >> 2, wn = wave & 3;
+  const int nwg = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
+  const int v = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  const int split = v / p.ntiles, wg = v % p.ntiles;
+  const int m0 = (wg / p.tiles_n) * BM, n0 = (wg % p.tiles_n) * BN;
+  const int kbeg = split * p.kps;  // tokens
+  const int nt = (min(p.K, kbeg + p.kps) - kbeg) / 128;
+  HSD_DASSERT(v < nwg && m0 + BM <= p.M && n0 + BN <= p.N && nt >= 1);
+  const uint8_t* A8 = reinterpret_cast<const uint8_t*>(p.A) + (int64_t)kbeg * p.lda + m0;
+  const uint8_t* B8 = reinterpret_cast<const uint8_t*>(p.B) + (int64_t)kbeg * p.ldb + n0;
+  uint32_t aoff[G];
+#pragma unroll
+  for (int q = 0; q < G; ++q)
+    aoff[q] = q < GA ? lane_off8t(p.lda, wave * GA + q, lane) : lane_off8t(p.ldb, wave * GB + (q - GA), lane);
+  const uint32_t smem_lds = (uint32_t)(size_t)(__attribute__((address_space(3))) bf16_t*)smem;
+  // k0: the main loop's K offset in bf16 units (BK = 64 per K-tile) = half the token offset
+  auto dma_slot = [&](int q, bf16_t* stage, int k0) {
+    const int64_t tok = 2 * (int64_t)k0;
+    const uint32_t st = smem_lds + (uint32_t)(stage - smem) * 2u;
+    if (q < GA)
+      dma_lds_asm(reinterpret_cast<const bf16_t*>(A8 + tok * p.lda), aoff[q], st + (wave * GA + q) * 1024u);
+    else
+      dma_lds_asm(reinterpret_cast<const bf16_t*>(B8 + tok * p.ldb), aoff[q],
+                  st + (TA + (wave * GB + (q - GA)) * 512) * 2u);
+  };
+#pragma unroll
+  for (int q = 0; q < G; ++q) dma_slot(q, smem, 0);
+  if (nt > 1) {
+#pragma unroll
+    for (int q = 0; q < D0; ++q) dma_slot(q, smem + STAGE, BK);
+  }
+  vmcnt<0>();
+  G2_BARRIER();
+  f32x4 acc[8][NREP];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < NREP; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int arow = wm * 128, bcol = wn * (BN / 4);
+  mainloop_staggered8<BN, G, D0, FA, FB, 1>(acc, smem, dma_slot, nt, wm, arow, bcol, lane);
+  // acc[i][j]: lane l holds m = 16i + (l&15), n = 16j + 4(l>>4) .. +3 of the wave tile
+  const float dq = sa[0] * sb[0];
+  float* ws = reinterpret_cast<float*>(p.C) + (int64_t)split * p.M * p.N;
+  const int q4 = lane >> 4, lr = lane & 15;
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int m = m0 + arow + 16 * i + lr;
+#pragma unroll
+    for (int j = 0; j < NREP; ++j) {
+      const int n = n0 + bcol + 16 * j + 4 * q4;
+      *reinterpret_cast<f32x4*>(ws + (int64_t)m * p.N + n) = acc[i][j] * dq;
+    }
   }
 }
 
@@ -1513,6 +1624,60 @@ void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const b
   } else {
     abort();
   }
+}
+
+// ---- fp8 TT weight gradient (g2::gemm8tt_kernel) ----------------------------------------------------------------------
+bool gemm8_wgrad_supported(int M, int N, int T) { return M % 256 == 0 && N % 256 == 0 && T % 128 == 0 && T >= 128; }
+
+// K-splits: wgrad_plan's cost model for the 256-tile kernel with one fp8 K-tile (128 tokens: the bytes and MFMA cycles
+// of one bf16 K-tile of 64) per bf16 K-tile
+int gemm8_wgrad_splits(int M, int N, int T) {
+  const int env = HSD_KNOB("HSD_G8_WGRAD_SPLITS", 0);
+  if (env > 0) return env;
+  const int kt_all = T / 128;
+  int best = 1;
+  double best_cost = 1e30;
+  for (int sp = 1; sp <= 32 && (sp == 1 || kt_all / sp >= 2); ++sp) {
+    const double c = wgrad_cost(M, N, T / 2, sp, false);
+    if (c < best_cost) { best_cost = c; best = sp; }
+  }
+  return best;
+}
+
+// token splits actually launched for `splits` requested (each a multiple of 128 tokens); the workspace holds that
+// many [M][N] fp32 slabs
+static int g8tt_kps(int T, int splits) {
+  int kps = (T + splits - 1) / splits;
+  return (kps + 127) / 128 * 128;
+}
+int64_t gemm8_wgrad_ws_numel(int M, int N, int T, int splits) {
+  if (splits <= 0) splits = gemm8_wgrad_splits(M, N, T);
+  const int kps = g8tt_kps(T, splits);
+  return (int64_t)((T + kps - 1) / kps) * M * N;
+}
+
+// C[M][N] (fp32, ldc) += sdy·sx · dY8ᵀ · X8: dY8 [T][M] (ldd bytes, format fdy), X8 [T][N] (ldx bytes, e4m3)
+void launch_gemm8_wgrad(const uint8_t* dy, int64_t ldd, int fdy, const float* sdy, const uint8_t* x, int64_t ldx,
+                        int fx, const float* sx, int M, int N, int T, float* C, int64_t ldc, int splits, float* ws,
+                        hipStream_t st) {
+  if (!gemm8_wgrad_supported(M, N, T) || fx != 0 || (fdy != 0 && fdy != 1) || ws == nullptr) abort();
+  if (splits <= 0) splits = gemm8_wgrad_splits(M, N, T);
+  G2Params p{};
+  p.A = reinterpret_cast<const bf16_t*>(dy); p.lda = ldd;
+  p.B = reinterpret_cast<const bf16_t*>(x); p.ldb = ldx;
+  p.M = M; p.N = N; p.K = T; p.C = ws; p.ldc = N;
+  p.kps = g8tt_kps(T, splits);
+  const int real = (T + p.kps - 1) / p.kps;
+  p.tiles_n = N / 256;
+  p.ntiles = (M / 256) * p.tiles_n;
+  const dim3 grid(p.ntiles * real);
+  if (fdy == 0) hipLaunchKernelGGL((g2::gemm8tt_kernel<0, 0>), grid, dim3(512), 0, st, p, sdy, sx);
+  else hipLaunchKernelGGL((g2::gemm8tt_kernel<1, 0>), grid, dim3(512), 0, st, p, sdy, sx);
+  HSD_CHECK_LAUNCH();
+  const int64_t n4 = (int64_t)M * N / 4;
+  const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
+  hipLaunchKernelGGL(g2::slab_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, C, ldc, M, N, real);
+  HSD_CHECK_LAUNCH();
 }
 
 }  // namespace hsd

@@ -145,5 +145,12 @@ void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const b
                   double p_drop, uint64_t seed, int splits, float* ws, float* dbias, hipStream_t st);
 bool gemm2_supported(int la, int lb, int epi, int M, int N, int K);
 int gemm2_wgrad_splits(int M, int N, int K);
+// fp8 TT weight gradient (gemm2.hip gemm8tt_kernel + slab_reduce): C[M][N] (fp32) += sdy·sx · dY8ᵀ · X8
+bool gemm8_wgrad_supported(int M, int N, int T);
+int gemm8_wgrad_splits(int M, int N, int T);
+int64_t gemm8_wgrad_ws_numel(int M, int N, int T, int splits);
+void launch_gemm8_wgrad(const uint8_t* dy, int64_t ldd, int fdy, const float* sdy, const uint8_t* x, int64_t ldx,
+                        int fx, const float* sx, int M, int N, int T, float* C, int64_t ldc, int splits, float* ws,
+                        hipStream_t st);
 int gemm2_nt_splits(int M, int N, int K);
 }  // namespace hsd

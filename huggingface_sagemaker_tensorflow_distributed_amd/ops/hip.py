@@ -195,12 +195,13 @@ def _end_of_backward() -> None:
     join_side_streams()
 
 
-def wgrad_done(g: "_Grad", dy: torch.Tensor, x: torch.Tensor):
+def wgrad_done(g: "_Grad", dy: torch.Tensor, x: torch.Tensor, dyq=None, xq=None):
     """``g += dyᵀ·x`` then ``g.done()`` — on the wgrad side stream when the gradient lands in the flat
-    fp32 main_grad buffer (training with a FlatParamStore) and the step is small enough, synchronously otherwise."""
+    fp32 main_grad buffer (training with a FlatParamStore) and the step is small enough, synchronously otherwise.
+    ``dyq`` / ``xq``: the producers' fp8 copies (q, sinv) of dy / x: with both, the fp8 TT kernel runs instead."""
     s = side_stream(dy.device) if (g.mg is not None and g.buf is g.mg and _use_side_stream(dy.shape[0])) else None
     if s is None:
-        gemm_wgrad_(g, dy, x)
+        gemm_wgrad_(g, dy, x, dyq, xq)
         return g.done()
     if not _JOIN_QUEUED[0]:
         # join the compute stream to the side stream when this backward pass finishes
@@ -216,6 +217,10 @@ def wgrad_done(g: "_Grad", dy: torch.Tensor, x: torch.Tensor):
         with torch.cuda.stream(s):
             gemm_wgrad_(g, dy, x)
             r = g.done()
+    elif g.buf is g.mg and _wgrad8_ok(dyq, xq, N, K, T):
+        _C.stream_wait(s.cuda_stream, src)
+        _wgrad8(g.buf, dyq, xq, N, K, T, s)
+        r = None
     elif g.buf is g.mg and _C.gemm2_supported(1, 1, 7, N, K, T):
         _C.stream_wait(s.cuda_stream, src)
         # the common case without any Python stream plumbing: TT GEMM (+ split-K reduce) launched on the side stream
@@ -226,13 +231,13 @@ def wgrad_done(g: "_Grad", dy: torch.Tensor, x: torch.Tensor):
     else:
         _C.stream_wait(s.cuda_stream, src)
         with torch.cuda.stream(s):
-            gemm_wgrad_(g, dy, x)
+            gemm_wgrad_(g, dy, x, dyq, xq)
             r = g.done()
     if _WGRAD_STASH:
-        _STASH.append((dy, x))
+        _STASH.append((dy, x, dyq, xq))
     else:
-        dy.record_stream(s)
-        x.record_stream(s)
+        for t in (dy, x, *(dyq or ()), *(xq or ())):
+            t.record_stream(s)
     return r
 
 
@@ -759,10 +764,34 @@ def gemm_dgrad(dy, w, epi=EPI_STORE, aux=None, dbias=None, dyq=None, q8_for=None
     return dx
 
 
-def gemm_wgrad_(g: "_Grad", dy, x):
-    """g.buf[N, K] += dy[T, N]ᵀ · x[T, K]   (fp32; split-K over tokens into slabs + one reduce)."""
+# fp8 weight gradients (BASELINE.json configs[4]): when both operands of a weight gradient already have an fp8 copy
+# written by their producers (the fp8 forward / dgrad path's delayed-scaling sites), dW += dyᵀ·x runs on the fp8 TT
+# kernel (gemm2.hip gemm8tt_kernel: both copies read as written, transposed in LDS) instead of the bf16 one.
+# HSD_FP8_WGRAD=0 keeps the weight gradients bf16 under --fp8.
+_FP8_WGRAD = _os.environ.get("HSD_FP8_WGRAD", "1") == "1"
+WGRAD8_CALLS = [0]  # fp8 weight-gradient launches (tests)
+
+
+def _wgrad8_ok(dyq, xq, N, K, T) -> bool:
+    return (_FP8["on"] and _FP8_WGRAD and dyq is not None and xq is not None
+            and _C.gemm8_wgrad_supported(N, K, T))
+
+
+def _wgrad8(buf, dyq, xq, N, K, T, stream=None) -> None:
+    """buf[N, K] += dequant(dyq)ᵀ · dequant(xq) on ``stream`` (None: the current stream)."""
+    ws = _workspace(_C.gemm8_wgrad_ws_numel(N, K, T, 0), buf.device, stream)
+    _C.gemm8_wgrad(stream.cuda_stream if stream is not None else 0, dyq[0], _FP8["grad_fmt"], dyq[1], xq[0],
+                   FP8_E4M3, xq[1], buf, 0, ws)
+    WGRAD8_CALLS[0] += 1
+
+
+def gemm_wgrad_(g: "_Grad", dy, x, dyq=None, xq=None):
+    """g.buf[N, K] += dy[T, N]ᵀ · x[T, K]   (fp32; split-K over tokens into slabs + one reduce). With the fp8 copies
+    ``dyq`` / ``xq`` (q, sinv) of both operands: the fp8 TT kernel on them."""
     N, K, T = dy.shape[1], x.shape[1], dy.shape[0]
-    if _C.gemm2_supported(1, 1, 7, N, K, T):
+    if _wgrad8_ok(dyq, xq, N, K, T):
+        _wgrad8(g.buf, dyq, xq, N, K, T)
+    elif _C.gemm2_supported(1, 1, 7, N, K, T):
         sp = _C.gemm2_splits(N, K, T)
         ws = _workspace(sp * N * K, dy.device)
         _C.gemm2(dy, x, g.buf, 1, 1, 7, None, None, None, 0.0, 0, sp, ws, None)
@@ -814,7 +843,8 @@ class _AttnBlock(torch.autograd.Function):
     def forward(ctx, h, qkv_w, qkv_b, out_w, out_b, ln_w, ln_b, eps, mask_bias, B, S, heads, p_a, seed_a, p_h,
                 seed_h, q8_next=None):
         h2d = h.reshape(-1, h.shape[-1])
-        qkv = gemm_fwd(h2d, qkv_w, EPI_BIAS, bias=qkv_b, xq=_take_q8(h2d))
+        hq = _take_q8(h2d)
+        qkv = gemm_fwd(h2d, qkv_w, EPI_BIAS, bias=qkv_b, xq=hq)
         H = out_w.shape[0]
         actx = torch.empty((h2d.shape[0], H), dtype=h.dtype, device=h.device)
         lse = torch.empty(B * heads * S, dtype=torch.float32, device=h.device)
@@ -837,6 +867,8 @@ class _AttnBlock(torch.autograd.Function):
                               mb if mb is not None else lse, km if km is not None else lse)
         ctx.cfg = (B, S, heads, float(p_a), seed_a, float(p_h), seed_h, mb is not None)
         ctx.has_km = km is not None
+        # fp8 copies of the weight gradients' activation operands (kept only on the fp8 weight-gradient path)
+        ctx.q8 = (hq, xq) if _FP8_WGRAD else (None, None)
         return out.view(h.shape)
 
     @staticmethod
@@ -851,7 +883,9 @@ class _AttnBlock(torch.autograd.Function):
         if dz is None:
             dz = dy
         r_lnw, r_lnb, r_ob = g_lnw.done(), g_lnb.done(), g_ob.done()
-        r_ow = wgrad_done(g_ow, dy, actx)
+        hq, actq = ctx.q8
+        ctx.q8 = None
+        r_ow = wgrad_done(g_ow, dy, actx, dyq, actq)
         dctx = gemm_dgrad(dy, out_w, dyq=dyq)
         dqkv = torch.empty_like(qkv)
         dq_acc = _attn_ws(B, S, heads, actx.device)
@@ -871,7 +905,7 @@ class _AttnBlock(torch.autograd.Function):
             _C.attn_bwd(qkv, mb if has_mask else None, actx, dctx, lse, dqkv, dq_acc, B, S, heads, p_a, _s64(seed_a),
                         g_qb.buf, km if ctx.has_km else None)
         r_qb = g_qb.done()
-        r_qw = wgrad_done(g_qw, dqkv, h2d)
+        r_qw = wgrad_done(g_qw, dqkv, h2d, dqq, hq)
         dh = gemm_dgrad(dqkv, qkv_w, EPI_RES, aux=dz, dyq=dqq) if ctx.needs_input_grad[0] else None
         return (dh.view(dout.shape) if dh is not None else None, r_qw, r_qb, r_ow, r_ob, r_lnw, r_lnb,
                 None, None, None, None, None, None, None, None, None, None)
@@ -900,10 +934,12 @@ class _FFNBlock(torch.autograd.Function):
         keep_grad = _nt_ok(h2d.shape[0], w1.shape[0], h2d.shape[1], EPI_BIAS_GELU_D) and \
             _nt_ok(h2d.shape[0], w1.shape[0], w2.shape[0], EPI_MUL)
         pre = gemm_fwd(h2d, w1, EPI_BIAS_GELU_D if keep_grad else EPI_BIAS_GELU, bias=b1, out2=act, xq=xq, q8_for=w2)
-        z = gemm_fwd(act, w2, EPI_BIAS_DROP_RES, bias=b2, aux=h2d, p=p, seed=seed, xq=_take_q8(act))
+        actq = _take_q8(act)
+        z = gemm_fwd(act, w2, EPI_BIAS_DROP_RES, bias=b2, aux=h2d, p=p, seed=seed, xq=actq)
         out, mean, rstd = _ln_fwd(z, ln_w, ln_b, eps, q8_for=q8_next)
         ctx.save_for_backward(h2d, w1, b1, w2, b2, ln_w, ln_b, pre, act, z, mean, rstd)
         ctx.cfg = (float(p), seed, keep_grad)
+        ctx.q8 = (xq, actq) if _FP8_WGRAD else (None, None)
         return out.view(h.shape)
 
     @staticmethod
@@ -918,13 +954,15 @@ class _FFNBlock(torch.autograd.Function):
         if dz is None:
             dz = dy
         r_lnw, r_lnb, r_b2 = g_lnw.done(), g_lnb.done(), g_b2.done()
-        r_w2 = wgrad_done(g_w2, dy, act)
+        hq, actq = ctx.q8
+        ctx.q8 = None
+        r_w2 = wgrad_done(g_w2, dy, act, dyq, actq)
         g_w1, g_b1 = _Grad(w1), _Grad(b1)
         da = gemm_dgrad(dy, w2, EPI_MUL if keep_grad else EPI_DGELU, aux=pre, dbias=g_b1.buf, dyq=dyq,
                         q8_for=w1 if ctx.needs_input_grad[0] else None)
         daq = _take_q8(da)
         r_b1 = g_b1.done()
-        r_w1 = wgrad_done(g_w1, da, h2d)
+        r_w1 = wgrad_done(g_w1, da, h2d, daq, hq)
         dh = gemm_dgrad(da, w1, EPI_RES, aux=dz, dyq=daq) if ctx.needs_input_grad[0] else None
         return (dh.view(dout.shape) if dh is not None else None, r_w1, r_b1, r_w2, r_b2, r_lnw, r_lnb,
                 None, None, None, None)

@@ -310,7 +310,7 @@ def test_fp8_fused_ln_quant_in_the_step(gpu):
     m = build_model(cfg, seed=0).to(gpu)
     store = FlatParamStore(m, gpu, compute_dtype=torch.bfloat16, fp8=True)
     hip.set_fp8(True)
-    calls = {"ln_fwd_q8": 0, "ln_bwd_q8": 0, "fp8_quant": 0, "embed_fwd": 0}
+    calls = {"ln_fwd_q8": 0, "ln_bwd_q8": 0, "fp8_quant": 0, "embed_fwd": 0, "gemm8_wgrad": 0}
     orig = {k: getattr(hip._C, k) for k in calls}
 
     class _Count:
@@ -345,6 +345,8 @@ def test_fp8_fused_ln_quant_in_the_step(gpu):
     assert calls["ln_fwd_q8"] == 3 and calls["ln_bwd_q8"] == 4, calls
     # ... and the embedding writes the first layer's: a calibrated step runs no standalone activation quantiser
     assert calls["embed_fwd"] == 1 and calls["fp8_quant"] == 0, calls
+    # ... and every encoder weight gradient (4 per layer) runs on the fp8 TT kernel from those same copies
+    assert calls["gemm8_wgrad"] == 8, calls
     assert torch.isfinite(grads[-1][1]).all()
     cos = torch.nn.functional.cosine_similarity(grads[1][1], grads[2][1], dim=0)
     assert cos > 0.999, float(cos)
@@ -436,3 +438,71 @@ def test_gemm8_epilogue_q8_equals_gemm8_then_quant(gpu, M, N, K, epi, fmt):
     assert torch.equal(a[2], b[2]) and torch.equal(a[3], b[3]) and torch.equal(a[4], b[4])
     if a[5] is not None:
         torch.testing.assert_close(b[5], a[5], rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("M,N,T", [(768, 256, 384), (2304, 768, 4096), (512, 1024, 1152), (1024, 4096, 2048)])
+@pytest.mark.parametrize("fdy", [0, 1])
+def test_gemm8_wgrad_matches_dequantised_fp32(gpu, M, N, T, fdy):
+    """fp8 TT weight gradient (gemm2.hip gemm8tt_kernel + slab reduce): C += dequant(dy8)ᵀ · dequant(x8), both
+    operands read as the producers write them ([T][M], [T][N]); fp32 reference of the same dequantised values."""
+    hip = _hip()
+    torch.manual_seed(5)
+    dy = (torch.randn(T, M, device=gpu) * 0.01).bfloat16()
+    x = torch.randn(T, N, device=gpu).bfloat16()
+    qd, sd = hip.quant_fp8(dy, fdy)
+    qx, sx = hip.quant_fp8(x, 0)
+    c0 = torch.randn(M, N, device=gpu)
+    ref = c0.double() + _deq(qd, sd, fdy).double().t() @ _deq(qx, sx, 0).double()
+    for splits in (0, 1, 3):
+        c = c0.clone()
+        ws = torch.empty(hip._C.gemm8_wgrad_ws_numel(M, N, T, splits), device=gpu)
+        hip._C.gemm8_wgrad(0, qd, fdy, sd, qx, 0, sx, c, splits, ws)
+        torch.cuda.synchronize()
+        err = (c.double() - ref).abs()
+        scale = (_deq(qd, sd, fdy).double().abs().t() @ _deq(qx, sx, 0).double().abs()) + c0.double().abs()
+        assert (err <= 1e-5 * scale + 1e-7).all(), (splits, float((err / (scale + 1e-12)).max()))
+
+
+def test_fp8_wgrad_step_tracks_bf16_wgrad(gpu):
+    """roberta-large (2 layers) MLM, calibrated fp8 step: weight gradients on the fp8 TT kernel vs the same step with
+    bf16 weight gradients (HSD_FP8_WGRAD=0) from the same fp8 forward / dgrad."""
+    from huggingface_sagemaker_tensorflow_distributed_amd import data as hdata
+    from huggingface_sagemaker_tensorflow_distributed_amd.models import build_model, resolve_config
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel import FlatParamStore
+
+    hip = _hip()
+    cfg = resolve_config("roberta-large").replace(num_hidden_layers=2, hidden_dropout_prob=0.0,
+                                                  attention_probs_dropout_prob=0.0)
+    ds = hdata.synthetic_mlm(8, 256, cfg.vocab_size, seed=3)
+    ids = torch.from_numpy(ds.input_ids).long().to(gpu)
+    am = torch.from_numpy(ds.attention_mask).long().to(gpu)
+    labels = torch.from_numpy(ds.labels).long().to(gpu)
+    m = build_model(cfg, task="masked-lm", seed=0).to(gpu)
+    store = FlatParamStore(m, gpu, compute_dtype=torch.bfloat16, fp8=True)
+    hip.set_fp8(True)
+    prev = hip._FP8_WGRAD
+    out = {}
+    try:
+        for step, w8 in enumerate((False, False, False, True)):
+            hip._FP8_WGRAD = w8
+            n0 = hip.WGRAD8_CALLS[0]
+            m.train()
+            m.rng.new_step(0)
+            store.zero_grad()
+            loss, _ = m(ids, attention_mask=am, labels=labels)
+            loss.backward()
+            torch.cuda.synchronize()
+            out[w8] = store.grad.float().clone()
+            if step < 2:
+                store.refresh_fp8()
+            if w8:
+                assert hip.WGRAD8_CALLS[0] - n0 == 8
+    finally:
+        hip._FP8_WGRAD = prev
+        hip.set_fp8(False)
+    g0, g1 = out[False], out[True]
+    assert torch.isfinite(g1).all()
+    cos = torch.nn.functional.cosine_similarity(g0, g1, dim=0)
+    assert cos > 0.995, float(cos)
+    rel = float((g1 - g0).norm() / g0.norm())
+    assert rel < 0.1, rel
