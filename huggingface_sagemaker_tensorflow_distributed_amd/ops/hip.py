@@ -56,14 +56,16 @@ class _Grad:
 # pass ends with the compute stream joined to it (an autograd final callback), so gradients read after
 # ``loss.backward()`` are complete on the compute stream.
 #
-# HSD_WGRAD_STREAM: "auto" (default) = on for steps of < 65,536 tokens, where the GEMM grids leave CUs idle and
-# the side stream measured +1.6 % (bert-base B = 256) to +8.4 % (bert-base B = 64) and +5.8 % at the reference's
-# bert-large B = 8 S = 512 (profiles/wgrad_stream_small_ab_r2.log); off above (neutral at B = 1024, where one
-# weight-gradient grid holds every CU). "1" = always, "0" = never. Never while a HIP graph is being captured.
+# HSD_WGRAD_STREAM: "auto" (default) = on for steps of <= 131,072 tokens. Small steps, where the GEMM grids leave CUs
+# idle, measured +1.6 % (bert-base B = 256) to +8.4 % (bert-base B = 64) and +5.8 % at the reference's bert-large
+# B = 8 S = 512 (profiles/wgrad_stream_small_ab_r2.log). At the headline's 131,072 tokens it was neutral while the
+# persistent GEMMs walked static tile lists; with dynamic tile claims a persistent dgrad kernel shares the CUs with the
+# one-shot weight-gradient grid and the side stream measured +0.7 % (13,385 vs 13,285 seq/s,
+# profiles/wgrad_side_stream_b1024_ab_r4.log). Off above. "1" = always, "0" = never.
 import os as _os
 
 _WGRAD_MODE = _os.environ.get("HSD_WGRAD_STREAM", "auto").strip().lower()
-_WGRAD_AUTO_MAX_TOKENS = int(_os.environ.get("HSD_WGRAD_STREAM_MAX_TOKENS", "65535"))
+_WGRAD_AUTO_MAX_TOKENS = int(_os.environ.get("HSD_WGRAD_STREAM_MAX_TOKENS", "131072"))
 # HSD_WGRAD_STASH=1 (default): instead of record_stream, the side stream's operands stay referenced until the
 # next join_side_streams() (the compute stream has then waited for the side stream, so their blocks go back to
 # the compute stream's pool with no cross-stream event bookkeeping in the allocator; record_stream collapsed
