@@ -1077,21 +1077,26 @@ __device__ __forceinline__ void dma_asm(bf16_t* img, const bf16_t* __restrict__ 
                : "memory");
 }
 
-// wait until at most `left` (wave-uniform) K-tiles of DMA (8 instructions each) are still in flight
-template <int NSTG>
+// wait until at most `left` (wave-uniform) K-tiles of DMA (PER instructions per wave each) are still in flight
+template <int NSTG, int PER>
 __device__ __forceinline__ void wait_tiles(int left) {
   if constexpr (NSTG >= 4) {
-    if (left >= 2) { vmcnt<16>(); return; }
+    if (left >= 2) { vmcnt<2 * PER>(); return; }
   }
   if constexpr (NSTG >= 3) {
-    if (left >= 1) { vmcnt<8>(); return; }
+    if (left >= 1) { vmcnt<PER>(); return; }
   }
   vmcnt<0>();
 }
 
-template <int LA, int LB, int EPI, int NSTG>
-__global__ __launch_bounds__(256, NSTG <= 2 ? 2 : 1) void gemm2s_kernel(G2Params p) {
+// KW = 2: 8 waves, two per SIMD -- wave groups kg = 0 / 1 take the first / second 32 k of every K-tile for the same
+// 2 x 2 arrangement of 64 x 64 wave tiles (a K-split inside the workgroup), so on each SIMD one wave's MFMAs run
+// while the other's LDS reads are in flight; group 1 hands its partial tile to group 0 through LDS (64 KiB after
+// the 32 KiB epilogue staging: NSTG 3 or 4) and group 0 runs the epilogue. KW = 1: 4 waves, one per SIMD.
+template <int LA, int LB, int EPI, int NSTG, int KW = 1>
+__global__ __launch_bounds__(256 * KW, (NSTG <= 2 && KW == 1) ? 2 : 1) void gemm2s_kernel(G2Params p) {
   static_assert(NSTG >= 2 && NSTG <= 4, "2-4 stages");
+  static_assert(KW == 1 || (KW == 2 && NSTG >= 3), "the in-workgroup K-split needs the 3rd stage's LDS for its handoff");
   static_assert(LA == 0 ? (epi_bf16_out(EPI) || EPI == E2_F32_SLAB) : (LB == 1 && EPI == E2_F32_SLAB),
                 "NT / NT with k-strided B: bf16 epilogues or split-K slabs; TT: fp32");
   p.dp = resolve_seed(p.dp);
@@ -1099,7 +1104,9 @@ __global__ __launch_bounds__(256, NSTG <= 2 ? 2 : 1) void gemm2s_kernel(G2Params
   __shared__ __attribute__((aligned(16))) bf16_t smem[NSTG * STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave >> 1, wn = wave & 1;
+  const int kg = KW == 2 ? wave >> 2 : 0;
+  const int w4 = wave & 3;
+  const int wm = w4 >> 1, wn = w4 & 1;
   // 1-D grid over (split, tile), XCD-aware bijective remap (as gemm2): the tiles one XCD runs are neighbours
   const int nwg = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q8 = nwg >> 3, r8 = nwg & 7;
@@ -1111,12 +1118,13 @@ __global__ __launch_bounds__(256, NSTG <= 2 ? 2 : 1) void gemm2s_kernel(G2Params
   const int nt = (min(p.K, kbeg + p.kps) - kbeg) / BK;
   HSD_DASSERT(v < nwg && m0 < p.M && n0 < p.N && kbeg < p.K && p.kps % BK == 0 && p.K % BK == 0);
 
-  // 16 DMA wave-instructions per operand image per stage, 4 + 4 per wave
+  // 16 DMA wave-instructions per operand image per stage, DW + DW per wave
+  constexpr int DW = 4 / KW;
   auto dma_tile = [&](bf16_t* stage, int k0) {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) dma_asm<LA>(stage, p.A, p.lda, m0, p.M, k0, wave * 4 + q, lane);
+    for (int q = 0; q < DW; ++q) dma_asm<LA>(stage, p.A, p.lda, m0, p.M, k0, wave * DW + q, lane);
 #pragma unroll
-    for (int q = 0; q < 4; ++q) dma_asm<LB>(stage + TA, p.B, p.ldb, n0, p.N, k0, wave * 4 + q, lane);
+    for (int q = 0; q < DW; ++q) dma_asm<LB>(stage + TA, p.B, p.ldb, n0, p.N, k0, wave * DW + q, lane);
   };
 
   f32x4 acc[4][4];
@@ -1135,11 +1143,12 @@ __global__ __launch_bounds__(256, NSTG <= 2 ? 2 : 1) void gemm2s_kernel(G2Params
     const bf16_t* cB = cA + TA;
     // tile t landed (this wave's part) and every wave's part visible; every wave finished reading tile t-1,
     // whose stage tile t+NSTG-1 now refills
-    wait_tiles<NSTG>(min(NSTG - 2, nt - 1 - t));
+    wait_tiles<NSTG, 2 * DW>(min(NSTG - 2, nt - 1 - t));
     G2_BARRIER();
     if (t + NSTG - 1 < nt) dma_tile(smem + ws * STAGE, kbeg + (t + NSTG - 1) * BK);
 #pragma unroll
-    for (int ks = 0; ks < 2; ++ks) {
+    for (int kk = 0; kk < 2 / KW; ++kk) {
+      const int ks = KW == 1 ? kk : kg;
       bf16x8 fa[4], fb[4];
 #pragma unroll
       for (int i = 0; i < 4; ++i) fa[i] = frag<LA, SBM>(cA, arow + 16 * i, ks, lane);
@@ -1153,6 +1162,23 @@ __global__ __launch_bounds__(256, NSTG <= 2 ? 2 : 1) void gemm2s_kernel(G2Params
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     rs = rs == NSTG - 1 ? 0 : rs + 1;
     ws = ws == NSTG - 1 ? 0 : ws + 1;
+  }
+  if constexpr (KW == 2) {
+    // every wave done with the operand stages; group 1's partial tile -> LDS [32 KiB, 96 KiB) -> group 0
+    G2_BARRIER();
+    f32x4* red = reinterpret_cast<f32x4*>(smem + 16384) + w4 * (16 * 64);
+    if (kg == 1) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) red[(i * 4 + j) * 64 + lane] = acc[i][j];
+    }
+    G2_BARRIER();
+    if (kg == 1) return;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] += red[(i * 4 + j) * 64 + lane];
   }
   const int mw = m0 + arow, nw = n0 + bcol;
   if constexpr (EPI == E2_F32_SLAB) {
@@ -1178,8 +1204,8 @@ __global__ __launch_bounds__(256, NSTG <= 2 ? 2 : 1) void gemm2s_kernel(G2Params
     }
   } else {
     // every wave done with the operand images: they become the epilogue staging (4 x 8 KiB slices)
-    G2_BARRIER();
-    epilogue_bf16<EPI, 256, 4>(acc, p, smem, wave, lane, mw, nw);
+    if constexpr (KW == 1) G2_BARRIER();
+    epilogue_bf16<EPI, 256, 4>(acc, p, smem, w4, lane, mw, nw);
   }
 }
 
@@ -1436,10 +1462,22 @@ static int g2s_stages(int grid) {
   return v < 2 ? 2 : (v > 4 ? 4 : v);
 }
 
+// gemm2s workgroup for grids of one workgroup per CU (3 stages): 8 waves with the in-workgroup K-split (2 waves per
+// SIMD, default) or 4 (one per SIMD). Measured end to end (profiles/g2s_kw2_ab_r4.log, interleaved x2): bert-large
+// S = 512 B = 8 488 -> 500-502 seq/s, bert-base B = 32 5,581-5,666 -> 5,723-5,734. HSD_G2S_KW = 1 / 2 overrides.
+static int g2s_kw(int grid) {
+  const int e = HSD_KNOB("HSD_G2S_KW", kKnobUnset);
+  if (e != kKnobUnset) return e == 2 ? 2 : 1;
+  (void)grid;
+  return 2;
+}
+
 template <int LA, int LB, int EPI>
 static void g2s_launch(const G2Params& q, int grid, hipStream_t st) {
   const int ns = g2s_stages(grid);
   if (ns == 2) hipLaunchKernelGGL((g2::gemm2s_kernel<LA, LB, EPI, 2>), dim3(grid), dim3(256), 0, st, q);
+  else if (ns == 3 && g2s_kw(grid) == 2)
+    hipLaunchKernelGGL((g2::gemm2s_kernel<LA, LB, EPI, 3, 2>), dim3(grid), dim3(512), 0, st, q);
   else if (ns == 3) hipLaunchKernelGGL((g2::gemm2s_kernel<LA, LB, EPI, 3>), dim3(grid), dim3(256), 0, st, q);
   else hipLaunchKernelGGL((g2::gemm2s_kernel<LA, LB, EPI, 4>), dim3(grid), dim3(256), 0, st, q);
   HSD_CHECK_LAUNCH();

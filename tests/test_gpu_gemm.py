@@ -321,14 +321,59 @@ def test_gemm2_small_tiles_match_256_tiles(gpu, monkeypatch, M, N, K, epi, stage
         torch.testing.assert_close(d1, d0, rtol=1e-4, atol=1e-4 * float(d0.abs().max()) + 1e-6)
 
 
-@pytest.mark.parametrize("stages", [2, 3, 4])
+@pytest.mark.parametrize("M,N,K", [(4096, 1024, 1024), (300, 512, 1024), (128, 768, 3072), (4096, 1024, 4096)])
+@pytest.mark.parametrize("epi", [0, 1, 2, 3, 4, 5, 8, 9])
+@pytest.mark.parametrize("lb", [0, 1])
+def test_gemm2_small_tiles_kw2_matches_kw1(gpu, monkeypatch, M, N, K, epi, lb):
+    """gemm2s with the in-workgroup K-split (HSD_G2S_KW=2: 8 waves, wave groups on the two halves of every K-tile,
+    partial tiles summed through LDS) vs the 4-wave kernel: same epilogues and dropout sites, the fp32 sum in another
+    order (one bf16 ulp of the rounded intermediates), for k-contiguous and k-strided (W read directly) B."""
+    torch.manual_seed(7 + epi)
+    C_ = _C()
+    A = _mk((M, K), gpu)
+    W = _mk((N, K), gpu, 0.05)  # lb 0: B = W [N][K]; lb 1: B = Wᵀ stored as [K][N]
+    B = W if lb == 0 else W.t().contiguous()
+    bias = _mk((N,), gpu)
+    aux = _mk((M, N), gpu) if epi != 9 else torch.rand(M, N, device=gpu).bfloat16()
+    two = epi in (2, 8)
+    if lb == 1 and not C_.gemm2_supported(0, 1, epi, M, N, K):
+        pytest.skip("layout (0, 1) epilogue not supported at this shape")
+    outs = []
+    monkeypatch.setenv("HSD_G2S_STAGES", "3")
+    monkeypatch.setenv("HSD_G2_SMALL", "1")
+    monkeypatch.setenv("HSD_G2_SPLITK", "1")
+    for kw in ("1", "2"):
+        monkeypatch.setenv("HSD_G2S_KW", kw)
+        C_.refresh_env()
+        C = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+        C2 = torch.empty_like(C) if two else None
+        db = torch.zeros(N, device=gpu) if epi in (5, 9) and N % 256 == 0 else None
+        C_.gemm2(A, B, C, 0, lb, epi, bias if epi in (1, 2, 3, 8) else None, aux if epi in (3, 4, 5, 9) else None,
+                 C2, 0.1 if epi == 3 else 0.0, 77, 0, None, db)
+        torch.cuda.synchronize()
+        outs.append((C, C2, db))
+    monkeypatch.delenv("HSD_G2S_KW")
+    C_.refresh_env()
+    (c1, c21, d1), (c2, c22, d2) = outs
+    y = A.float() @ W.float().t() + (bias.float() if epi in (1, 2, 3, 8) else 0.0)
+    mag = c1.float().abs() + y.abs() + (aux.float().abs() if epi in (3, 4) else 0.0)
+    _check(c2, c1.float(), mag=mag, acc=2 * _absmm(A, W, 0, 0) * (aux.float().abs() + 1 if epi in (5, 9) else 1))
+    if two:
+        _check(c22, c21.float(), mag=c21.float().abs() + y.abs(), acc=2 * _absmm(A, W, 0, 0))
+    if d1 is not None:
+        torch.testing.assert_close(d2, d1, rtol=2e-2, atol=1e-2 * float(d1.abs().max()) + 1e-3)
+
+
+@pytest.mark.parametrize("stages,kw", [(2, 1), (3, 1), (3, 2), (4, 1)])
 @pytest.mark.parametrize("M,N,K,splits", [(1024, 1024, 4096, 0), (1024, 1024, 4096, 1), (3072, 1024, 4096, 0),
                                           (1000, 768, 512, 0), (1024, 4096, 128, 0), (200, 384, 1024, 3)])
-def test_gemm2_small_tt_wgrad(gpu, monkeypatch, M, N, K, splits, stages):
+def test_gemm2_small_tt_wgrad(gpu, monkeypatch, M, N, K, splits, stages, kw):
     """gemm2s TT (128 x 128 tiles): weight gradient C += Aᵀ·B in fp32, one split accumulating in place or K-splits
-    into slabs + reduce, every stage depth, against the fp32 reference."""
+    into slabs + reduce, every stage depth and both workgroup shapes (kw 2: in-workgroup K-split), against the fp32
+    reference."""
     monkeypatch.setenv("HSD_G2_SMALL_TT", "1")
     monkeypatch.setenv("HSD_G2S_STAGES", str(stages))
+    monkeypatch.setenv("HSD_G2S_KW", str(kw))
     torch.manual_seed(31)
     C_ = _C()
     A, B = _mk((K, M), gpu), _mk((K, N), gpu)
