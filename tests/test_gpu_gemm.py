@@ -303,6 +303,9 @@ def test_gemm2_small_tiles_match_256_tiles(gpu, monkeypatch, M, N, K, epi, stage
     two = epi in (2, 8)
     outs = []
     monkeypatch.setenv("HSD_G2S_STAGES", str(stages))
+    # the 4-wave kernel (the 8-wave in-workgroup K-split sums the K halves in another order:
+    # test_gemm2_small_tiles_kw2_matches_kw1)
+    monkeypatch.setenv("HSD_G2S_KW", "1")
     for small in ("0", "1"):
         monkeypatch.setenv("HSD_G2_SMALL", small)
         monkeypatch.setenv("HSD_G2_SPLITK", "1")
