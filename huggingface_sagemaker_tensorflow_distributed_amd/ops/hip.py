@@ -885,7 +885,8 @@ class _AttnBlock(torch.autograd.Function):
         if dz is None:
             dz = dy
         r_lnw, r_lnb, r_ob = g_lnw.done(), g_lnb.done(), g_ob.done()
-        hq, actq = ctx.q8
+        # the fp8 copies are released after the first backward (a retained-graph second backward runs bf16)
+        hq, actq = ctx.q8 or (None, None)
         ctx.q8 = None
         r_ow = wgrad_done(g_ow, dy, actx, dyq, actq)
         dctx = gemm_dgrad(dy, out_w, dyq=dyq)
@@ -956,7 +957,8 @@ class _FFNBlock(torch.autograd.Function):
         if dz is None:
             dz = dy
         r_lnw, r_lnb, r_b2 = g_lnw.done(), g_lnb.done(), g_b2.done()
-        hq, actq = ctx.q8
+        # the fp8 copies are released after the first backward (a retained-graph second backward runs bf16)
+        hq, actq = ctx.q8 or (None, None)
         ctx.q8 = None
         r_w2 = wgrad_done(g_w2, dy, act, dyq, actq)
         g_w1, g_b1 = _Grad(w1), _Grad(b1)
