@@ -476,6 +476,9 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
           atomicAdd(c + 1, acc[i][j][1]);
           atomicAdd(c + 2, acc[i][j][2]);
           atomicAdd(c + 3, acc[i][j][3]);
+        } else if (p.accum_direct) {
+          f32x4* c = reinterpret_cast<f32x4*>(reinterpret_cast<float*>(p.C) + (int64_t)m * p.ldc + n);
+          *c = *c + acc[i][j];
         } else {
           float* c = reinterpret_cast<float*>(p.C) + (int64_t)split * p.M * p.N + (int64_t)m * p.N + n;
           *reinterpret_cast<f32x4*>(c) = acc[i][j];
@@ -1654,6 +1657,12 @@ void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const b
       hipLaunchKernelGGL(g2::slab_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, reinterpret_cast<float*>(C), ldc,
                          M, N, real);
       HSD_CHECK_LAUNCH();
+    } else if (epi == E2_F32_SLAB && splits <= 1 && ldc % 4 == 0 && !HSD_KNOB("HSD_G2_TT_ATOMIC", 0)) {
+      // one K-split: every output element has one owner -> C += acc in place instead of fp32 atomics (the tied MLM
+      // decoder weight gradient: Vp x H = 51.6 M atomics per roberta-large step; HSD_G2_TT_ATOMIC=1 = the old path)
+      G2Params q = p;
+      q.accum_direct = 1;
+      g2_launch<1, 1, E2_F32_SLAB, 256>(q, 1, st);
     } else {
       g2_launch<1, 1, E2_F32_ATOMIC, 256>(p, splits, st);
     }

@@ -46,6 +46,8 @@ struct G2Params {
   int q8_fmt;
   // persistent kernels: dynamic tile queue (tq_* below; one ring slot per launch), nullptr = static tile walk
   int* tq;
+  // E2_F32_SLAB with one K-split: C[m][n] += acc in place (ldc; each element has one owner) instead of a slab
+  int accum_direct;
 };
 
 // ---- dynamic tile queue of the persistent NT GEMMs (gemm2pk / gemm8pk) ----------------------------------------------

@@ -191,6 +191,31 @@ def test_gemm2_tt_wgrad(gpu, M, N, K, epi):
     _check(C, C0 + A.float().t() @ B.float(), acc=A.float().abs().t() @ B.float().abs() + C0.abs(), fp32=True)
 
 
+@pytest.mark.parametrize("M,N,K", [(50432, 1024, 4928), (2304, 768, 512), (768, 256, 320)])
+@pytest.mark.parametrize("small", ["0", "1"])
+def test_gemm2_tt_one_split_accumulates_in_place(gpu, monkeypatch, M, N, K, small):
+    """TT weight gradient with one K-split (the tied MLM decoder table: Vp x H over the masked tokens): C += Aᵀ·B in
+    place, each element written by its one owner (no fp32 atomics), on the 256 and the 128 tile kernels; against the
+    fp32 reference and the atomic-epilogue path (HSD_G2_TT_ATOMIC=1)."""
+    monkeypatch.setenv("HSD_G2_SMALL_TT", small)
+    torch.manual_seed(13)
+    C_ = _C()
+    A, B = _mk((K, M), gpu), _mk((K, N), gpu)
+    C0 = torch.randn(M, N, device=gpu)
+    outs = []
+    for atomic in ("0", "1"):
+        monkeypatch.setenv("HSD_G2_TT_ATOMIC", atomic)
+        C = C0.clone()
+        ws = torch.empty(M * N, device=gpu)  # the binding's workspace contract (unused with one split)
+        C_.gemm2(A, B, C, 1, 1, 7, None, None, None, 0.0, 0, 1, ws, None)
+        torch.cuda.synchronize()
+        outs.append(C)
+    ref = C0 + A.float().t() @ B.float()
+    acc = A.float().abs().t() @ B.float().abs() + C0.abs()
+    _check(outs[0], ref, acc=acc, fp32=True)
+    torch.testing.assert_close(outs[0], outs[1], rtol=0, atol=0)  # one owner per element: same sum either way
+
+
 @pytest.mark.parametrize("sync", [0, 1, 4, 5, 6, 7])
 @pytest.mark.parametrize("M,N,K", [(1000, 960, 192), (768, 3072, 512), (2048, 768, 3072)])
 def test_gemm2_schedules(gpu, monkeypatch, sync, M, N, K):
