@@ -1410,6 +1410,10 @@ bool gemm2s_use(int M, int N, int K) {
   if (N % SBN_HOST != 0 || K % 64 != 0) return false;
   const int e = HSD_KNOB("HSD_G2_SMALL", kKnobUnset);
   if (e != kKnobUnset) return e != 0;
+  // long K (>= 16,384: the MLM head's dgrad over the ~50k-word table): the 256 x 256 kernel with K-splits filling the
+  // CUs beats 128 x 128 tiles at one split -- 4,928 x 1,024 x 50,432: 446 us at 3 splits vs 770 us
+  // (tools/mlm_dgrad_probe.py, profiles/mlm_dgrad_probe_r4.jsonl)
+  if (K >= 16384) return false;
   const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
   return tiles * 2 <= 256;
 }

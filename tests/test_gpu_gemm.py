@@ -416,7 +416,7 @@ def test_gemm2_small_tt_wgrad(gpu, monkeypatch, M, N, K, splits, stages, kw):
 
 
 @pytest.mark.parametrize("M,N,K", [(4096, 1024, 1024), (4096, 4096, 1024), (4096, 1024, 4096), (1000, 768, 3072),
-                                   (131072 // 16, 768, 3072), (64, 1024, 1024)])
+                                   (131072 // 16, 768, 3072), (64, 1024, 1024), (1024, 1024, 16384)])
 @pytest.mark.parametrize("epi", [0, 4, 5, 9])
 def test_gemm2_dgrad_reading_w_directly_matches_stored_wt(gpu, M, N, K, epi):
     """The dgrad on W [K][N] as the NT kernel's k-strided B operand (layout (0, 1): small steps keep no Wᵀ copy)
