@@ -24,6 +24,20 @@ __device__ __forceinline__ void st1(void* x, int64_t i, float v) {
   else reinterpret_cast<float*>(x)[i] = v;
 }
 
+// one 16-B load: 8 bf16 or 4 fp32 values from element index i (16-B aligned)
+template <bool kBF16>
+__device__ __forceinline__ void ldvec(const void* __restrict__ x, int64_t i, float (&v)[kBF16 ? 8 : 4]) {
+  if constexpr (kBF16) {
+    const u32x4 w = *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(x) + i);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) { v[2 * k] = lo_bf(w[k]); v[2 * k + 1] = hi_bf(w[k]); }
+  } else {
+    const f32x4 w = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(x) + i);
+#pragma unroll
+    for (int k = 0; k < 4; ++k) v[k] = w[k];
+  }
+}
+
 template <bool kBF16>
 __global__ __launch_bounds__(256) void xent_kernel(const void* __restrict__ logits, const int64_t* __restrict__ labels,
                                                    void* __restrict__ dlogits, float* __restrict__ stats,
@@ -36,21 +50,14 @@ __global__ __launch_bounds__(256) void xent_kernel(const void* __restrict__ logi
   const bool valid = y >= 0 && y < V;
   float m = -INFINITY, s = 0.f, best = -INFINITY;
   int besti = 0;
-  // vector path: 8 bf16 (or 4 fp32) per 16-B load over the 16-B-aligned part of the row, scalar tail
+  // vector path: 8 bf16 (or 4 fp32) per 16-B load over the 16-B-aligned part of the row, scalar tail. XU 16-B loads
+  // per lane are issued before any is used: one wave per row holds XU KiB in flight instead of 1 (the MLM head's
+  // 4,928 x 50,432 logits were latency-bound at one load per wave)
   constexpr int VEC = kBF16 ? 8 : 4;
+  constexpr int XU = 4;
   const bool vec = (ld % VEC) == 0;
   const int Vv = vec ? V - V % VEC : 0;
-  for (int j = lane * VEC; j < Vv; j += 64 * VEC) {
-    float v[VEC];
-    if constexpr (kBF16) {
-      const u32x4 w = *reinterpret_cast<const u32x4*>(reinterpret_cast<const bf16_t*>(logits) + base + j);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) { v[2 * k] = lo_bf(w[k]); v[2 * k + 1] = hi_bf(w[k]); }
-    } else {
-      const f32x4 w = *reinterpret_cast<const f32x4*>(reinterpret_cast<const float*>(logits) + base + j);
-#pragma unroll
-      for (int k = 0; k < 4; ++k) v[k] = w[k];
-    }
+  auto consume = [&](const float (&v)[VEC], int j) {
     float cm = v[0];
 #pragma unroll
     for (int k = 1; k < VEC; ++k) cm = fmaxf(cm, v[k]);
@@ -62,6 +69,19 @@ __global__ __launch_bounds__(256) void xent_kernel(const void* __restrict__ logi
       if (v[k] > best) { best = v[k]; besti = j + k; }
     }
     m = nm;
+  };
+  int j0 = lane * VEC;
+  for (; j0 + (XU - 1) * 64 * VEC < Vv; j0 += XU * 64 * VEC) {
+    float v[XU][VEC];
+#pragma unroll
+    for (int u = 0; u < XU; ++u) ldvec<kBF16>(logits, base + j0 + u * 64 * VEC, v[u]);
+#pragma unroll
+    for (int u = 0; u < XU; ++u) consume(v[u], j0 + u * 64 * VEC);
+  }
+  for (; j0 < Vv; j0 += 64 * VEC) {
+    float v[VEC];
+    ldvec<kBF16>(logits, base + j0, v);
+    consume(v, j0);
   }
   for (int j = Vv + lane; j < V; j += 64) {
     const float v = ld1<kBF16>(logits, base + j);
@@ -91,12 +111,12 @@ __global__ __launch_bounds__(256) void xent_kernel(const void* __restrict__ logi
     // gradient over the whole padded row: columns >= V (a padded vocabulary) get exact zeros
     const float scale = valid ? inv_n : 0.f;
     if (vec) {
-      for (int j = lane * VEC; j < ld; j += 64 * VEC) {
+      auto emit = [&](const float (&v)[VEC], int j) {
         float g[VEC];
 #pragma unroll
         for (int k = 0; k < VEC; ++k) {
           const int jj = j + k;
-          g[k] = jj < V ? scale * (__expf(ld1<kBF16>(logits, base + jj) - lse) - (jj == y ? 1.0f : 0.0f)) : 0.0f;
+          g[k] = jj < V ? scale * (__expf(v[k] - lse) - (jj == y ? 1.0f : 0.0f)) : 0.0f;
         }
         if constexpr (kBF16) {
           *reinterpret_cast<u32x4*>(reinterpret_cast<bf16_t*>(dlogits) + base + j) =
@@ -104,6 +124,20 @@ __global__ __launch_bounds__(256) void xent_kernel(const void* __restrict__ logi
         } else {
           *reinterpret_cast<f32x4*>(reinterpret_cast<float*>(dlogits) + base + j) = f32x4{g[0], g[1], g[2], g[3]};
         }
+      };
+      // 16-B loads (the padded columns beyond V read the padding, which is then zeroed), XU in flight per lane
+      int j = lane * VEC;
+      for (; j + (XU - 1) * 64 * VEC < ld; j += XU * 64 * VEC) {
+        float v[XU][VEC];
+#pragma unroll
+        for (int u = 0; u < XU; ++u) ldvec<kBF16>(logits, base + j + u * 64 * VEC, v[u]);
+#pragma unroll
+        for (int u = 0; u < XU; ++u) emit(v[u], j + u * 64 * VEC);
+      }
+      for (; j < ld; j += 64 * VEC) {
+        float v[VEC];
+        ldvec<kBF16>(logits, base + j, v);
+        emit(v, j);
       }
     } else {
       for (int j = lane; j < ld; j += 64) {

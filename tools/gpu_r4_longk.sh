@@ -4,7 +4,7 @@ set -o pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest -x -q --timeout 120 --timeout-method thread tests/test_gpu_gemm.py tests/test_gpu_fp8.py tests/test_gpu_e2e.py \
-  -k "dgrad_reading_w or mlm or splitk" > gpurun_out/longk_tests.log 2>&1 || { tail -30 gpurun_out/longk_tests.log; exit 1; }
+  -k "dgrad_reading_w or mlm or splitk or xent or cross_entropy" > gpurun_out/longk_tests.log 2>&1 || { tail -30 gpurun_out/longk_tests.log; exit 1; }
 tail -2 gpurun_out/longk_tests.log
 : > gpurun_out/longk_ab.log
 A="--model roberta-large --task masked-lm --seq_len 512 --batch_size 64 --steps 20 --warmup 5"
