@@ -17,4 +17,6 @@ timeout -k 10 300 python bench.py --model bert-large-uncased --seq_len 512 --bat
 tail -1 gpurun_out/r4_bench_bl8.log | cut -c1-220
 timeout -k 10 300 python bench.py --model roberta-large --task masked-lm --seq_len 512 --batch_size 64 --dtype fp8 > gpurun_out/r4_bench_fp8.log 2>&1 || exit 1
 tail -1 gpurun_out/r4_bench_fp8.log | cut -c1-220
+timeout -k 10 300 python bench.py --model roberta-large --task masked-lm --seq_len 512 --batch_size 64 --dtype bf16 > gpurun_out/r4_bench_mlm_bf16.log 2>&1 || exit 1
+tail -1 gpurun_out/r4_bench_mlm_bf16.log | cut -c1-220
 PROF_NAME=r4_head bash tools/prof_r4.sh --steps 8 --warmup 3
