@@ -1443,6 +1443,16 @@ static WgradPlan wgrad_plan(int M, int N, int K) {
   const int force = HSD_KNOB("HSD_G2_SMALL_TT", -1);
   const bool can_small = N % SBN_HOST == 0 && M % 8 == 0 && K % 64 == 0 && force != 0;
   const bool can_big = N % 256 == 0 && force != 1;
+  // small steps, whose weight gradients run on the side stream under the backward: the fewest K-splits of the 128 x 128
+  // kernel that still give HSD_WGRAD_MIN_GRID workgroups (0 = off: the latency cost model below), so a weight
+  // gradient takes no more CUs and slab traffic than it needs beside the critical path
+  const int min_grid = HSD_KNOB("HSD_WGRAD_MIN_GRID", 0);
+  if (min_grid > 0 && can_small) {
+    const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
+    int sp = 1;
+    while (tiles * sp < min_grid && sp < 32 && (K / 64) / (sp + 1) >= 2) ++sp;
+    return WgradPlan{true, sp};
+  }
   const int min_kt = std::max(1, HSD_KNOB("HSD_WGRAD_MIN_KT", 2));
   const int kt_all = K / 64;
   WgradPlan best{can_small && !can_big, 1};
