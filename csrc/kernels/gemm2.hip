@@ -1443,10 +1443,13 @@ static WgradPlan wgrad_plan(int M, int N, int K) {
   const int force = HSD_KNOB("HSD_G2_SMALL_TT", -1);
   const bool can_small = N % SBN_HOST == 0 && M % 8 == 0 && K % 64 == 0 && force != 0;
   const bool can_big = N % 256 == 0 && force != 1;
-  // small steps, whose weight gradients run on the side stream under the backward: the fewest K-splits of the 128 x 128
-  // kernel that still give HSD_WGRAD_MIN_GRID workgroups (0 = off: the latency cost model below), so a weight
-  // gradient takes no more CUs and slab traffic than it needs beside the critical path
-  const int min_grid = HSD_KNOB("HSD_WGRAD_MIN_GRID", 0);
+  // small steps (<= 8,192 tokens), whose weight gradients run on the side stream under the backward: the fewest K-splits
+  // of the 128 x 128 kernel that still give 192 workgroups, so a weight gradient takes no more CUs and slab traffic
+  // than it needs beside the critical path (the latency cost model below minimises its own time instead). Measured
+  // (profiles/wgrad_min_grid_ab_r4.log): bert-large S=512 B=8 504-505 -> 524-526 seq/s, bert-base B=64 +1.8 %.
+  // HSD_WGRAD_MIN_GRID overrides (0 = the cost model at every size).
+  const int grid_knob = HSD_KNOB("HSD_WGRAD_MIN_GRID", kKnobUnset);
+  const int min_grid = grid_knob != kKnobUnset ? grid_knob : (K <= 8192 ? 192 : 0);
   if (min_grid > 0 && can_small) {
     const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
     int sp = 1;
