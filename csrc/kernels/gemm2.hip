@@ -1447,9 +1447,12 @@ static WgradPlan wgrad_plan(int M, int N, int K) {
   // of the 128 x 128 kernel that still give 192 workgroups, so a weight gradient takes no more CUs and slab traffic
   // than it needs beside the critical path (the latency cost model below minimises its own time instead). Measured
   // (profiles/wgrad_min_grid_ab_r4.log): bert-large S=512 B=8 504-505 -> 524-526 seq/s, bert-base B=64 +1.8 %.
-  // HSD_WGRAD_MIN_GRID overrides (0 = the cost model at every size).
+  // HSD_WGRAD_MIN_GRID sets the workgroup target (0 = the cost model at every size).
   const int grid_knob = HSD_KNOB("HSD_WGRAD_MIN_GRID", kKnobUnset);
-  const int min_grid = grid_knob != kKnobUnset ? grid_knob : (K <= 8192 ? 192 : 0);
+  // opt-in (HSD_WGRAD_MIN_GRID=192): the whole-step HIP graph with the native engine (opt-in HSD_GRAPH_DP) once
+  // diverged from eager under it in a full GPU-tier run (tests/test_gpu_comm.py::test_whole_step_graph_with_native_
+  // engine; passes in isolation) -- an ordering edge of that capture to re-check before this becomes the default
+  const int min_grid = grid_knob != kKnobUnset ? grid_knob : 0;
   if (min_grid > 0 && can_small) {
     const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
     int sp = 1;
