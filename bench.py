@@ -41,8 +41,10 @@ def main():
     ap.add_argument("--model", default="bert-base-uncased")
     ap.add_argument("--bucket_mb", type=float, default=None)
     ap.add_argument("--grad_dtype", default=None)
-    ap.add_argument("--dtype", choices=["bf16", "fp8"], default="bf16",
-                    help="fp8: fp8 forward/dgrad GEMMs (secondary config; the headline is bf16)")
+    ap.add_argument("--dtype", choices=["bf16", "fp8", "fp32"], default="bf16",
+                    help="fp8: fp8 forward/dgrad GEMMs (secondary config; the headline is bf16); fp32: the reference's "
+                         "own precision (scripts/train.py:113-123 sets no mixed-precision policy) on the fp32 kernels "
+                         "of ops/hip32.py")
     ap.add_argument("--task", choices=["sequence-classification", "masked-lm"], default="sequence-classification")
     ap.add_argument("--hip_graph", action="store_true", help="replay fwd+bwd from a captured HIP graph (N=1)")
     a = ap.parse_args()

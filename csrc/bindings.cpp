@@ -237,8 +237,10 @@ void colsum(torch::Tensor x, torch::Tensor dbias) {
 
 void dropout(torch::Tensor x, torch::Tensor out, double p, int64_t seed) {
   check_bf16(x, "x"); check_bf16(out, "out");
-  TORCH_CHECK(x.numel() == out.numel() && x.numel() % 4 == 0, "dropout shapes");
-  hsd::launch_dropout(CBF(x), BF(out), x.numel(), p, (uint64_t)seed, cur_stream());
+  // the mask's row width is the last dimension (ops/rng.py); 4-element vectors never straddle a row
+  const int64_t W = x.dim() ? x.size(-1) : 1;
+  TORCH_CHECK(x.numel() == out.numel() && W % 4 == 0, "dropout shapes");
+  hsd::launch_dropout(CBF(x), BF(out), x.numel(), (int)W, p, (uint64_t)seed, cur_stream());
 }
 
 static uint32_t* keep_mask_ptr(const c10::optional<torch::Tensor>& km, int64_t B, int64_t S, int64_t heads) {
@@ -582,8 +584,9 @@ void epi32(torch::Tensor y, c10::optional<torch::Tensor> bias, c10::optional<tor
 
 void dropout32(torch::Tensor x, torch::Tensor out, double p, int64_t seed) {
   check_f32(x, "x"); check_f32(out, "out");
-  TORCH_CHECK(x.numel() == out.numel() && x.numel() % 4 == 0, "dropout32 sizes");
-  hsd::launch_dropout32(x.data_ptr<float>(), out.data_ptr<float>(), x.numel(), p, (uint64_t)seed, cur_stream());
+  const int64_t W = x.dim() ? x.size(-1) : 1;
+  TORCH_CHECK(x.numel() == out.numel() && W % 4 == 0, "dropout32 sizes");
+  hsd::launch_dropout32(x.data_ptr<float>(), out.data_ptr<float>(), x.numel(), (int)W, p, (uint64_t)seed, cur_stream());
 }
 
 void colsum32(torch::Tensor x, torch::Tensor dbias) {
@@ -862,6 +865,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cls32_fwd", &cls32_fwd);
   m.def("cls32_bwd", &cls32_bwd);
   m.def("refresh_env", &hsd::refresh_env_knobs, "re-read the HSD_* launch knobs (cached per generation)");
+  // the kernels' dropout mask definition evaluated on the host (common.h): tests pin ops/rng.py to it bit for bit
+  m.def("dropout_pair_bits", [](int64_t seed, int64_t row, int64_t cp) -> int64_t {
+    return (int64_t)hsd::dropout_pair_bits_host((uint64_t)seed, (uint32_t)row, (uint32_t)cp);
+  });
   m.def("fp8_quant", &fp8_quant, py::arg("x"), py::arg("amax"), py::arg("q"), py::arg("sinv"), py::arg("fmt"),
         py::arg("compute_amax"), py::arg("amax_track") = py::none());
   m.def("fp8_quant_many", &fp8_quant_many);

@@ -92,11 +92,21 @@ class CommEngine {
     HIP_OK(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
   }
 
-  ~CommEngine() {
-    // drain, then release the communicator; the stream and events are left to process teardown (the
-    // caching allocator may still hold blocks whose last use was recorded on this stream)
+  ~CommEngine() { close(); }
+
+  // Drain, then release the communicator (idempotent); the stream and events are left to process teardown (the
+  // caching allocator may still hold blocks whose last use was recorded on this stream). Python may run this from
+  // its cyclic garbage collector at any allocation -- also while this thread captures a HIP graph, where a stream
+  // synchronisation or a device free is an unsafe call that invalidates the capture (a corrupt graph: a host fault
+  // at replay). The thread's capture mode is relaxed around the teardown.
+  void close() {
+    if (comm_ == nullptr) return;
+    hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
+    const bool swapped = hipThreadExchangeStreamCaptureMode(&mode) == hipSuccess;
     if (stream_) (void)hipStreamSynchronize(stream_);
-    if (comm_) (void)ncclCommDestroy(comm_);
+    (void)ncclCommDestroy(comm_);
+    comm_ = nullptr;  // collectives after close() fail in RCCL (invalid communicator)
+    if (swapped) (void)hipThreadExchangeStreamCaptureMode(&mode);
   }
 
   static std::string unique_id() {
@@ -263,8 +273,17 @@ class CommEngine {
     dep_events_.push_back(e);
   }
 
-  // 0 = the current stream (default); otherwise every caller-side event record / wait uses this stream
-  void set_caller_stream(int64_t stream_ptr) { caller_override_ = reinterpret_cast<hipStream_t>(stream_ptr); }
+  // 0 = the current stream (default); otherwise every caller-side event record / wait uses this stream (a HIP-graph
+  // capture). A new caller stream starts with its dependency streams outside the capture (see set_capture_deps).
+  void set_caller_stream(int64_t stream_ptr) {
+    caller_override_ = reinterpret_cast<hipStream_t>(stream_ptr);
+    capture_deps_ = false;
+  }
+
+  // Inside a capture: whether the registered dependency streams are branches of it now (the capture forked the wgrad
+  // side stream: ops/hip.py side_stream_in_capture). From then on every bucket is ordered after them as in eager
+  // steps; before the fork they hold no captured work, and an event of an uncaptured stream is no capture edge.
+  void set_capture_deps(bool on) { capture_deps_ = on; }
 
   int64_t num_buckets() const { return (int64_t)buckets_.size(); }
   int64_t launched_count() const {
@@ -288,9 +307,10 @@ class CommEngine {
   void order_after_caller() {
     HIP_OK(hipEventRecord(ready_, caller()));
     HIP_OK(hipStreamWaitEvent(stream_, ready_, 0));
-    // gradients may also be produced on registered side streams (the wgrad stream): order after them too -- not
-    // inside a capture (set_caller_stream), which runs no side stream and must not wait on uncaptured work
-    if (caller_override_) return;
+    // gradients may also be produced on registered side streams (the wgrad stream): order after them too. Inside a
+    // capture (set_caller_stream) only once the capture has forked them (set_capture_deps): the wgrad branch writes
+    // the same main_grad slices this bucket's all-reduce and Adam slice read
+    if (caller_override_ && !capture_deps_) return;
     for (size_t i = 0; i < deps_.size(); ++i) {
       HIP_OK(hipEventRecord(dep_events_[i], deps_[i]));
       HIP_OK(hipStreamWaitEvent(stream_, dep_events_[i], 0));
@@ -343,6 +363,7 @@ class CommEngine {
   int rank_, world_, device_;
   hipStream_t stream_ = nullptr;
   hipStream_t caller_override_ = nullptr;
+  bool capture_deps_ = false;
   ncclComm_t comm_ = nullptr;
   hipEvent_t ready_ = nullptr;
   bool timing_ = false;
@@ -385,6 +406,8 @@ void register_comm(pybind11::module& m) {
       .def("launched_count", &CommEngine::launched_count)
       .def("stream_ptr", &CommEngine::stream_ptr)
       .def("set_caller_stream", &CommEngine::set_caller_stream)
+      .def("set_capture_deps", &CommEngine::set_capture_deps)
+      .def("close", &CommEngine::close)
       .def_property_readonly("rank", &CommEngine::rank)
       .def_property_readonly("world", &CommEngine::world);
 }

@@ -146,13 +146,13 @@ __global__ __launch_bounds__(256) void attn_fwd_kernel(const bf16_t* __restrict_
     o0 *= alpha;
     o1 *= alpha;
     if (dp.enabled) {
-      const uint32_t rowbase = (uint32_t)(((size_t)bh * S + qc) * S);
+      // mask row bh S + qc, column pair key / 2 = 32 kt + 16 kb + 4 (reg >> 2) + (reg >> 1 & 1) + 2 hf (disjoint bits)
+      const uint32_t xt = dropout_row((uint32_t)(bh * S + qc), dp) ^ drop_col(32u * (uint32_t)kt + 2u * (uint32_t)hf);
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int reg = 0; reg < 16; reg += 2) {
-          const int key = kt * 64 + kb * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * hf;
-          const uint32_t bits = dropout_bits((rowbase + key) >> 1, dp);
+          const uint32_t bits = drop_fin(xt ^ drop_col((uint32_t)(16 * kb + 4 * (reg >> 2) + ((reg >> 1) & 1))));
           st[kb][reg] *= keep_factor(bits, 0, dp);
           st[kb][reg + 1] *= keep_factor(bits, 1, dp);
         }
@@ -206,6 +206,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const bf16_t* __restrict_
   const int kbase = blockIdx.x * 128;
   const int key = kbase + wave * 32 + r;
   const int kc = min(key, S - 1);
+  const uint32_t ck = drop_col((uint32_t)kc >> 1);  // dropout column word of this lane's key
   const bf16_t* base = qkv + (size_t)b * S * ld;
 
   // per-wave K and V B-fragments (key on the lane)
@@ -270,8 +271,7 @@ __global__ __launch_bounds__(256) void attn_bwd_kernel(const bf16_t* __restrict_
       float p = (qq < S) ? exp2f(sacc[reg] * sl2 + kb2 - lse_s[qi]) : 0.f;
       float kf_ = 1.0f;
       if (dp.enabled) {
-        const uint32_t e = (uint32_t)(((size_t)bh * S + min(qq, S - 1)) * S + kc);
-        kf_ = keep_factor(dropout_bits(e >> 1, dp), (int)(e & 1), dp);
+        kf_ = keep_factor(drop_fin(dropout_row((uint32_t)(bh * S + min(qq, S - 1)), dp) ^ ck), kc & 1, dp);
       }
       pd[reg] = p * kf_;
       ds[reg] = p * (dpacc[reg] * kf_ - del_s[qi]);

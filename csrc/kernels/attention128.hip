@@ -92,17 +92,21 @@ __global__ __launch_bounds__(256, 4) void attn128_fwd_kernel(const bf16_t* __res
       st[kb][reg] = p;
     }
   l = sum_xor32(l);
+  float oscale = 1.0f / l;
   if (dp.enabled) {
-    const uint32_t rowbase = (uint32_t)(((int64_t)bh * S + q) * S);
+    // mask row bh S + q, column pair key / 2 = 16 kb + 4 (reg >> 2) + (reg >> 1 & 1) + 2 hf (disjoint bits): one row
+    // word per lane, the hf term folded in, each register's C(...) a literal. P is kept or zeroed (the 1/(1-p) scale
+    // rides on the output normalisation)
+    const uint32_t xq = dropout_row((uint32_t)(bh * S + q), dp) ^ drop_col(2u * (uint32_t)hf);
 #pragma unroll
     for (int kb = 0; kb < 4; ++kb)
 #pragma unroll
       for (int reg = 0; reg < 16; reg += 2) {
-        const int key = kb * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * hf;
-        const uint32_t bits = dropout_bits((rowbase + key) >> 1, dp);
-        st[kb][reg] *= keep_factor(bits, 0, dp);
-        st[kb][reg + 1] *= keep_factor(bits, 1, dp);
+        const uint32_t bits = drop_fin(xq ^ drop_col((uint32_t)(16 * kb + 4 * (reg >> 2) + ((reg >> 1) & 1))));
+        st[kb][reg] = keep_lo(bits, dp.thr) ? st[kb][reg] : 0.f;
+        st[kb][reg + 1] = keep_hi(bits, dp.thr) ? st[kb][reg + 1] : 0.f;
       }
+    oscale *= dp.scale;
   }
   // Oᵀ[d][q] = Σ_key Vᵀ[d][key] Pᵀ[key][q]
   f32x16 o0 = {}, o1 = {};
@@ -118,7 +122,7 @@ __global__ __launch_bounds__(256, 4) void attn128_fwd_kernel(const bf16_t* __res
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   __builtin_amdgcn_s_barrier();  // every wave's K reads done: K's slot becomes the output staging
   asm volatile("" ::: "memory");
-  store_rows(stg_all + wave * 32 * D, o0, o1, 1.0f / l, out + ((int64_t)b * S + wave * 32) * H + hh * D, H, lane);
+  store_rows(stg_all + wave * 32 * D, o0, o1, oscale, out + ((int64_t)b * S + wave * 32) * H + hh * D, H, lane);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -141,13 +145,14 @@ __global__ __launch_bounds__(256, 2) void attn128_bwd_kernel(const bf16_t* __res
   }
   // [Q | dO | dS | lse | delta | bias-grad partials]; after the main loop Q's slot holds K, dO's slot the
   // output staging
-  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * S * D + S * S + 4 * S + 2 * 3 * 4 * D];
+  __shared__ __attribute__((aligned(16))) bf16_t lds[2 * S * D + S * S + 4 * S + 2 * 3 * 4 * D + 2 * S];
   bf16_t* Qs = lds;
   bf16_t* dOs = lds + S * D;
   bf16_t* dSt = lds + 2 * S * D;
   float* lse_s = reinterpret_cast<float*>(lds + 2 * S * D + S * S);
   float* del_s = lse_s + S;
   float* bsum = del_s + S;  // [3 (q,k,v)][4 waves][64]
+  uint32_t* rw_s = reinterpret_cast<uint32_t*>(bsum + 3 * 4 * D);  // dropout row words R(bh S + q) of the 128 queries
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int r = lane & 31, hf = lane >> 5;
@@ -177,6 +182,9 @@ __global__ __launch_bounds__(256, 2) void attn128_bwd_kernel(const bf16_t* __res
     ov[i] = *reinterpret_cast<const u32x4*>(obase + (int64_t)row * H + c * 8);
   }
   if (tid < S) lse_s[tid] = lse2[(int64_t)bh * S + tid];
+  if constexpr (DROP) {
+    if (tid < S) rw_s[tid] = dropout_row((uint32_t)(bh * S + tid), dp);
+  }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   if (diag) ts[1] = __builtin_amdgcn_s_memtime();
@@ -218,8 +226,10 @@ __global__ __launch_bounds__(256, 2) void attn128_bwd_kernel(const bf16_t* __res
         off_tr[s2][cb][1] = toff(r0 + 8, col);
       }
   }
-  // dropout pair index of (query qi0 (+1 on odd lanes), this lane's key): ((bh S + q) S + key) >> 1
-  const uint32_t pair_lane = (uint32_t)bh * (S * S / 2) + (uint32_t)(key >> 1) + (odd ? S / 2 : 0);
+  // dropout: mask row bh S + query, column pair key / 2 -- the same 32-bit word for lanes l and l ^ 1 (keys 2j, 2j + 1):
+  // the even lane computes query qi0's word, the odd lane query qi0 + 1's, and they swap (one DPP move)
+  const uint32_t ck = drop_col((uint32_t)key >> 1);
+  const int qsel = 4 * hf + (odd ? 1 : 0);
 #pragma unroll 1
   for (int qb = 0; qb < 4; ++qb) {
     const int qoff = qb * 32 * 64;  // element offset of the block's first row in a [rows][64] image
@@ -233,7 +243,6 @@ __global__ __launch_bounds__(256, 2) void attn128_bwd_kernel(const bf16_t* __res
     }
     // rows: query qi = (reg&3) + 8(reg>>2) + 4hf of the block; col (lane): key
     f32x16 pd, ds;
-    const uint32_t pair_qb = pair_lane + (uint32_t)(qb * 32 + 4 * hf) * (S / 2);
 #pragma unroll
     for (int reg = 0; reg < 16; reg += 2) {
       const int qi0 = qb * 32 + (reg & 3) + 8 * (reg >> 2) + 4 * hf;  // rows qi0, qi0 + 1
@@ -243,9 +252,7 @@ __global__ __launch_bounds__(256, 2) void attn128_bwd_kernel(const bf16_t* __res
       const float p1 = __builtin_amdgcn_exp2f(fmaf(sacc[reg + 1], sl2, kb2) - lse[1]);
       float k0 = 1.f, k1 = 1.f;
       if constexpr (DROP) {
-        // element ((bh*S + q)*S + key): keys 2j, 2j+1 (lanes l, l^1) share one hash per query row.
-        // even lane hashes row qi0, odd lane row qi0+1, then they swap (a DPP lane move, no LDS round trip)
-        const uint32_t bits = dropout_bits(pair_qb + (uint32_t)((reg & 3) + 8 * (reg >> 2)) * (S / 2), dp);
+        const uint32_t bits = drop_fin(rw_s[qb * 32 + (reg & 3) + 8 * (reg >> 2) + qsel] ^ ck);
         const uint32_t other = dpp_xor1(bits);
         const uint32_t b0 = odd ? other : bits;   // hash of row qi0
         const uint32_t b1 = odd ? bits : other;   // hash of row qi0 + 1

@@ -68,6 +68,12 @@ __device__ __forceinline__ void settle(const T& v) {
   asm volatile("" ::"v"(v));
 }
 
+// lane L of v <- the wave-uniform x (one v_writelane_b32: no per-lane select masks held in SGPRs)
+__device__ int llvm_writelane(int val, int lane, int old) __asm("llvm.amdgcn.writelane.i32");
+__device__ __forceinline__ void put_lane(uint32_t& v, int lane, uint32_t x) {
+  v = (uint32_t)llvm_writelane((int)x, lane, (int)v);
+}
+
 template <int INFLIGHT, int EXTRA = 0>
 __device__ __forceinline__ void tile_barrier() {
   // EXTRA: younger vector-memory ops issued since the in-flight tiles' DMA (the forward's keep-mask stores)
@@ -114,8 +120,14 @@ __global__ __launch_bounds__(256, 2) void attnS_fwd_kernel(const bf16_t* __restr
 
   f32x16 o0 = {}, o1 = {};
   float m = -INFINITY, l = 0.f;
-  // dropout pair of (q, key): ((bh S + q) S + key) >> 1 = pair_q + key / 2 (key even in every hashed pair)
-  const uint32_t pair_q = (uint32_t)(((int64_t)bh * S + q) * (S / 2)) + 2 * hf;
+  // dropout: mask row bh S + q, column pair key / 2 = 32 kt + 16 kb + 4 (reg >> 2) + (reg >> 1 & 1) + 2 hf (disjoint
+  // bits). One row word per lane with the hf term folded in; C(32 kt) from lane kt of a per-kernel table (one
+  // readlane per tile); each register's C(...) is a literal. P is kept or zeroed, the 1/(1-p) scale rides on 1/l.
+  uint32_t xq = 0, ctile = 0;
+  if constexpr (DROP) {
+    xq = dropout_row((uint32_t)(bh * S + q), dp) ^ drop_col(2u * (uint32_t)hf);
+    ctile = drop_col(32u * (uint32_t)lane);  // lane kt: C(32 kt), kt < S / 64 <= 16
+  }
   const bool km_on = DROP && kmask != nullptr;
   // keep-mask words of this wave: key-major [bh][q0 / 32][key], query-major [bh][kt][q][hf] (header)
   uint32_t* const km_k = km_on ? kmask + ((int64_t)bh * (S / 32) + q0 / 32) * S : nullptr;
@@ -179,25 +191,25 @@ __global__ __launch_bounds__(256, 2) void attnS_fwd_kernel(const bf16_t* __restr
       o1[reg] *= alpha;
     }
     if constexpr (DROP) {
-      const uint32_t pair_t = pair_q + (uint32_t)kt * 32;
+      const uint32_t xt = xq ^ (uint32_t)__builtin_amdgcn_readlane((int)ctile, kt);
       uint32_t wk = 0;  // keep-mask word of key 64 kt + lane (the wave's 32 queries)
-      auto put = [&](int k, uint32_t v) { wk = lane == k ? v : wk; };  // lane k <- the wave-uniform v
 #pragma unroll
       for (int kb = 0; kb < 2; ++kb)
 #pragma unroll
         for (int reg = 0; reg < 16; reg += 2) {
           // key = kt*64 + kb*32 + (reg & 3) + 8 (reg >> 2) + 4 hf
-          const uint32_t bits = dropout_bits(pair_t + (uint32_t)(kb * 16 + ((reg & 3) >> 1) + 4 * (reg >> 2)), dp);
-          const float f0 = keep_factor(bits, 0, dp), f1 = keep_factor(bits, 1, dp);
-          st[kb][reg] *= f0;
-          st[kb][reg + 1] *= f1;
+          const uint32_t bits = drop_fin(xt ^ drop_col((uint32_t)(16 * kb + 4 * (reg >> 2) + ((reg >> 1) & 1))));
+          const bool k0 = keep_lo(bits, dp.thr), k1 = keep_hi(bits, dp.thr);
+          st[kb][reg] = k0 ? st[kb][reg] : 0.f;
+          st[kb][reg + 1] = k1 ? st[kb][reg + 1] : 0.f;
           if (km_on) {
-            const unsigned long long m0 = __ballot(f0 != 0.f), m1 = __ballot(f1 != 0.f);
+            // the wave's keep bits of this register's two keys per half-wave -> lanes (tile keys) kl, kl + 4, ...
+            const unsigned long long m0 = __ballot(k0), m1 = __ballot(k1);
             const int kl = kb * 32 + (reg & 3) + 8 * (reg >> 2);  // tile key of `reg` on lanes 0-31
-            put(kl, (uint32_t)m0);
-            put(kl + 4, (uint32_t)(m0 >> 32));
-            put(kl + 1, (uint32_t)m1);
-            put(kl + 5, (uint32_t)(m1 >> 32));
+            put_lane(wk, kl, (uint32_t)m0);
+            put_lane(wk, kl + 4, (uint32_t)(m0 >> 32));
+            put_lane(wk, kl + 1, (uint32_t)m1);
+            put_lane(wk, kl + 5, (uint32_t)(m1 >> 32));
           }
         }
       if (km_on) km_k[kt * 64 + lane] = wk;
@@ -216,16 +228,17 @@ __global__ __launch_bounds__(256, 2) void attnS_fwd_kernel(const bf16_t* __restr
   l = sum_xor32(l);
   if (hf == 0) lse2[(int64_t)bh * S + q] = m + __log2f(l);
   __syncthreads();  // K images no longer read: reuse as staging
+  const float oscale = (DROP ? dp.scale : 1.0f) / l;  // the dropout scale of the kept probabilities
   if (q8o.q != nullptr) {  // fp8 e4m3 copy of the output for the fp8 out-projection GEMM (delayed scaling)
     const float qs = fmt_scale(0, *q8o.amax_in);
     if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) *q8o.sinv = 1.0f / qs;
     float qm = 0.f;
     const int64_t off = ((int64_t)b * S + q0) * H + hh * D;
-    store_rows(Kb + wave * 32 * D, o0, o1, 1.0f / l, out + off, H, lane, nullptr, q8o.q + off, 0, qs, &qm);
+    store_rows(Kb + wave * 32 * D, o0, o1, oscale, out + off, H, lane, nullptr, q8o.q + off, 0, qs, &qm);
     wave_amax_track(qm, q8o.amax_track);
     return;
   }
-  store_rows(Kb + wave * 32 * D, o0, o1, 1.0f / l, out + ((int64_t)b * S + q0) * H + hh * D, H, lane);
+  store_rows(Kb + wave * 32 * D, o0, o1, oscale, out + ((int64_t)b * S + q0) * H + hh * D, H, lane);
 }
 
 // ------------------------------------------------------------------------------------------------
@@ -298,6 +311,9 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_kv_kernel(const bf16_t* __re
   if (km_on) {
     const uint32_t* src = kmask + (int64_t)bh * (S / 32) * S + blockIdx.x * 128;
     for (int i = tid; i < (S / 32) * 128; i += 256) km_s[i] = src[(int64_t)(i >> 7) * S + (i & 127)];
+  } else if (DROP) {
+    // re-hashing: the dropout row words R(bh S + q) of every query, in the keep-mask slot
+    for (int i = tid; i < S; i += 256) km_s[i] = dropout_row((uint32_t)(bh * S + i), dp);
   }
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
@@ -312,9 +328,10 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_kv_kernel(const bf16_t* __re
 
   f32x16 dk0 = {}, dk1 = {}, dv0 = {}, dv1 = {};
   const bool odd = (lane & 1) != 0;
-  // dropout pair of (query qi0 (+1 on odd lanes), this lane's key): ((bh S + q) S + key) >> 1
-  const uint32_t pair_lane = (uint32_t)((int64_t)bh * S * (S / 2)) + (uint32_t)(key >> 1) +
-                             (uint32_t)(4 * hf + (odd ? 1 : 0)) * (S / 2);
+  // dropout (re-hashing): mask row bh S + query, column pair key / 2 -- one 32-bit word for lanes l and l ^ 1: the
+  // even lane computes query qi0's, the odd lane query qi0 + 1's, and they swap (one DPP move)
+  const uint32_t ck = drop_col((uint32_t)key >> 1);
+  const int qsel = 4 * hf + (odd ? 1 : 0);
   auto tile = [&](const int stg, const int qt) {
 
     if (qt + 1 < nt) tile_barrier<1>();
@@ -338,7 +355,6 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_kv_kernel(const bf16_t* __re
       }
       // rows: query qi = (reg&3) + 8(reg>>2) + 4hf of the sub-block; col (lane): key
       f32x16 pd, ds;
-      const uint32_t pair_qs = pair_lane + (uint32_t)(qt * 64 + qs * 32) * (S / 2);
       // this query block's keep bits of the lane's key, shifted to the lane's rows (4 hf)
       const uint32_t kmw = km_on ? km_s[(qt * 2 + qs) * 128 + wave * 32 + r] >> (4 * hf) : 0u;
 #pragma unroll
@@ -357,7 +373,7 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_kv_kernel(const bf16_t* __re
           } else {
             // keys 2j, 2j+1 (lanes l, l^1) share one hash per query row: the even lane hashes row qi0,
             // the odd lane row qi0 + 1, then they swap
-            const uint32_t bits = dropout_bits(pair_qs + (uint32_t)((reg & 3) + 8 * (reg >> 2)) * (S / 2), dp);
+            const uint32_t bits = drop_fin(km_s[qt * 64 + qs * 32 + (reg & 3) + 8 * (reg >> 2) + qsel] ^ ck);
             const uint32_t other = dpp_xor1(bits);
             f0 = keep_factor(odd ? other : bits, key & 1, dp);
             f1 = keep_factor(odd ? bits : other, key & 1, dp);
@@ -463,8 +479,12 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_q_kernel(const bf16_t* __res
   }
 
   f32x16 dq0 = {}, dq1 = {};
-  // dropout pair of (q, key): ((bh S + q) S + key) >> 1 = pair_q + key / 2 (key even in every hashed pair)
-  const uint32_t pair_q = (uint32_t)(((int64_t)bh * S + q) * (S / 2)) + 2 * hf;
+  // dropout (re-hashing): as the forward -- row word of (bh, q) with the hf term folded in, C(32 kt) by readlane
+  uint32_t xq = 0, ctile = 0;
+  if (DROP && !km_on) {
+    xq = dropout_row((uint32_t)(bh * S + q), dp) ^ drop_col(2u * (uint32_t)hf);
+    ctile = drop_col(32u * (uint32_t)lane);
+  }
   auto tile = [&](const int stg, const int kt) {
 
     if (kt + 1 < nt) tile_barrier<1>();
@@ -489,7 +509,7 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_q_kernel(const bf16_t* __res
         dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(av, df[s], dpacc, 0, 0, 0);
       }
       f32x16 ds;
-      const uint32_t pair_kb = pair_q + (uint32_t)(kt * 32 + kb * 16);
+      const uint32_t xt = DROP && !km_on ? xq ^ (uint32_t)__builtin_amdgcn_readlane((int)ctile, kt) : 0u;
 #pragma unroll
       for (int g4 = 0; g4 < 4; ++g4) {
         const int kk = kt * 64 + kb * 32 + 8 * g4 + 4 * hf;  // keys kk .. kk+3 in regs 4g4 .. 4g4+3
@@ -507,7 +527,7 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_q_kernel(const bf16_t* __res
               f0 = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)kw4[e], r, 1) & __float_as_uint(dp.scale));
               f1 = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)kw4[e + 1], r, 1) & __float_as_uint(dp.scale));
             } else {
-              const uint32_t bits = dropout_bits(pair_kb + (uint32_t)(4 * g4 + (e >> 1)), dp);
+              const uint32_t bits = drop_fin(xt ^ drop_col((uint32_t)(16 * kb + 4 * g4 + (e >> 1))));
               f0 = keep_factor(bits, 0, dp);
               f1 = keep_factor(bits, 1, dp);
             }

@@ -48,11 +48,15 @@ __device__ __forceinline__ u32x4 pack8(const float (&v)[8]) {
   return u32x4{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3]), pack_bf2(v[4], v[5]), pack_bf2(v[6], v[7])};
 }
 
-// dropped value of element e (row-major [R][H]) from the stored bf16 activation t: bf16(t · keep · scale)
-__device__ __forceinline__ float dropped(float t, int64_t e, const DropoutParams& dp) {
-  if (!dp.enabled) return t;
-  const uint32_t b = dropout_bits((uint32_t)(e >> 1), dp);
-  return bf2f(f2bf(t * keep_factor(b, (int)(e & 1), dp)));
+// keep factors of the 8 elements from column h0 (h0 % 8 == 0) of row `row` ([R][H] site, mask rows of width H)
+__device__ __forceinline__ void keep8(int row, int h0, const DropoutParams& dp, float (&kf)[8]) {
+  const uint32_t x = dropout_row((uint32_t)row, dp) ^ drop_col((uint32_t)h0 >> 1);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {  // (h0 / 2) % 4 == 0: pair h0 / 2 + j = h0 / 2 ^ j
+    const uint32_t b = drop_fin(x ^ drop_col((uint32_t)j));
+    kf[2 * j] = keep_factor(b, 0, dp);
+    kf[2 * j + 1] = keep_factor(b, 1, dp);
+  }
 }
 
 template <int C>
@@ -82,8 +86,12 @@ __global__ __launch_bounds__(256) void cls_fwd_kernel(const bf16_t* __restrict__
 #pragma unroll
       for (int k = 0; k < 8; ++k) v[k] = bf2f(f2bf(act_fwd(v[k], act)));  // the bf16 activation the backward sees
       *reinterpret_cast<u32x4*>(t_out + (int64_t)row * H + h0) = pack8(v);
+      if (dp.enabled) {  // bf16(t · keep · scale)
+        float kf[8];
+        keep8(row, h0, dp, kf);
 #pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = dropped(v[k], (int64_t)row * H + h0 + k, dp);
+        for (int k = 0; k < 8; ++k) v[k] = bf2f(f2bf(v[k] * kf[k]));
+      }
 #pragma unroll
       for (int c = 0; c < C; ++c) {
         float w[8];
@@ -219,14 +227,11 @@ __global__ __launch_bounds__(256) void cls_bwd_kernel(const bf16_t* __restrict__
 #pragma unroll
         for (int k = 0; k < 8; ++k) dd[k] = fmaf(g[c], w[k], dd[k]);
       }
-      float o[8];
+      float o[8], kf[8] = {1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f, 1.f};
+      if (dp.enabled) keep8(row, h0, dp, kf);
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
-        float keep = 1.0f;
-        if (dp.enabled) {
-          const uint32_t b = dropout_bits((uint32_t)((e0 + k) >> 1), dp);
-          keep = keep_factor(b, (int)((e0 + k) & 1), dp);
-        }
+        const float keep = kf[k];
         const float dv = bf2f(f2bf(t[k] * keep));  // the dropped activation (classifier input)
 #pragma unroll
         for (int c = 0; c < C; ++c) aw[c][i][k] = fmaf(g[c], dv, aw[c][i][k]);

@@ -82,14 +82,16 @@ __global__ __launch_bounds__(256) void colsum_kernel(const bf16_t* __restrict__ 
 }
 
 __global__ __launch_bounds__(256) void dropout_kernel(const bf16_t* __restrict__ x, bf16_t* __restrict__ out, int64_t n4,
-                                                      DropoutParams dp) {
+                                                      int W, DropoutParams dp) {
   dp = resolve_seed(dp);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     u32x2 w = reinterpret_cast<const u32x2*>(x)[i];
-    uint32_t pair0 = (uint32_t)(i * 2);
-    uint32_t b0 = dropout_bits(pair0, dp);
-    uint32_t b1 = dropout_bits(pair0 + 1, dp);
+    // 4 elements of one row (W % 4 == 0): column pairs cp0 (even) and cp0 + 1 = cp0 ^ 1
+    const int64_t row = (i * 4) / W;
+    const uint32_t cp0 = (uint32_t)((i * 4 - row * W) >> 1);
+    const uint32_t xw = drop_row((uint32_t)row, dp.key) ^ drop_col(cp0);
+    const uint32_t b0 = drop_fin(xw), b1 = drop_fin(xw ^ drop_col(1));
     u32x2 o;
     o.x = pack_bf2(lo_bf(w.x) * keep_factor(b0, 0, dp), hi_bf(w.x) * keep_factor(b0, 1, dp));
     o.y = pack_bf2(lo_bf(w.y) * keep_factor(b1, 0, dp), hi_bf(w.y) * keep_factor(b1, 1, dp));
@@ -178,10 +180,15 @@ void launch_mask_bias(const void* mask, bool i64, float* out, int64_t n, hipStre
   HSD_CHECK_LAUNCH();
 }
 
-void launch_dropout(const bf16_t* x, bf16_t* out, int64_t n, double p, uint64_t seed, hipStream_t st) {
+uint32_t dropout_pair_bits_host(uint64_t seed, uint32_t row, uint32_t cp) {
+  const DropoutParams d = make_dropout(0.1, seed);
+  return drop_fin(drop_row(row, d.key) ^ drop_col(cp));
+}
+
+void launch_dropout(const bf16_t* x, bf16_t* out, int64_t n, int W, double p, uint64_t seed, hipStream_t st) {
   DropoutParams dp = make_dropout(p, seed);
   int64_t n4 = n / 4;  // caller guarantees n % 4 == 0
-  hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(n4)), dim3(256), 0, st, x, out, n4, dp);
+  hipLaunchKernelGGL(dropout_kernel, dim3(grid_for(n4)), dim3(256), 0, st, x, out, n4, W, dp);
   HSD_CHECK_LAUNCH();
 }
 

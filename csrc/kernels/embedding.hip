@@ -74,6 +74,8 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
 #pragma unroll
       for (int k = 0; k < 4; ++k) { float d = e[i][k] - mean; ss += d * d; }
   const float rstd = rsqrtf(wave_sum(ss) / (float)H + eps);
+  // dropout: mask row `row`, column pairs 2c and 2c + 1 of chunk c = lane + 64 i: C(2c) = C(2 lane) ^ C(128 i)
+  const uint32_t xr = dp.enabled ? dropout_row((uint32_t)row, dp) ^ drop_col(2u * (uint32_t)lane) : 0u;
 #pragma unroll
   for (int i = 0; i < NCH; ++i) {
     int c = lane + 64 * i;
@@ -85,9 +87,8 @@ __global__ __launch_bounds__(256) void embed_fwd_kernel(const int64_t* __restric
                     (e[i][2] - mean) * rstd * lo_bf(gw.y) + lo_bf(bw.y), (e[i][3] - mean) * rstd * hi_bf(gw.y) + hi_bf(bw.y)};
       if (dp.enabled) {
         // dropout is applied to the bf16-rounded LN output (matches the reference op order)
-        uint32_t pair0 = (uint32_t)(off >> 1);
-        uint32_t b0 = dropout_bits(pair0, dp);
-        uint32_t b1 = dropout_bits(pair0 + 1, dp);
+        const uint32_t x = xr ^ drop_col(128u * (uint32_t)i);
+        const uint32_t b0 = drop_fin(x), b1 = drop_fin(x ^ drop_col(1));
         o[0] = bf2f(f2bf(o[0])) * keep_factor(b0, 0, dp);
         o[1] = bf2f(f2bf(o[1])) * keep_factor(b0, 1, dp);
         o[2] = bf2f(f2bf(o[2])) * keep_factor(b1, 0, dp);
@@ -144,6 +145,8 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const bf16_t* __restrict
     const int64_t id = ids[row], pid = pos_ids[row];
     const int64_t tid = type ? type_ids[row] : 0;
     const float mean = mean_in[row], rstd = rstd_in[row];
+    // dropout: mask row `row`, element e = lane + 64 i in column pair e / 2: C(e / 2) = C(lane / 2) ^ C(32 i)
+    const uint32_t xr = dp.enabled ? dropout_row((uint32_t)row, dp) ^ drop_col((uint32_t)lane >> 1) : 0u;
     float xh[NE], g[NE], d[NE];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -154,7 +157,7 @@ __global__ __launch_bounds__(256) void embed_bwd_kernel(const bf16_t* __restrict
         if (type) ev += bf2f(type[tid * H + e]);
         const size_t off = (size_t)row * H + e;
         float dv = bf2f(dout[off]);
-        if (dp.enabled) dv *= keep_factor(dropout_bits((uint32_t)(off >> 1), dp), (int)(off & 1), dp);
+        if (dp.enabled) dv *= keep_factor(drop_fin(xr ^ drop_col(32u * (uint32_t)i)), lane & 1, dp);
         d[i] = dv;
         xh[i] = (ev - mean) * rstd;
         g[i] = dv * gam[i];
@@ -268,6 +271,8 @@ __global__ __launch_bounds__(256, 2) void embed_bwd16_kernel(const bf16_t* __res
   };
   auto process = [&](int b, const Row& r) {
     const int row = b * S + s;
+    // dropout: mask row `row`, pairs 4c + k of chunk c = lane + 64 i: C(4c + k) = C(4 lane) ^ C(256 i) ^ C(k)
+    const uint32_t xr = dp.enabled ? dropout_row((uint32_t)row, dp) ^ drop_col(4u * (uint32_t)lane) : 0u;
     float xh[NC8][8], g[NC8][8];
     float s1 = 0.f, s2 = 0.f;
 #pragma unroll
@@ -278,7 +283,7 @@ __global__ __launch_bounds__(256, 2) void embed_bwd16_kernel(const bf16_t* __res
 #pragma unroll
       for (int k = 0; k < 4; ++k) {
         uint32_t bits = 0;
-        if (dp.enabled) bits = dropout_bits((uint32_t)(off0 >> 1) + k, dp);
+        if (dp.enabled) bits = drop_fin(xr ^ drop_col(256u * (uint32_t)i) ^ drop_col((uint32_t)k));
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int e = 2 * k + h;

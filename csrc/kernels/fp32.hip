@@ -76,7 +76,8 @@ __global__ __launch_bounds__(256) void epi32_kernel(float* __restrict__ y, const
       for (int e = 0; e < 4; ++e) o[e] = 0.5f * v[e] * (1.0f + erff(v[e] * 0.70710678118654752f));
     } else if (kind == 2) {
       if (dp.enabled) {
-        const uint32_t b0 = dropout_bits((uint32_t)(e0 >> 1), dp), b1 = dropout_bits((uint32_t)(e0 >> 1) + 1, dp);
+        uint32_t b0, b1;
+        dropout_bits4((uint32_t)(e0 / N), (uint32_t)n0, dp, b0, b1);
         v[0] *= keep_factor(b0, 0, dp);
         v[1] *= keep_factor(b0, 1, dp);
         v[2] *= keep_factor(b1, 0, dp);
@@ -98,15 +99,16 @@ __global__ __launch_bounds__(256) void epi32_kernel(float* __restrict__ y, const
   }
 }
 
-// out = x · keep (element index = flat index), in place allowed
+// out = x · keep (mask rows of width W = the last dimension, W % 4 == 0), in place allowed
 __global__ __launch_bounds__(256) void dropout32_kernel(const float* __restrict__ x, float* __restrict__ out,
-                                                        int64_t n4, DropoutParams dp) {
+                                                        int64_t n4, int W, DropoutParams dp) {
   dp = resolve_seed(dp);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     f32x4 v = reinterpret_cast<const f32x4*>(x)[i];
-    const uint32_t p0 = (uint32_t)(i * 2);
-    const uint32_t b0 = dropout_bits(p0, dp), b1 = dropout_bits(p0 + 1, dp);
+    const int64_t row = (i * 4) / W;
+    uint32_t b0, b1;
+    dropout_bits4((uint32_t)row, (uint32_t)(i * 4 - row * W), dp, b0, b1);
     v[0] *= keep_factor(b0, 0, dp);
     v[1] *= keep_factor(b0, 1, dp);
     v[2] *= keep_factor(b1, 0, dp);
@@ -311,7 +313,8 @@ __global__ __launch_bounds__(64) void attn32_fwd_kernel(const float* __restrict_
     o[d] = o[d + 1] = o[d + 2] = o[d + 3] = 0.f;
   }
   float m = -INFINITY, l = 0.f;
-  const uint32_t rowpair = (uint32_t)(((int64_t)bh * S + q) * S) >> 1;  // S even: pair index of (q, key 0)
+  // dropout row word of (bh, q): mask row bh S + q, column pair key / 2 (ops/rng.py)
+  const uint32_t rw = dropout_row((uint32_t)(bh * S + q), dp);
   for (int k0 = 0; k0 < S; k0 += KT) {
     __syncthreads();
     // stage K / V rows k0 .. k0 + KT (64 lanes x 8 float4 each per matrix)
@@ -351,12 +354,14 @@ __global__ __launch_bounds__(64) void attn32_fwd_kernel(const float* __restrict_
 #pragma unroll
       for (int d = 0; d < AD; ++d) o[d] *= corr;
       m = mx;
+      // (k0 + j0) / 2 is a multiple of CH / 2 (powers of two): C((k0 + j0 + j) / 2) = C((k0 + j0) / 2) ^ C(j / 2)
+      const uint32_t xc = dp.enabled ? rw ^ drop_col((uint32_t)(k0 + j0) >> 1) : 0u;
 #pragma unroll
       for (int j = 0; j < CH; j += 2) {
         float p0 = exp2f(s[j] - m), p1 = exp2f(s[j + 1] - m);
         l += p0 + p1;
         if (dp.enabled) {
-          const uint32_t bits = dropout_bits(rowpair + (uint32_t)((k0 + j0 + j) >> 1), dp);
+          const uint32_t bits = drop_fin(xc ^ drop_col((uint32_t)j >> 1));
           p0 *= keep_factor(bits, 0, dp);
           p1 *= keep_factor(bits, 1, dp);
         }
@@ -424,7 +429,7 @@ __global__ __launch_bounds__(64) void attn32_dq_kernel(const float* __restrict__
   }
   const float ls = valid ? lse[(int64_t)bh * S + q] : 0.f;
   const float dl = valid ? delta[(int64_t)bh * S + q] : 0.f;
-  const uint32_t rowpair = (uint32_t)(((int64_t)bh * S + q) * S) >> 1;
+  const uint32_t rw = dropout_row((uint32_t)(bh * S + q), dp);
   for (int k0 = 0; k0 < S; k0 += KT) {
     __syncthreads();
     for (int i = lane; i < KT * AD / 4; i += 64) {
@@ -460,7 +465,7 @@ __global__ __launch_bounds__(64) void attn32_dq_kernel(const float* __restrict__
       }
       float k0f = 1.f, k1f = 1.f;
       if (dp.enabled) {
-        const uint32_t bits = dropout_bits(rowpair + (uint32_t)((k0 + j) >> 1), dp);
+        const uint32_t bits = dropout_bits_rc(rw, (uint32_t)(k0 + j) >> 1);
         k0f = keep_factor(bits, 0, dp);
         k1f = keep_factor(bits, 1, dp);
       }
@@ -516,8 +521,8 @@ __global__ __launch_bounds__(64) void attn32_dkv_kernel(const float* __restrict_
       for (int e = 0; e < 4; ++e) vv[d + e] = u[e];
     }
   }
-  // dropout pair of (q, k): ((bh S + q) S + k) >> 1, element k & 1
-  const uint32_t keypair = (uint32_t)k >> 1;
+  // dropout mask of (q, k): row bh S + q (the row word is wave-uniform per query), column pair k / 2, element k & 1
+  const uint32_t kc = drop_col((uint32_t)k >> 1);
   for (int q0 = 0; q0 < S; q0 += KT) {
     __syncthreads();
     for (int i = lane; i < KT * AD / 4; i += 64) {
@@ -552,8 +557,7 @@ __global__ __launch_bounds__(64) void attn32_dkv_kernel(const float* __restrict_
       const float p = exp2f(a + kbias - lse_s[i]);
       float kf = 1.f;
       if (dp.enabled) {
-        const uint32_t pair = (uint32_t)(((int64_t)bh * S + q0 + i) * S >> 1) + keypair;
-        kf = keep_factor(dropout_bits(pair, dp), k & 1, dp);
+        kf = keep_factor(drop_fin(dropout_row((uint32_t)(bh * S + q0 + i), dp) ^ kc), k & 1, dp);
       }
       if constexpr (DV) {
         const float w = p * kf;
@@ -602,7 +606,7 @@ __global__ __launch_bounds__(64) void cls32_fwd_kernel(const float* __restrict__
       t[e] = act == 0 ? tanhf(x) : fmaxf(x, 0.f);
     }
     if (dp.enabled) {
-      const uint32_t bits = dropout_bits((uint32_t)(((int64_t)r * H + c0) >> 1), dp);
+      const uint32_t bits = dropout_bits2((uint32_t)r, (uint32_t)c0 >> 1, dp);
       t[0] *= keep_factor(bits, 0, dp);
       t[1] *= keep_factor(bits, 1, dp);
     }
@@ -648,7 +652,7 @@ __global__ __launch_bounds__(64) void cls32_bwd_kernel(const float* __restrict__
   for (int c0 = lane * 2; c0 < H; c0 += 128) {
     float kf[2] = {1.f, 1.f};
     if (dp.enabled) {
-      const uint32_t bits = dropout_bits((uint32_t)(((int64_t)r * H + c0) >> 1), dp);
+      const uint32_t bits = dropout_bits2((uint32_t)r, (uint32_t)c0 >> 1, dp);
       kf[0] = keep_factor(bits, 0, dp);
       kf[1] = keep_factor(bits, 1, dp);
     }
@@ -693,9 +697,9 @@ void launch_epi32(float* y, const float* bias, const float* aux, float* out, int
   HSD_CHECK_LAUNCH();
 }
 
-void launch_dropout32(const float* x, float* out, int64_t n, double p, uint64_t seed, hipStream_t st) {
-  if (n % 4) abort();
-  hipLaunchKernelGGL(f32k::dropout32_kernel, dim3(ew_blocks(n / 4)), dim3(256), 0, st, x, out, n / 4,
+void launch_dropout32(const float* x, float* out, int64_t n, int W, double p, uint64_t seed, hipStream_t st) {
+  if (n % 4 || W % 4 || W <= 0) abort();
+  hipLaunchKernelGGL(f32k::dropout32_kernel, dim3(ew_blocks(n / 4)), dim3(256), 0, st, x, out, n / 4, W,
                      make_dropout(p, seed));
   HSD_CHECK_LAUNCH();
 }

@@ -169,9 +169,8 @@ __device__ __forceinline__ void epi_block(const f32x16& a, int mb, int nb, int l
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = bf2f(f2bf(v[e]));
         if (p.dp.enabled) {
-          const uint32_t pair0 = (uint32_t)(((int64_t)m * p.N + n) >> 1);
-          const uint32_t b0 = dropout_bits(pair0, p.dp);
-          const uint32_t b1 = dropout_bits(pair0 + 1, p.dp);
+          uint32_t b0, b1;
+          dropout_bits4((uint32_t)m, (uint32_t)n, p.dp, b0, b1);  // mask row m of width N, n % 4 == 0
           v[0] = bf2f(f2bf(v[0] * keep_factor(b0, 0, p.dp)));
           v[1] = bf2f(f2bf(v[1] * keep_factor(b0, 1, p.dp)));
           v[2] = bf2f(f2bf(v[2] * keep_factor(b1, 0, p.dp)));

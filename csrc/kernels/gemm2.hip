@@ -1016,6 +1016,7 @@ __global__ __launch_bounds__(256) void splitk_epi_kernel(const float* __restrict
     }
     const int64_t plane = (int64_t)p.M * p.N;
     bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
+    const uint32_t cw = epi_col_word<EPI>(n, p);
     for (int m = m0 + rl; m < m1; m += 32) {
       const float* w = ws + (int64_t)m * p.N + n;
       f32x4 a0 = *reinterpret_cast<const f32x4*>(w);
@@ -1032,7 +1033,7 @@ __global__ __launch_bounds__(256) void splitk_epi_kernel(const float* __restrict
       u32x4 o = {lo.x, lo.y, hi.x, hi.y}, o2;
       u32x4 x = {0, 0, 0, 0};
       if constexpr (epi_aux(EPI)) x = *reinterpret_cast<const u32x4*>(p.aux + (int64_t)m * p.ldaux + n);
-      epi_chunk<EPI>(o, o2, x, m, n, p, csum);
+      epi_chunk<EPI>(o, o2, x, m, n, p, csum, cw);
       st16(C + (int64_t)m * p.ldc + n, o, p.nt_store);
       if constexpr (epi_two_out(EPI)) st16(p.C2 + (int64_t)m * p.ldc + n, o2, p.nt_store);
     }
@@ -1449,10 +1450,7 @@ static WgradPlan wgrad_plan(int M, int N, int K) {
   // (profiles/wgrad_min_grid_ab_r4.log): bert-large S=512 B=8 504-505 -> 524-526 seq/s, bert-base B=64 +1.8 %.
   // HSD_WGRAD_MIN_GRID sets the workgroup target (0 = the cost model at every size).
   const int grid_knob = HSD_KNOB("HSD_WGRAD_MIN_GRID", kKnobUnset);
-  // opt-in (HSD_WGRAD_MIN_GRID=192): the whole-step HIP graph with the native engine (opt-in HSD_GRAPH_DP) once
-  // diverged from eager under it in a full GPU-tier run (tests/test_gpu_comm.py::test_whole_step_graph_with_native_
-  // engine; passes in isolation) -- an ordering edge of that capture to re-check before this becomes the default
-  const int min_grid = grid_knob != kKnobUnset ? grid_knob : 0;
+  const int min_grid = grid_knob != kKnobUnset ? grid_knob : (K <= 8192 ? 192 : 0);
   if (min_grid > 0 && can_small) {
     const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
     int sp = 1;

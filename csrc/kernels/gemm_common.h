@@ -147,9 +147,11 @@ __device__ __forceinline__ u32x2 pack4(const f32x4& v) {
 
 // Epilogue math for one 16-B chunk (8 consecutive n of row m) of the staged bf16(acc [+ bias]) tile `o`;
 // `x` is the aux chunk. Returns the primary output in `o` and (two-output epilogues) the second in `o2`.
+// `cw`: the dropout column word C(n / 2) of this lane's chunk column n (E2_BIAS_DROP_RES; epi_col_word), hoisted out
+// of the row loops by the caller
 template <int EPI>
 __device__ __forceinline__ void epi_chunk(u32x4& o, u32x4& o2, const u32x4& x, int m, int n, const G2Params& p,
-                                          float (&csum)[8]) {
+                                          float (&csum)[8], uint32_t cw = 0u) {
   if constexpr (EPI == E2_BIAS_GELU) {
     o2.x = pack_bf2(gelu_erf(lo_bf(o.x)), gelu_erf(hi_bf(o.x)));
     o2.y = pack_bf2(gelu_erf(lo_bf(o.y)), gelu_erf(hi_bf(o.y)));
@@ -170,10 +172,11 @@ __device__ __forceinline__ void epi_chunk(u32x4& o, u32x4& o2, const u32x4& x, i
     // z = bf16(bf16(y · keep · scale) + residual)
     float v[8] = {lo_bf(o.x), hi_bf(o.x), lo_bf(o.y), hi_bf(o.y), lo_bf(o.z), hi_bf(o.z), lo_bf(o.w), hi_bf(o.w)};
     if (p.dp.enabled) {
-      const uint32_t pair0 = (uint32_t)(((int64_t)m * p.N + n) >> 1);
+      // mask row m (width N), pairs n / 2 + e = n / 2 ^ e (n % 8 == 0): one row word per chunk
+      const uint32_t xw = drop_row((uint32_t)m, p.dp.key) ^ cw;
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
-        const uint32_t b = dropout_bits(pair0 + e, p.dp);
+        const uint32_t b = drop_fin(xw ^ drop_col((uint32_t)e));
         v[2 * e] = bf2f(f2bf(v[2 * e] * keep_factor(b, 0, p.dp)));
         v[2 * e + 1] = bf2f(f2bf(v[2 * e + 1] * keep_factor(b, 1, p.dp)));
       }
@@ -202,6 +205,12 @@ __device__ __forceinline__ void epi_chunk(u32x4& o, u32x4& o2, const u32x4& x, i
     csum[0] += lo_bf(o.x); csum[1] += hi_bf(o.x); csum[2] += lo_bf(o.y); csum[3] += hi_bf(o.y);
     csum[4] += lo_bf(o.z); csum[5] += hi_bf(o.z); csum[6] += lo_bf(o.w); csum[7] += hi_bf(o.w);
   }
+}
+
+template <int EPI>
+__device__ __forceinline__ uint32_t epi_col_word(int n, const G2Params& p) {
+  if constexpr (EPI == E2_BIAS_DROP_RES) return p.dp.enabled ? drop_col((uint32_t)n >> 1) : 0u;
+  return 0u;
 }
 
 // column sums of 8 columns per lane, lanes with equal (lane & 7) hold the same columns: reduce + atomics
@@ -300,6 +309,9 @@ __device__ __forceinline__ void epilogue_bf16(f32x4 (&acc)[MB][BN / 64], const G
   // BEFORE this pass's stores: the vector-memory counter retires loads and stores in issue order, so a load issued
   // after the previous pass's stores made its consumer wait for all of them (s_waitcnt vmcnt(0) per pass)
   constexpr bool kAuxPf = epi_aux(EPI) && !G2_AUX_NO_PREFETCH;
+  // dropout column word of the lane's chunk column: the same in every pass when CPR divides 64 (hoisted)
+  constexpr bool kColFixed = 64 % CPR == 0;
+  const uint32_t cw = kColFixed ? epi_col_word<EPI>(nw + (lane % CPR) * 8, p) : 0u;
   u32x4 xnext[ITER];
 #pragma unroll
   for (int h = 0; h < MB / PB; ++h) {
@@ -349,7 +361,7 @@ __device__ __forceinline__ void epilogue_bf16(f32x4 (&acc)[MB][BN / 64], const G
       if (m >= p.M) continue;
       const int64_t co = (int64_t)m * p.ldc + n;
       u32x4 o = sv[it], o2;
-      epi_chunk<EPI>(o, o2, xv[it], m, n, p, csum);
+      epi_chunk<EPI>(o, o2, xv[it], m, n, p, csum, kColFixed ? cw : epi_col_word<EPI>(n, p));
       if (p.nt_store) {
         const uint32_t bo = (uint32_t)(((int64_t)(m - mw) * p.ldc + n) * 2);
         st16nt(rc, bo, o);

@@ -45,7 +45,9 @@ void launch_gelu_fwd(const bf16_t* y, bf16_t* g, int64_t n, hipStream_t st);
 void launch_gelu_bwd_colsum(const bf16_t* dg, const bf16_t* y, bf16_t* da, float* dbias, int rows, int N,
                             hipStream_t st);
 void launch_colsum(const bf16_t* x, float* dbias, int rows, int N, hipStream_t st);
-void launch_dropout(const bf16_t* x, bf16_t* out, int64_t n, double p, uint64_t seed, hipStream_t st);
+// the 32 mask bits of column pair cp of row `row` of a dropout site with 64-bit `seed` (common.h), on the host
+uint32_t dropout_pair_bits_host(uint64_t seed, uint32_t row, uint32_t cp);
+void launch_dropout(const bf16_t* x, bf16_t* out, int64_t n, int W, double p, uint64_t seed, hipStream_t st);
 void launch_mask_bias(const void* mask, bool i64, float* out, int64_t n, hipStream_t st);
 // C[N][K] (fp32, ldc) += dy[T][N]ᵀ · x[T][K] for small T (K % 4 == 0)
 void launch_small_wgrad(const bf16_t* dy, int64_t ldy, const bf16_t* x, int64_t ldx, float* C, int64_t ldc, int T,
@@ -103,7 +105,7 @@ void refresh_env_knobs();
 void launch_split3(const float* x, bf16_t* out, int64_t R, int64_t C, int pat, bool rows, hipStream_t st);
 void launch_epi32(float* y, const float* bias, const float* aux, float* out, int64_t M, int N, int kind, double p,
                   uint64_t seed, hipStream_t st);
-void launch_dropout32(const float* x, float* out, int64_t n, double p, uint64_t seed, hipStream_t st);
+void launch_dropout32(const float* x, float* out, int64_t n, int W, double p, uint64_t seed, hipStream_t st);
 void launch_colsum32(const float* x, float* dbias, int M, int N, hipStream_t st);
 void launch_ln32_fwd(const float* x, const float* g, const float* b, float* out, float* mean, float* rstd, int R,
                      int H, float eps, hipStream_t st);

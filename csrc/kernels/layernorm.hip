@@ -31,6 +31,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
   const int row = blockIdx.x * kLnWaves + (threadIdx.x >> 6);
   if (row >= rows) return;
   const int nq = H >> 2;  // 4-element chunks in the row
+  // dropout: mask row `row`, pairs 2c and 2c + 1 of chunk c = lane + 64 i: C(2c) = C(2 lane) ^ C(128 i)
+  const uint32_t xr = dp.enabled ? dropout_row((uint32_t)row, dp) ^ drop_col(2u * (uint32_t)lane) : 0u;
   float v[NCH][4];
   float s = 0.f;
 #pragma unroll
@@ -41,10 +43,8 @@ __global__ __launch_bounds__(256) void ln_fwd_kernel(const bf16_t* __restrict__ 
       u32x2 w = *reinterpret_cast<const u32x2*>(y + off);
       float a[4] = {lo_bf(w.x), hi_bf(w.x), lo_bf(w.y), hi_bf(w.y)};
       if (dp.enabled) {
-        // element index within the site tensor = off + k ; pairs (off+0,off+1), (off+2,off+3)
-        uint32_t pair0 = (uint32_t)(off >> 1);
-        uint32_t b0 = dropout_bits(pair0, dp);
-        uint32_t b1 = dropout_bits(pair0 + 1, dp);
+        const uint32_t x = xr ^ drop_col(128u * (uint32_t)i);
+        const uint32_t b0 = drop_fin(x), b1 = drop_fin(x ^ drop_col(1));
         a[0] *= keep_factor(b0, 0, dp);
         a[1] *= keep_factor(b0, 1, dp);
         a[2] *= keep_factor(b1, 0, dp);
@@ -258,9 +258,9 @@ __device__ __forceinline__ void ln_bwd_row(const u32x2 (&zw)[NCH], const u32x2 (
     if (dy_out) {
       float dy[4] = {dz[0], dz[1], dz[2], dz[3]};
       if (dp.enabled) {
-        const uint32_t pair0 = (uint32_t)(off >> 1);
-        const uint32_t b0 = dropout_bits(pair0, dp);
-        const uint32_t b1 = dropout_bits(pair0 + 1, dp);
+        // mask row `row`, pairs 2c and 2c + 1: C(2c) = C(2 lane) ^ C(128 i) (C(2 lane) is loop-invariant: hoisted)
+        const uint32_t x = dropout_row((uint32_t)row, dp) ^ drop_col(2u * (uint32_t)lane) ^ drop_col(128u * (uint32_t)i);
+        const uint32_t b0 = drop_fin(x), b1 = drop_fin(x ^ drop_col(1));
         dy[0] *= keep_factor(b0, 0, dp);
         dy[1] *= keep_factor(b0, 1, dp);
         dy[2] *= keep_factor(b1, 0, dp);

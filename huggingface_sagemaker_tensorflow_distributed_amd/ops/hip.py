@@ -82,6 +82,8 @@ _JOIN_QUEUED = [False]
 # capture forked it. HSD_GRAPH_SIDE=0: captured steps keep every weight gradient on the capture stream (round 3).
 _CAPTURE = {"parent": None, "forked": False}
 _GRAPH_SIDE = _os.environ.get("HSD_GRAPH_SIDE", "1") == "1"
+# HSD_TEST_SIDE_DELAY_US: test-only stall queued on the side stream before each backward's first weight gradient
+_SIDE_DELAY_US = float(_os.environ.get("HSD_TEST_SIDE_DELAY_US", "0"))
 
 
 def begin_capture(parent) -> None:
@@ -205,15 +207,21 @@ def wgrad_done(g: "_Grad", dy: torch.Tensor, x: torch.Tensor, dyq=None, xq=None)
     if s is None:
         gemm_wgrad_(g, dy, x, dyq, xq)
         return g.done()
-    if not _JOIN_QUEUED[0]:
-        # join the compute stream to the side stream when this backward pass finishes
-        torch.autograd.Variable._execution_engine.queue_callback(_end_of_backward)
-        _JOIN_QUEUED[0] = True
     N, K, T = dy.shape[1], x.shape[1], dy.shape[0]
     parent = _CAPTURE["parent"]
     if parent is not None:
         _CAPTURE["forked"] = True  # a branch of the graph capture, forked from the capture stream itself
     src = parent.cuda_stream if parent is not None else 0
+    if not _JOIN_QUEUED[0]:
+        # join the compute stream to the side stream when this backward pass finishes
+        torch.autograd.Variable._execution_engine.queue_callback(_end_of_backward)
+        _JOIN_QUEUED[0] = True
+        if _SIDE_DELAY_US > 0:
+            # ordering test hook (tests/test_gpu_comm.py): stall the side stream before this backward's first weight
+            # gradient, so any consumer of main_grad not ordered after the side stream reads it unfinished
+            _C.stream_wait(s.cuda_stream, src)
+            with torch.cuda.stream(s):
+                _C.cu_hog(1, _SIDE_DELAY_US)
     if not _WGRAD_CXX and parent is None:
         s.wait_stream(torch.cuda.current_stream())
         with torch.cuda.stream(s):
@@ -435,7 +443,7 @@ class _Dropout(torch.autograd.Function):
 
 
 def dropout(x, p, seed):
-    if x.dtype != torch.bfloat16 or x.numel() % 4:
+    if x.dtype != torch.bfloat16 or x.dim() == 0 or x.shape[-1] % 4:
         from .reference import dropout as ref
 
         return ref(x, p, seed, True)
@@ -574,9 +582,12 @@ _WS = {}
 
 
 def _workspace(numel: int, device, stream=None) -> torch.Tensor:
-    """Split-K slab workspace (fp32), grown on demand, reused stream-ordered across wgrad GEMMs. ``stream``: the
-    stream that will use it (a grown buffer is allocated from that stream's pool)."""
-    key = (device.type, device.index)
+    """Split-K slab workspace (fp32), grown on demand, reused stream-ordered across wgrad GEMMs. One buffer PER STREAM
+    (``stream``: the stream that will use it; default the current one): the side-stream weight gradients and the
+    compute-stream ones never share slabs, and a grown buffer is allocated from its own stream's pool, so the old one
+    goes back to the pool of the only stream that used it (no cross-stream reuse while a kernel still writes it)."""
+    sid = stream.cuda_stream if stream is not None else torch.cuda.current_stream(device).cuda_stream
+    key = (device.type, device.index, sid)
     buf = _WS.get(key)
     if buf is None or buf.numel() < numel:
         if stream is not None:

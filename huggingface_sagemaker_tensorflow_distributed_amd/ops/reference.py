@@ -19,7 +19,7 @@ from .rng import keep_mask
 def dropout(x: torch.Tensor, p: float, seed: int, training: bool = True) -> torch.Tensor:
     if not training or p <= 0.0:
         return x
-    m = keep_mask(seed, x.numel(), p, device=x.device).view_as(x)
+    m = keep_mask(seed, x.shape, p, device=x.device)
     return x * m.to(x.dtype) * (1.0 / (1.0 - p))
 
 
@@ -64,7 +64,7 @@ def attention(qkv: torch.Tensor, mask_bias: Optional[torch.Tensor], batch: int, 
               p: float, seed: int, training: bool) -> torch.Tensor:
     """Self-attention over a packed ``[B*S, 3H]`` QKV tensor -> ``[B*S, H]`` context.
 
-    Dropout on the probabilities indexes element ``((b*heads + h)*S + i)*S + j``.
+    Dropout on the probabilities: row ``(b*heads + h)*S + i``, column ``j`` of the site's [rows, S] view (ops/rng.py).
     """
     H3 = qkv.shape[-1]
     H = H3 // 3

@@ -98,6 +98,8 @@ class GradBucketer:
         self._on_reduced = None
         self.last_launched: Optional[int] = None  # index of the last bucket whose all-reduce was issued (watchdog)
         self._prescale = 1.0
+        self._hip = None
+        self._capture_deps_pending = False
         self.engine = engine
         if engine is None and (native is None or native) and group is None:
             from .comm import get_engine
@@ -114,6 +116,7 @@ class GradBucketer:
                 side = _hip.side_stream(store.device)
                 if side is not None:
                     self.engine.add_dependency_stream(side.cuda_stream)
+                    self._hip = _hip
             param_bucket = [0] * len(store.segments)
             for b in self.buckets:
                 for pi in b.params:
@@ -132,6 +135,11 @@ class GradBucketer:
             return
         if self.engine is not None:
             if self.overlap:
+                if self._capture_deps_pending and self._hip.side_stream_in_capture():
+                    # a whole-step graph capture (train/graph.py) has forked the wgrad side stream: from here on every
+                    # bucket waits on that branch too, as in eager steps (the branch writes this bucket's main_grad)
+                    self.engine.set_capture_deps(True)
+                    self._capture_deps_pending = False
                 idx = self.engine.mark_ready(i)
                 if idx >= 0:
                     self.last_launched = idx
@@ -173,6 +181,9 @@ class GradBucketer:
         if self.engine is not None:
             if self.compression == "fp16":
                 self.engine.set_prescale(self._prescale)
+            # inside a capture the engine waits on the wgrad branch only once the capture has forked it (mark_ready)
+            # (HSD_ENGINE_CAPTURE_DEPS=0 drops that edge: only to show the ordering test detects the race)
+            self._capture_deps_pending = self._hip is not None and os.environ.get("HSD_ENGINE_CAPTURE_DEPS", "1") == "1"
             self.engine.begin_step()
             return
         for b in self.buckets:
@@ -185,6 +196,12 @@ class GradBucketer:
         if not self.sync_enabled:
             return
         if self.engine is not None:
+            if self._hip is not None and self._hip.side_stream_in_capture():
+                # a capture's last buckets: join the wgrad branch into the capture stream once, and order them after
+                # the capture stream only -- an event recorded on the side stream after its final join would leave a
+                # trailing node on a forked stream that no edge joins back
+                self._hip.join_side_streams()
+                self.engine.set_capture_deps(False)
             self.engine.finish()  # launches unlaunched buckets; compute stream waits (host does not)
             if self._on_reduced is not None:
                 self.engine.wait_all()  # ... and for the optimizer slices queued behind the all-reduces

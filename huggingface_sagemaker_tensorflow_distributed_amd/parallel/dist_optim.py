@@ -55,9 +55,10 @@ class DistributedOptimizer:
         if not self._begun:
             self._begin()
         self._passes[i] += 1
-        if self._passes[i] > self.backward_passes_per_step:
+        if self._passes[i] > self.backward_passes_per_step and self.bucketer is not None:
             # Horovod raises here too: the bucket holding this gradient was already reduced, so the extra pass would
-            # be applied on this rank only and the replicas would diverge
+            # be applied on this rank only and the replicas would diverge. A world of one has no bucket (Horovod
+            # registers no hooks at size() == 1): extra local passes just accumulate
             raise RuntimeError(
                 f"parameter {i} received {self._passes[i]} gradients before step(), more than "
                 f"backward_passes_per_step={self.backward_passes_per_step}")

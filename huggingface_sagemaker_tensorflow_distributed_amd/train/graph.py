@@ -16,12 +16,14 @@ What makes a replay a *fresh* step:
   seed, so eager and replayed steps draw identical masks for the same step index;
 * gradients: the flat ``main_grad`` buffer is zeroed before the replay (kernels accumulate into it).
 
-Limits: one process (world 1; data-parallel steps keep the eager path so the bucketed all-reduce stays
-overlapped with backward), fixed batch shape per captured graph (a new shape captures a new graph),
-models without data-dependent shapes (the MLM head's masked-token gather syncs the host: eager only).
+Limits: fixed batch shape per captured graph (a new shape captures a new graph), models without data-dependent
+shapes (the MLM head's masked-token gather syncs the host: eager only). Data-parallel steps are captured whole only
+on request (HSD_GRAPH_DP=1, :class:`CapturedTrainStep` with the native RCCL engine's bucket all-reduces inside the
+graph); by default they keep the eager path.
 """
 from __future__ import annotations
 
+import gc
 import logging
 from typing import Dict
 
@@ -30,6 +32,23 @@ import torch
 from ..ops.rng import mix32_int
 
 logger = logging.getLogger(__name__)
+
+
+class _NoGC:
+    """Python's cyclic collector stays off while a graph is captured: a collection frees whatever cycles are due, and
+    a finaliser that synchronises a stream or frees device memory (an RCCL communicator's teardown) is an unsafe call
+    inside a capture (it invalidates it; the replay of such a graph faulted on the host). torch.cuda.graph collects
+    right before the capture begins."""
+
+    def __enter__(self):
+        self.was = gc.isenabled()
+        gc.disable()
+        return self
+
+    def __exit__(self, *exc):
+        if self.was:
+            gc.enable()
+        return False
 
 
 def step_seed(base_seed: int, rank: int, step: int, micro: int = 0):
@@ -95,7 +114,7 @@ class CapturedStep:
         from ..ops import hip
 
         try:
-            with torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
+            with torch.cuda.graph(self.graph, capture_error_mode="thread_local"), _NoGC():
                 hip.begin_capture(torch.cuda.current_stream(trainer.device))
                 model.rng.new_step(0)  # per-site seeds fixed; the device step seed varies per replay
                 self.loss, self.logits = trainer._forward_loss(self.static)
@@ -157,7 +176,7 @@ class CapturedTrainStep:
         self.graph = torch.cuda.CUDAGraph()
         step0 = opt.step_count
         try:
-            with opt.capturing(), torch.cuda.graph(self.graph, capture_error_mode="thread_local"):
+            with opt.capturing(), torch.cuda.graph(self.graph, capture_error_mode="thread_local"), _NoGC():
                 cap = torch.cuda.current_stream(trainer.device)  # the capture stream
                 # the weight-gradient side stream runs as a branch of the graph (ops/hip.py begin_capture), as in
                 # eager steps: captured sequentially it made the replay slower than eager (round 3)

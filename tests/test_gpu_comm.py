@@ -206,6 +206,56 @@ def test_whole_step_graph_with_native_engine(gpu, monkeypatch):
         res[replay] = (losses, store.master.clone())
         tr._seed.close()
         buck.detach()
+        eng.close()  # its teardown syncs and frees: not from a garbage collection inside the next capture
+    (l0, w0), (l1, w1) = res[False], res[True]
+    for a, b in zip(l0, l1):
+        assert abs(a - b) <= 2e-3 * max(1.0, abs(a)), (l0, l1)
+    assert float((w0 - w1).norm() / w0.norm()) < 1e-4
+
+
+def test_whole_step_graph_waits_for_delayed_wgrad_branch(gpu, monkeypatch):
+    """Ordering inside the data-parallel whole-step capture: the side stream is stalled 4 ms before each backward's
+    first weight gradient (ops/hip.py HSD_TEST_SIDE_DELAY_US), so a bucket all-reduce / Adam slice that is ordered only
+    after the capture stream reads main_grad before the wgrad branch has written it. The engine must wait on the wgrad
+    branch once the capture has forked it (comm_engine.cpp set_capture_deps): replayed steps then equal eager steps."""
+    from huggingface_sagemaker_tensorflow_distributed_amd import data as hdata
+    from huggingface_sagemaker_tensorflow_distributed_amd.ops import hip
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel import GradBucketer
+    from huggingface_sagemaker_tensorflow_distributed_amd.train.runner import build
+    from huggingface_sagemaker_tensorflow_distributed_amd.train.trainer import Trainer
+    from huggingface_sagemaker_tensorflow_distributed_amd.utils.args import build_parser
+
+    monkeypatch.setenv("HSD_OPT_OVERLAP", "1")
+    monkeypatch.setenv("HSD_GRAPH_FULL", "1")
+    monkeypatch.setenv("HSD_GRAPH_DP", "1")
+    monkeypatch.setattr(hip, "_SIDE_DELAY_US", 4000.0)
+    ds = hdata.synthetic_classification(32, 128, 30522, seed=2)
+    batches = [{k: torch.from_numpy(v[16 * i:16 * (i + 1)]).long().to(gpu) for k, v in
+                (("input_ids", ds.input_ids), ("attention_mask", ds.attention_mask), ("labels", ds.labels))}
+               for i in range(2)]
+    res = {}
+    C = _C()
+    for replay in (False, True):
+        args, _ = build_parser("train").parse_known_args(
+            ["--model_name_or_path", "bert-base-uncased", "--train_batch_size", "16", "--dtype", "bf16",
+             "--learning_rate", "1e-4", "--log_every", "0", "--seed", "5"])
+        parts = build(args, "train")
+        model, store, opt = parts["model"], parts["store"], parts["optimizer"]
+        eng = C.CommEngine(0, 1, C.CommEngine.unique_id(), gpu.index, True)
+        buck = GradBucketer(store, bucket_mb=4, engine=eng)
+        tr = Trainer(model, store, opt, buck, gpu, hip_graph=True)
+        tr._graph_replay = replay
+        assert tr._opt_overlap == "engine"
+        n0 = hip.CAPTURES_WITH_SIDE_STREAM[0]
+        losses = [float(tr.train_step([batches[s % 2]])) for s in range(3)]
+        torch.cuda.synchronize()
+        if replay:
+            assert any(k[0] == "full" for k in tr._graphs)
+            assert hip.CAPTURES_WITH_SIDE_STREAM[0] > n0  # the capture really branched the wgrad side stream
+        res[replay] = (losses, store.master.clone())
+        tr._seed.close()
+        buck.detach()
+        eng.close()  # its teardown syncs and frees: not from a garbage collection inside the next capture
     (l0, w0), (l1, w1) = res[False], res[True]
     for a, b in zip(l0, l1):
         assert abs(a - b) <= 2e-3 * max(1.0, abs(a)), (l0, l1)

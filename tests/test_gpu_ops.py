@@ -43,7 +43,7 @@ def test_dropout_mask_matches_reference(gpu):
     x = torch.ones(4096 * 3, device=gpu, dtype=torch.bfloat16)
     seed = 0xDEADBEEF12345678
     y = hip.dropout(x, 0.1, seed)
-    m = keep_mask(seed, x.numel(), 0.1, device=gpu)
+    m = keep_mask(seed, x.shape, 0.1, device=gpu)
     assert torch.equal(y.float() != 0, m)
     frac = m.float().mean().item()
     assert abs(frac - 0.9) < 0.02
@@ -141,7 +141,7 @@ def test_embed_ln(gpu, p, type_vocab, arange):
     r = ref.embed_ln(ids, pos, tt, word32, pw32, tw32, g32, be32, 1e-12, 0.0, 0, False)
     if p > 0:
         # kernel applies dropout to the bf16-rounded LN output
-        r = r.bfloat16().float() * keep_mask(99, r.numel(), p, device=gpu).view_as(r).float() / (1 - p)
+        r = r.bfloat16().float() * keep_mask(99, r.shape, p, device=gpu).float() / (1 - p)
     _close(out, r, 3e-2, 2e-2, "fwd")
     d = torch.randn_like(out)
     out.backward(d)

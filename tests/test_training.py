@@ -162,12 +162,12 @@ def test_gemm_nt_split_policy(monkeypatch):
     monkeypatch.delenv("HSD_G2_SMALL")
     assert C.gemm2_splits(2304, 768, 131072) == 9        # headline wgrads: 256^2 tiles, one wave of 256 CUs
     assert C.gemm2_splits(768, 768, 131072) == 28
-    assert C.gemm2_splits(1024, 1024, 4096) == 4         # 128^2 tiles x 4 splits (256^2 would need 13+)
-    # opt-in small-step plan (HSD_WGRAD_MIN_GRID=192): the fewest 128^2 K-splits giving 192 workgroups
-    monkeypatch.setenv("HSD_WGRAD_MIN_GRID", "192")
+    # small steps (<= 8,192 tokens): the fewest 128^2 K-splits giving 192 workgroups
     assert C.gemm2_splits(1024, 1024, 4096) == 3
     assert C.gemm2_splits(3072, 1024, 4096) == 1         # 192 tiles: one split, accumulated in place
     assert C.gemm2_splits(2304, 768, 8192) == 2          # 108 tiles -> 216 workgroups
+    monkeypatch.setenv("HSD_WGRAD_MIN_GRID", "0")        # the latency cost model at every size
+    assert C.gemm2_splits(1024, 1024, 4096) == 4         # 128^2 tiles x 4 splits (256^2 would need 13+)
 
 
 def test_tiny_bert_learns_the_marker_task_on_cpu():
