@@ -180,9 +180,13 @@ class CommEngine {
   // 0 = none (all-reduce the gradient buffer in place), 1 = bf16 on the wire, 2 = fp16 on the wire
   void set_compression(int64_t mode) {
     if (mode < 0 || mode > 2) throw std::runtime_error("set_compression: mode 0 (none), 1 (bf16) or 2 (fp16)");
+    if (mode != 0) {
+      if (!flat_.defined()) throw std::runtime_error("set_compression: call set_buckets first");
+      for (auto& b : buckets_)  // the 16-B vectorised casts (launch_wire_cast)
+        if (b.start % 4 || b.end % 4) throw std::runtime_error("set_compression: bucket ranges must be multiples of 4");
+    }
     comp_ = (int)mode;
     if (comp_ != 0) {
-      if (!flat_.defined()) throw std::runtime_error("set_compression: call set_buckets first");
       const auto dt = comp_ == 1 ? at::kBFloat16 : at::kHalf;
       if (!shadow_.defined() || shadow_.numel() != flat_.numel() || shadow_.scalar_type() != dt)
         shadow_ = at::empty({flat_.numel()}, flat_.options().dtype(dt));

@@ -19,6 +19,7 @@ C = load()
 dev = torch.device("cuda", 0)
 BUCKET = 64 << 20
 for name, numel in (("bert-base-uncased", 109_483_778), ("bert-large-uncased", 335_143_938)):
+    numel = (numel + 63) // 64 * 64  # FlatParamStore segments are 64-element aligned
     flat = torch.randn(numel, device=dev)
     per = BUCKET // 4
     starts = list(range(0, numel, per))
