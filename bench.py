@@ -131,6 +131,7 @@ def main():
                        "seq_len": a.seq_len, "parallelism": f"dp{world}",
                        "ops": "torch-reference" if os.environ.get("HSD_OPS") == "torch" else "hip",
                        "hip_graph": trainer._seed is not None,
+                       "grad_wire": trainer.bucketer.compression if trainer.bucketer is not None else None,
                        "comm": ("native-rccl" if getattr(trainer.bucketer, "engine", None) is not None
                                 else ("torch-" + backend.state().backend if world > 1 else "none"))},
             "validation": validation,

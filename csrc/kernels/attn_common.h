@@ -36,10 +36,10 @@ __device__ __forceinline__ bf16x8 cat8(bf16x4 a, bf16x4 b) {
   return r;
 }
 __device__ __forceinline__ bf16x8 pack8(const f32x16& acc, int s) {
-  bf16x8 r;
-#pragma unroll
-  for (int j = 0; j < 8; ++j) r[j] = (short)f2bf(acc[8 * s + j]);
-  return r;
+  // four two-source v_cvt_pk_bf16_f32 (pack_bf2), not eight single converts + shifts / ors
+  const u32x4 w = {pack_bf2(acc[8 * s], acc[8 * s + 1]), pack_bf2(acc[8 * s + 2], acc[8 * s + 3]),
+                   pack_bf2(acc[8 * s + 4], acc[8 * s + 5]), pack_bf2(acc[8 * s + 6], acc[8 * s + 7])};
+  return __builtin_bit_cast(bf16x8, w);
 }
 // Transposed A operand from a [rows][64] image: rows rb + 16s + 8(j>>2) + 4h + (j&3) (the accumulator's
 // permuted k order), columns colblk*32 + (lane & 31).

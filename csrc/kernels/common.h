@@ -50,9 +50,12 @@ __device__ __forceinline__ bf16_t f2bf(float f) {
   return *reinterpret_cast<bf16_t*>(&b);
 }
 
-// two floats -> packed bf16x2 in one u32 (lo = a, hi = b)
+// two floats -> packed bf16x2 in one u32 (lo = a, hi = b): ONE v_cvt_pk_bf16_f32 with both sources (RNE, as f2bf).
+// Built from two f2bf calls the compiler emitted two single-source converts + a shift + an SDWA or per pair -- about
+// one extra VALU instruction per element in every bf16 epilogue.
+typedef __bf16 bf16x2_native __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
-  return (uint32_t)f2bf(a) | ((uint32_t)f2bf(b) << 16);
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2{a, b}, bf16x2_native));
 }
 __device__ __forceinline__ float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float hi_bf(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }

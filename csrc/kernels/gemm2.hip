@@ -1033,7 +1033,8 @@ __global__ __launch_bounds__(256) void splitk_epi_kernel(const float* __restrict
       u32x4 o = {lo.x, lo.y, hi.x, hi.y}, o2;
       u32x4 x = {0, 0, 0, 0};
       if constexpr (epi_aux(EPI)) x = *reinterpret_cast<const u32x4*>(p.aux + (int64_t)m * p.ldaux + n);
-      epi_chunk<EPI>(o, o2, x, m, n, p, csum, cw);
+      epi_chunk<EPI>(o, o2, x, m, n, p, csum,
+                     EPI == E2_BIAS_DROP_RES && p.dp.enabled ? drop_row((uint32_t)m, p.dp.key) ^ cw : 0u);
       st16(C + (int64_t)m * p.ldc + n, o, p.nt_store);
       if constexpr (epi_two_out(EPI)) st16(p.C2 + (int64_t)m * p.ldc + n, o2, p.nt_store);
     }

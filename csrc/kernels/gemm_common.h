@@ -147,11 +147,11 @@ __device__ __forceinline__ u32x2 pack4(const f32x4& v) {
 
 // Epilogue math for one 16-B chunk (8 consecutive n of row m) of the staged bf16(acc [+ bias]) tile `o`;
 // `x` is the aux chunk. Returns the primary output in `o` and (two-output epilogues) the second in `o2`.
-// `cw`: the dropout column word C(n / 2) of this lane's chunk column n (E2_BIAS_DROP_RES; epi_col_word), hoisted out
-// of the row loops by the caller
+// `xw`: the dropout word R(m) ^ C(n / 2) of the chunk's row m and column n (E2_BIAS_DROP_RES; the caller keeps the
+// column word in a register across rows and gets the row word from a lane that hashed it -- epilogue_bf16)
 template <int EPI>
 __device__ __forceinline__ void epi_chunk(u32x4& o, u32x4& o2, const u32x4& x, int m, int n, const G2Params& p,
-                                          float (&csum)[8], uint32_t cw = 0u) {
+                                          float (&csum)[8], uint32_t xw = 0u) {
   if constexpr (EPI == E2_BIAS_GELU) {
     o2.x = pack_bf2(gelu_erf(lo_bf(o.x)), gelu_erf(hi_bf(o.x)));
     o2.y = pack_bf2(gelu_erf(lo_bf(o.y)), gelu_erf(hi_bf(o.y)));
@@ -169,16 +169,16 @@ __device__ __forceinline__ void epi_chunk(u32x4& o, u32x4& o2, const u32x4& x, i
     o.x = pack_bf2(d[0], d[1]); o.y = pack_bf2(d[2], d[3]); o.z = pack_bf2(d[4], d[5]); o.w = pack_bf2(d[6], d[7]);
     o2.x = pack_bf2(a[0], a[1]); o2.y = pack_bf2(a[2], a[3]); o2.z = pack_bf2(a[4], a[5]); o2.w = pack_bf2(a[6], a[7]);
   } else if constexpr (EPI == E2_BIAS_DROP_RES) {
-    // z = bf16(bf16(y · keep · scale) + residual)
+    // z = bf16(y · keep · scale + residual), y = bf16(acc + bias): one rounding of the sum (the dropped value is not
+    // rounded to bf16 on its own -- a pack / unpack pair per element less, and no less accurate)
     float v[8] = {lo_bf(o.x), hi_bf(o.x), lo_bf(o.y), hi_bf(o.y), lo_bf(o.z), hi_bf(o.z), lo_bf(o.w), hi_bf(o.w)};
     if (p.dp.enabled) {
-      // mask row m (width N), pairs n / 2 + e = n / 2 ^ e (n % 8 == 0): one row word per chunk
-      const uint32_t xw = drop_row((uint32_t)m, p.dp.key) ^ cw;
+      // mask row m (width N), pairs n / 2 + e = n / 2 ^ e (n % 8 == 0)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const uint32_t b = drop_fin(xw ^ drop_col((uint32_t)e));
-        v[2 * e] = bf2f(f2bf(v[2 * e] * keep_factor(b, 0, p.dp)));
-        v[2 * e + 1] = bf2f(f2bf(v[2 * e + 1] * keep_factor(b, 1, p.dp)));
+        v[2 * e] = keep_lo(b, p.dp.thr) ? v[2 * e] * p.dp.scale : 0.f;
+        v[2 * e + 1] = keep_hi(b, p.dp.thr) ? v[2 * e + 1] * p.dp.scale : 0.f;
       }
     }
     o.x = pack_bf2(v[0] + lo_bf(x.x), v[1] + hi_bf(x.x));
@@ -309,8 +309,12 @@ __device__ __forceinline__ void epilogue_bf16(f32x4 (&acc)[MB][BN / 64], const G
   // BEFORE this pass's stores: the vector-memory counter retires loads and stores in issue order, so a load issued
   // after the previous pass's stores made its consumer wait for all of them (s_waitcnt vmcnt(0) per pass)
   constexpr bool kAuxPf = epi_aux(EPI) && !G2_AUX_NO_PREFETCH;
-  // dropout column word of the lane's chunk column: the same in every pass when CPR divides 64 (hoisted)
+  // dropout: the column word of the lane's chunk column is the same in every pass when CPR divides 64 (hoisted); the
+  // row words of a pass's 16·PB rows are hashed once, one row per lane, and each chunk takes its row's word from that
+  // lane (ds_bpermute: an LDS-pipe move, not 9 VALU instructions of lowbias32 per chunk)
   constexpr bool kColFixed = 64 % CPR == 0;
+  constexpr bool kDrop = EPI == E2_BIAS_DROP_RES;
+  const bool drop_on = kDrop && p.dp.enabled;
   const uint32_t cw = kColFixed ? epi_col_word<EPI>(nw + (lane % CPR) * 8, p) : 0u;
   u32x4 xnext[ITER];
 #pragma unroll
@@ -352,16 +356,23 @@ __device__ __forceinline__ void epilogue_bf16(f32x4 (&acc)[MB][BN / 64], const G
     } else if (!kAuxPf || h == 0) {
       epi_aux_regs<EPI, BN, PB>(xv, p, lane, mw, nw, h);
     }
+    uint32_t rw_lane = 0u;  // R(row `lane` of this pass)
+    if (kDrop && drop_on && kColFixed) rw_lane = drop_row((uint32_t)(mw + 16 * PB * h + lane), p.dp.key);
 #pragma unroll
     for (int it = 0; it < ITER; ++it) {
       const int idx = lane + 64 * it;
       const int row = idx / CPR, c8 = idx % CPR;
       const int m = mw + 16 * PB * h + row;
       const int n = nw + c8 * 8;
+      uint32_t xw = 0u;
+      if (kDrop && drop_on) {
+        xw = kColFixed ? (uint32_t)__builtin_amdgcn_ds_bpermute(4 * row, (int)rw_lane) ^ cw
+                       : drop_row((uint32_t)m, p.dp.key) ^ epi_col_word<EPI>(n, p);
+      }
       if (m >= p.M) continue;
       const int64_t co = (int64_t)m * p.ldc + n;
       u32x4 o = sv[it], o2;
-      epi_chunk<EPI>(o, o2, xv[it], m, n, p, csum, kColFixed ? cw : epi_col_word<EPI>(n, p));
+      epi_chunk<EPI>(o, o2, xv[it], m, n, p, csum, xw);
       if (p.nt_store) {
         const uint32_t bo = (uint32_t)(((int64_t)(m - mw) * p.ldc + n) * 2);
         st16nt(rc, bo, o);

@@ -25,6 +25,7 @@ from .. import data as hdata
 from .. import ops
 from ..models import from_pretrained, save_pretrained
 from ..optim import FusedAdam
+from ..parallel.ddp import resolve_compression
 from ..parallel.flat_params import keep_transposed_weights
 from ..parallel import FlatParamStore, GradBucketer, ShardSampler, backend, broadcast_parameters
 from ..utils.args import parse_args
@@ -134,7 +135,8 @@ def build(args, mode: str):
         # sized on the device before any readiness hook / bucketer exists (the probes are plain fwd + bwd)
         batch_plan = batch_planner.plan(model, store, max_len, dev, headroom=args.auto_batch_headroom,
                                         max_tokens=args.auto_batch_max_tokens or None,
-                                        compression=getattr(args, "grad_compression", "none") if world > 1 else "none")
+                                        compression=resolve_compression(getattr(args, "grad_compression", "none"),
+                                                                        world, on_gpu, 1 << 30))
         per_gpu = batch_planner.agree_min(batch_plan.per_gpu_batch, dev)
         batch_plan.per_gpu_batch = per_gpu
         args.train_batch_size = per_gpu if mode == "train" else per_gpu * world
@@ -142,8 +144,12 @@ def build(args, mode: str):
                     "%.1f GB, capped by %s) -> train_batch_size %d", per_gpu, batch_plan.method,
                     batch_plan.per_seq_bytes / 2**20, batch_plan.fixed_bytes / 2**30, batch_plan.budget_bytes / 2**30,
                     batch_plan.total_bytes / 2**30, batch_plan.capped_by, args.train_batch_size)
-    bucketer = (GradBucketer(store, bucket_mb=args.bucket_mb, compression=getattr(args, "grad_compression", "none"))
-                if world > 1 else None)
+    per_rank = int(args.train_batch_size) // (1 if mode == "train" else world)
+    wire = resolve_compression(getattr(args, "grad_compression", "none"), world, on_gpu,
+                               per_rank * max_len * max(1, args.gradient_accumulation_steps))
+    if world > 1:
+        logger.info("gradient wire format: %s (--grad_compression %s)", wire, getattr(args, "grad_compression", "none"))
+    bucketer = GradBucketer(store, bucket_mb=args.bucket_mb, compression=wire) if world > 1 else None
     trainer = Trainer(model, store, opt, bucketer, dev, grad_accum=args.gradient_accumulation_steps,
                       lr_schedule=getattr(args, "lr_schedule", "constant"),
                       lr_warmup_steps=getattr(args, "lr_warmup_steps", 0),

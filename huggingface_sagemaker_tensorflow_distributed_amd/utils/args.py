@@ -76,8 +76,9 @@ def _add_framework_flags(p: argparse.ArgumentParser) -> None:
     g.add_argument("--seed", type=int, default=42)
     g.add_argument("--bucket_mb", type=float, default=None, help="gradient all-reduce bucket size (MiB)")
     g.add_argument("--grad_dtype", choices=["fp32", "bf16"], default=None)
-    g.add_argument("--grad_compression", choices=["none", "bf16", "fp16"], default="none",
-                   help="dtype fp32 gradient buckets are all-reduced in (Horovod's hvd.Compression.fp16)")
+    g.add_argument("--grad_compression", choices=["auto", "none", "bf16", "fp16"], default="auto",
+                   help="dtype fp32 gradient buckets are all-reduced in (Horovod's hvd.Compression.fp16); auto: bf16 "
+                        "from 32,768 tokens per rank and step on GPUs, fp32 below (parallel/ddp.py resolve_compression)")
     g.add_argument("--optimizer", choices=["adam", "adamw"], default="adam")
     g.add_argument("--weight_decay", type=float, default=0.0)
     g.add_argument("--adam_eps_mode", choices=["keras", "torch"], default="keras")

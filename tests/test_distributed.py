@@ -457,11 +457,34 @@ def _worker_compression(rank, world, port, mode):
     backend.shutdown()
 
 
-@pytest.mark.parametrize("mode", ["bf16", "fp16"])
+@pytest.mark.parametrize("mode", ["auto", "bf16", "fp16"])
 def test_gradient_wire_compression_world2(mode):
     """Horovod's ``hvd.Compression.fp16`` (``--grad_compression``): fp32 gradient buckets all-reduced in 16 bits,
-    cast back to fp32, identical on every rank, within 16-bit rounding of the fp32 sum (gloo world 2)."""
+    cast back to fp32, identical on every rank, within 16-bit rounding of the fp32 sum (gloo world 2). ``auto`` is the
+    default's resolution for the headline job (GPU ranks, 131,072 tokens per rank and step): bf16 on the wire."""
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel.ddp import resolve_compression
+
+    if mode == "auto":
+        mode = resolve_compression("auto", 2, True, 1024 * 128)
+        assert mode == "bf16"
     mp.spawn(_worker_compression, args=(2, _port(), mode), nprocs=2, join=True)
+
+
+def test_wire_policy_auto():
+    """``--grad_compression auto`` (default): bf16 from 32,768 tokens per rank and optimizer step on GPUs (the two
+    casts <= 2 % of the backward, profiles/wire_cast_r5.jsonl), fp32 below, on CPUs and for one rank; explicit choices
+    are kept."""
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel.ddp import resolve_compression
+    from huggingface_sagemaker_tensorflow_distributed_amd.utils.args import build_parser
+
+    assert build_parser("train").parse_known_args([])[0].grad_compression == "auto"
+    assert resolve_compression("auto", 8, True, 1024 * 128) == "bf16"      # headline bert-base B=1024 S=128
+    assert resolve_compression("auto", 8, True, 8 * 512) == "none"         # the reference's bert-large B=8 S=512
+    assert resolve_compression("auto", 8, True, 8 * 512 * 8) == "bf16"     # ... with 8 accumulation micro-steps
+    assert resolve_compression("auto", 1, True, 1 << 20) == "none"
+    assert resolve_compression("auto", 2, False, 1 << 20) == "none"
+    assert resolve_compression("fp16", 2, True, 16) == "fp16"
+    assert resolve_compression("none", 8, True, 1 << 20) == "none"
 
 
 def _worker_fp16_range(rank, world, port):
