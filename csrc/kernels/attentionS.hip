@@ -83,7 +83,8 @@ __device__ __forceinline__ void tile_barrier() {
 }
 
 // ------------------------------------------------------------------------------------------------
-template <bool DROP>
+// KM: the keep bits are written (kmask non-null), a compile-time choice so the per-register ballots carry no branch
+template <bool DROP, bool KM = false>
 __global__ __launch_bounds__(256, 2) void attnS_fwd_kernel(const bf16_t* __restrict__ qkv,
                                                            const float* __restrict__ mask, bf16_t* __restrict__ out,
                                                            float* __restrict__ lse2, int S, int heads, float sl2,
@@ -128,7 +129,7 @@ __global__ __launch_bounds__(256, 2) void attnS_fwd_kernel(const bf16_t* __restr
     xq = dropout_row((uint32_t)(bh * S + q), dp) ^ drop_col(2u * (uint32_t)hf);
     ctile = drop_col(32u * (uint32_t)lane);  // lane kt: C(32 kt), kt < S / 64 <= 16
   }
-  const bool km_on = DROP && kmask != nullptr;
+  constexpr bool km_on = DROP && KM;
   // keep-mask words of this wave: key-major [bh][q0 / 32][key], query-major [bh][kt][q][hf] (header)
   uint32_t* const km_k = km_on ? kmask + ((int64_t)bh * (S / 32) + q0 / 32) * S : nullptr;
   auto tile = [&](const int stg, const int kt) {
@@ -202,9 +203,10 @@ __global__ __launch_bounds__(256, 2) void attnS_fwd_kernel(const bf16_t* __restr
           const bool k0 = keep_lo(bits, dp.thr), k1 = keep_hi(bits, dp.thr);
           st[kb][reg] = k0 ? st[kb][reg] : 0.f;
           st[kb][reg + 1] = k1 ? st[kb][reg + 1] : 0.f;
-          if (km_on) {
+          if constexpr (km_on) {
             // the wave's keep bits of this register's two keys per half-wave -> lanes (tile keys) kl, kl + 4, ...
-            const unsigned long long m0 = __ballot(k0), m1 = __ballot(k1);
+            // (the ballot of the very compare the selects above use: the lane mask v_cmp already wrote)
+            const unsigned long long m0 = __builtin_amdgcn_ballot_w64(k0), m1 = __builtin_amdgcn_ballot_w64(k1);
             const int kl = kb * 32 + (reg & 3) + 8 * (reg >> 2);  // tile key of `reg` on lanes 0-31
             put_lane(wk, kl, (uint32_t)m0);
             put_lane(wk, kl + 4, (uint32_t)(m0 >> 32));
@@ -212,7 +214,7 @@ __global__ __launch_bounds__(256, 2) void attnS_fwd_kernel(const bf16_t* __restr
             put_lane(wk, kl + 5, (uint32_t)(m1 >> 32));
           }
         }
-      if (km_on) km_k[kt * 64 + lane] = wk;
+      if constexpr (km_on) km_k[kt * 64 + lane] = wk;
     }
 #pragma unroll
     for (int kb = 0; kb < 2; ++kb)
@@ -262,7 +264,7 @@ __global__ __launch_bounds__(256) void attnS_delta_kernel(const bf16_t* __restri
 }
 
 // ------------------------------------------------------------------------------------------------
-template <bool DROP>
+template <bool DROP, bool KM = false>
 __global__ __launch_bounds__(256, 2) void attnS_bwd_kv_kernel(const bf16_t* __restrict__ qkv,
                                                               const float* __restrict__ mask,
                                                               const bf16_t* __restrict__ dout,
@@ -307,8 +309,8 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_kv_kernel(const bf16_t* __re
     lse_s[i] = lse2[(int64_t)bh * S + i];
     del_s[i] = delta[(int64_t)bh * S + i];
   }
-  const bool km_on = DROP && kmask != nullptr;
-  if (km_on) {
+  constexpr bool km_on = DROP && KM;  // the forward's keep bits are read (compile-time: no per-register branch)
+  if constexpr (km_on) {
     const uint32_t* src = kmask + (int64_t)bh * (S / 32) * S + blockIdx.x * 128;
     for (int i = tid; i < (S / 32) * 128; i += 256) km_s[i] = src[(int64_t)(i >> 7) * S + (i & 127)];
   } else if (DROP) {
@@ -366,7 +368,7 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_kv_kernel(const bf16_t* __re
         const float p1 = __builtin_amdgcn_exp2f(fmaf(sacc[reg + 1], sl2, kb2) - lse[1]);
         float f0 = 1.f, f1 = 1.f;
         if constexpr (DROP) {
-          if (km_on) {
+          if constexpr (km_on) {
             const int pos = (reg & 3) + 8 * (reg >> 2);
             f0 = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)kmw, pos, 1) & __float_as_uint(dp.scale));
             f1 = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)kmw, pos + 1, 1) & __float_as_uint(dp.scale));
@@ -421,7 +423,7 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_kv_kernel(const bf16_t* __re
 }
 
 // ------------------------------------------------------------------------------------------------
-template <bool DROP>
+template <bool DROP, bool KM = false>
 __global__ __launch_bounds__(256, 2) void attnS_bwd_q_kernel(const bf16_t* __restrict__ qkv,
                                                              const float* __restrict__ mask,
                                                              const bf16_t* __restrict__ dout,
@@ -461,8 +463,8 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_q_kernel(const bf16_t* __res
   const float lse_q = lse2[(int64_t)bh * S + q];
   const float del_q = delta[(int64_t)bh * S + q];
   for (int k = tid; k < S; k += 256) mb_s[k] = mask ? fmaxf(mask[(int64_t)b * S + k] * kLog2e, -1e30f) : 0.f;
-  const bool km_on = DROP && kmask != nullptr;
-  if (km_on) {
+  constexpr bool km_on = DROP && KM;  // the forward's keep bits are read (compile-time: no per-register branch)
+  if constexpr (km_on) {
     const uint32_t* src = kmask + ((int64_t)bh * (S / 32) + blockIdx.x * 4) * S;  // the 4 query blocks, contiguous
     for (int i = tid; i < 4 * S; i += 256) km_s[i] = src[i];
   }
@@ -523,7 +525,7 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_q_kernel(const bf16_t* __res
           const float p1 = __builtin_amdgcn_exp2f(fmaf(sacc[reg + 1], sl2, mb[e + 1]) - lse_q);
           float f0 = 1.f, f1 = 1.f;
           if constexpr (DROP) {
-            if (km_on) {
+            if constexpr (km_on) {
               f0 = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)kw4[e], r, 1) & __float_as_uint(dp.scale));
               f1 = __uint_as_float((uint32_t)__builtin_amdgcn_sbfe((int)kw4[e + 1], r, 1) & __float_as_uint(dp.scale));
             } else {
@@ -573,9 +575,12 @@ void launch_attnS_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* 
                       double p, uint64_t seed, hipStream_t st, Q8Out q8o, uint32_t* kmask) {
   DropoutParams dp = make_dropout(p, seed);
   const float sl2 = attn::kLog2e / sqrtf((float)attn::D);
-  if (dp.enabled)
-    hipLaunchKernelGGL(aS::attnS_fwd_kernel<true>, dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, out, lse2, S,
-                       heads, sl2, dp, q8o, kmask);
+  if (dp.enabled && kmask != nullptr)
+    hipLaunchKernelGGL((aS::attnS_fwd_kernel<true, true>), dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, out,
+                       lse2, S, heads, sl2, dp, q8o, kmask);
+  else if (dp.enabled)
+    hipLaunchKernelGGL((aS::attnS_fwd_kernel<true, false>), dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, out,
+                       lse2, S, heads, sl2, dp, q8o, (uint32_t*)nullptr);
   else
     hipLaunchKernelGGL(aS::attnS_fwd_kernel<false>, dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, out, lse2, S,
                        heads, sl2, dp, q8o, (uint32_t*)nullptr);
@@ -591,12 +596,18 @@ void launch_attnS_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, con
   const float scale = 1.0f / sqrtf((float)attn::D);
   hipLaunchKernelGGL(aS::attnS_delta_kernel, dim3(S / 32, B * heads), dim3(256), 0, st, o, dout, delta_ws, S, heads);
   HSD_CHECK_LAUNCH();
-  if (dp.enabled) {
-    hipLaunchKernelGGL(aS::attnS_bwd_kv_kernel<true>, dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, dout,
-                       lse2, delta_ws, dqkv, dbias, S, heads, sl2, scale, dp, q8o, qfmt, kmask);
+  if (dp.enabled && kmask != nullptr) {
+    hipLaunchKernelGGL((aS::attnS_bwd_kv_kernel<true, true>), dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask,
+                       dout, lse2, delta_ws, dqkv, dbias, S, heads, sl2, scale, dp, q8o, qfmt, kmask);
     HSD_CHECK_LAUNCH();
-    hipLaunchKernelGGL(aS::attnS_bwd_q_kernel<true>, dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, dout,
-                       lse2, delta_ws, dqkv, dbias, S, heads, sl2, scale, dp, q8o, qfmt, kmask);
+    hipLaunchKernelGGL((aS::attnS_bwd_q_kernel<true, true>), dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask,
+                       dout, lse2, delta_ws, dqkv, dbias, S, heads, sl2, scale, dp, q8o, qfmt, kmask);
+  } else if (dp.enabled) {
+    hipLaunchKernelGGL((aS::attnS_bwd_kv_kernel<true, false>), dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask,
+                       dout, lse2, delta_ws, dqkv, dbias, S, heads, sl2, scale, dp, q8o, qfmt, nullptr);
+    HSD_CHECK_LAUNCH();
+    hipLaunchKernelGGL((aS::attnS_bwd_q_kernel<true, false>), dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask,
+                       dout, lse2, delta_ws, dqkv, dbias, S, heads, sl2, scale, dp, q8o, qfmt, nullptr);
   } else {
     hipLaunchKernelGGL(aS::attnS_bwd_kv_kernel<false>, dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask, dout,
                        lse2, delta_ws, dqkv, dbias, S, heads, sl2, scale, dp, q8o, qfmt, nullptr);

@@ -272,8 +272,8 @@ __device__ __forceinline__ void gelu_and_grad(float x, float& g, float& dg) {
 // only v_rcp / v_exp stay scalar) for the VALU-bound GELU epilogue of the FFN1 GEMM; same FMAs, same results
 // as gelu_and_grad.
 __device__ __forceinline__ void gelu_and_grad2(f32x2 x, f32x2& g, f32x2& dg) {
-  const f32x2 a = {fabsf(x.x), fabsf(x.y)};
-  const f32x2 den = __builtin_elementwise_fma(a, f32x2{0.23164189784f, 0.23164189784f}, f32x2{1.0f, 1.0f});
+  // |x| rides on two scalar FMAs as a source modifier (a packed FMA has no |.| modifier: it took two v_and first)
+  const f32x2 den = {fmaf(0.23164189784f, fabsf(x.x), 1.0f), fmaf(0.23164189784f, fabsf(x.y), 1.0f)};
   const f32x2 t = {__builtin_amdgcn_rcpf(den.x), __builtin_amdgcn_rcpf(den.y)};
   f32x2 P = __builtin_elementwise_fma(t, f32x2{1.061405429f, 1.061405429f}, f32x2{-1.453152027f, -1.453152027f});
   P = __builtin_elementwise_fma(t, P, f32x2{1.421413741f, 1.421413741f});
@@ -283,9 +283,10 @@ __device__ __forceinline__ void gelu_and_grad2(f32x2 x, f32x2& g, f32x2& dg) {
   const f32x2 q = x * x * f32x2{-0.72134752044f, -0.72134752044f};
   const f32x2 e = {__builtin_amdgcn_exp2f(q.x), __builtin_amdgcn_exp2f(q.y)};
   const f32x2 pe = P * e;
-  const f32x2 pos = __builtin_elementwise_fma(f32x2{-0.5f, -0.5f}, pe, f32x2{1.0f, 1.0f});
-  const f32x2 neg = f32x2{0.5f, 0.5f} * pe;
-  const f32x2 h = {x.x >= 0.0f ? pos.x : neg.x, x.y >= 0.0f ? pos.y : neg.y};
+  // ½(1 + erf(x/√2)) = ½ + sign(x)·(½ - ½·P·E): one packed FMA, two sign copies (v_bfi_b32) and one packed add, in
+  // place of two candidates + two compares + two selects
+  const f32x2 u = __builtin_elementwise_fma(f32x2{-0.5f, -0.5f}, pe, f32x2{0.5f, 0.5f});
+  const f32x2 h = f32x2{copysignf(u.x, x.x), copysignf(u.y, x.y)} + f32x2{0.5f, 0.5f};
   g = x * h;
   dg = __builtin_elementwise_fma(x * f32x2{0.3989422804014327f, 0.3989422804014327f}, e, h);
 }
