@@ -665,6 +665,41 @@ void attn32_bwd(torch::Tensor qkv, c10::optional<torch::Tensor> mask, torch::Ten
                          (int)heads, p, (uint64_t)seed, cur_stream());
 }
 
+// fp32 attention on split bf16 MFMA products (attention32m.hip): qkv / dout carried as hi + lo bf16 pairs
+void split2(torch::Tensor x, torch::Tensor hi, torch::Tensor lo) {
+  check_f32(x, "x"); check_bf16(hi, "hi"); check_bf16(lo, "lo");
+  TORCH_CHECK(x.numel() == hi.numel() && x.numel() == lo.numel() && x.numel() % 4 == 0, "split2 sizes");
+  hsd::launch_split2(x.data_ptr<float>(), BF(hi), BF(lo), x.numel(), cur_stream());
+}
+
+void attn32m_fwd(torch::Tensor qh, torch::Tensor ql, c10::optional<torch::Tensor> mask, torch::Tensor out,
+                 torch::Tensor lse, int64_t B, int64_t S, int64_t heads, double p, int64_t seed) {
+  check_bf16(qh, "qkv_hi"); check_bf16(ql, "qkv_lo"); check_f32(out, "out"); check_f32(lse, "lse");
+  TORCH_CHECK(hsd::attn32m_supported((int)S, 64), "attn32m_fwd: S must be a multiple of 128 in [128, 1024]");
+  TORCH_CHECK(qh.sizes() == ql.sizes() && qh.size(0) == B * S && qh.size(1) == 3 * heads * 64 && out.size(0) == B * S &&
+              out.size(1) == heads * 64 && lse.numel() == B * heads * S, "attn32m_fwd shapes (head dim 64)");
+  if (mask.has_value()) { check_f32(*mask, "mask"); TORCH_CHECK(mask->numel() == B * S, "mask"); }
+  hsd::launch_attn32m_fwd(CBF(qh), CBF(ql), OPT_F(mask), out.data_ptr<float>(), lse.data_ptr<float>(), (int)B, (int)S,
+                          (int)heads, p, (uint64_t)seed, cur_stream());
+}
+
+void attn32m_bwd(torch::Tensor qh, torch::Tensor ql, torch::Tensor doh, torch::Tensor dol,
+                 c10::optional<torch::Tensor> mask, torch::Tensor o, torch::Tensor dout, torch::Tensor lse,
+                 torch::Tensor dqkv, torch::Tensor delta, int64_t B, int64_t S, int64_t heads, double p, int64_t seed) {
+  check_bf16(qh, "qkv_hi"); check_bf16(ql, "qkv_lo"); check_bf16(doh, "dout_hi"); check_bf16(dol, "dout_lo");
+  check_f32(o, "o"); check_f32(dout, "dout"); check_f32(lse, "lse"); check_f32(dqkv, "dqkv"); check_f32(delta, "delta");
+  TORCH_CHECK(hsd::attn32m_supported((int)S, 64), "attn32m_bwd: S must be a multiple of 128 in [128, 1024]");
+  TORCH_CHECK(qh.sizes() == ql.sizes() && qh.sizes() == dqkv.sizes() && doh.sizes() == dol.sizes() &&
+              doh.sizes() == o.sizes() && o.sizes() == dout.sizes() && o.size(0) == B * S && o.size(1) == heads * 64 &&
+              lse.numel() == B * heads * S && delta.numel() >= B * heads * S, "attn32m_bwd shapes");
+  if (mask.has_value()) { check_f32(*mask, "mask"); TORCH_CHECK(mask->numel() == B * S, "mask"); }
+  hsd::launch_attn32_delta(o.data_ptr<float>(), dout.data_ptr<float>(), delta.data_ptr<float>(), (int)B, (int)S,
+                           (int)heads, cur_stream());
+  hsd::launch_attn32m_bwd(CBF(qh), CBF(ql), CBF(doh), CBF(dol), OPT_F(mask), lse.data_ptr<float>(),
+                          delta.data_ptr<float>(), dqkv.data_ptr<float>(), (int)B, (int)S, (int)heads, p,
+                          (uint64_t)seed, cur_stream());
+}
+
 void cls32_fwd(torch::Tensor pre, torch::Tensor W2, torch::Tensor b2, torch::Tensor labels, torch::Tensor t_out,
                torch::Tensor logits, torch::Tensor stats, int64_t act, double p, int64_t seed) {
   check_f32(pre, "pre"); check_f32(W2, "W2"); check_f32(b2, "b2"); check_f32(t_out, "t_out"); check_f32(logits, "logits");
@@ -862,6 +897,10 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("embed32_scatter", &embed32_scatter);
   m.def("attn32_fwd", &attn32_fwd);
   m.def("attn32_bwd", &attn32_bwd);
+  m.def("split2", &split2);
+  m.def("attn32m_supported", [](int64_t S) { return hsd::attn32m_supported((int)S, 64); });
+  m.def("attn32m_fwd", &attn32m_fwd);
+  m.def("attn32m_bwd", &attn32m_bwd);
   m.def("cls32_fwd", &cls32_fwd);
   m.def("cls32_bwd", &cls32_bwd);
   m.def("refresh_env", &hsd::refresh_env_knobs, "re-read the HSD_* launch knobs (cached per generation)");

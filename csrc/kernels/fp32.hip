@@ -784,6 +784,12 @@ void launch_attn32_bwd(const float* qkv, const float* mask, const float* o, cons
   HSD_CHECK_LAUNCH();
 }
 
+void launch_attn32_delta(const float* o, const float* dout, float* delta, int B, int S, int heads, hipStream_t st) {
+  const int n = B * heads * S;
+  hipLaunchKernelGGL(f32k::attn32_delta_kernel, dim3((n + 255) / 256), dim3(256), 0, st, o, dout, delta, B, S, heads);
+  HSD_CHECK_LAUNCH();
+}
+
 void launch_cls32_fwd(const float* pre, const float* W2, const float* b2, const int64_t* labels, float* t_out,
                       float* logits, float* stats, int R, int H, int C, int act, double p, uint64_t seed,
                       hipStream_t st) {

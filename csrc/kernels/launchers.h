@@ -119,6 +119,15 @@ void launch_attn32_fwd(const float* qkv, const float* mask, float* out, float* l
                        uint64_t seed, hipStream_t st);
 void launch_attn32_bwd(const float* qkv, const float* mask, const float* o, const float* dout, const float* lse,
                        float* dqkv, float* delta, int B, int S, int heads, double p, uint64_t seed, hipStream_t st);
+void launch_attn32_delta(const float* o, const float* dout, float* delta, int B, int S, int heads, hipStream_t st);
+// fp32 attention on split bf16 MFMA products (attention32m.hip)
+bool attn32m_supported(int S, int head_dim);
+void launch_split2(const float* x, bf16_t* hi, bf16_t* lo, int64_t n, hipStream_t st);
+void launch_attn32m_fwd(const bf16_t* qkv_hi, const bf16_t* qkv_lo, const float* mask, float* out, float* lse2, int B,
+                        int S, int heads, double p, uint64_t seed, hipStream_t st);
+void launch_attn32m_bwd(const bf16_t* qkv_hi, const bf16_t* qkv_lo, const bf16_t* do_hi, const bf16_t* do_lo,
+                        const float* mask, const float* lse2, const float* delta, float* dqkv, int B, int S, int heads,
+                        double p, uint64_t seed, hipStream_t st);
 void launch_cls32_fwd(const float* pre, const float* W2, const float* b2, const int64_t* labels, float* t_out,
                       float* logits, float* stats, int R, int H, int C, int act, double p, uint64_t seed,
                       hipStream_t st);

@@ -309,6 +309,50 @@ class _Attention32(torch.autograd.Function):
         return dqkv, None, None, None, None, None, None
 
 
+def _split2(x: torch.Tensor):
+    hi = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+    lo = torch.empty_like(hi)
+    _C.split2(x, hi, lo)
+    return hi, lo
+
+
+class _Attention32M(torch.autograd.Function):
+    """fp32 attention on the bf16 matrix cores (attention32m.hip): qkv and dout carried as hi + lo bf16 pairs, every
+    product the three-term split product, softmax / dropout / accumulation fp32. S a multiple of 128 up to 1024."""
+
+    @staticmethod
+    def forward(ctx, qkv, mask_bias, B, S, heads, p, seed):
+        qkv = qkv.contiguous()
+        H = qkv.shape[-1] // 3
+        qh, ql = _split2(qkv)
+        out = torch.empty((B * S, H), dtype=torch.float32, device=qkv.device)
+        lse = torch.empty(B * heads * S, dtype=torch.float32, device=qkv.device)
+        mb = mask_bias.contiguous().float() if mask_bias is not None else None
+        _C.attn32m_fwd(qh, ql, mb, out, lse, B, S, heads, float(p), _s64(seed))
+        ctx.save_for_backward(qh, ql, out, lse, mb if mb is not None else lse)
+        ctx.has_mask = mb is not None
+        ctx.cfg = (B, S, heads, float(p), seed)
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        qh, ql, out, lse, mb = ctx.saved_tensors
+        B, S, heads, p, seed = ctx.cfg
+        dout = dout.contiguous()
+        dh, dl = _split2(dout)
+        dqkv = torch.empty(qh.shape, dtype=torch.float32, device=qh.device)
+        delta = torch.empty(B * heads * S, dtype=torch.float32, device=qh.device)
+        _C.attn32m_bwd(qh, ql, dh, dl, mb if ctx.has_mask else None, out, dout, lse, dqkv, delta, B, S, heads, p,
+                       _s64(seed))
+        return dqkv, None, None, None, None, None, None
+
+
+import os as _os
+
+# HSD_ATTN32M=0: the round-4 fp32 attention on the vector ALUs (exact fp32 FMAs) instead of the split MFMA products
+_ATTN32M = _os.environ.get("HSD_ATTN32M", "1") != "0"
+
+
 def attention_ok(qkv, seq, heads) -> bool:
     return qkv.shape[-1] == 3 * heads * 64 and seq % 2 == 0
 
@@ -318,6 +362,8 @@ def attention(qkv, mask_bias, batch, seq, heads, p, seed):
         from .reference import attention as ref
 
         return ref(qkv, mask_bias, batch, seq, heads, p, seed, p > 0)
+    if _ATTN32M and _C.attn32m_supported(seq):
+        return _Attention32M.apply(qkv, mask_bias, batch, seq, heads, p, seed)
     return _Attention32.apply(qkv, mask_bias, batch, seq, heads, p, seed)
 
 

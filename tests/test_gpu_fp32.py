@@ -54,11 +54,15 @@ def _grads(fn, *args):
     return out.detach(), [a.grad.detach().clone() for a in args if isinstance(a, torch.Tensor) and a.requires_grad]
 
 
+@pytest.mark.parametrize("path", ["mfma", "valu"])
 @pytest.mark.parametrize("p", [0.0, 0.1])
 @pytest.mark.parametrize("S", [128, 512])
-def test_attention32_fwd_bwd(gpu, p, S):
-    """Streaming fp32 attention forward + three-pass backward == the reference ops (same dropout masks), fp32."""
+def test_attention32_fwd_bwd(gpu, p, S, path, monkeypatch):
+    """fp32 attention forward + backward == the fp64 reference ops (same dropout masks): the split-product MFMA kernels
+    (attention32m.hip, default; measured ~6e-6 / ~8e-6 relative error) and the exact-FMA vector kernels (fp32.hip)."""
     from huggingface_sagemaker_tensorflow_distributed_amd.ops import reference as R
+
+    monkeypatch.setattr(_h32(), "_ATTN32M", path == "mfma")
 
     B, heads = 2, 4
     H = heads * 64
