@@ -266,8 +266,10 @@ void attn_fwd(torch::Tensor qkv, c10::optional<torch::Tensor> mask, torch::Tenso
 void attn_bwd(torch::Tensor qkv, c10::optional<torch::Tensor> mask, torch::Tensor o, torch::Tensor dout,
               torch::Tensor lse2, torch::Tensor dqkv, c10::optional<torch::Tensor> dq_acc, int64_t B, int64_t S,
               int64_t heads, double p, int64_t seed, c10::optional<torch::Tensor> dbias,
-              c10::optional<torch::Tensor> kmask) {
+              c10::optional<torch::Tensor> kmask, bool delta_ready) {
   check_bf16(qkv, "qkv"); check_bf16(o, "o"); check_bf16(dout, "dout"); check_bf16(dqkv, "dqkv");
+  TORCH_CHECK(!delta_ready || (S > 128 && hsd::attn_streaming((int)S) && dq_acc.has_value()),
+              "attn_bwd delta_ready: streaming attention with the delta rows in dq_acc");
   check_f32(lse2, "lse2");
   TORCH_CHECK(qkv.size(-1) == 3 * heads * 64 && dqkv.numel() == qkv.numel(), "attn_bwd shapes");
   TORCH_CHECK(o.numel() == B * S * heads * 64 && dout.numel() == o.numel(), "attn_bwd o shapes");
@@ -280,7 +282,7 @@ void attn_bwd(torch::Tensor qkv, c10::optional<torch::Tensor> mask, torch::Tenso
   if (dbias.has_value()) { check_f32(*dbias, "dbias"); TORCH_CHECK(dbias->numel() == 3 * heads * 64, "dbias shape"); }
   hsd::launch_attn_bwd(CBF(qkv), OPT_F(mask), CBF(o), CBF(dout), lse2.data_ptr<float>(), BF(dqkv), OPT_F(dq_acc),
                        OPT_F(dbias), (int)B, (int)S, (int)heads, p, (uint64_t)seed, cur_stream(),
-                       keep_mask_ptr(kmask, B, S, heads));
+                       keep_mask_ptr(kmask, B, S, heads), delta_ready);
 }
 
 // attention + fp8 copy of its output (forward: e4m3 of the context; backward: dqkv in format qfmt), S > 128 streaming
@@ -491,7 +493,7 @@ void set_dropout_device_seed(c10::optional<torch::Tensor> t) {
 void gemm2(torch::Tensor A, torch::Tensor B, torch::Tensor C, int64_t la, int64_t lb, int64_t epi,
            c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> aux, c10::optional<torch::Tensor> C2,
            double p, int64_t seed, int64_t splits, c10::optional<torch::Tensor> ws,
-           c10::optional<torch::Tensor> dbias) {
+           c10::optional<torch::Tensor> dbias, c10::optional<torch::Tensor> rd, int64_t rd_seq) {
   TORCH_CHECK(A.is_cuda() && B.is_cuda() && C.is_cuda(), "gemm2 operands must be GPU tensors");
   TORCH_CHECK(A.scalar_type() == torch::kBFloat16 && B.scalar_type() == torch::kBFloat16, "gemm2 inputs must be bf16");
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2, "gemm2 operands must be 2-D");
@@ -511,7 +513,7 @@ void gemm2(torch::Tensor A, torch::Tensor B, torch::Tensor C, int64_t la, int64_
     TORCH_CHECK(bias.has_value() && bias->numel() == N && bias->scalar_type() == torch::kBFloat16 &&
                 bias->is_contiguous(), "gemm2 bias");
   }
-  if (epi == 3 || epi == 4 || epi == 5 || epi == 9) {
+  if (epi == 3 || epi == 4 || epi == 5 || epi == 9 || epi == 10) {
     TORCH_CHECK(aux.has_value() && aux->dim() == 2 && aux->size(0) == M && aux->size(1) == N &&
                 aux->stride(1) == 1 && aux->stride(0) % 8 == 0 && aux->scalar_type() == torch::kBFloat16, "gemm2 aux");
   }
@@ -545,10 +547,18 @@ void gemm2(torch::Tensor A, torch::Tensor B, torch::Tensor C, int64_t la, int64_
     TORCH_CHECK(dbias->numel() == N, "dbias size");
     dbp = dbias->data_ptr<float>();
   }
+  float* rdp = nullptr;
+  if (epi == 10) {
+    // delta rows of the attention backward: [M / rd_seq][N / 64][rd_seq] fp32
+    TORCH_CHECK(rd.has_value() && rd_seq > 0 && M % rd_seq == 0, "gemm2 row dots: rd and the sequence length");
+    check_f32(*rd, "rd");
+    TORCH_CHECK(rd->numel() == M * (N / 64), "gemm2 row dots: rd size");
+    rdp = rd->data_ptr<float>();
+  }
   hsd::launch_gemm2((int)la, (int)lb, (int)epi, CBF(A), A.stride(0), CBF(B), B.stride(0), (int)M, (int)N, (int)K,
                     C.data_ptr(), C.stride(0), bias.has_value() ? CBF(*bias) : nullptr,
                     aux.has_value() ? CBF(*aux) : nullptr, aux.has_value() ? aux->stride(0) : 0,
-                    C2.has_value() ? BF(*C2) : nullptr, p, (uint64_t)seed, sp, wsp, dbp, cur_stream());
+                    C2.has_value() ? BF(*C2) : nullptr, p, (uint64_t)seed, sp, wsp, dbp, cur_stream(), rdp, (int)rd_seq);
 }
 
 // ---- fp32 step (fp32.hip, ops/hip32.py) ---------------------------------------------------------------------------
@@ -732,7 +742,7 @@ void gemm2_on(int64_t stream_ptr, torch::Tensor A, torch::Tensor B, torch::Tenso
               c10::optional<torch::Tensor> dbias) {
   c10::hip::HIPStreamGuard guard(
       c10::hip::getStreamFromExternal(reinterpret_cast<hipStream_t>(stream_ptr), A.get_device()));
-  gemm2(A, B, C, la, lb, epi, bias, aux, C2, p, seed, splits, ws, dbias);
+  gemm2(A, B, C, la, lb, epi, bias, aux, C2, p, seed, splits, ws, dbias, c10::nullopt, 0);
 }
 
 // logits [R, V] (bf16 | fp32), labels int64 [R] (-100 = ignore); stats fp32 [2] += {Σ loss, correct};
@@ -930,9 +940,11 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   });
   m.def("attn_bwd", &attn_bwd, py::arg("qkv"), py::arg("mask"), py::arg("o"), py::arg("dout"), py::arg("lse2"),
         py::arg("dqkv"), py::arg("dq_acc"), py::arg("B"), py::arg("S"), py::arg("heads"), py::arg("p"), py::arg("seed"),
-        py::arg("dbias") = py::none(), py::arg("kmask") = py::none());
+        py::arg("dbias") = py::none(), py::arg("kmask") = py::none(), py::arg("delta_ready") = false);
   m.def("gemm", &gemm);
-  m.def("gemm2", &gemm2);
+  m.def("gemm2", &gemm2, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("la"), py::arg("lb"), py::arg("epi"),
+        py::arg("bias"), py::arg("aux"), py::arg("C2"), py::arg("p"), py::arg("seed"), py::arg("splits"), py::arg("ws"),
+        py::arg("dbias"), py::arg("rd") = py::none(), py::arg("rd_seq") = 0);
   m.def("gemm2_splits", &gemm2_splits);
   m.def("gemm8_wgrad", &gemm8_wgrad);
   m.def("gemm8_wgrad_supported", [](int64_t M, int64_t N, int64_t T) {

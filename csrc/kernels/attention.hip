@@ -379,7 +379,7 @@ void launch_attnS_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* 
                       double p, uint64_t seed, hipStream_t st, Q8Out q8o, uint32_t* kmask);
 void launch_attnS_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
                       bf16_t* dqkv, float* delta_ws, float* dbias, int B, int S, int heads, double p, uint64_t seed,
-                      hipStream_t st, Q8Out q8o, int qfmt, const uint32_t* kmask);
+                      hipStream_t st, Q8Out q8o, int qfmt, const uint32_t* kmask, bool delta_ready);
 
 // S in 256..1024 (multiple of 128) runs the streaming kernels of attentionS.hip; its backward takes
 // an fp32 [B*heads*S] scratch (no zeroing) where the generic kernel takes a zeroed [B*S, H] dq accumulator.
@@ -413,13 +413,14 @@ void launch_attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* l
 
 void launch_attn_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
                      bf16_t* dqkv, float* dq_acc, float* dbias, int B, int S, int heads, double p, uint64_t seed,
-                     hipStream_t st, const uint32_t* kmask) {
+                     hipStream_t st, const uint32_t* kmask, bool delta_ready) {
   if (attn128_supported(S, kD) && !HSD_KNOB("HSD_ATTN_GENERIC", 0)) {
     launch_attn128_bwd(qkv, mask, o, dout, lse2, dqkv, dbias, B, heads, p, seed, st);
     return;
   }
   if (attn_streaming(S)) {
-    launch_attnS_bwd(qkv, mask, o, dout, lse2, dqkv, dq_acc, dbias, B, S, heads, p, seed, st, Q8Out{}, 0, kmask);
+    launch_attnS_bwd(qkv, mask, o, dout, lse2, dqkv, dq_acc, dbias, B, S, heads, p, seed, st, Q8Out{}, 0, kmask,
+                     delta_ready);
     return;
   }
   DropoutParams dp = make_dropout(p, seed);

@@ -256,10 +256,7 @@ __global__ __launch_bounds__(256) void attnS_delta_kernel(const bf16_t* __restri
   const int64_t off = (((int64_t)b * S + s) * heads + hh) * D + c * 8;
   const u32x4 ov = *reinterpret_cast<const u32x4*>(o + off);
   const u32x4 dv = *reinterpret_cast<const u32x4*>(dout + off);
-  float acc = 0.f;
-#pragma unroll
-  for (int k = 0; k < 4; ++k) acc += lo_bf(dv[k]) * lo_bf(ov[k]) + hi_bf(dv[k]) * hi_bf(ov[k]);
-  acc = sum8_dpp(acc);
+  const float acc = sum8_dpp(dot8_bf16(dv, ov));
   if (c == 0) delta[(int64_t)bh * S + s] = acc;
 }
 
@@ -587,15 +584,18 @@ void launch_attnS_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* 
   HSD_CHECK_LAUNCH();
 }
 
-// delta_ws: fp32 [B*heads*S] scratch
+// delta_ws: fp32 [B*heads*S] scratch; delta_ready: it already holds the delta rows (written by the out-projection
+// dgrad's E2_STORE_RDOT epilogue, ops/hip.py), so the delta pass is skipped
 void launch_attnS_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
                       bf16_t* dqkv, float* delta_ws, float* dbias, int B, int S, int heads, double p, uint64_t seed,
-                      hipStream_t st, Q8Out q8o, int qfmt, const uint32_t* kmask) {
+                      hipStream_t st, Q8Out q8o, int qfmt, const uint32_t* kmask, bool delta_ready) {
   DropoutParams dp = make_dropout(p, seed);
   const float sl2 = attn::kLog2e / sqrtf((float)attn::D);
   const float scale = 1.0f / sqrtf((float)attn::D);
-  hipLaunchKernelGGL(aS::attnS_delta_kernel, dim3(S / 32, B * heads), dim3(256), 0, st, o, dout, delta_ws, S, heads);
-  HSD_CHECK_LAUNCH();
+  if (!delta_ready) {
+    hipLaunchKernelGGL(aS::attnS_delta_kernel, dim3(S / 32, B * heads), dim3(256), 0, st, o, dout, delta_ws, S, heads);
+    HSD_CHECK_LAUNCH();
+  }
   if (dp.enabled && kmask != nullptr) {
     hipLaunchKernelGGL((aS::attnS_bwd_kv_kernel<true, true>), dim3(S / 128, B * heads), dim3(256), 0, st, qkv, mask,
                        dout, lse2, delta_ws, dqkv, dbias, S, heads, sl2, scale, dp, q8o, qfmt, kmask);
@@ -630,7 +630,7 @@ void launch_attnS_bwd_q8(const bf16_t* qkv, const float* mask, const bf16_t* o, 
                          bf16_t* dqkv, float* delta_ws, float* dbias, int B, int S, int heads, double p, uint64_t seed,
                          uint8_t* q8, const float* amax_in, float* sinv, float* amax_track, int qfmt, hipStream_t st) {
   launch_attnS_bwd(qkv, mask, o, dout, lse2, dqkv, delta_ws, dbias, B, S, heads, p, seed, st,
-                   Q8Out{q8, amax_in, sinv, amax_track}, qfmt, nullptr);
+                   Q8Out{q8, amax_in, sinv, amax_track}, qfmt, nullptr, false);
 }
 
 }  // namespace hsd

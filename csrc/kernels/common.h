@@ -80,6 +80,15 @@ __device__ __forceinline__ float sum8_dpp(float v) {
   return v + dpp_half_mirror(v);
 }
 
+// Σ over 8 bf16 pairs of (a·b): the attention backward's delta row partials -- ONE definition for the delta kernel and
+// the out-projection dgrad epilogue that writes the same rows (E2_STORE_RDOT), so both give identical bits
+__device__ __forceinline__ float dot8_bf16(const u32x4& a, const u32x4& b) {
+  float acc = 0.f;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) acc += lo_bf(a[k]) * lo_bf(b[k]) + hi_bf(a[k]) * hi_bf(b[k]);
+  return acc;
+}
+
 // sum over the 8 lanes {l & 7 + 8 j}: lane-bit 3 by DPP row_ror:8, bits 4 and 5 by the gfx950 permlane swaps (each swap
 // of v with itself returns both halves of the xor-16 / xor-32 pair); the same pairwise additions as the xor-8/16/32
 // butterfly, so bit-identical to it, with no LDS round trip

@@ -1035,6 +1035,7 @@ __global__ __launch_bounds__(256) void splitk_epi_kernel(const float* __restrict
       if constexpr (epi_aux(EPI)) x = *reinterpret_cast<const u32x4*>(p.aux + (int64_t)m * p.ldaux + n);
       epi_chunk<EPI>(o, o2, x, m, n, p, csum,
                      EPI == E2_BIAS_DROP_RES && p.dp.enabled ? drop_row((uint32_t)m, p.dp.key) ^ cw : 0u);
+      if constexpr (EPI == E2_STORE_RDOT) rdot_group(o, x, m, n, p, c8 == 0, true);  // 8 lanes of one row, all in
       st16(C + (int64_t)m * p.ldc + n, o, p.nt_store);
       if constexpr (epi_two_out(EPI)) st16(p.C2 + (int64_t)m * p.ldc + n, o2, p.nt_store);
     }
@@ -1507,6 +1508,7 @@ static void g2s_launch(const G2Params& q, int grid, hipStream_t st) {
 
 bool gemm2_supported(int la, int lb, int epi, int M, int N, int K) {
   if (K % 64 || M < 1 || N % 8) return false;
+  if (epi == E2_STORE_RDOT && (la != 0 || N % 256)) return false;
   if (la == 0 && epi == E2_F32_SLAB) return N % 256 == 0;  // fp32-output NT, one pass (launch_gemm2)
   if (la == 0 && lb == 0) return epi_bf16_out(epi) && gemm2_pick_bn(M, N) != 0;
   if (la == 0 && lb == 1) return epi_bf16_out(epi) && (N % 256 == 0 || gemm2s_use(M, N, K));
@@ -1545,6 +1547,7 @@ static void launch_nt(const G2Params& p, int epi, int M, int N, int K, int split
       G2_SMALL(E2_DGELU)
       G2_SMALL(E2_BIAS_GELU_D)
       G2_SMALL(E2_MUL)
+      G2_SMALL(E2_STORE_RDOT)
       default: abort();
     }
 #undef G2_SMALL
@@ -1584,6 +1587,7 @@ static void launch_nt(const G2Params& p, int epi, int M, int N, int K, int split
       G2_SK(E2_DGELU)
       G2_SK(E2_BIAS_GELU_D)
       G2_SK(E2_MUL)
+      G2_SK(E2_STORE_RDOT)
       default: abort();
     }
 #undef G2_SK
@@ -1591,7 +1595,7 @@ static void launch_nt(const G2Params& p, int epi, int M, int N, int K, int split
     return;
   }
   {
-    int bn = LB == 1 ? 256 : gemm2_pick_bn(M, N);  // k-strided B images are 256 wide
+    int bn = LB == 1 || epi == E2_STORE_RDOT ? 256 : gemm2_pick_bn(M, N);  // k-strided B images are 256 wide
     if (dbias != nullptr) {
       if ((epi != E2_DGELU && epi != E2_MUL) || N % 256) abort();  // fused column sums: 8 columns per lane (BN 256)
       bn = 256;
@@ -1617,6 +1621,10 @@ static void launch_nt(const G2Params& p, int epi, int M, int N, int K, int split
       G2_NT(E2_DGELU)
       G2_NT(E2_BIAS_GELU_D)
       G2_NT(E2_MUL)
+      case E2_STORE_RDOT:  // 64-column wave tiles only (one head per 8-lane group): BN 256
+        if (pk) g2pk_launch<E2_STORE_RDOT, 256>(p, st);
+        else g2_launch<0, LB, E2_STORE_RDOT, 256>(p, 1, st);
+        return;
       default: abort();
     }
 #undef G2_NT
@@ -1628,9 +1636,13 @@ void gemm2_set_diag(void* p) { g_diag = (unsigned long long*)p; }
 
 void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, int M, int N,
                   int K, void* C, int64_t ldc, const bf16_t* bias, const bf16_t* aux, int64_t ldaux, bf16_t* C2,
-                  double p_drop, uint64_t seed, int splits, float* ws, float* dbias, hipStream_t st) {
+                  double p_drop, uint64_t seed, int splits, float* ws, float* dbias, hipStream_t st, float* rd,
+                  int rd_seq) {
   G2Params p{};
   p.dbias = dbias;
+  p.rd = rd;
+  p.rd_seq = rd_seq;
+  if (epi == E2_STORE_RDOT && (rd == nullptr || rd_seq <= 0 || M % rd_seq || N % 64)) abort();
   p.diag = g_diag;
   p.nt_store = HSD_KNOB("HSD_G2_NT", 1);
   p.A = A; p.lda = lda; p.B = B; p.ldb = ldb; p.M = M; p.N = N; p.K = K; p.C = C; p.ldc = ldc;

@@ -10,13 +10,20 @@ namespace hsd {
 // E2_BIAS_GELU_D: C = gelu'(y), C2 = gelu(y) (y = acc + bias) — the FFN1 forward keeps the GELU DERIVATIVE
 // for backward, so the FFN2 dgrad epilogue is a plain product (E2_MUL: C = bf16(acc) * aux) instead of
 // re-evaluating erf/exp per element.
+// E2_STORE_RDOT: C = bf16(acc), plus the attention backward's delta rows rd[(b·heads + h)·S + s] = Σ_{64 columns of head h}
+// C·aux over row m = b·S + s (aux = the attention output O, heads = N / 64): the out-projection dgrad writes dO AND the
+// row dots the streaming attention backward would otherwise recompute in a separate pass (re-reading dO and O)
 enum Epi2 : int { E2_STORE = 0, E2_BIAS = 1, E2_BIAS_GELU = 2, E2_BIAS_DROP_RES = 3, E2_RES = 4, E2_DGELU = 5,
-                  E2_F32_ATOMIC = 6, E2_F32_SLAB = 7, E2_BIAS_GELU_D = 8, E2_MUL = 9 };
+                  E2_F32_ATOMIC = 6, E2_F32_SLAB = 7, E2_BIAS_GELU_D = 8, E2_MUL = 9, E2_STORE_RDOT = 10 };
 
 __host__ __device__ constexpr bool epi_bias(int e) { return e == E2_BIAS || e == E2_BIAS_GELU || e == E2_BIAS_DROP_RES || e == E2_BIAS_GELU_D; }
-__host__ __device__ constexpr bool epi_aux(int e) { return e == E2_BIAS_DROP_RES || e == E2_RES || e == E2_DGELU || e == E2_MUL; }
+__host__ __device__ constexpr bool epi_aux(int e) {
+  return e == E2_BIAS_DROP_RES || e == E2_RES || e == E2_DGELU || e == E2_MUL || e == E2_STORE_RDOT;
+}
 __host__ __device__ constexpr bool epi_two_out(int e) { return e == E2_BIAS_GELU || e == E2_BIAS_GELU_D; }
-__host__ __device__ constexpr bool epi_bf16_out(int e) { return e <= E2_DGELU || e == E2_BIAS_GELU_D || e == E2_MUL; }
+__host__ __device__ constexpr bool epi_bf16_out(int e) {
+  return e <= E2_DGELU || e == E2_BIAS_GELU_D || e == E2_MUL || e == E2_STORE_RDOT;
+}
 
 struct G2Params {
   const bf16_t* A;
@@ -48,7 +55,21 @@ struct G2Params {
   int* tq;
   // E2_F32_SLAB with one K-split: C[m][n] += acc in place (ldc; each element has one owner) instead of a slab
   int accum_direct;
+  // E2_STORE_RDOT: fp32 [M / rd_seq · N / 64][rd_seq] row dots (rd_seq = the attention's sequence length)
+  float* rd;
+  int rd_seq;
 };
+
+// E2_STORE_RDOT: the 8 lanes holding the 8 chunks (64 columns = one head) of row m reduce their chunk dots; the first
+// writes the head's delta. Called by every lane of the group (DPP), `store` false for rows past M.
+__device__ __forceinline__ void rdot_group(const u32x4& o, const u32x4& x, int m, int n, const G2Params& p, bool lead,
+                                           bool store) {
+  const float d = sum8_dpp(dot8_bf16(o, x));
+  if (lead && store) {
+    const int b = m / p.rd_seq, s = m - b * p.rd_seq;
+    p.rd[((int64_t)b * (p.N >> 6) + (n >> 6)) * p.rd_seq + s] = d;
+  }
+}
 
 // ---- dynamic tile queue of the persistent NT GEMMs (gemm2pk / gemm8pk) ----------------------------------------------
 // A persistent workgroup that starts late (its CU held by a co-running RCCL kernel or optimizer slice) must not own a
@@ -368,6 +389,10 @@ __device__ __forceinline__ void epilogue_bf16(f32x4 (&acc)[MB][BN / 64], const G
       if (kDrop && drop_on) {
         xw = kColFixed ? (uint32_t)__builtin_amdgcn_ds_bpermute(4 * row, (int)rw_lane) ^ cw
                        : drop_row((uint32_t)m, p.dp.key) ^ epi_col_word<EPI>(n, p);
+      }
+      if constexpr (EPI == E2_STORE_RDOT) {
+        static_assert(CPR == 8, "row dots: 8 chunks (one 64-column head) per row");
+        rdot_group(sv[it], xv[it], m, n, p, c8 == 0, m < p.M);
       }
       if (m >= p.M) continue;
       const int64_t co = (int64_t)m * p.ldc + n;

@@ -86,7 +86,7 @@ void launch_attnS_bwd_q8(const bf16_t* qkv, const float* mask, const bf16_t* o, 
 // dbias (optional): fp32 [3H] += column sums of dqkv (the fused QKV bias gradient)
 void launch_attn_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
                      bf16_t* dqkv, float* dq_acc, float* dbias, int B, int S, int heads, double p, uint64_t seed,
-                     hipStream_t st, const uint32_t* kmask = nullptr);
+                     hipStream_t st, const uint32_t* kmask = nullptr, bool delta_ready = false);
 }  // namespace hsd
 
 namespace hsd {
@@ -153,7 +153,8 @@ void attn128_set_diag(void* p);  // diagnostic phase stamps of the S=128 attenti
 void gemm2_set_diag(void* p);  // diagnostic timestamps of the persistent NT kernel ([grid][64][4] u64), nullptr = off
 void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, int M, int N,
                   int K, void* C, int64_t ldc, const bf16_t* bias, const bf16_t* aux, int64_t ldaux, bf16_t* C2,
-                  double p_drop, uint64_t seed, int splits, float* ws, float* dbias, hipStream_t st);
+                  double p_drop, uint64_t seed, int splits, float* ws, float* dbias, hipStream_t st,
+                  float* rd = nullptr, int rd_seq = 0);
 bool gemm2_supported(int la, int lb, int epi, int M, int N, int K);
 int gemm2_wgrad_splits(int M, int N, int K);
 // fp8 TT weight gradient (gemm2.hip gemm8tt_kernel + slab_reduce): C[M][N] (fp32) += sdy·sx · dY8ᵀ · X8

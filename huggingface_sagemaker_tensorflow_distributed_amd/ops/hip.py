@@ -557,7 +557,9 @@ def attention(qkv, mask_bias, batch, seq, heads, p, seed):
 
 # ------------------------------------------------------------------------------------------ GEMM helpers
 EPI_STORE, EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_DROP_RES, EPI_RES, EPI_DGELU, EPI_F32_ATOMIC = range(7)
-EPI_F32_SLAB, EPI_BIAS_GELU_D, EPI_MUL = 7, 8, 9  # gemm2 only
+EPI_F32_SLAB, EPI_BIAS_GELU_D, EPI_MUL, EPI_STORE_RDOT = 7, 8, 9, 10  # gemm2 only
+# HSD_ATTN_DELTA_EPI=0: the streaming attention backward computes its delta rows in its own pass (A/B)
+_DELTA_EPI = _os.environ.get("HSD_ATTN_DELTA_EPI", "1") != "0"
 
 # split-K factors for the wgrad GEMM (fp32 atomic epilogue), measured with tools/bench_gemm.py at
 # T = 32768 tokens; key = (out_features, in_features)
@@ -734,6 +736,27 @@ def gemm_fwd(x, w, epi, bias=None, aux=None, out2=None, p=0.0, seed=0, xq=None, 
     return y
 
 
+def gemm_dgrad_rd(dy, w, o, rd, seq):
+    """The out-projection dgrad dx = dy · w (the attention backward's dO) whose epilogue also writes the streaming
+    attention backward's delta rows rd[(b·heads + h)·S + s] = Σ_head dx·o (E2_STORE_RDOT; gemm_common.h), so the
+    backward skips its own delta pass (re-reading dO and O, one more launch). Returns ``(dx, True)``, or
+    ``(gemm_dgrad(dy, w), False)`` when no bf16 gemm2 path takes the shape (fp8 weights, N % 256)."""
+    M, N, K = dy.shape[0], w.shape[1], dy.shape[1]
+    if _DELTA_EPI and _fp8_w(w, "_hsd_qt") is None and o.is_contiguous() and o.shape == (M, N):
+        wt = getattr(w, "_hsd_wt", None)
+        if wt is not None and (wt.shape[0] != N or wt.shape[1] != K):
+            wt = None
+        if wt is None and w.is_contiguous() and _C.gemm2_supported(0, 1, EPI_STORE_RDOT, M, N, K):
+            dx = torch.empty((M, N), dtype=dy.dtype, device=dy.device)
+            _C.gemm2(dy, w, dx, 0, 1, EPI_STORE_RDOT, None, o, None, 0.0, 0, 0, None, None, rd, seq)
+            return dx, True
+        if wt is not None and _C.gemm2_supported(0, 0, EPI_STORE_RDOT, M, N, K):
+            dx = torch.empty((M, N), dtype=dy.dtype, device=dy.device)
+            _C.gemm2(dy, wt, dx, 0, 0, EPI_STORE_RDOT, None, o, None, 0.0, 0, 0, None, None, rd, seq)
+            return dx, True
+    return gemm_dgrad(dy, w), False
+
+
 def gemm_dgrad(dy, w, epi=EPI_STORE, aux=None, dbias=None, dyq=None, q8_for=None):
     """dx[T, K] = dy[T, N] · w[N, K]  (NT kernel on the transposed weight wᵀ [K, N]).
 
@@ -900,9 +923,14 @@ class _AttnBlock(torch.autograd.Function):
         hq, actq = ctx.q8 or (None, None)
         ctx.q8 = None
         r_ow = wgrad_done(g_ow, dy, actx, dyq, actq)
-        dctx = gemm_dgrad(dy, out_w, dyq=dyq)
-        dqkv = torch.empty_like(qkv)
         dq_acc = _attn_ws(B, S, heads, actx.device)
+        delta_ready = False
+        if dyq is None and dq_acc is not None and dq_acc.numel() == B * heads * S:
+            # streaming attention backward: its delta rows come out of this dgrad's epilogue
+            dctx, delta_ready = gemm_dgrad_rd(dy, out_w, actx, dq_acc, S)
+        else:
+            dctx = gemm_dgrad(dy, out_w, dyq=dyq)
+        dqkv = torch.empty_like(qkv)
         g_qw, g_qb = _Grad(qkv_w), _Grad(qkv_b)
         # the QKV bias gradient (column sums of dqkv) comes out of the attention backward itself
         st = _site_ready(qkv_w, "_hsd_fp8_g", "_hsd_qt") if ctx.needs_input_grad[0] else None
@@ -917,7 +945,7 @@ class _AttnBlock(torch.autograd.Function):
             dqq = (q, sinv)
         else:
             _C.attn_bwd(qkv, mb if has_mask else None, actx, dctx, lse, dqkv, dq_acc, B, S, heads, p_a, _s64(seed_a),
-                        g_qb.buf, km if ctx.has_km else None)
+                        g_qb.buf, km if ctx.has_km else None, delta_ready)
         r_qb = g_qb.done()
         r_qw = wgrad_done(g_qw, dqkv, h2d, dqq, hq)
         dh = gemm_dgrad(dqkv, qkv_w, EPI_RES, aux=dz, dyq=dqq) if ctx.needs_input_grad[0] else None

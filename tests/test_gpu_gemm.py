@@ -475,3 +475,50 @@ def test_gemm2_persistent_matches_one_shot(gpu, monkeypatch, M, N, K, epi):
         torch.testing.assert_close(d1, d0, rtol=1e-4, atol=1e-4 * float(d0.abs().max()) + 1e-6)
     if epi == 0:
         _check(c1, A.float() @ B.float().t(), acc=_absmm(A, B, 0, 0))
+
+
+@pytest.mark.parametrize("path", ["pk", "oneshot", "small", "splitk"])
+@pytest.mark.parametrize("lb", [0, 1])
+@pytest.mark.parametrize("B_,S,heads,K", [(16, 512, 12, 768), (2, 512, 16, 1024), (3, 384, 16, 4096)])
+def test_gemm2_row_dot_epilogue_feeds_attention_backward(gpu, monkeypatch, path, lb, B_, S, heads, K):
+    """E2_STORE_RDOT (the out-projection dgrad also writing the streaming attention backward's delta rows): dx is
+    bit-identical to the plain store epilogue on every kernel path (persistent, one-shot, 128-tile, split-K), the rows
+    are bit-identical to the attention's own delta pass (one shared dot8_bf16 + sum8_dpp), and the backward fed those
+    rows (delta_ready) gives the same dqkv bits as the one that computes them itself."""
+    if path == "pk" and lb == 1:
+        pytest.skip("the persistent kernel reads a stored Wᵀ (lb = 0) only")
+    torch.manual_seed(11 + K)
+    C_ = _C()
+    monkeypatch.setenv("HSD_G2_PERSIST", "1" if path == "pk" else "0")
+    monkeypatch.setenv("HSD_G2_SMALL", "1" if path == "small" else "0")
+    monkeypatch.setenv("HSD_G2_SPLITK", "3" if path == "splitk" else "1")
+    H = heads * 64
+    T = B_ * S
+    dy = _mk((T, K), gpu)
+    W = _mk((K, H), gpu, 0.05)            # B[K][N] (lb = 1)
+    Bop = W if lb == 1 else W.t().contiguous()  # Wᵀ [N][K] (lb = 0)
+    qkv = _mk((T, 3 * H), gpu)
+    o = torch.empty(T, H, device=gpu, dtype=torch.bfloat16)
+    lse = torch.empty(B_ * heads * S, device=gpu)
+    C_.attn_fwd(qkv, None, o, lse, B_, S, heads, 0.1, 99, None)
+    dx0 = torch.empty(T, H, device=gpu, dtype=torch.bfloat16)
+    C_.gemm2(dy, Bop, dx0, 0, lb, 0, None, None, None, 0.0, 0, 0, None, None)
+    dx1 = torch.empty_like(dx0)
+    rd = torch.full((B_ * heads * S,), float("nan"), device=gpu)
+    C_.gemm2(dy, Bop, dx1, 0, lb, 10, None, o, None, 0.0, 0, 0, None, None, rd, S)
+    torch.cuda.synchronize()
+    assert torch.equal(dx0, dx1)
+    ref = (dx0.float() * o.float()).view(B_, S, heads, 64).sum(-1).permute(0, 2, 1).reshape(-1)
+    torch.testing.assert_close(rd, ref, rtol=1e-5, atol=1e-5 * float(ref.abs().max()))
+    outs = []
+    for ready in (False, True):
+        ws = rd.clone() if ready else torch.empty_like(rd)
+        dqkv = torch.empty_like(qkv)
+        db = torch.zeros(3 * H, device=gpu)
+        C_.attn_bwd(qkv, None, o, dx0, lse, dqkv, ws, B_, S, heads, 0.1, 99, db, None, ready)
+        torch.cuda.synchronize()
+        outs.append((ws, dqkv, db))
+    (ws0, dq0, db0), (ws1, dq1, db1) = outs
+    assert torch.equal(ws0, rd)  # the attention's own delta pass wrote the same bits
+    assert torch.equal(dq0, dq1)
+    torch.testing.assert_close(db1, db0, rtol=1e-5, atol=1e-5 * float(db0.abs().max()) + 1e-6)
