@@ -296,7 +296,7 @@ static void check_q8(const torch::Tensor& q8, int64_t numel, const torch::Tensor
 
 void attn_fwd_q8(torch::Tensor qkv, c10::optional<torch::Tensor> mask, torch::Tensor out, torch::Tensor lse2, int64_t B,
                  int64_t S, int64_t heads, double p, int64_t seed, torch::Tensor q8, torch::Tensor amax_in,
-                 torch::Tensor sinv, torch::Tensor amax_track) {
+                 torch::Tensor sinv, torch::Tensor amax_track, c10::optional<torch::Tensor> kmask) {
   check_bf16(qkv, "qkv"); check_bf16(out, "out"); check_f32(lse2, "lse2");
   TORCH_CHECK(S > 128 && hsd::attn_streaming((int)S), "attn_fwd_q8: streaming attention (S > 128) only");
   TORCH_CHECK(qkv.size(-1) == 3 * heads * 64, "attention requires head_dim 64");
@@ -306,13 +306,14 @@ void attn_fwd_q8(torch::Tensor qkv, c10::optional<torch::Tensor> mask, torch::Te
   check_q8(q8, out.numel(), amax_in, sinv, amax_track);
   hsd::launch_attnS_fwd_q8(CBF(qkv), OPT_F(mask), BF(out), lse2.data_ptr<float>(), (int)B, (int)S, (int)heads, p,
                            (uint64_t)seed, q8.data_ptr<uint8_t>(), amax_in.data_ptr<float>(), sinv.data_ptr<float>(),
-                           amax_track.data_ptr<float>(), cur_stream());
+                           amax_track.data_ptr<float>(), cur_stream(), keep_mask_ptr(kmask, B, S, heads));
 }
 
 void attn_bwd_q8(torch::Tensor qkv, c10::optional<torch::Tensor> mask, torch::Tensor o, torch::Tensor dout,
                  torch::Tensor lse2, torch::Tensor dqkv, torch::Tensor ws, int64_t B, int64_t S, int64_t heads, double p,
                  int64_t seed, c10::optional<torch::Tensor> dbias, torch::Tensor q8, torch::Tensor amax_in,
-                 torch::Tensor sinv, torch::Tensor amax_track, int64_t qfmt) {
+                 torch::Tensor sinv, torch::Tensor amax_track, int64_t qfmt, c10::optional<torch::Tensor> kmask,
+                 bool delta_ready) {
   check_bf16(qkv, "qkv"); check_bf16(o, "o"); check_bf16(dout, "dout"); check_bf16(dqkv, "dqkv");
   check_f32(lse2, "lse2"); check_f32(ws, "ws");
   TORCH_CHECK(S > 128 && hsd::attn_streaming((int)S), "attn_bwd_q8: streaming attention (S > 128) only");
@@ -326,7 +327,8 @@ void attn_bwd_q8(torch::Tensor qkv, c10::optional<torch::Tensor> mask, torch::Te
   hsd::launch_attnS_bwd_q8(CBF(qkv), OPT_F(mask), CBF(o), CBF(dout), lse2.data_ptr<float>(), BF(dqkv),
                            ws.data_ptr<float>(), OPT_F(dbias), (int)B, (int)S, (int)heads, p, (uint64_t)seed,
                            q8.data_ptr<uint8_t>(), amax_in.data_ptr<float>(), sinv.data_ptr<float>(),
-                           amax_track.data_ptr<float>(), (int)qfmt, cur_stream());
+                           amax_track.data_ptr<float>(), (int)qfmt, cur_stream(), keep_mask_ptr(kmask, B, S, heads),
+                           delta_ready);
 }
 
 // C[M,N] (+)= A·B with fused epilogue. la=0: A [M,K]; la=1: A [K,M]. lb=0: B [N,K]; lb=1: B [K,N].
@@ -406,7 +408,7 @@ void gemm8(torch::Tensor A, int64_t fa, torch::Tensor sa, torch::Tensor B, int64
            torch::Tensor C, int64_t epi, c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> aux,
            c10::optional<torch::Tensor> C2, double p, int64_t seed, c10::optional<torch::Tensor> dbias,
            c10::optional<torch::Tensor> q8, c10::optional<torch::Tensor> q8_amax, c10::optional<torch::Tensor> q8_sinv,
-           c10::optional<torch::Tensor> q8_track, int64_t q8fmt) {
+           c10::optional<torch::Tensor> q8_track, int64_t q8fmt, c10::optional<torch::Tensor> rd, int64_t rd_seq) {
   uint8_t* q8p = nullptr;
   float *q8s = nullptr, *q8t = nullptr;
   const float* q8a = nullptr;
@@ -434,7 +436,7 @@ void gemm8(torch::Tensor A, int64_t fa, torch::Tensor sa, torch::Tensor B, int64
     TORCH_CHECK(bias.has_value() && bias->numel() == N && bias->scalar_type() == torch::kBFloat16 &&
                 bias->is_contiguous(), "gemm8 bias");
   }
-  if (epi == 3 || epi == 4 || epi == 5 || epi == 9) {
+  if (epi == 3 || epi == 4 || epi == 5 || epi == 9 || epi == 10) {
     TORCH_CHECK(aux.has_value() && aux->dim() == 2 && aux->size(0) == M && aux->size(1) == N &&
                 aux->stride(1) == 1 && aux->stride(0) % 8 == 0 && aux->scalar_type() == torch::kBFloat16, "gemm8 aux");
   }
@@ -449,11 +451,18 @@ void gemm8(torch::Tensor A, int64_t fa, torch::Tensor sa, torch::Tensor B, int64
     TORCH_CHECK(dbias->numel() == N, "dbias size");
     dbp = dbias->data_ptr<float>();
   }
+  float* rdp = nullptr;
+  if (epi == 10) {
+    TORCH_CHECK(rd.has_value() && rd_seq > 0 && M % rd_seq == 0, "gemm8 row dots: rd and the sequence length");
+    check_f32(*rd, "rd");
+    TORCH_CHECK(rd->numel() == M * (N / 64), "gemm8 row dots: rd size");
+    rdp = rd->data_ptr<float>();
+  }
   hsd::launch_gemm8((int)epi, A.data_ptr<uint8_t>(), A.stride(0), (int)fa, sa.data_ptr<float>(), B.data_ptr<uint8_t>(),
                     B.stride(0), (int)fb, sb.data_ptr<float>(), (int)M, (int)N, (int)K, BF(C), C.stride(0),
                     bias.has_value() ? CBF(*bias) : nullptr, aux.has_value() ? CBF(*aux) : nullptr,
                     aux.has_value() ? aux->stride(0) : 0, C2.has_value() ? BF(*C2) : nullptr, p, (uint64_t)seed, dbp,
-                    cur_stream(), q8p, q8a, q8s, q8t, (int)q8fmt);
+                    cur_stream(), q8p, q8a, q8s, q8t, (int)q8fmt, rdp, (int)rd_seq);
 }
 
 // C[M][N] fp32 += sdy·sx · dY8ᵀ · X8 (fp8 TT weight gradient): dY8 uint8 [T][M] (format fdy), X8 uint8 [T][N] (e4m3),
@@ -879,8 +888,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("stream_wait", &stream_wait);
   m.def("gemm2_on", &gemm2_on);
   m.def("ln_bwd_q8", &ln_bwd_q8);
-  m.def("attn_fwd_q8", &attn_fwd_q8);
-  m.def("attn_bwd_q8", &attn_bwd_q8);
+  m.def("attn_fwd_q8", &attn_fwd_q8, py::arg("qkv"), py::arg("mask"), py::arg("out"), py::arg("lse2"), py::arg("B"),
+        py::arg("S"), py::arg("heads"), py::arg("p"), py::arg("seed"), py::arg("q8"), py::arg("amax_in"),
+        py::arg("sinv"), py::arg("amax_track"), py::arg("kmask") = py::none());
+  m.def("attn_bwd_q8", &attn_bwd_q8, py::arg("qkv"), py::arg("mask"), py::arg("o"), py::arg("dout"), py::arg("lse2"),
+        py::arg("dqkv"), py::arg("ws"), py::arg("B"), py::arg("S"), py::arg("heads"), py::arg("p"), py::arg("seed"),
+        py::arg("dbias"), py::arg("q8"), py::arg("amax_in"), py::arg("sinv"), py::arg("amax_track"), py::arg("qfmt"),
+        py::arg("kmask") = py::none(), py::arg("delta_ready") = false);
   m.def("attn_q8_supported", [](int64_t S) { return S > 128 && hsd::attn_streaming((int)S); });
   m.def("ln_fwd", &ln_fwd);
   m.def("ln_bwd", &ln_bwd);
@@ -926,7 +940,8 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("C"), py::arg("epi"), py::arg("bias") = py::none(), py::arg("aux") = py::none(),
         py::arg("C2") = py::none(), py::arg("p") = 0.0, py::arg("seed") = 0, py::arg("dbias") = py::none(),
         py::arg("q8") = py::none(), py::arg("q8_amax") = py::none(),
-        py::arg("q8_sinv") = py::none(), py::arg("q8_track") = py::none(), py::arg("q8fmt") = 0);
+        py::arg("q8_sinv") = py::none(), py::arg("q8_track") = py::none(), py::arg("q8fmt") = 0,
+        py::arg("rd") = py::none(), py::arg("rd_seq") = 0);
   m.def("gemm8_supported", &hsd::gemm8_supported);
   m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("mask"), py::arg("out"), py::arg("lse2"), py::arg("B"),
         py::arg("S"), py::arg("heads"), py::arg("p"), py::arg("seed"), py::arg("kmask") = py::none());

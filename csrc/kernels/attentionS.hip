@@ -622,15 +622,16 @@ void launch_attnS_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, con
 // GEMM's A operand), the backward dqkv's copy in format qfmt (the QKV dgrad's A operand); delayed-scaling sites
 void launch_attnS_fwd_q8(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse2, int B, int S, int heads,
                          double p, uint64_t seed, uint8_t* q8, const float* amax_in, float* sinv, float* amax_track,
-                         hipStream_t st) {
-  launch_attnS_fwd(qkv, mask, out, lse2, B, S, heads, p, seed, st, Q8Out{q8, amax_in, sinv, amax_track}, nullptr);
+                         hipStream_t st, uint32_t* kmask) {
+  launch_attnS_fwd(qkv, mask, out, lse2, B, S, heads, p, seed, st, Q8Out{q8, amax_in, sinv, amax_track}, kmask);
 }
 
 void launch_attnS_bwd_q8(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
                          bf16_t* dqkv, float* delta_ws, float* dbias, int B, int S, int heads, double p, uint64_t seed,
-                         uint8_t* q8, const float* amax_in, float* sinv, float* amax_track, int qfmt, hipStream_t st) {
+                         uint8_t* q8, const float* amax_in, float* sinv, float* amax_track, int qfmt, hipStream_t st,
+                         const uint32_t* kmask, bool delta_ready) {
   launch_attnS_bwd(qkv, mask, o, dout, lse2, dqkv, delta_ws, dbias, B, S, heads, p, seed, st,
-                   Q8Out{q8, amax_in, sinv, amax_track}, qfmt, nullptr, false);
+                   Q8Out{q8, amax_in, sinv, amax_track}, qfmt, kmask, delta_ready);
 }
 
 }  // namespace hsd

@@ -1360,6 +1360,10 @@ void launch_gemm8pk(int epi, int bn, const G2Params& p0, int fa, const float* sa
     G8PK(E2_DGELU)
     G8PK(E2_BIAS_GELU_D)
     G8PK(E2_MUL)
+    case E2_STORE_RDOT:  // 64-column wave tiles (one head per 8-lane group): BN 256
+      if (fa == 0) g8pk_launch<E2_STORE_RDOT, 256, 0>(p, sa, sb, st);
+      else g8pk_launch<E2_STORE_RDOT, 256, 1>(p, sa, sb, st);
+      return;
     default: abort();
   }
 #undef G8PK

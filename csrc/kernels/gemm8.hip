@@ -156,6 +156,7 @@ int gemm2_pick_bn(int M, int N);
 void launch_gemm8pk(int epi, int bn, const G2Params& p, int fa, const float* sa, const float* sb, hipStream_t st);
 
 bool gemm8_supported(int epi, int M, int N, int K) {
+  if (epi == E2_STORE_RDOT && N % 256) return false;  // 256-wide tiles: one 64-column head per 8-lane group
   return K % g8::BK == 0 && M >= 1 && N % 8 == 0 && epi_bf16_out(epi) && gemm2_pick_bn(M, N) != 0;
 }
 
@@ -174,9 +175,13 @@ static void g8_launch(const G2Params& p0, const float* sa, const float* sb, hipS
 void launch_gemm8(int epi, const uint8_t* A, int64_t lda, int fa, const float* sa, const uint8_t* B, int64_t ldb,
                   int fb, const float* sb, int M, int N, int K, bf16_t* C, int64_t ldc, const bf16_t* bias,
                   const bf16_t* aux, int64_t ldaux, bf16_t* C2, double p_drop, uint64_t seed, float* dbias,
-                  hipStream_t st, uint8_t* q8, const float* q8_amax, float* q8_sinv, float* q8_track, int q8_fmt) {
+                  hipStream_t st, uint8_t* q8, const float* q8_amax, float* q8_sinv, float* q8_track, int q8_fmt,
+                  float* rd, int rd_seq) {
   if (!gemm8_supported(epi, M, N, K)) abort();
   G2Params p{};
+  p.rd = rd;
+  p.rd_seq = rd_seq;
+  if (epi == E2_STORE_RDOT && (rd == nullptr || rd_seq <= 0 || M % rd_seq || lda % 2 || ldb % 2)) abort();
   p.q8 = q8; p.q8_amax = q8_amax; p.q8_sinv = q8_sinv; p.q8_track = q8_track; p.q8_fmt = q8_fmt;
   p.A = reinterpret_cast<const bf16_t*>(A); p.lda = lda;
   p.B = reinterpret_cast<const bf16_t*>(B); p.ldb = ldb;
@@ -184,7 +189,7 @@ void launch_gemm8(int epi, const uint8_t* A, int64_t lda, int fa, const float* s
   p.bias = bias; p.aux = aux; p.ldaux = ldaux; p.C2 = C2;
   p.dp = make_dropout(p_drop, seed);
   p.dbias = dbias;
-  int bn = gemm2_pick_bn(M, N);
+  int bn = epi == E2_STORE_RDOT ? 256 : gemm2_pick_bn(M, N);
   if (dbias != nullptr) {
     if ((epi != E2_DGELU && epi != E2_MUL) || N % 256) abort();
     bn = 256;
@@ -194,7 +199,7 @@ void launch_gemm8(int epi, const uint8_t* A, int64_t lda, int fa, const float* s
   // default: the persistent staggered-schedule kernel (gemm2.hip gemm8pk_kernel); HSD_G8_LEGACY=1: this file's
   // one-barrier-per-K-tile kernel (A/B reference)
   {
-    if (!HSD_KNOB("HSD_G8_LEGACY", 0) && lda % 2 == 0 && ldb % 2 == 0) {
+    if ((!HSD_KNOB("HSD_G8_LEGACY", 0) || epi == E2_STORE_RDOT) && lda % 2 == 0 && ldb % 2 == 0) {
       launch_gemm8pk(epi, bn, p, fa, sa, sb, st);
       return;
     }

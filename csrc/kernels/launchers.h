@@ -79,10 +79,11 @@ void launch_attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* l
 // attentionS.hip fp8 variants (S > 128 streaming kernels only: attn_streaming(S) && S > 128)
 void launch_attnS_fwd_q8(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse2, int B, int S, int heads,
                          double p, uint64_t seed, uint8_t* q8, const float* amax_in, float* sinv, float* amax_track,
-                         hipStream_t st);
+                         hipStream_t st, uint32_t* kmask = nullptr);
 void launch_attnS_bwd_q8(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
                          bf16_t* dqkv, float* delta_ws, float* dbias, int B, int S, int heads, double p, uint64_t seed,
-                         uint8_t* q8, const float* amax_in, float* sinv, float* amax_track, int qfmt, hipStream_t st);
+                         uint8_t* q8, const float* amax_in, float* sinv, float* amax_track, int qfmt, hipStream_t st,
+                         const uint32_t* kmask = nullptr, bool delta_ready = false);
 // dbias (optional): fp32 [3H] += column sums of dqkv (the fused QKV bias gradient)
 void launch_attn_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
                      bf16_t* dqkv, float* dq_acc, float* dbias, int B, int S, int heads, double p, uint64_t seed,
@@ -143,7 +144,7 @@ void launch_gemm8(int epi, const uint8_t* A, int64_t lda, int fa, const float* s
                   int fb, const float* sb, int M, int N, int K, bf16_t* C, int64_t ldc, const bf16_t* bias,
                   const bf16_t* aux, int64_t ldaux, bf16_t* C2, double p_drop, uint64_t seed, float* dbias,
                   hipStream_t st, uint8_t* q8 = nullptr, const float* q8_amax = nullptr, float* q8_sinv = nullptr,
-                  float* q8_track = nullptr, int q8_fmt = 0);
+                  float* q8_track = nullptr, int q8_fmt = 0, float* rd = nullptr, int rd_seq = 0);
 void launch_fp8_quant(const bf16_t* x, int64_t n, float* amax, uint8_t* q, float* sinv, int fmt, bool compute_amax,
                       float* amax_track, hipStream_t st);
 void launch_fp8_quant_many(const int64_t* amax_desc, int n_amax, int amax_blocks, const int64_t* quant_desc,

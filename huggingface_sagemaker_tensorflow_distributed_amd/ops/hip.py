@@ -736,13 +736,23 @@ def gemm_fwd(x, w, epi, bias=None, aux=None, out2=None, p=0.0, seed=0, xq=None, 
     return y
 
 
-def gemm_dgrad_rd(dy, w, o, rd, seq):
+def gemm_dgrad_rd(dy, w, o, rd, seq, dyq=None):
     """The out-projection dgrad dx = dy · w (the attention backward's dO) whose epilogue also writes the streaming
     attention backward's delta rows rd[(b·heads + h)·S + s] = Σ_head dx·o (E2_STORE_RDOT; gemm_common.h), so the
-    backward skips its own delta pass (re-reading dO and O, one more launch). Returns ``(dx, True)``, or
-    ``(gemm_dgrad(dy, w), False)`` when no bf16 gemm2 path takes the shape (fp8 weights, N % 256)."""
+    backward skips its own delta pass (re-reading dO and O, one more launch). fp8 weights: the fp8 persistent kernel
+    (dy's fp8 copy ``dyq``, or quantised here like gemm_dgrad). Returns ``(dx, True)``, or
+    ``(gemm_dgrad(dy, w, dyq=dyq), False)`` when no kernel path takes the shape (N % 256)."""
     M, N, K = dy.shape[0], w.shape[1], dy.shape[1]
-    if _DELTA_EPI and _fp8_w(w, "_hsd_qt") is None and o.is_contiguous() and o.shape == (M, N):
+    wqt = _fp8_w(w, "_hsd_qt")
+    if _DELTA_EPI and wqt is not None and o.is_contiguous() and o.shape == (M, N) and \
+            _C.gemm8_supported(EPI_STORE_RDOT, M, N, K):
+        fmt = _FP8["grad_fmt"]
+        qdy, sdy = dyq if dyq is not None else quant_fp8(dy, fmt, getattr(w, "_hsd_fp8_g", None))
+        dx = torch.empty((M, N), dtype=dy.dtype, device=dy.device)
+        _C.gemm8(qdy, fmt, sdy, wqt, FP8_E4M3, w._hsd_qs, dx, EPI_STORE_RDOT, None, o, None, 0.0, 0, None, rd=rd,
+                 rd_seq=seq)
+        return dx, True
+    if _DELTA_EPI and wqt is None and o.is_contiguous() and o.shape == (M, N):
         wt = getattr(w, "_hsd_wt", None)
         if wt is not None and (wt.shape[0] != N or wt.shape[1] != K):
             wt = None
@@ -754,7 +764,7 @@ def gemm_dgrad_rd(dy, w, o, rd, seq):
             dx = torch.empty((M, N), dtype=dy.dtype, device=dy.device)
             _C.gemm2(dy, wt, dx, 0, 0, EPI_STORE_RDOT, None, o, None, 0.0, 0, 0, None, None, rd, seq)
             return dx, True
-    return gemm_dgrad(dy, w), False
+    return gemm_dgrad(dy, w, dyq=dyq), False
 
 
 def gemm_dgrad(dy, w, epi=EPI_STORE, aux=None, dbias=None, dyq=None, q8_for=None):
@@ -891,9 +901,9 @@ class _AttnBlock(torch.autograd.Function):
             # the attention kernel writes the context's fp8 copy for the fp8 out-projection (no quant pass)
             q = torch.empty((h2d.shape[0], H), dtype=torch.uint8, device=h.device)
             sinv = torch.empty(1, dtype=torch.float32, device=h.device)
-            _C.attn_fwd_q8(qkv, mb, actx, lse, B, S, heads, float(p_a), _s64(seed_a), q, st[0:1], sinv, st[1:2])
+            km = _keep_mask(B, S, heads, p_a, h.device)
+            _C.attn_fwd_q8(qkv, mb, actx, lse, B, S, heads, float(p_a), _s64(seed_a), q, st[0:1], sinv, st[1:2], km)
             xq = (q, sinv)
-            km = None
         else:
             km = _keep_mask(B, S, heads, p_a, h.device)
             _C.attn_fwd(qkv, mb, actx, lse, B, S, heads, float(p_a), _s64(seed_a), km)
@@ -925,9 +935,9 @@ class _AttnBlock(torch.autograd.Function):
         r_ow = wgrad_done(g_ow, dy, actx, dyq, actq)
         dq_acc = _attn_ws(B, S, heads, actx.device)
         delta_ready = False
-        if dyq is None and dq_acc is not None and dq_acc.numel() == B * heads * S:
+        if dq_acc is not None and dq_acc.numel() == B * heads * S:
             # streaming attention backward: its delta rows come out of this dgrad's epilogue
-            dctx, delta_ready = gemm_dgrad_rd(dy, out_w, actx, dq_acc, S)
+            dctx, delta_ready = gemm_dgrad_rd(dy, out_w, actx, dq_acc, S, dyq=dyq)
         else:
             dctx = gemm_dgrad(dy, out_w, dyq=dyq)
         dqkv = torch.empty_like(qkv)
@@ -941,7 +951,8 @@ class _AttnBlock(torch.autograd.Function):
             q = torch.empty(dqkv.shape, dtype=torch.uint8, device=dqkv.device)
             sinv = torch.empty(1, dtype=torch.float32, device=dqkv.device)
             _C.attn_bwd_q8(qkv, mb if has_mask else None, actx, dctx, lse, dqkv, dq_acc, B, S, heads, p_a,
-                           _s64(seed_a), g_qb.buf, q, st[0:1], sinv, st[1:2], _FP8["grad_fmt"])
+                           _s64(seed_a), g_qb.buf, q, st[0:1], sinv, st[1:2], _FP8["grad_fmt"],
+                           km if ctx.has_km else None, delta_ready)
             dqq = (q, sinv)
         else:
             _C.attn_bwd(qkv, mb if has_mask else None, actx, dctx, lse, dqkv, dq_acc, B, S, heads, p_a, _s64(seed_a),

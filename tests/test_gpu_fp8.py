@@ -352,10 +352,11 @@ def test_fp8_fused_ln_quant_in_the_step(gpu):
     assert cos > 0.999, float(cos)
 
 
-@pytest.mark.parametrize("S,p,fmt", [(512, 0.1, 0), (256, 0.0, 1)])
-def test_attention_q8_equals_attention_then_quant(gpu, S, p, fmt):
+@pytest.mark.parametrize("S,p,fmt,use_km", [(512, 0.1, 0, False), (256, 0.0, 1, False), (512, 0.1, 0, True),
+                                            (384, 0.1, 1, True)])
+def test_attention_q8_equals_attention_then_quant(gpu, S, p, fmt, use_km):
     """Streaming attention writing the fp8 copy of its output (forward) / of dqkv (backward) == the bf16 kernels,
-    then the standalone quantiser with the same delayed-scaling site."""
+    then the standalone quantiser with the same delayed-scaling site (use_km: both with the forward's keep bits)."""
     hip = _hip()
     C = hip._C
     assert C.attn_q8_supported(S) and not C.attn_q8_supported(128)
@@ -367,14 +368,16 @@ def test_attention_q8_equals_attention_then_quant(gpu, S, p, fmt):
     mb[1, S - 37:] = -10000.0
     res = {}
     for fused in (False, True):
+        km = hip._keep_mask(B, S, heads, p, gpu) if use_km else None
+        assert (km is not None) == use_km
         out = torch.empty(B * S, H, device=gpu, dtype=torch.bfloat16)
         lse = torch.empty(B * heads * S, device=gpu)
         st = torch.tensor([2.0, 0.0], device=gpu)
         if fused:
             q, sinv = torch.empty(B * S, H, dtype=torch.uint8, device=gpu), torch.empty(1, device=gpu)
-            C.attn_fwd_q8(qkv, mb, out, lse, B, S, heads, p, 9, q, st[0:1], sinv, st[1:2])
+            C.attn_fwd_q8(qkv, mb, out, lse, B, S, heads, p, 9, q, st[0:1], sinv, st[1:2], km)
         else:
-            C.attn_fwd(qkv, mb, out, lse, B, S, heads, p, 9)
+            C.attn_fwd(qkv, mb, out, lse, B, S, heads, p, 9, km)
             st._hsd_cal = True
             q, sinv = hip.quant_fp8(out, 0, st)
         dout = torch.randn_like(out)
@@ -386,9 +389,10 @@ def test_attention_q8_equals_attention_then_quant(gpu, S, p, fmt):
         dout = torch.randn_like(out)
         if fused:
             gq, gs = torch.empty(B * S, 3 * H, dtype=torch.uint8, device=gpu), torch.empty(1, device=gpu)
-            C.attn_bwd_q8(qkv, mb, out, dout, lse, dqkv, ws, B, S, heads, p, 9, db, gq, gst[0:1], gs, gst[1:2], fmt)
+            C.attn_bwd_q8(qkv, mb, out, dout, lse, dqkv, ws, B, S, heads, p, 9, db, gq, gst[0:1], gs, gst[1:2], fmt,
+                          km)
         else:
-            C.attn_bwd(qkv, mb, out, dout, lse, dqkv, ws, B, S, heads, p, 9, db)
+            C.attn_bwd(qkv, mb, out, dout, lse, dqkv, ws, B, S, heads, p, 9, db, km)
             gst._hsd_cal = True
             gq, gs = hip.quant_fp8(dqkv, fmt, gst)
         torch.cuda.synchronize()
@@ -506,3 +510,42 @@ def test_fp8_wgrad_step_tracks_bf16_wgrad(gpu):
     assert cos > 0.995, float(cos)
     rel = float((g1 - g0).norm() / g0.norm())
     assert rel < 0.1, rel
+
+
+@pytest.mark.parametrize("B_,S,heads,K,fa", [(4, 512, 16, 1024, 0), (3, 384, 12, 768, 1)])
+def test_gemm8_row_dot_epilogue(gpu, B_, S, heads, K, fa):
+    """fp8 out-projection dgrad with the attention backward's delta rows (E2_STORE_RDOT on gemm8pk): dx bit-identical
+    to the plain store epilogue, the rows bit-identical to the streaming attention's own delta pass, and the fp8
+    attention backward fed them (delta_ready) bit-identical to the one that computes them."""
+    hip = _hip()
+    C = hip._C
+    torch.manual_seed(3 + K)
+    H = heads * 64
+    T = B_ * S
+    dy = torch.randn(T, K, device=gpu).bfloat16()
+    wt = (torch.randn(H, K, device=gpu) * 0.05).bfloat16()  # Wᵀ [N][K]
+    qdy, sdy = hip.quant_fp8(dy, fa)
+    qw, sw = hip.quant_fp8(wt, 0)
+    qkv = torch.randn(T, 3 * H, device=gpu).bfloat16()
+    o = torch.empty(T, H, device=gpu, dtype=torch.bfloat16)
+    lse = torch.empty(B_ * heads * S, device=gpu)
+    C.attn_fwd(qkv, None, o, lse, B_, S, heads, 0.1, 7)
+    dx0 = torch.empty(T, H, device=gpu, dtype=torch.bfloat16)
+    C.gemm8(qdy, fa, sdy, qw, 0, sw, dx0, 0)
+    dx1 = torch.empty_like(dx0)
+    rd = torch.full((B_ * heads * S,), float("nan"), device=gpu)
+    C.gemm8(qdy, fa, sdy, qw, 0, sw, dx1, 10, None, o, rd=rd, rd_seq=S)
+    torch.cuda.synchronize()
+    assert torch.equal(dx0, dx1)
+    outs = []
+    for ready in (False, True):
+        ws = rd.clone() if ready else torch.empty_like(rd)
+        dqkv = torch.empty_like(qkv)
+        gst = torch.tensor([3.0, 0.0], device=gpu)
+        gq, gs = torch.empty(T, 3 * H, dtype=torch.uint8, device=gpu), torch.empty(1, device=gpu)
+        C.attn_bwd_q8(qkv, None, o, dx0, lse, dqkv, ws, B_, S, heads, 0.1, 7, None, gq, gst[0:1], gs, gst[1:2], 0,
+                      None, ready)
+        torch.cuda.synchronize()
+        outs.append((ws, dqkv, gq))
+    assert torch.equal(outs[0][0], rd)
+    assert torch.equal(outs[0][1], outs[1][1]) and torch.equal(outs[0][2], outs[1][2])
