@@ -579,8 +579,13 @@ void gemm2_f32nt(torch::Tensor A, torch::Tensor B, torch::Tensor C, int64_t lb) 
   const int64_t N = lb == 0 ? B.size(0) : B.size(1), KB = lb == 0 ? B.size(1) : B.size(0);
   TORCH_CHECK(K == KB && C.size(0) == M && C.size(1) == N, "gemm2_f32nt shapes");
   TORCH_CHECK(hsd::gemm2_supported(0, (int)lb, 7, (int)M, (int)N, (int)K), "gemm2_f32nt: unsupported shape");
+  TORCH_CHECK(C.is_contiguous(), "gemm2_f32nt: contiguous C");
+  const int sp = hsd::gemm2_f32nt_splits((int)M, (int)N, (int)K);
+  torch::Tensor ws;
+  if (sp > 1) ws = torch::empty({(int64_t)sp * M * N}, C.options());  // K-split slabs (stream-ordered pool)
   hsd::launch_gemm2(0, (int)lb, 7, CBF(A), A.stride(0), CBF(B), B.stride(0), (int)M, (int)N, (int)K, C.data_ptr(),
-                    C.stride(0), nullptr, nullptr, 0, nullptr, 0.0, 0, 1, nullptr, nullptr, cur_stream());
+                    C.stride(0), nullptr, nullptr, 0, nullptr, 0.0, 0, sp, sp > 1 ? ws.data_ptr<float>() : nullptr,
+                    nullptr, cur_stream());
 }
 
 void split3(torch::Tensor x, torch::Tensor out, int64_t pat, bool rows) {

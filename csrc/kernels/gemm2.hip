@@ -976,9 +976,9 @@ __global__ __launch_bounds__(512, 1) void gemm8tt_kernel(G2Params p, const float
   }
 }
 
-// main_grad[i] += Σ_s ws[s][i]   (float4 lanes, grid-stride)
+// main_grad[i] += Σ_s ws[s][i]   (float4 lanes, grid-stride); assign: C = Σ_s ws[s] (the split-K fp32 NT output)
 __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restrict__ ws, float* __restrict__ C,
-                                                          int64_t ldc, int M, int N, int splits) {
+                                                          int64_t ldc, int M, int N, int splits, int assign) {
   const int64_t n4 = (int64_t)M * N / 4;
   const int64_t plane = (int64_t)M * N;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += (int64_t)gridDim.x * blockDim.x) {
@@ -987,7 +987,7 @@ __global__ __launch_bounds__(256) void slab_reduce_kernel(const float* __restric
     for (int k = 1; k < splits; ++k) s += *reinterpret_cast<const f32x4*>(ws + k * plane + e);
     const int64_t m = e / N, n = e % N;
     f32x4* c = reinterpret_cast<f32x4*>(C + m * ldc + n);
-    *c = *c + s;
+    *c = assign ? s : *c + s;
   }
 }
 
@@ -1522,6 +1522,18 @@ bool gemm2_supported(int la, int lb, int epi, int M, int N, int K) {
   return false;
 }
 
+// K-splits of the fp32-output NT GEMM (the fp32 step's split-product forward / dgrad): a 256 x 256 grid of at most
+// half the CUs (bert-large B = 8: M = 4,096 tokens, N = 1,024 -> 64 workgroups on 256 CUs) is split over K until it
+// fills the chip, keeping >= 8 K-tiles per split. HSD_F32NT_SPLITS: 1 = off, n = force n.
+int gemm2_f32nt_splits(int M, int N, int K) {
+  const int force = HSD_KNOB("HSD_F32NT_SPLITS", 0);
+  if (force > 0) return std::max(1, std::min(force, K / 64));
+  const int tiles = ((M + 255) / 256) * ((N + 255) / 256);
+  const int cus = g2_num_cus();
+  if (2 * tiles > cus) return 1;
+  return std::max(1, std::min(cus / tiles, K / (64 * 8)));
+}
+
 // K-splits of the TT wgrad (wgrad_plan)
 int gemm2_wgrad_splits(int M, int N, int K) {
   return wgrad_plan(M, N, K).splits;
@@ -1653,10 +1665,23 @@ void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const b
   p.bias = bias; p.aux = aux; p.ldaux = ldaux; p.C2 = C2;
   p.dp = make_dropout(p_drop, seed);
   if (la == 0 && epi == E2_F32_SLAB) {
-    // fp32 output [M][N] (ldc == N), one pass: the split-product GEMMs of the fp32 step (fp32.hip, ops/hip32.py)
-    if (ldc != N || splits > 1) abort();
-    if (lb == 0) g2_launch<0, 0, E2_F32_SLAB, 256>(p, 1, st);
-    else g2_launch<0, 1, E2_F32_SLAB, 256>(p, 1, st);
+    // fp32 output [M][N] (ldc == N): the split-product GEMMs of the fp32 step (fp32.hip, ops/hip32.py). splits > 1
+    // (gemm2_f32nt_splits: grids that would leave most CUs idle): K-split fp32 slabs in ws, then C = Σ slabs
+    if (ldc != N || (splits > 1 && ws == nullptr)) abort();
+    G2Params q = p;
+    if (splits > 1) q.C = ws;
+    if (lb == 0) g2_launch<0, 0, E2_F32_SLAB, 256>(q, splits, st);
+    else g2_launch<0, 1, E2_F32_SLAB, 256>(q, splits, st);
+    if (splits > 1) {
+      int kps = (K + splits - 1) / splits;
+      kps = (kps + 63) / 64 * 64;
+      const int real = (K + kps - 1) / kps;
+      const int64_t n4 = (int64_t)M * N / 4;
+      const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
+      hipLaunchKernelGGL(g2::slab_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, reinterpret_cast<float*>(C), ldc,
+                         M, N, real, 1);
+      HSD_CHECK_LAUNCH();
+    }
     return;
   }
   if (la == 0 && lb == 0) {
@@ -1677,7 +1702,7 @@ void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const b
         const int64_t n4 = (int64_t)M * N / 4;
         int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
         hipLaunchKernelGGL(g2::slab_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, reinterpret_cast<float*>(C),
-                           ldc, M, N, real);
+                           ldc, M, N, real, 0);
         HSD_CHECK_LAUNCH();
       }
     } else if (epi == E2_F32_SLAB && splits > 1 && ws != nullptr) {
@@ -1690,7 +1715,7 @@ void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const b
       const int64_t n4 = (int64_t)M * N / 4;
       int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
       hipLaunchKernelGGL(g2::slab_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, reinterpret_cast<float*>(C), ldc,
-                         M, N, real);
+                         M, N, real, 0);
       HSD_CHECK_LAUNCH();
     } else if (epi == E2_F32_SLAB && splits <= 1 && ldc % 4 == 0 && !HSD_KNOB("HSD_G2_TT_ATOMIC", 0)) {
       // one K-split: every output element has one owner -> C += acc in place instead of fp32 atomics (the tied MLM
@@ -1758,7 +1783,7 @@ void launch_gemm8_wgrad(const uint8_t* dy, int64_t ldd, int fdy, const float* sd
   HSD_CHECK_LAUNCH();
   const int64_t n4 = (int64_t)M * N / 4;
   const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
-  hipLaunchKernelGGL(g2::slab_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, C, ldc, M, N, real);
+  hipLaunchKernelGGL(g2::slab_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, C, ldc, M, N, real, 0);
   HSD_CHECK_LAUNCH();
 }
 

@@ -158,6 +158,7 @@ void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const b
                   float* rd = nullptr, int rd_seq = 0);
 bool gemm2_supported(int la, int lb, int epi, int M, int N, int K);
 int gemm2_wgrad_splits(int M, int N, int K);
+int gemm2_f32nt_splits(int M, int N, int K);
 // fp8 TT weight gradient (gemm2.hip gemm8tt_kernel + slab_reduce): C[M][N] (fp32) += sdy·sx · dY8ᵀ · X8
 bool gemm8_wgrad_supported(int M, int N, int T);
 int gemm8_wgrad_splits(int M, int N, int T);

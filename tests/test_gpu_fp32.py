@@ -19,10 +19,15 @@ def _rel(a, b):
     return float((a.double() - b.double()).norm() / (b.double().norm() + 1e-30))
 
 
-@pytest.mark.parametrize("M,K,N", [(300, 768, 768), (1024, 768, 3072), (256, 3072, 768), (64, 768, 2304)])
-def test_split_product_gemms(gpu, M, K, N):
+@pytest.mark.parametrize("ksplit", ["auto", "1"])
+@pytest.mark.parametrize("M,K,N", [(300, 768, 768), (1024, 768, 3072), (256, 3072, 768), (64, 768, 2304),
+                                   (4096, 1024, 1024)])
+def test_split_product_gemms(gpu, M, K, N, ksplit, monkeypatch):
     """x·wᵀ, dy·w and the weight gradient on the split-product MFMA GEMM: per element within 2^-14 of Σ|products|
-    (the three-term split's bound is ~2^-15), and ~1e-6 relative overall against fp64."""
+    (the three-term split's bound is ~2^-15), and ~1e-6 relative overall against fp64. ksplit "auto": grids of at most
+    half the CUs run as K-split fp32 slabs + one summing pass (gemm2_f32nt_splits); "1": one pass."""
+    if ksplit == "1":
+        monkeypatch.setenv("HSD_F32NT_SPLITS", "1")
     h = _h32()
     torch.manual_seed(M + N)
     x, w = torch.randn(M, K, device=gpu), torch.randn(N, K, device=gpu) * 0.05
