@@ -1,7 +1,7 @@
 // Self-attention for S == 128, head_dim 64 (the headline BERT-base seq-128 config; SURVEY.md §2.10
 // K4-K7 forward, K14 backward): ONE workgroup per (batch, head) holds the whole 128x128 problem, so
-// Q/K/V/dO are read from HBM exactly once, probabilities never leave registers, and the only
-// workgroup-wide synchronisation is one barrier after the operand DMA (forward) or three (backward).
+// Q/K/V/dO are read from HBM exactly once and probabilities never leave registers; the forward synchronises
+// once after the operand DMA, the backward once per query block (V3, below) plus its phase changes.
 //
 // * operands are staged HBM -> LDS with global_load_lds_dwordx4 (1 KiB per wave instruction) into
 //   [128][64] bf16 images whose 16-B chunks are XOR-swizzled (chunk ^ bitrev3((row>>1)&7)) — the
@@ -12,10 +12,12 @@
 //   its 64 accumulator registers -> exact (not online) softmax in registers, Oᵀ = Vᵀ·Pᵀ with the
 //   accumulator as the B operand, O staged through a wave-private LDS slice to 128-B row stores.
 // * backward: wave w owns keys 32w..32w+31 on the lanes; loops over 4 query blocks recomputing P from
-//   the saved log-sum-exp, accumulates dKᵀ, dVᵀ in registers, writes dS once to a [128 key][128 q] LDS
-//   image (chunk ^ 4((r&3)^((r>>4)&3)) + ((r>>2)&3): conflict-free for its b64 writes and tr reads),
-//   then dQᵀ = Kᵀ·dSᵀ with wave w owning queries 32w..32w+31. The dropout hash of a key pair is
-//   computed once per lane pair and exchanged (keys sit on adjacent lanes here).
+//   the saved log-sum-exp, accumulates dKᵀ, dVᵀ in registers, writes dS once, then dQᵀ = Kᵀ·dSᵀ with wave w
+//   owning queries 32w..32w+31. V3 (default): the dS of query block qb ([128 key][32 q], 64-B rows, 8-B units
+//   swizzled by key) is written over the Q / dO rows of that block once every wave is past it (one barrier per
+//   block), K has its own slot (re-read per block instead of held in VGPRs): 52.5 KiB of LDS and 168 VGPRs, three
+//   workgroups per CU (HSD_A128_BWD_V3=0: the [128 key][128 q] dS image, 68.5 KiB, two per CU). The dropout hash of
+//   a key pair is computed once per lane pair and exchanged (keys sit on adjacent lanes here).
 // Dropout / mask / lse conventions are identical to attention.hip (ops/rng.py site indexing).
 #include "attn_common.h"
 
