@@ -12,6 +12,7 @@
 // partial sums for the weight/bias gradients accumulate in registers across the rows a block
 // walks, with no atomics until the block ends.
 #include "common.h"
+#include "ln_common.h"
 #include "fp8_common.h"
 #include <stdlib.h>
 #include <algorithm>
@@ -109,7 +110,6 @@ __global__ __launch_bounds__(256) void ln_fwd_plain16_kernel(const bf16_t* __res
                                                              float* __restrict__ mean_out, float* __restrict__ rstd_out,
                                                              int rows, int H, int rpw, float eps, Q8Out q8o) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int n8 = H >> 3;
   const int r0 = (blockIdx.x * kLnWaves + wave) * rpw;
   const int r1 = min(rows, r0 + rpw);
   // fp8 copy of the output (Q8: e4m3, delayed scaling from q8o.amax_in; this pass's amax into q8o.amax_track)
@@ -120,72 +120,18 @@ __global__ __launch_bounds__(256) void ln_fwd_plain16_kernel(const bf16_t* __res
   }
   if (r0 >= r1) return;
   u32x4 gw[NC8], bw[NC8];
-#pragma unroll
-  for (int i = 0; i < NC8; ++i) {
-    const int c = lane + 64 * i;
-    gw[i] = bw[i] = u32x4{0, 0, 0, 0};
-    if (c < n8) {
-      gw[i] = *reinterpret_cast<const u32x4*>(gamma + 8 * c);
-      bw[i] = *reinterpret_cast<const u32x4*>(beta + 8 * c);
-    }
-  }
-  auto load = [&](int row, u32x4(&yw)[NC8]) {
-#pragma unroll
-    for (int i = 0; i < NC8; ++i) {
-      const int c = lane + 64 * i;
-      yw[i] = u32x4{0, 0, 0, 0};
-      if (c < n8) yw[i] = *reinterpret_cast<const u32x4*>(y + (size_t)row * H + 8 * c);
-    }
-  };
+  ln_params16<NC8>(gamma, beta, H, lane, gw, bw);
   auto process = [&](int row, const u32x4(&yw)[NC8]) {
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < NC8; ++i)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) s += lo_bf(yw[i][k]) + hi_bf(yw[i][k]);
-    const float mean = wave_sum(s) / (float)H;
-    float ss = 0.f;
-#pragma unroll
-    for (int i = 0; i < NC8; ++i) {
-      if (lane + 64 * i < n8) {
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const float d0 = lo_bf(yw[i][k]) - mean, d1 = hi_bf(yw[i][k]) - mean;
-          ss += d0 * d0;
-          ss += d1 * d1;
-        }
-      }
-    }
-    const float rstd = rsqrtf(wave_sum(ss) / (float)H + eps);
-#pragma unroll
-    for (int i = 0; i < NC8; ++i) {
-      const int c = lane + 64 * i;
-      if (c < n8) {
-        u32x4 o;
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-          o[k] = pack_bf2((lo_bf(yw[i][k]) - mean) * rstd * lo_bf(gw[i][k]) + lo_bf(bw[i][k]),
-                          (hi_bf(yw[i][k]) - mean) * rstd * hi_bf(gw[i][k]) + hi_bf(bw[i][k]));
-        *reinterpret_cast<u32x4*>(out + (size_t)row * H + 8 * c) = o;
-        if constexpr (Q8) {
-          qm = absmax8(o, qm);
-          *reinterpret_cast<u32x2*>(q8o.q + (size_t)row * H + 8 * c) = quant8<0>(o, qs);
-        }
-      }
-    }
-    if (lane == 0) {
-      mean_out[row] = mean;
-      rstd_out[row] = rstd;
-    }
+    ln_row16<NC8, Q8>(yw, gw, bw, row, H, lane, eps, out, mean_out, rstd_out, q8o.q, qs, &qm);
   };
   u32x4 ya[NC8], yb[NC8];
-  load(r0, ya);
+  ln_load16<NC8>(y, r0, H, lane, ya);
   for (int r = r0; r < r1; r += 2) {
     const bool more = r + 1 < r1;
-    if (more) load(r + 1, yb);
+    if (more) ln_load16<NC8>(y, r + 1, H, lane, yb);
     process(r, ya);
     if (!more) break;
-    if (r + 2 < r1) load(r + 2, ya);
+    if (r + 2 < r1) ln_load16<NC8>(y, r + 2, H, lane, ya);
     process(r + 1, yb);
   }
   if constexpr (Q8) wave_amax_track(qm, q8o.amax_track);
