@@ -51,15 +51,19 @@ __device__ __forceinline__ void mainloop_staggered(f32x4 (&acc)[8][BN / 64], bf1
   //   the lagging group's DMAs of tile t+1 have landed before the leading group reads them in P1(t+1).
   // Tile t+1's DMA: SYNC 4 issues it in P1 / P2 (two MFMA phases to land), SYNC 5 spreads it over
   // P1 / P2 / P3 (2 pieces per phase, fewer issue stalls per phase); D0 slots of tile t+2 go out in P4.
+#ifndef G2_STATIC_PRIO
+#define G2_STATIC_PRIO 1
+#endif
+  constexpr bool kStaticPrio = G2_STATIC_PRIO;
   constexpr int E1 = SYNC != 5 ? D0 + (G - D0 + 1) / 2 : D0 + 2;
   constexpr int E2 = SYNC != 5 ? G : (D0 + 4 < G ? D0 + 4 : G);
 #define G2_LGKM0() asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory")
 #define G2_CLUSTER(ACC_I0, FA, FB, NBX, J0)                                                                  \
-  __builtin_amdgcn_s_setprio(1);                                                                             \
+  if constexpr (!kStaticPrio) __builtin_amdgcn_s_setprio(1);                                                 \
   _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) _Pragma("unroll") for (int i = 0; i < 4; ++i)               \
       _Pragma("unroll") for (int j = 0; j < NBX; ++j) acc[ACC_I0 + i][J0 + j] =                                \
           __builtin_amdgcn_mfma_f32_16x16x32_bf16(FB[j][ks], FA[i][ks], acc[ACC_I0 + i][J0 + j], 0, 0, 0);     \
-  __builtin_amdgcn_s_setprio(0);
+  if constexpr (!kStaticPrio) __builtin_amdgcn_s_setprio(0);
   if constexpr (PRO) {
 #pragma unroll
     for (int q = 0; q < G; ++q) dma_slot(q, smem, kbeg);
@@ -71,6 +75,11 @@ __device__ __forceinline__ void mainloop_staggered(f32x4 (&acc)[8][BN / 64], bf1
       vmcnt<0>();
     }
     G2_BARRIER();
+  }
+  // static priority (MI355X_MICROARCH.md 'Two waves per SIMD' item 4): the second-dispatched half (waves 4-7, the
+  // lagging group) at prio 1 for the whole loop instead of per-cluster flips. G2_STATIC_PRIO=0: per-cluster flips.
+  if constexpr (kStaticPrio) {
+    if (wm == 1) __builtin_amdgcn_s_setprio(1);
   }
   if (wm == 1) G2_BARRIER();
   for (int t = 0; t < nt; ++t) {
@@ -135,6 +144,7 @@ __device__ __forceinline__ void mainloop_staggered(f32x4 (&acc)[8][BN / 64], bf1
     G2_BARRIER();
   }
   if (wm == 0) G2_BARRIER();
+  if constexpr (kStaticPrio) __builtin_amdgcn_s_setprio(0);
 #undef G2_CLUSTER
 #undef G2_LGKM0
 }
