@@ -730,10 +730,13 @@ __device__ __forceinline__ void mainloop_staggered8(f32x4 (&acc)[8][BN / 64], bf
   constexpr int E1 = D0 + (G - D0 + 1) / 2;
   i32x8 fa[4], fb0[NB0], fb1[NB1];
 #define G8_CLUSTER(ACC_I0, FB_, NBX, J0)                                                                     \
-  __builtin_amdgcn_s_setprio(1);                                                                             \
+  if constexpr (!G2_STATIC_PRIO) __builtin_amdgcn_s_setprio(1);                                             \
   _Pragma("unroll") for (int i = 0; i < 4; ++i) _Pragma("unroll") for (int j = 0; j < NBX; ++j)              \
       acc[ACC_I0 + i][J0 + j] = mma8<FB, FA>(FB_[j], fa[i], acc[ACC_I0 + i][J0 + j]);                        \
-  __builtin_amdgcn_s_setprio(0);
+  if constexpr (!G2_STATIC_PRIO) __builtin_amdgcn_s_setprio(0);
+  if constexpr (G2_STATIC_PRIO) {  // static priority of the lagging group, as in mainloop_staggered
+    if (wm == 1) __builtin_amdgcn_s_setprio(1);
+  }
   if (wm == 1) G2_BARRIER();
   for (int t = 0; t < nt; ++t) {
     const bf16_t* cA = smem + (t & 1) * STAGE;
@@ -785,6 +788,7 @@ __device__ __forceinline__ void mainloop_staggered8(f32x4 (&acc)[8][BN / 64], bf
     G2_BARRIER();
   }
   if (wm == 0) G2_BARRIER();
+  if constexpr (G2_STATIC_PRIO) __builtin_amdgcn_s_setprio(0);
 #undef G8_CLUSTER
 }
 
