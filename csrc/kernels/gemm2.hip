@@ -23,6 +23,12 @@
 // next K-tile's LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave instruction) is spread over
 // P4(prev) / P1 / P2 / P3 into the other LDS stage and retired by ONE counted vmcnt at the end of P4.
 #include "gemm2_dev.h"
+// DMA slots of K-tile t+2 issued in P4 of K-tile t (of G = 7-8 per wave) by the staggered 4-phase loop (bf16 NT / TT):
+// 4 measured best (tools/gpu_tree_gemm_ab.sh, profiles/dma_depth_d0_ab_r5.log: vs 2, every headline GEMM 0.3-6.9 %
+// faster and the step +1.9 %; 3, 5 and 6 slower than 4)
+#ifndef G2_D0
+#define G2_D0 4
+#endif
 #include <stdlib.h>
 
 #include <cmath>
@@ -164,7 +170,7 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
   constexpr int G = GA + GB;                         // 8 (BN 256) or 7 (BN 192)
   // slots of tile t+2 issued in P4 of tile t (the rest in P1-P3 of t+1); SYNC 6 / 7 = SYNC 0 / 4 with the
   // WHOLE next-next tile issued in P4, so every DMA has a full K-tile of MFMAs to land
-  constexpr int D0 = (SYNC == 6 || SYNC == 7) ? G : 2;
+  constexpr int D0 = (SYNC == 6 || SYNC == 7) ? G : G2_D0;
   constexpr bool F32OUT = EPI == E2_F32_ATOMIC || EPI == E2_F32_SLAB;
 
   __shared__ __attribute__((aligned(16))) bf16_t smem[2 * STAGE];
@@ -521,7 +527,7 @@ __global__ __launch_bounds__(512, 1) void gemm2pk_kernel(G2Params p) {
   static_assert(epi_bf16_out(EPI), "bf16 epilogues");
   constexpr int WN = BN / 4, NREP = WN / 16;
   constexpr int TA = BM * 64, STAGE = TA + BN * 64;
-  constexpr int GA = 4, GB = BN / 64, G = GA + GB, D0 = 2;
+  constexpr int GA = 4, GB = BN / 64, G = GA + GB, D0 = G2_D0;
   constexpr int PB = 2;                                  // 32-row epilogue passes
   constexpr int STG = 8 * 16 * PB * epi_srow<BN>();      // epilogue staging, elements
   constexpr int ITER = epi_iter<BN, PB>();
