@@ -29,6 +29,10 @@
 #ifndef G2_D0
 #define G2_D0 4
 #endif
+// the same for the fp8 persistent NT / TT kernels (gemm8pk, gemm8tt)
+#ifndef G8_D0
+#define G8_D0 4
+#endif
 #include <stdlib.h>
 
 #include <cmath>
@@ -810,7 +814,7 @@ __global__ __launch_bounds__(512, 1) void gemm8pk_kernel(G2Params p, const float
   static_assert(epi_bf16_out(EPI), "bf16 epilogues");
   constexpr int WN = BN / 4, NREP = WN / 16;
   constexpr int TA = BM * 64, STAGE = TA + BN * 64;
-  constexpr int GA = 4, GB = BN / 64, G = GA + GB, D0 = 2;
+  constexpr int GA = 4, GB = BN / 64, G = GA + GB, D0 = G8_D0;
   constexpr int PB = 2;
   constexpr int STG = 8 * 16 * PB * epi_srow<BN>();
   constexpr int ITER = epi_iter<BN, PB>();
@@ -936,7 +940,7 @@ __global__ __launch_bounds__(512, 1) void gemm8tt_kernel(G2Params p, const float
                                                          const float* __restrict__ sb) {
   constexpr int BN = 256, NREP = 4;
   constexpr int TA = BM * 64, STAGE = TA + BN * 64;
-  constexpr int GA = 4, GB = 4, G = GA + GB, D0 = 2;
+  constexpr int GA = 4, GB = 4, G = GA + GB, D0 = G8_D0;
   __shared__ __attribute__((aligned(16))) bf16_t smem[2 * STAGE];
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
