@@ -198,9 +198,13 @@ namespace hsd {
 
 // Batched bf16 transpose for the dgrad weights: dst_i [cols][rows] = src_i [rows][cols]ᵀ for every matrix
 // of a descriptor table {src, dst, rows, cols, first_tile} (int64 x 5, device memory), one launch for
-// all of them after the optimizer step. Block = 256 threads = one 64x64 tile through a padded LDS tile.
+// all of them after the optimizer step. Block = 256 threads = one 64x64 tile.
+// Full tiles (the common case: every BERT weight dimension is a multiple of 64): 16-B global loads and stores, the
+// tile staged through LDS as 16-B chunks (one ds_write_b128 per chunk) with the chunk index XOR-swizzled by the row
+// block, so the column gathers (8 lanes = 8 row blocks of one column) hit 8 different chunk positions — conflict-free;
+// each 8-lane group stores one 128-B output row. Edge tiles (dimensions multiple of 4 only): 8-B element path.
 __global__ __launch_bounds__(256) void transpose_many_kernel(const int64_t* __restrict__ desc, int n) {
-  __shared__ bf16_t tile[64][64 + 2];
+  __shared__ __attribute__((aligned(16))) u32x4 t16[64 * 8 + 16];  // + 16: the edge path's 64 x 66 bf16 tile
   const int bid = blockIdx.x;
   int mi = 0;
   while (mi + 1 < n && desc[(mi + 1) * 5 + 4] <= bid) ++mi;
@@ -211,7 +215,38 @@ __global__ __launch_bounds__(256) void transpose_many_kernel(const int64_t* __re
   const int tcols = (cols + 63) / 64;
   const int r0 = (t / tcols) * 64, c0 = (t % tcols) * 64;
   const int tid = threadIdx.x;
-  // load 64 rows x 64 cols: thread -> (row tid>>2 (+0, 64/... ), 16 cols chunk (tid&3)*16)
+  const bool full = r0 + 64 <= rows && c0 + 64 <= cols && (rows & 7) == 0 && (cols & 7) == 0;
+  if (full) {
+    u32x4 v[2];
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int q = tid + 256 * it, r = q >> 3, cc = q & 7;
+      v[it] = *reinterpret_cast<const u32x4*>(src + (int64_t)(r0 + r) * cols + c0 + 8 * cc);
+    }
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int q = tid + 256 * it, r = q >> 3, cc = q & 7;
+      t16[r * 8 + (cc ^ ((r >> 3) & 7))] = v[it];
+    }
+    __syncthreads();
+    const uint16_t* th = reinterpret_cast<const uint16_t*>(t16);
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int q = tid + 256 * it, rg = q & 7, c = q >> 3;  // output row c (input column), input rows 8 rg .. 8 rg + 7
+      const int pc = (c >> 3) ^ rg;                         // swizzled chunk of column c in row block rg
+      uint32_t w[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) w[j] = th[(rg * 8 + j) * 64 + pc * 8 + (c & 7)];
+      u32x4 o;
+      o.x = w[0] | (w[1] << 16);
+      o.y = w[2] | (w[3] << 16);
+      o.z = w[4] | (w[5] << 16);
+      o.w = w[6] | (w[7] << 16);
+      *reinterpret_cast<u32x4*>(dst + (int64_t)(c0 + c) * rows + r0 + 8 * rg) = o;
+    }
+    return;
+  }
+  bf16_t(*tile)[66] = reinterpret_cast<bf16_t(*)[66]>(t16);  // 64 x 66 bf16 = 8,448 B
 #pragma unroll
   for (int it = 0; it < 4; ++it) {
     const int r = (tid >> 4) + 16 * it, c = (tid & 15) * 4;
