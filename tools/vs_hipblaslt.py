@@ -1,6 +1,7 @@
 """This framework's GEMMs vs hipBLASLt (torch.addmm / torch.mm) on the headline layer's shapes, one process.
 
-    python tools/vs_hipblaslt.py [T]      (default T = 131072 tokens = bert-base B = 1024, S = 128)
+    python tools/vs_hipblaslt.py [T [H]]  (default T = 131072 tokens = bert-base B = 1024, S = 128; H = 768;
+                                          bert-large B = 8 S = 512: 4096 1024)
 
 For each bert-base projection (QKV, attention output, FFN1, FFN2) and each of its three GEMMs:
   forward  y = x Wᵀ + b        ours: gemm2 NT, bias epilogue      library: torch.addmm(b, x, Wᵀ)
@@ -40,12 +41,13 @@ def _addmm_f32(c, a, b):
 
 def main():
     T = int(sys.argv[1]) if len(sys.argv) > 1 else 131072
+    H = int(sys.argv[2]) if len(sys.argv) > 2 else 768
     dev = torch.device("cuda", 0)
     torch.manual_seed(0)
-    out = {"tokens": T}
+    out = {"tokens": T, "hidden": H}
     tot = {"ours_s": 0.0, "lib_s": 0.0, "flop": 0.0}
-    for name, (N, K) in {"qkv": (2304, 768), "attn_out": (768, 768), "ffn1": (3072, 768),
-                         "ffn2": (768, 3072)}.items():
+    for name, (N, K) in {"qkv": (3 * H, H), "attn_out": (H, H), "ffn1": (4 * H, H),
+                         "ffn2": (H, 4 * H)}.items():
         x = torch.randn(T, K, device=dev).bfloat16()
         w = torch.randn(N, K, device=dev).bfloat16() * 0.05
         wt = w.t().contiguous()
