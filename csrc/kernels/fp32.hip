@@ -22,29 +22,50 @@ namespace f32k {
 
 // ------------------------------------------------------------------------------------------------ split3
 // out = 3 blocks of x [R][C], block b = lo(x) if (pat >> b) & 1 else hi(x); blocks side by side along the columns
-// (out [R][3C]) or stacked along the rows (out [3R][C]). C % 4 == 0.
+// (out [R][3C]) or stacked along the rows (out [3R][C]). C % 4 == 0; V = 8 elements per step (16-B stores) when
+// C % 8 == 0. The (row, column) of a thread's element group advance incrementally by the grid stride: one 64-bit
+// division per thread instead of a 64-bit division and remainder per step (those dominated the kernel's VALU).
+template <int V>
 __global__ __launch_bounds__(256) void split3_kernel(const float* __restrict__ x, bf16_t* __restrict__ out, int64_t R,
                                                      int64_t C, int pat, int rows) {
-  const int64_t c4n = C / 4, n = R * c4n;
+  const int64_t cvn = C / V, n = R * cvn;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) {
-    const int64_t r = i / c4n, c = (i % c4n) * 4;
-    const f32x4 v = *reinterpret_cast<const f32x4*>(x + r * C + c);
-    u32x2 hi, lo;
-    float h[4], l[4];
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  int64_t r = i / cvn, cv = i - r * cvn;
+  const int64_t sr = stride / cvn, sc = stride - sr * cvn;
+  for (; i < n; i += stride) {
+    const int64_t c = cv * V;
+    uint32_t hw[V / 2], lw[V / 2];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      h[e] = bf2f(f2bf(v[e]));
-      l[e] = v[e] - h[e];
+    for (int q = 0; q < V / 4; ++q) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(x + r * C + c + 4 * q);
+      float h[4], l[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        h[e] = bf2f(f2bf(v[e]));
+        l[e] = v[e] - h[e];
+      }
+      hw[2 * q] = pack_bf2(h[0], h[1]);
+      hw[2 * q + 1] = pack_bf2(h[2], h[3]);
+      lw[2 * q] = pack_bf2(l[0], l[1]);
+      lw[2 * q + 1] = pack_bf2(l[2], l[3]);
     }
-    hi.x = pack_bf2(h[0], h[1]);
-    hi.y = pack_bf2(h[2], h[3]);
-    lo.x = pack_bf2(l[0], l[1]);
-    lo.y = pack_bf2(l[2], l[3]);
 #pragma unroll
-    for (int b = 0; b < 3; ++b) {
-      const int64_t off = rows ? ((int64_t)b * R + r) * C + c : r * 3 * C + (int64_t)b * C + c;
-      *reinterpret_cast<u32x2*>(out + off) = ((pat >> b) & 1) ? lo : hi;
+    for (int bb = 0; bb < 3; ++bb) {
+      const int64_t off = rows ? ((int64_t)bb * R + r) * C + c : r * 3 * C + (int64_t)bb * C + c;
+      const uint32_t* w = ((pat >> bb) & 1) ? lw : hw;
+      if constexpr (V == 8) {
+        *reinterpret_cast<u32x4*>(out + off) = u32x4{w[0], w[1], w[2], w[3]};
+      } else {
+        *reinterpret_cast<u32x2*>(out + off) = u32x2{w[0], w[1]};
+      }
+    }
+    cv += sc;
+    r += sr;
+    if (cv >= cvn) {
+      cv -= cvn;
+      ++r;
     }
   }
 }
@@ -62,9 +83,16 @@ __global__ __launch_bounds__(256) void epi32_kernel(float* __restrict__ y, const
   dp = resolve_seed(dp);
   const int64_t n4 = M * N / 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
-    const int64_t e0 = i * 4;
-    const int n0 = (int)(e0 % N);
+  const int N4 = N / 4;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  // row m / column n0 of group i, advanced by the grid stride (no 64-bit division per step, as split3_kernel)
+  int64_t m = i / N4;
+  int c4 = (int)(i - m * N4);
+  const int64_t sr = stride / N4;
+  const int sc = (int)(stride - sr * N4);
+  for (; i < n4; i += stride) {
+    const int n0 = 4 * c4;
     f32x4 v = reinterpret_cast<const f32x4*>(y)[i];
     if (bias != nullptr) v += *reinterpret_cast<const f32x4*>(bias + n0);
     f32x4 o;
@@ -77,7 +105,7 @@ __global__ __launch_bounds__(256) void epi32_kernel(float* __restrict__ y, const
     } else if (kind == 2) {
       if (dp.enabled) {
         uint32_t b0, b1;
-        dropout_bits4((uint32_t)(e0 / N), (uint32_t)n0, dp, b0, b1);
+        dropout_bits4((uint32_t)m, (uint32_t)n0, dp, b0, b1);
         v[0] *= keep_factor(b0, 0, dp);
         v[1] *= keep_factor(b0, 1, dp);
         v[2] *= keep_factor(b1, 0, dp);
@@ -96,6 +124,12 @@ __global__ __launch_bounds__(256) void epi32_kernel(float* __restrict__ y, const
       }
     }
     reinterpret_cast<f32x4*>(out)[i] = o;
+    c4 += sc;
+    m += sr;
+    if (c4 >= N4) {
+      c4 -= N4;
+      ++m;
+    }
   }
 }
 
@@ -104,16 +138,28 @@ __global__ __launch_bounds__(256) void dropout32_kernel(const float* __restrict_
                                                         int64_t n4, int W, DropoutParams dp) {
   dp = resolve_seed(dp);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-  for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+  const int W4 = W / 4;
+  int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n4) return;
+  int64_t row = i / W4;
+  int c4 = (int)(i - row * W4);
+  const int64_t sr = stride / W4;
+  const int sc = (int)(stride - sr * W4);
+  for (; i < n4; i += stride) {
     f32x4 v = reinterpret_cast<const f32x4*>(x)[i];
-    const int64_t row = (i * 4) / W;
     uint32_t b0, b1;
-    dropout_bits4((uint32_t)row, (uint32_t)(i * 4 - row * W), dp, b0, b1);
+    dropout_bits4((uint32_t)row, (uint32_t)(4 * c4), dp, b0, b1);
     v[0] *= keep_factor(b0, 0, dp);
     v[1] *= keep_factor(b0, 1, dp);
     v[2] *= keep_factor(b1, 0, dp);
     v[3] *= keep_factor(b1, 1, dp);
     reinterpret_cast<f32x4*>(out)[i] = v;
+    c4 += sc;
+    row += sr;
+    if (c4 >= W4) {
+      c4 -= W4;
+      ++row;
+    }
   }
 }
 
@@ -691,8 +737,12 @@ static int ew_blocks(int64_t n) { return (int)std::min<int64_t>(2048, std::max<i
 
 void launch_split3(const float* x, bf16_t* out, int64_t R, int64_t C, int pat, bool rows, hipStream_t st) {
   if (C % 4) abort();
-  hipLaunchKernelGGL(f32k::split3_kernel, dim3(ew_blocks(R * C / 4)), dim3(256), 0, st, x, out, R, C, pat,
-                     rows ? 1 : 0);
+  if (C % 8 == 0)
+    hipLaunchKernelGGL(f32k::split3_kernel<8>, dim3(ew_blocks(R * C / 8)), dim3(256), 0, st, x, out, R, C, pat,
+                       rows ? 1 : 0);
+  else
+    hipLaunchKernelGGL(f32k::split3_kernel<4>, dim3(ew_blocks(R * C / 4)), dim3(256), 0, st, x, out, R, C, pat,
+                       rows ? 1 : 0);
   HSD_CHECK_LAUNCH();
 }
 
