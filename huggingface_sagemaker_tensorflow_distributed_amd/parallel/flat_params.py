@@ -165,12 +165,18 @@ class FlatParamStore:
         of them are re-quantised by two batched launches (amax, quantise) after every optimizer step."""
         from ..ops import hip
 
+        import os
+
         per_block = hip._C.fp8_elems_per_block()
         total = sum(self.segments[i].numel for i in idx)
         self.fp8_w = torch.empty(total, dtype=torch.uint8, device=self.device)
         self.fp8_wt = torch.empty(total, dtype=torch.uint8, device=self.device)
-        self.fp8_amax = torch.zeros(len(idx), dtype=torch.float32, device=self.device)
-        self.fp8_sinv = torch.ones(len(idx), dtype=torch.float32, device=self.device)
+        # one 128-B line per weight for its amax / scale: every block of the amax pass ends with an atomic on its
+        # weight's slot, and packed slots put all ~18k of them on one L2 line (roberta-large: 514 us for a 604 MB
+        # read, 1.2 TB/s; profiles/fp8_refresh_r5.log). HSD_FP8_SLOT = floats per slot (1 = packed).
+        slot = max(1, int(os.environ.get("HSD_FP8_SLOT", "32")))
+        self.fp8_amax = torch.zeros(len(idx) * slot, dtype=torch.float32, device=self.device)
+        self.fp8_sinv = torch.ones(len(idx) * slot, dtype=torch.float32, device=self.device)
         # delayed-scaling history of the two activation-side quantisation sites of each weight:
         # [weight][0 = forward input x, 1 = dgrad input dy][0 = amax used for this step's scale, 1 = running]
         self.fp8_act = torch.zeros(len(idx), 2, 2, dtype=torch.float32, device=self.device)
@@ -181,14 +187,14 @@ class FlatParamStore:
             p = self.params[i]
             q = self.fp8_w[off:off + n].view(rows, cols)
             qt = self.fp8_wt[off:off + n].view(cols, rows)
-            p._hsd_q, p._hsd_qt, p._hsd_qs = q, qt, self.fp8_sinv[t:t + 1]
+            p._hsd_q, p._hsd_qt, p._hsd_qs = q, qt, self.fp8_sinv[t * slot:t * slot + 1]
             p._hsd_fp8_x, p._hsd_fp8_g = self.fp8_act[t, 0], self.fp8_act[t, 1]
             nb = (n + per_block - 1) // per_block
-            amax_rows.append([p.data.data_ptr(), 0, n, t, ab])
+            amax_rows.append([p.data.data_ptr(), 0, n, t * slot, ab])
             ab += nb
-            quant_rows.append([p.data.data_ptr(), q.data_ptr(), n, t, qb])
+            quant_rows.append([p.data.data_ptr(), q.data_ptr(), n, t * slot, qb])
             qb += nb
-            quant_rows.append([p._hsd_wt.data_ptr(), qt.data_ptr(), n, t, qb])
+            quant_rows.append([p._hsd_wt.data_ptr(), qt.data_ptr(), n, t * slot, qb])
             qb += nb
             off += n
         self._fp8_desc = (torch.tensor(amax_rows, dtype=torch.int64, device=self.device), ab,
