@@ -596,6 +596,16 @@ void split3(torch::Tensor x, torch::Tensor out, int64_t pat, bool rows) {
   hsd::launch_split3(x.data_ptr<float>(), BF(out), x.size(0), x.size(1), (int)pat, rows, cur_stream());
 }
 
+// both layouts from one read: out_cols [R][3C] (pattern pat_cols) and out_rows [3R][C] (pattern pat_rows)
+void split3_dual(torch::Tensor x, torch::Tensor out_cols, int64_t pat_cols, torch::Tensor out_rows, int64_t pat_rows) {
+  check_f32(x, "x"); check_bf16(out_cols, "out_cols"); check_bf16(out_rows, "out_rows");
+  TORCH_CHECK(x.dim() == 2 && x.size(1) % 4 == 0, "split3_dual x");
+  TORCH_CHECK(out_cols.size(0) == x.size(0) && out_cols.size(1) == 3 * x.size(1), "split3_dual out_cols shape");
+  TORCH_CHECK(out_rows.size(0) == 3 * x.size(0) && out_rows.size(1) == x.size(1), "split3_dual out_rows shape");
+  hsd::launch_split3(x.data_ptr<float>(), BF(out_cols), x.size(0), x.size(1), (int)pat_cols, false, cur_stream(),
+                     BF(out_rows), (int)pat_rows);
+}
+
 void epi32(torch::Tensor y, c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> aux, torch::Tensor out,
            int64_t kind, double p, int64_t seed) {
   check_f32(y, "y"); check_f32(out, "out");
@@ -917,6 +927,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         "contention emulation: hold `blocks` whole CUs for `usec` us on the current stream");
   m.def("gemm2_f32nt", &gemm2_f32nt);
   m.def("split3", &split3);
+  m.def("split3_dual", &split3_dual);
   m.def("epi32", &epi32);
   m.def("dropout32", &dropout32);
   m.def("colsum32", &colsum32);

@@ -25,9 +25,12 @@ namespace f32k {
 // (out [R][3C]) or stacked along the rows (out [3R][C]). C % 4 == 0; V = 8 elements per step (16-B stores) when
 // C % 8 == 0. The (row, column) of a thread's element group advance incrementally by the grid stride: one 64-bit
 // division per thread instead of a 64-bit division and remainder per step (those dominated the kernel's VALU).
+// out2 (optional): a second copy in the row-stacked layout [3R][C] with pattern pat2, written from the same read (the
+// incoming gradient of a linear layer feeds both its dgrad, column blocks, and its weight gradient, row blocks)
 template <int V>
 __global__ __launch_bounds__(256) void split3_kernel(const float* __restrict__ x, bf16_t* __restrict__ out, int64_t R,
-                                                     int64_t C, int pat, int rows) {
+                                                     int64_t C, int pat, int rows, bf16_t* __restrict__ out2,
+                                                     int pat2) {
   const int64_t cvn = C / V, n = R * cvn;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -59,6 +62,18 @@ __global__ __launch_bounds__(256) void split3_kernel(const float* __restrict__ x
         *reinterpret_cast<u32x4*>(out + off) = u32x4{w[0], w[1], w[2], w[3]};
       } else {
         *reinterpret_cast<u32x2*>(out + off) = u32x2{w[0], w[1]};
+      }
+    }
+    if (out2 != nullptr) {
+#pragma unroll
+      for (int bb = 0; bb < 3; ++bb) {
+        const int64_t off = ((int64_t)bb * R + r) * C + c;
+        const uint32_t* w = ((pat2 >> bb) & 1) ? lw : hw;
+        if constexpr (V == 8) {
+          *reinterpret_cast<u32x4*>(out2 + off) = u32x4{w[0], w[1], w[2], w[3]};
+        } else {
+          *reinterpret_cast<u32x2*>(out2 + off) = u32x2{w[0], w[1]};
+        }
       }
     }
     cv += sc;
@@ -735,14 +750,15 @@ __global__ __launch_bounds__(64) void cls32_bwd_kernel(const float* __restrict__
 
 static int ew_blocks(int64_t n) { return (int)std::min<int64_t>(2048, std::max<int64_t>(1, (n + 255) / 256)); }
 
-void launch_split3(const float* x, bf16_t* out, int64_t R, int64_t C, int pat, bool rows, hipStream_t st) {
+void launch_split3(const float* x, bf16_t* out, int64_t R, int64_t C, int pat, bool rows, hipStream_t st,
+                   bf16_t* out2, int pat2) {
   if (C % 4) abort();
   if (C % 8 == 0)
     hipLaunchKernelGGL(f32k::split3_kernel<8>, dim3(ew_blocks(R * C / 8)), dim3(256), 0, st, x, out, R, C, pat,
-                       rows ? 1 : 0);
+                       rows ? 1 : 0, out2, pat2);
   else
     hipLaunchKernelGGL(f32k::split3_kernel<4>, dim3(ew_blocks(R * C / 4)), dim3(256), 0, st, x, out, R, C, pat,
-                       rows ? 1 : 0);
+                       rows ? 1 : 0, out2, pat2);
   HSD_CHECK_LAUNCH();
 }
 

@@ -103,7 +103,8 @@ void set_dropout_dev_seed(const uint32_t* p);
 void refresh_env_knobs();
 // fp32.hip: the fp32 (reference precision) step -- split-product operands for the bf16 MFMA GEMMs, fp32 epilogues,
 // LayerNorm, embeddings, streaming attention, classification head (ops/hip32.py)
-void launch_split3(const float* x, bf16_t* out, int64_t R, int64_t C, int pat, bool rows, hipStream_t st);
+void launch_split3(const float* x, bf16_t* out, int64_t R, int64_t C, int pat, bool rows, hipStream_t st,
+                   bf16_t* out2 = nullptr, int pat2 = 0);
 void launch_epi32(float* y, const float* bias, const float* aux, float* out, int64_t M, int N, int kind, double p,
                   uint64_t seed, hipStream_t st);
 void launch_dropout32(const float* x, float* out, int64_t n, int W, double p, uint64_t seed, hipStream_t st);

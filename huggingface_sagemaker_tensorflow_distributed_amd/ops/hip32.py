@@ -19,6 +19,9 @@ reference's masks bit for bit (``tests/test_gpu_fp32.py``).
 """
 from __future__ import annotations
 
+import os
+from typing import Optional
+
 import torch
 
 from . import hip
@@ -45,6 +48,23 @@ def _split(x: torch.Tensor, pat: int, rows: bool = False, pad_rows: int = 0) -> 
     return out
 
 
+# HSD_F32_DUAL_SPLIT=1 (default): a linear layer's incoming gradient is split ONCE into both layouts its backward
+# needs (column blocks for the dgrad, row blocks for the weight gradient): one read of dy and one launch instead of two
+_DUAL = os.environ.get("HSD_F32_DUAL_SPLIT", "1") == "1"
+
+
+def _split_grad(dy: torch.Tensor, need_dgrad: bool):
+    """(column-block split for :func:`mm_dgrad` or None, row-block split for :func:`wgrad_` or None) of ``dy``."""
+    if not (_DUAL and need_dgrad and dy.dim() == 2 and dy.shape[0] % 64 == 0 and dy.shape[1] % 4 == 0):
+        return None, None
+    dy = dy.contiguous()
+    R, C = dy.shape
+    cols = torch.empty((R, 3 * C), dtype=torch.bfloat16, device=dy.device)
+    rows = torch.empty((3 * R, C), dtype=torch.bfloat16, device=dy.device)
+    _C.split3_dual(dy, cols, PAT_A, rows, PAT_A)
+    return cols, rows
+
+
 def _nt_ok(M: int, N: int, K: int) -> bool:
     return N % 256 == 0 and (3 * K) % 64 == 0 and K % 4 == 0 and _C.gemm2_supported(0, 0, 7, M, N, 3 * K)
 
@@ -60,27 +80,27 @@ def mm_nt(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return y
 
 
-def mm_dgrad(dy: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+def mm_dgrad(dy: torch.Tensor, w: torch.Tensor, dys: Optional[torch.Tensor] = None) -> torch.Tensor:
     """dy [M, N] · w [N, K] -> [M, K] fp32: NT with W read k-strided (layout (0, 1)), the split blocks of W stacked
-    along its rows (= the product's K)."""
+    along its rows (= the product's K). ``dys``: dy's column-block split, already made (:func:`_split_grad`)."""
     M, N = dy.shape
     K = w.shape[1]
     if not (K % 256 == 0 and (3 * N) % 64 == 0 and N % 4 == 0 and _C.gemm2_supported(0, 1, 7, M, K, 3 * N)):
         return dy @ w
     dx = torch.empty((M, K), dtype=torch.float32, device=dy.device)
-    _C.gemm2_f32nt(_split(dy, PAT_A), _split(w, PAT_B, rows=True), dx, 1)
+    _C.gemm2_f32nt(dys if dys is not None else _split(dy, PAT_A), _split(w, PAT_B, rows=True), dx, 1)
     return dx
 
 
-def wgrad_(g: _Grad, dy: torch.Tensor, x: torch.Tensor) -> None:
+def wgrad_(g: _Grad, dy: torch.Tensor, x: torch.Tensor, dys: Optional[torch.Tensor] = None) -> None:
     """g.buf [N, K] += dyᵀ [N, T] · x [T, K] in fp32 (TT kernel, split blocks stacked along the tokens, padded to
-    64-token K-tiles)."""
+    64-token K-tiles). ``dys``: dy's row-block split (T % 64 == 0), already made (:func:`_split_grad`)."""
     N, K, T = dy.shape[1], x.shape[1], dy.shape[0]
     Tp = -(-T // 64) * 64
     if not (N % 8 == 0 and K % 256 == 0 and N % 4 == 0 and K % 4 == 0 and _C.gemm2_supported(1, 1, 7, N, K, 3 * Tp)):
         g.buf.add_(dy.t() @ x)
         return
-    a = _split(dy, PAT_A, rows=True, pad_rows=64)
+    a = dys if dys is not None else _split(dy, PAT_A, rows=True, pad_rows=64)
     b = _split(x, PAT_B, rows=True, pad_rows=64)
     sp = _C.gemm2_splits(N, K, 3 * Tp)
     ws = hip._workspace(sp * N * K, dy.device)
@@ -106,9 +126,10 @@ class _Linear32(torch.autograd.Function):
     def backward(ctx, dy):
         x2, w, b = ctx.saved_tensors
         dy2 = dy.reshape(-1, w.shape[0]).contiguous()
-        dx = mm_dgrad(dy2, w).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+        sc, sr = _split_grad(dy2, ctx.needs_input_grad[0])
+        dx = mm_dgrad(dy2, w, sc).view(ctx.xshape) if ctx.needs_input_grad[0] else None
         gw, gb = _Grad(w), _Grad(b)
-        wgrad_(gw, dy2, x2)
+        wgrad_(gw, dy2, x2, sr)
         _colsum_(gb, dy2)
         return dx, gw.done(), gb.done()
 
@@ -135,8 +156,9 @@ class _LinearGelu32(torch.autograd.Function):
         _C.epi32(dg.reshape(y.shape).contiguous(), None, y, da, 4, 0.0, 0)
         gw, gb = _Grad(w), _Grad(b)
         _colsum_(gb, da)
-        dx = mm_dgrad(da, w).view(ctx.xshape) if ctx.needs_input_grad[0] else None
-        wgrad_(gw, da, x2)
+        sc, sr = _split_grad(da, ctx.needs_input_grad[0])
+        dx = mm_dgrad(da, w, sc).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+        wgrad_(gw, da, x2, sr)
         return dx, gw.done(), gb.done()
 
 
@@ -173,8 +195,9 @@ class _DenseResidualLN32(torch.autograd.Function):
             dy = torch.empty_like(dz)
             _C.dropout32(dz, dy, ctx.p, _s64(ctx.seed))
         _colsum_(gb, dy)
-        dx = mm_dgrad(dy, w).view(ctx.xshape) if ctx.needs_input_grad[0] else None
-        wgrad_(gw, dy, x2)
+        sc, sr = _split_grad(dy, ctx.needs_input_grad[0])
+        dx = mm_dgrad(dy, w, sc).view(ctx.xshape) if ctx.needs_input_grad[0] else None
+        wgrad_(gw, dy, x2, sr)
         return dx, gw.done(), gb.done(), dz.view(dout.shape), gg.done(), gbe.done(), None, None, None
 
 

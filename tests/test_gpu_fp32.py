@@ -59,6 +59,23 @@ def _grads(fn, *args):
     return out.detach(), [a.grad.detach().clone() for a in args if isinstance(a, torch.Tensor) and a.requires_grad]
 
 
+@pytest.mark.parametrize("R,C", [(4096, 1024), (128, 772), (64, 3072)])
+def test_split3_dual_matches_two_splits(gpu, R, C):
+    """split3_dual (both layouts of a linear layer's incoming gradient from one read) == two split3 passes, bit for
+    bit, for the 16-B (C % 8 == 0) and 8-B paths."""
+    from huggingface_sagemaker_tensorflow_distributed_amd.ops import hip32
+
+    x = torch.randn(R, C, device=gpu) * 3.0
+    cols = torch.empty(R, 3 * C, device=gpu, dtype=torch.bfloat16)
+    rows = torch.empty(3 * R, C, device=gpu, dtype=torch.bfloat16)
+    hip32._C.split3_dual(x, cols, hip32.PAT_A, rows, hip32.PAT_B)
+    assert torch.equal(cols, hip32._split(x, hip32.PAT_A))
+    assert torch.equal(rows, hip32._split(x, hip32.PAT_B, rows=True))
+    hi, lo = cols[:, :C].float(), cols[:, 2 * C:].float()
+    assert torch.equal(cols[:, :C], cols[:, C:2 * C])
+    assert float((hi + lo - x).abs().max()) <= 2.0 ** -16 * float(x.abs().max())
+
+
 @pytest.mark.parametrize("path", ["mfma", "valu"])
 @pytest.mark.parametrize("p", [0.0, 0.1])
 @pytest.mark.parametrize("S", [128, 512])
