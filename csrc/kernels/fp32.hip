@@ -178,9 +178,9 @@ __global__ __launch_bounds__(256) void dropout32_kernel(const float* __restrict_
   }
 }
 
-// column sums: dbias[n] += Σ_m x[m][n]. Block: 64 columns x 4 row groups; one atomic per column per block.
-__global__ __launch_bounds__(256) void colsum32_kernel(const float* __restrict__ x, float* __restrict__ dbias, int M,
-                                                       int N, int rows_per_block) {
+// column sums: dbias[n] += Σ_m x[m][n]. Block: 64 columns x 4 row groups; one atomic per column per block (N % 4 != 0)
+__global__ __launch_bounds__(256) void colsum32_scalar_kernel(const float* __restrict__ x, float* __restrict__ dbias,
+                                                              int M, int N, int rows_per_block) {
   __shared__ float red[4][64];
   const int c = blockIdx.x * 64 + (threadIdx.x & 63), rg = threadIdx.x >> 6;
   const int r0 = blockIdx.y * rows_per_block, r1 = min(M, r0 + rows_per_block);
@@ -191,6 +191,37 @@ __global__ __launch_bounds__(256) void colsum32_kernel(const float* __restrict__
   __syncthreads();
   if (rg == 0 && c < N) atomicAdd(dbias + c, red[0][threadIdx.x] + red[1][threadIdx.x] + red[2][threadIdx.x] +
                                                  red[3][threadIdx.x]);
+}
+
+// N % 4 == 0: block = 256 columns x 4 row groups, >= 64 rows per block (fewer, longer blocks: each ends with 256
+// column atomics)
+__global__ __launch_bounds__(256) void colsum32_kernel(const float* __restrict__ x, float* __restrict__ dbias, int M,
+                                                       int N, int rows_per_block) {
+  // 16-B column chunks (4 columns per lane, 256 per block row group), four rows' loads in flight per lane
+  __shared__ f32x4 red[4][64];
+  const int lane = threadIdx.x & 63, rg = threadIdx.x >> 6;
+  const int c = (blockIdx.x * 64 + lane) * 4;
+  const int r0 = blockIdx.y * rows_per_block, r1 = min(M, r0 + rows_per_block);
+  f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+  if (c < N) {
+    const float* xc = x + c;
+    int r = r0 + rg;
+    for (; r + 12 < r1; r += 16) {
+      const f32x4 a0 = *reinterpret_cast<const f32x4*>(xc + (int64_t)r * N);
+      const f32x4 a1 = *reinterpret_cast<const f32x4*>(xc + (int64_t)(r + 4) * N);
+      const f32x4 a2 = *reinterpret_cast<const f32x4*>(xc + (int64_t)(r + 8) * N);
+      const f32x4 a3 = *reinterpret_cast<const f32x4*>(xc + (int64_t)(r + 12) * N);
+      acc += (a0 + a1) + (a2 + a3);
+    }
+    for (; r < r1; r += 4) acc += *reinterpret_cast<const f32x4*>(xc + (int64_t)r * N);
+  }
+  red[rg][lane] = acc;
+  __syncthreads();
+  if (rg == 0 && c < N) {
+    const f32x4 t = (red[0][lane] + red[1][lane]) + (red[2][lane] + red[3][lane]);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) atomicAdd(dbias + c + e, t[e]);
+  }
 }
 
 // ------------------------------------------------------------------------------------------------ LayerNorm
@@ -778,10 +809,19 @@ void launch_dropout32(const float* x, float* out, int64_t n, int W, double p, ui
 }
 
 void launch_colsum32(const float* x, float* dbias, int M, int N, hipStream_t st) {
+  if (N % 4 == 0) {
+    const int gx = (N + 255) / 256;
+    const int gy = std::max(1, std::min(std::min(1024, 2048 / gx), (M + 63) / 64));
+    const int rpb = (M + gy - 1) / gy;
+    hipLaunchKernelGGL(f32k::colsum32_kernel, dim3(gx, (M + rpb - 1) / rpb), dim3(256), 0, st, x, dbias, M, N, rpb);
+    HSD_CHECK_LAUNCH();
+    return;
+  }
   const int gx = (N + 63) / 64;
   const int gy = std::max(1, std::min(1024, 2048 / gx));
   const int rpb = (M + gy - 1) / gy;
-  hipLaunchKernelGGL(f32k::colsum32_kernel, dim3(gx, (M + rpb - 1) / rpb), dim3(256), 0, st, x, dbias, M, N, rpb);
+  hipLaunchKernelGGL(f32k::colsum32_scalar_kernel, dim3(gx, (M + rpb - 1) / rpb), dim3(256), 0, st, x, dbias, M, N,
+                     rpb);
   HSD_CHECK_LAUNCH();
 }
 

@@ -59,6 +59,20 @@ def _grads(fn, *args):
     return out.detach(), [a.grad.detach().clone() for a in args if isinstance(a, torch.Tensor) and a.requires_grad]
 
 
+@pytest.mark.parametrize("M,N", [(4096, 1024), (4096, 4096), (300, 36), (64, 2), (1000, 772), (3, 1028)])
+def test_colsum32_accumulates_column_sums(gpu, M, N):
+    """colsum32 (the fp32 bias gradients): dbias += column sums, 16-B path (N % 4 == 0) and scalar path."""
+    from huggingface_sagemaker_tensorflow_distributed_amd.ops import hip32
+
+    x = torch.randn(M, N, device=gpu)
+    d = torch.randn(N, device=gpu)
+    want = d.double() + x.double().sum(0)
+    hip32._C.colsum32(x, d)
+    torch.cuda.synchronize()
+    err = float((d.double() - want).abs().max())
+    assert err <= 1e-5 * max(1.0, float(x.abs().sum(0).max())), err
+
+
 @pytest.mark.parametrize("R,C", [(4096, 1024), (128, 772), (64, 3072)])
 def test_split3_dual_matches_two_splits(gpu, R, C):
     """split3_dual (both layouts of a linear layer's incoming gradient from one read) == two split3 passes, bit for
