@@ -22,7 +22,7 @@ from huggingface_sagemaker_tensorflow_distributed_amd import data as hdata  # no
 from huggingface_sagemaker_tensorflow_distributed_amd.parallel import backend, rccl_env  # noqa: E402
 from huggingface_sagemaker_tensorflow_distributed_amd.parallel.collectives import params_in_sync  # noqa: E402
 from huggingface_sagemaker_tensorflow_distributed_amd.train.runner import build  # noqa: E402
-from huggingface_sagemaker_tensorflow_distributed_amd.utils.args import batch_size_arg, build_parser  # noqa: E402
+from huggingface_sagemaker_tensorflow_distributed_amd.utils.args import batch_size_arg, bool_or_auto, build_parser  # noqa: E402
 
 METRIC = "sequences/sec (whole node) BERT-base seq128 at 1/2/4/8 MI355X"
 BASELINE_VALUE = None  # the reference publishes no number
@@ -46,12 +46,17 @@ def main():
                          "own precision (scripts/train.py:113-123 sets no mixed-precision policy) on the fp32 kernels "
                          "of ops/hip32.py")
     ap.add_argument("--task", choices=["sequence-classification", "masked-lm"], default="sequence-classification")
-    ap.add_argument("--hip_graph", action="store_true", help="replay fwd+bwd from a captured HIP graph (N=1)")
+    ap.add_argument("--hip_graph", type=bool_or_auto, default="auto",
+                    help="replay the whole step from a captured HIP graph (N=1); auto = the CLI's rule (launch-bound "
+                         "steps of <= 2,048 tokens only: off for the headline's 131,072)")
     a = ap.parse_args()
 
     world_env = int(os.environ.get("WORLD_SIZE", "1"))
     if a.gpus != world_env:
-        print(f"warning: --gpus {a.gpus} but WORLD_SIZE={world_env}; using WORLD_SIZE", file=sys.stderr)
+        # a world-1 number printed for `--gpus 8` would be recorded as the 8-GPU point of the scaling curve
+        print(f"bench: --gpus {a.gpus} but WORLD_SIZE={world_env}: launch N ranks with torch.distributed.run "
+              f"--nproc-per-node {a.gpus}", file=sys.stderr, flush=True)
+        sys.exit(2)
     targs, _ = build_parser("train").parse_known_args(
         ["--model_name_or_path", a.model, "--train_batch_size", str(a.batch_size), "--dtype", a.dtype,
          "--task", a.task, "--hip_graph", str(a.hip_graph),

@@ -988,6 +988,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm2_supported", &gemm2_supported);
   m.def("gemm2_set_diag", &gemm2_set_diag);
   m.def("attn128_set_diag", &attn128_set_diag);
+  m.def("attn_set_force_generic", &hsd::attn_set_force_generic);
   m.def("transpose_many", &transpose_many);
   m.def("xent", &xent, py::arg("logits"), py::arg("labels"), py::arg("dlogits"), py::arg("stats"),
         py::arg("n_valid"), py::arg("V") = 0);

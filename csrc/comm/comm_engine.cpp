@@ -92,15 +92,34 @@ class CommEngine {
     HIP_OK(hipEventCreateWithFlags(&ready_, hipEventDisableTiming));
   }
 
-  ~CommEngine() { close(); }
+  ~CommEngine() { close_impl(false); }
 
   // Drain, then release the communicator (idempotent); the stream and events are left to process teardown (the
-  // caching allocator may still hold blocks whose last use was recorded on this stream). Python may run this from
-  // its cyclic garbage collector at any allocation -- also while this thread captures a HIP graph, where a stream
-  // synchronisation or a device free is an unsafe call that invalidates the capture (a corrupt graph: a host fault
-  // at replay). The thread's capture mode is relaxed around the teardown.
-  void close() {
+  // caching allocator may still hold blocks whose last use was recorded on this stream).
+  // Captures: synchronising a stream that is itself being captured is illegal in EVERY capture mode, and the engine's
+  // stream is part of a data-parallel whole-step capture once the capture forks it. close() therefore checks its own
+  // stream first: inside such a capture it refuses (Python's close() raises; the destructor leaves the communicator to
+  // process exit rather than corrupting the graph). When only ANOTHER stream of this thread captures (Python's cyclic
+  // collector may run a finaliser in the middle of any capture; train/graph.py also turns it off there), syncing the
+  // engine's own stream is legal in relaxed mode only, so the thread's mode is relaxed around the teardown.
+  void close() { close_impl(true); }
+
+  bool stream_capturing() const {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    return stream_ != nullptr && hipStreamIsCapturing(stream_, &st) == hipSuccess && st == hipStreamCaptureStatusActive;
+  }
+
+  void close_impl(bool strict) {
     if (comm_ == nullptr) return;
+    if (stream_capturing()) {
+      if (strict) {
+        throw std::runtime_error("CommEngine.close(): the comm stream is being captured into a HIP graph; close the "
+                                 "engine after the capture ends");
+      }
+      fprintf(stderr, "CommEngine: destroyed while its stream is captured; the communicator is left to process exit\n");
+      comm_ = nullptr;
+      return;
+    }
     hipStreamCaptureMode mode = hipStreamCaptureModeRelaxed;
     const bool swapped = hipThreadExchangeStreamCaptureMode(&mode) == hipSuccess;
     if (stream_) (void)hipStreamSynchronize(stream_);

@@ -81,22 +81,13 @@ void launch_adam(float* p, float* m, float* v, const void* g, bool grad_bf16, bf
                  const uint8_t* decay, int64_t n, float step, float eps, float b1, float b2, float gscale,
                  float lr_wd, const float* coef, hipStream_t stream) {
   int64_t n4 = n / 4;  // n is a multiple of 1024 (FlatParamStore)
-  const int U = HSD_KNOB("HSD_ADAM_UNROLL", 2);  // A/B: chunks per thread per trip (1, 2 or 4)
   int threads = 256;
   int64_t blocks = (n4 + threads - 1) / threads;
   if (blocks > 256 * 8) blocks = 256 * 8;  // grid-stride: 8 blocks (32 waves) per CU over 256 CUs
-#define HSD_ADAM(GB, WB)                                                                                         \
-  do {                                                                                                           \
-    if (U >= 4)                                                                                                  \
-      hipLaunchKernelGGL((adam_kernel<GB, WB, 4>), dim3((unsigned)blocks), dim3(threads), 0, stream, p, m, v, g, \
-                         out_bf16, decay, n4, step, eps, b1, b2, gscale, lr_wd, coef);                                 \
-    else if (U == 2)                                                                                             \
-      hipLaunchKernelGGL((adam_kernel<GB, WB, 2>), dim3((unsigned)blocks), dim3(threads), 0, stream, p, m, v, g, \
-                         out_bf16, decay, n4, step, eps, b1, b2, gscale, lr_wd, coef);                                 \
-    else                                                                                                         \
-      hipLaunchKernelGGL((adam_kernel<GB, WB, 1>), dim3((unsigned)blocks), dim3(threads), 0, stream, p, m, v, g, \
-                         out_bf16, decay, n4, step, eps, b1, b2, gscale, lr_wd, coef);                                 \
-  } while (0)
+  // two 16-B chunks per thread per trip (1 and 4 measured slower: profiles/bench_adam_r2.json)
+#define HSD_ADAM(GB, WB)                                                                                       \
+  hipLaunchKernelGGL((adam_kernel<GB, WB, 2>), dim3((unsigned)blocks), dim3(threads), 0, stream, p, m, v, g, \
+                     out_bf16, decay, n4, step, eps, b1, b2, gscale, lr_wd, coef)
   if (grad_bf16) {
     if (out_bf16) HSD_ADAM(true, true); else HSD_ADAM(true, false);
   } else {

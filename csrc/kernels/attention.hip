@@ -381,9 +381,14 @@ void launch_attnS_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, con
                       bf16_t* dqkv, float* delta_ws, float* dbias, int B, int S, int heads, double p, uint64_t seed,
                       hipStream_t st, Q8Out q8o, int qfmt, const uint32_t* kmask, bool delta_ready);
 
+// Tests only (attn_set_force_generic, tests/test_gpu_ops.py): route every S to the tiled generic kernels below, the
+// independent implementation the S = 128 / streaming kernels are checked against. Not an environment knob.
+static bool g_attn_force_generic = false;
+void attn_set_force_generic(bool on) { g_attn_force_generic = on; }
+
 // S in 256..1024 (multiple of 128) runs the streaming kernels of attentionS.hip; its backward takes
 // an fp32 [B*heads*S] scratch (no zeroing) where the generic kernel takes a zeroed [B*S, H] dq accumulator.
-bool attn_streaming(int S) { return attnS_supported(S, kD) && !HSD_KNOB("HSD_ATTN_GENERIC", 0); }
+bool attn_streaming(int S) { return attnS_supported(S, kD) && !g_attn_force_generic; }
 
 // the streaming (S > 128) kernels only: at S = 128 the one-workgroup forward is memory-bound with four workgroups per
 // CU, and writing the bits cost it more (+27 us at bert-base B = 1024, plus a lost workgroup per CU) than the
@@ -396,7 +401,7 @@ int64_t attn_keep_mask_numel(int B, int S, int heads) {
 
 void launch_attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* lse2, int B, int S, int heads,
                      double p, uint64_t seed, hipStream_t st, uint32_t* kmask) {
-  if (attn128_supported(S, kD) && !HSD_KNOB("HSD_ATTN_GENERIC", 0)) {
+  if (attn128_supported(S, kD) && !g_attn_force_generic) {
     launch_attn128_fwd(qkv, mask, out, lse2, B, heads, p, seed, st);
     return;
   }
@@ -414,7 +419,7 @@ void launch_attn_fwd(const bf16_t* qkv, const float* mask, bf16_t* out, float* l
 void launch_attn_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
                      bf16_t* dqkv, float* dq_acc, float* dbias, int B, int S, int heads, double p, uint64_t seed,
                      hipStream_t st, const uint32_t* kmask, bool delta_ready) {
-  if (attn128_supported(S, kD) && !HSD_KNOB("HSD_ATTN_GENERIC", 0)) {
+  if (attn128_supported(S, kD) && !g_attn_force_generic) {
     launch_attn128_bwd(qkv, mask, o, dout, lse2, dqkv, dbias, B, heads, p, seed, st);
     return;
   }

@@ -1,7 +1,7 @@
 // Self-attention for S == 128, head_dim 64 (the headline BERT-base seq-128 config; SURVEY.md §2.10
 // K4-K7 forward, K14 backward): ONE workgroup per (batch, head) holds the whole 128x128 problem, so
 // Q/K/V/dO are read from HBM exactly once and probabilities never leave registers; the forward synchronises
-// once after the operand DMA, the backward once per query block (V3, below) plus its phase changes.
+// once after the operand DMA, the backward once per query block (below) plus its phase changes.
 //
 // * operands are staged HBM -> LDS with global_load_lds_dwordx4 (1 KiB per wave instruction) into
 //   [128][64] bf16 images whose 16-B chunks are XOR-swizzled (chunk ^ bitrev3((row>>1)&7)) — the
@@ -13,10 +13,11 @@
 //   accumulator as the B operand, O staged through a wave-private LDS slice to 128-B row stores.
 // * backward: wave w owns keys 32w..32w+31 on the lanes; loops over 4 query blocks recomputing P from
 //   the saved log-sum-exp, accumulates dKᵀ, dVᵀ in registers, writes dS once, then dQᵀ = Kᵀ·dSᵀ with wave w
-//   owning queries 32w..32w+31. V3 (default): the dS of query block qb ([128 key][32 q], 64-B rows, 8-B units
-//   swizzled by key) is written over the Q / dO rows of that block once every wave is past it (one barrier per
-//   block), K has its own slot (re-read per block instead of held in VGPRs): 52.5 KiB of LDS and 168 VGPRs, three
-//   workgroups per CU (HSD_A128_BWD_V3=0: the [128 key][128 q] dS image, 68.5 KiB, two per CU). The dropout hash of
+//   owning queries 32w..32w+31. The dS of query block qb ([128 key][32 q], 64-B rows, 8-B units swizzled by key) is
+//   written over the Q / dO rows of that block once every wave is past it (one barrier per block), K has its own
+//   slot (re-read per block instead of held in VGPRs): 52.5 KiB of LDS and 168 VGPRs, three workgroups per CU (the
+//   round-4 [128 key][128 q] dS image took 68.5 KiB, two per CU: 422 -> 371-376 us, profiles/attn128_bwd_v3_ab_r5.log).
+//   The dropout hash of
 //   a key pair is computed once per lane pair and exchanged (keys sit on adjacent lanes here).
 // Dropout / mask / lse conventions are identical to attention.hip (ops/rng.py site indexing).
 #include "attn_common.h"
@@ -128,7 +129,7 @@ __global__ __launch_bounds__(256, 4) void attn128_fwd_kernel(const bf16_t* __res
 }
 
 // ------------------------------------------------------------------------------------------------
-// dS block image (V3): the dS of query block qb, [128 keys][32 queries] bf16, lives in the dead rows of that block in the
+// dS block image: the dS of query block qb, [128 keys][32 queries] bf16, lives in the dead rows of that block in the
 // Q image (keys 0-63) and the dO image (keys 64-127): 64-B rows, 8-B unit u of key row k stored at u ^ ((k >> 1) & 7) --
 // conflict-free for the b64 writes (16 consecutive keys per lane group) and for the dQ phase's tr reads (4 whole rows
 // per 32 lanes)
@@ -137,12 +138,11 @@ __device__ __forceinline__ int dsoff(int key, int qc) {
   return k * 32 + ((((qc >> 2) ^ (k >> 1)) & 7) << 2) + (qc & 3);
 }
 
-// V3 = false: [Q | dO | dS | ...] = 68.5 KiB, two workgroups per CU. V3 = true: dS of query block qb is written (one
-// barrier per block) over the Q / dO rows of that block, which no wave reads again; K gets its own slot, written from
-// the registers at the start, and serves as the output staging after the dQ phase: 52.5 KiB and <= 168 VGPRs, three
-// workgroups (twelve waves) per CU.
-template <bool DROP, bool V3>
-__global__ __launch_bounds__(256, V3 ? 3 : 2) void attn128_bwd_kernel(const bf16_t* __restrict__ qkv,
+// dS of query block qb is written (one barrier per block) over the Q / dO rows of that block, which no wave reads
+// again; K gets its own slot, written from the registers at the start, and serves as the output staging after the dQ
+// phase: 52.5 KiB and <= 168 VGPRs, three workgroups (twelve waves) per CU.
+template <bool DROP>
+__global__ __launch_bounds__(256, 3) void attn128_bwd_kernel(const bf16_t* __restrict__ qkv,
                                                              const float* __restrict__ mask,
                                                              const bf16_t* __restrict__ o,
                                                              const bf16_t* __restrict__ dout,
@@ -158,13 +158,13 @@ __global__ __launch_bounds__(256, V3 ? 3 : 2) void attn128_bwd_kernel(const bf16
     ts[0] = __builtin_amdgcn_s_memtime();
     rt0 = __builtin_amdgcn_s_memrealtime();
   }
-  // [Q | dO | dS | lse | delta | bias-grad partials]; after the main loop Q's slot holds K, dO's slot the
-  // output staging
-  constexpr int kImg = V3 ? 3 * S * D : 2 * S * D + S * S;
+  // [Q | dO | K | lse | delta | bias-grad partials]; dS blocks go over dead Q / dO rows, K's slot is the output
+  // staging after the dQ phase
+  constexpr int kImg = 3 * S * D;
   __shared__ __attribute__((aligned(16))) bf16_t lds[kImg + 4 * S + 2 * 3 * 4 * D + 2 * S];
   bf16_t* Qs = lds;
   bf16_t* dOs = lds + S * D;
-  bf16_t* dSt = lds + 2 * S * D;  // V3: K's slot
+  bf16_t* dSt = lds + 2 * S * D;  // K's slot
   float* lse_s = reinterpret_cast<float*>(lds + kImg);
   float* del_s = lse_s + S;
   float* bsum = del_s + S;  // [3 (q,k,v)][4 waves][64]
@@ -202,11 +202,9 @@ __global__ __launch_bounds__(256, V3 ? 3 : 2) void attn128_bwd_kernel(const bf16
     if (tid < S) rw_s[tid] = dropout_row((uint32_t)(bh * S + tid), dp);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  if constexpr (V3) {
-    // K -> its own slot now (dQ phase operand); visible to every wave after the barriers below
+  // K -> its own slot now (dQ phase operand); visible to every wave after the barriers below
 #pragma unroll
-    for (int s = 0; s < 4; ++s) *reinterpret_cast<bf16x8*>(dSt + toff(key, 16 * s + 8 * hf)) = kf[s];
-  }
+  for (int s = 0; s < 4; ++s) *reinterpret_cast<bf16x8*>(dSt + toff(key, 16 * s + 8 * hf)) = kf[s];
   __syncthreads();
   if (diag) ts[1] = __builtin_amdgcn_s_memtime();
   {
@@ -251,28 +249,26 @@ __global__ __launch_bounds__(256, V3 ? 3 : 2) void attn128_bwd_kernel(const bf16
   // the even lane computes query qi0's word, the odd lane query qi0 + 1's, and they swap (one DPP move)
   const uint32_t ck = drop_col((uint32_t)key >> 1);
   const int qsel = 4 * hf + (odd ? 1 : 0);
-  // V3: the previous block's packed dS, written after the next block's barrier
+  // the previous block's packed dS, written after the next block's barrier
   u32x2 dsw[4];
-  bf16_t* const dsb = key < 64 ? Qs : dOs;  // V3: region of this wave's keys (wave-uniform)
+  bf16_t* const dsb = key < 64 ? Qs : dOs;  // region of this wave's keys (wave-uniform)
   auto put_ds = [&](int blk) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) *reinterpret_cast<u32x2*>(dsb + blk * 32 * 64 + dsoff(key, 8 * i + 4 * hf)) = dsw[i];
   };
 #pragma unroll 1
   for (int qb = 0; qb < 4; ++qb) {
-    if constexpr (V3) {
-      if (qb > 0) {
-        __syncthreads();  // every wave is past block qb - 1: its Q / dO rows are dead
-        put_ds(qb - 1);
-      }
+    if (qb > 0) {
+      __syncthreads();  // every wave is past block qb - 1: its Q / dO rows are dead
+      put_ds(qb - 1);
     }
     const int qoff = qb * 32 * 64;  // element offset of the block's first row in a [rows][64] image
     f32x16 sacc = {}, dpacc = {};
 #pragma unroll
     for (int s4 = 0; s4 < 4; ++s4) {
       const bf16x8 aq = *reinterpret_cast<const bf16x8*>(Qs + qoff + off_row[s4]);
-      // V3: K fragments re-read from K's slot (16 VGPRs fewer across the loop)
-      const bf16x8 kq = V3 ? *reinterpret_cast<const bf16x8*>(dSt + toff(key, 16 * s4 + 8 * hf)) : kf[s4];
+      // K fragments re-read from K's slot (16 VGPRs fewer across the loop)
+      const bf16x8 kq = *reinterpret_cast<const bf16x8*>(dSt + toff(key, 16 * s4 + 8 * hf));
       sacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aq, kq, sacc, 0, 0, 0);
       const bf16x8 ad = *reinterpret_cast<const bf16x8*>(dOs + qoff + off_row[s4]);
       dpacc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ad, vf[s4], dpacc, 0, 0, 0);
@@ -313,15 +309,14 @@ __global__ __launch_bounds__(256, V3 ? 3 : 2) void attn128_bwd_kernel(const bf16
       dk0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr(Qs, 0), sb, dk0, 0, 0, 0);
       dk1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tr(Qs, 1), sb, dk1, 0, 0, 0);
     }
-    // dS -> [key][q] image (V3: held until the next block's barrier)
+    // dS, packed: held until the next block's barrier
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       dsw[i].x = pack_bf2(ds[4 * i], ds[4 * i + 1]);
       dsw[i].y = pack_bf2(ds[4 * i + 2], ds[4 * i + 3]);
-      if constexpr (!V3) *reinterpret_cast<u32x2*>(dSt + soff(key, qb * 32 + 8 * i + 4 * hf)) = dsw[i];
     }
   }
-  if constexpr (V3) {
+  {
     __syncthreads();  // every wave is past block 3
     put_ds(3);
     __syncthreads();  // every dS written
@@ -353,35 +348,6 @@ __global__ __launch_bounds__(256, V3 ? 3 : 2) void attn128_bwd_kernel(const bf16
     store_rows(stg, dv0, dv1, 1.0f, rowbase + 2 * H, ld, lane, dbias ? bs_w + 2 * 4 * D : nullptr);
     store_rows(stg, dk0, dk1, scale, rowbase + H, ld, lane, dbias ? bs_w + 4 * D : nullptr);
     store_rows(stg, dq0, dq1, scale, rowbase, ld, lane, bs_w);
-  } else {
-  __syncthreads();  // every dS written; Q / dO no longer read
-  if (diag) ts[3] = __builtin_amdgcn_s_memtime();
-  // K -> Q's slot for dQ, from the K fragments this wave already holds (keys 32w..32w+31, 8 consecutive d
-  // per lane and s): LDS writes instead of a second HBM/L2 read, and no s_waitcnt vmcnt before the dQ phase
-  // (a vmcnt would also wait for the dK / dV stores below, which count on the same counter).
-#pragma unroll
-  for (int s = 0; s < 4; ++s) *reinterpret_cast<bf16x8*>(Qs + toff(key, 16 * s + 8 * hf)) = kf[s];
-  // dK, dV out through this wave's staging slice (dO's slot)
-  bf16_t* stg = dOs + wave * 32 * D;
-  bf16_t* rowbase = dqkv + ((int64_t)b * S + wave * 32) * ld + hh * D;
-  float* bs_w = dbias ? bsum + wave * D : nullptr;
-  store_rows(stg, dv0, dv1, 1.0f, rowbase + 2 * H, ld, lane, dbias ? bs_w + 2 * 4 * D : nullptr);
-  store_rows(stg, dk0, dk1, scale, rowbase + H, ld, lane, dbias ? bs_w + 4 * D : nullptr);
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  asm volatile("" ::: "memory");
-  if (diag) ts[4] = __builtin_amdgcn_s_memtime();
-  // dQᵀ[d][q] = Σ_key Kᵀ[d][key] dSᵀ[key][q], wave w: queries 32w..32w+31
-  f32x16 dq0 = {}, dq1 = {};
-#pragma unroll
-  for (int kb = 0; kb < 4; ++kb)
-#pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      const bf16x8 bs = trS(dSt, kb * 32, s, wave * 32, lane);
-      dq0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(Qs, kb * 32, s, 0, lane), bs, dq0, 0, 0, 0);
-      dq1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(trA(Qs, kb * 32, s, 1, lane), bs, dq1, 0, 0, 0);
-    }
-  store_rows(stg, dq0, dq1, scale, rowbase, ld, lane, bs_w);
   }
   if (dbias) {
     // qkv bias gradient: column sums of this (batch, head)'s dQ | dK | dV, one atomic per column
@@ -425,16 +391,12 @@ void launch_attn128_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, c
   DropoutParams dp = make_dropout(p, seed);
   const float sl2 = a128::kLog2e / sqrtf((float)a128::D);
   const float scale = 1.0f / sqrtf((float)a128::D);
-  // HSD_A128_BWD_V3=0: the two-workgroups-per-CU layout (A/B)
-  const bool v3 = HSD_KNOB("HSD_A128_BWD_V3", 1) != 0;
   auto go = [&](auto kern) {
     hipLaunchKernelGGL(kern, dim3(B * heads), dim3(256), 0, st, qkv, mask, o, dout, lse2, dqkv, dbias, heads, sl2,
                        scale, dp, g_a128_diag);
   };
-  if (dp.enabled)
-    v3 ? go(a128::attn128_bwd_kernel<true, true>) : go(a128::attn128_bwd_kernel<true, false>);
-  else
-    v3 ? go(a128::attn128_bwd_kernel<false, true>) : go(a128::attn128_bwd_kernel<false, false>);
+  if (dp.enabled) go(a128::attn128_bwd_kernel<true>);
+  else go(a128::attn128_bwd_kernel<false>);
   HSD_CHECK_LAUNCH();
 }
 

@@ -409,12 +409,12 @@ void launch_embed_bwd(const bf16_t* dout, const int64_t* ids, const int64_t* pos
                       const float* mean, const float* rstd, float* gword, float* gpos, float* gtype, float* ggamma,
                       float* gbeta, int B, int S, int H, int pos_is_arange, double p, uint64_t seed, hipStream_t st) {
   DropoutParams dp = make_dropout(p, seed);
-  if (H % 8 == 0 && H <= 1024 && !HSD_KNOB("HSD_EMBED_BWD_SCALAR", 0)) {
-    // ~HSD_EMBED_BWD_BLOCKS blocks (at least one per position): every block ends with 3-4 x H column atomics
+  if (H % 8 == 0 && H <= 1024) {  // 16-B kernel (957 -> 414 us vs the round-1 scalar one, kept for other H)
+    // ~512 blocks (at least one per position): every block ends with 3-4 x H column atomics
     // (gamma / beta / position / type partials) on the same H addresses, so fewer, longer blocks win: 512 measured
     // best or within 3 % of best at all four shapes of tools/embed_bwd_probe.py (2048 before: bert-large B = 8
     // 81 -> 35 us, bert-base B = 32 120 -> 34 us, B = 1024 421 -> 393 us; profiles/embed_bwd_blocks_r5.log)
-    const int target = max(1, HSD_KNOB("HSD_EMBED_BWD_BLOCKS", 512));
+    const int target = 512;
     int chunks = max(1, min(B, (target + S - 1) / S));
     int bpc = (B + chunks - 1) / chunks;
     chunks = (B + bpc - 1) / bpc;

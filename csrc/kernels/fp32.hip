@@ -193,7 +193,7 @@ __global__ __launch_bounds__(256) void colsum32_scalar_kernel(const float* __res
                                                  red[3][threadIdx.x]);
 }
 
-// N % 4 == 0: block = 256 columns x 4 row groups, >= HSD_COLSUM_MIN_ROWS (256) rows per block: every block ends with
+// N % 4 == 0: block = 256 columns x 4 row groups, >= 256 rows per block: every block ends with
 // 256 column atomics on the same addresses, so few long blocks win (4096 x 1024: 51 us at 4 rows, 5.6 at 256;
 // profiles/colsum32_rows_r5.log)
 __global__ __launch_bounds__(256) void colsum32_kernel(const float* __restrict__ x, float* __restrict__ dbias, int M,
@@ -812,7 +812,7 @@ void launch_dropout32(const float* x, float* out, int64_t n, int W, double p, ui
 void launch_colsum32(const float* x, float* dbias, int M, int N, hipStream_t st) {
   if (N % 4 == 0) {
     const int gx = (N + 255) / 256;
-    const int min_rows = std::max(4, HSD_KNOB("HSD_COLSUM_MIN_ROWS", 256));
+    const int min_rows = 256;
     const int gy = std::max(1, std::min(std::min(1024, 2048 / gx), (M + min_rows - 1) / min_rows));
     const int rpb = (M + gy - 1) / gy;
     hipLaunchKernelGGL(f32k::colsum32_kernel, dim3(gx, (M + rpb - 1) / rpb), dim3(256), 0, st, x, dbias, M, N, rpb);

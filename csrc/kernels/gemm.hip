@@ -165,18 +165,20 @@ __device__ __forceinline__ void epi_block(const f32x16& a, int mb, int nb, int l
         *reinterpret_cast<u32x2*>(p.C2 + co) = g;
         continue;
       } else if constexpr (EPI == EPI_BIAS_DROP_RES) {
-        // y = bf16(acc + b); yd = bf16(y * keep * scale); z = bf16(yd + residual)
+        // y = bf16(acc + b); z = bf16(y * keep * scale + residual): ONE rounding of the sum, exactly as gemm2 / gemm8's
+        // E2_BIAS_DROP_RES (gemm_common.h epi_chunk), so a dropout + residual site gives the same bits on every path
 #pragma unroll
         for (int e = 0; e < 4; ++e) v[e] = bf2f(f2bf(v[e]));
         if (p.dp.enabled) {
           uint32_t b0, b1;
           dropout_bits4((uint32_t)m, (uint32_t)n, p.dp, b0, b1);  // mask row m of width N, n % 4 == 0
-          v[0] = bf2f(f2bf(v[0] * keep_factor(b0, 0, p.dp)));
-          v[1] = bf2f(f2bf(v[1] * keep_factor(b0, 1, p.dp)));
-          v[2] = bf2f(f2bf(v[2] * keep_factor(b1, 0, p.dp)));
-          v[3] = bf2f(f2bf(v[3] * keep_factor(b1, 1, p.dp)));
+          v[0] = __builtin_fmaf(v[0], keep_factor(b0, 0, p.dp), lo_bf(xw[q4].x));
+          v[1] = __builtin_fmaf(v[1], keep_factor(b0, 1, p.dp), hi_bf(xw[q4].x));
+          v[2] = __builtin_fmaf(v[2], keep_factor(b1, 0, p.dp), lo_bf(xw[q4].y));
+          v[3] = __builtin_fmaf(v[3], keep_factor(b1, 1, p.dp), hi_bf(xw[q4].y));
+        } else {
+          v[0] += lo_bf(xw[q4].x); v[1] += hi_bf(xw[q4].x); v[2] += lo_bf(xw[q4].y); v[3] += hi_bf(xw[q4].y);
         }
-        v[0] += lo_bf(xw[q4].x); v[1] += hi_bf(xw[q4].x); v[2] += lo_bf(xw[q4].y); v[3] += hi_bf(xw[q4].y);
       } else if constexpr (EPI == EPI_RES) {
         v[0] += lo_bf(xw[q4].x); v[1] += hi_bf(xw[q4].x); v[2] += lo_bf(xw[q4].y); v[3] += hi_bf(xw[q4].y);
       } else if constexpr (EPI == EPI_DGELU) {
@@ -464,7 +466,8 @@ void launch_gemm(int la, int lb, int epi, const bf16_t* A, int64_t lda, const bf
   p.A = A; p.lda = lda; p.B = B; p.ldb = ldb; p.M = M; p.N = N; p.K = K; p.C = C; p.ldc = ldc;
   p.bias = bias; p.aux = aux; p.ldaux = ldaux; p.C2 = C2;
   p.dp = make_dropout(p_drop, seed);
-  const bool dma = (K % 64 == 0) && (M >= 128) && (N >= 128) && !HSD_KNOB("HSD_GEMM_V1", 0);
+  // the v2 (LDS-DMA) kernel where the shape tiles it; the v1 register-staged kernel for the rest (K % 64, tiny M / N)
+  const bool dma = (K % 64 == 0) && (M >= 128) && (N >= 128);
   if (dma) {
     if (epi == EPI_F32_ATOMIC) {
       if (la == 1 && lb == 1) { gemm_dma_launch<1, 1, EPI_F32_ATOMIC, 256, 128, 4, 2>(p, splits, st); return; }

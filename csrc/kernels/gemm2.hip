@@ -1246,7 +1246,7 @@ __global__ __launch_bounds__(256 * KW, (NSTG <= 2 && KW == 1) ? 2 : 1) void gemm
 // every BERT shape (tools/gemm_probe.py, profiles/gemm_probe_r1_sync.json). TT (weight gradients), once its LDS-DMA
 // stopped draining every K-tile (dma_lds_asm): 1,018-1,134 TFLOP/s vs 920-1,065 for SYNC 7 and 979-1,074 for SYNC 0
 // on the four bert-base weights (tools/tt_probe.py, profiles/tt_probe_r3_sync_splits.json). HSD_G2_SYNC overrides
-// for A/B runs; HSD_G2_NT=0 makes the bf16 epilogue stores plain (default: non-temporal, st16nt).
+// for A/B runs; the bf16 epilogue stores are non-temporal (st16nt).
 static int g2_sync_mode(int la, int K) {
   const int e = HSD_KNOB("HSD_G2_SYNC", kKnobUnset);
   (void)la;
@@ -1328,8 +1328,7 @@ static void g2pk_launch(const G2Params& p0, hipStream_t st) {
   p.ntiles = tiles_m * p.tiles_n;
   p.kps = p.K;
   if (p.K % g2::BK) abort();
-  // HSD_G2_GRID, diagnostic (tools/epi_probe2.py): cap the persistent grid (multiple of 8)
-  const int grid = std::min(p.ntiles, HSD_KNOB("HSD_G2_GRID", g2_num_cus() & ~7));
+  const int grid = std::min(p.ntiles, g2_num_cus() & ~7);
   p.tq = g2_tq_slot(st);
   hipLaunchKernelGGL((g2::gemm2pk_kernel<EPI, BN>), dim3(grid), dim3(512), 0, st, p);
   HSD_CHECK_LAUNCH();
@@ -1361,7 +1360,7 @@ static void g8pk_launch(const G2Params& p0, const float* sa, const float* sb, hi
 // even leading dimensions; fa: A format (0 e4m3, 1 e5m2), B e4m3.
 void launch_gemm8pk(int epi, int bn, const G2Params& p0, int fa, const float* sa, const float* sb, hipStream_t st) {
   G2Params p = p0;
-  p.nt_store = HSD_KNOB("HSD_G2_NT", 1);
+  p.nt_store = 1;  // non-temporal epilogue stores (profiles/store_policy_r3.log)
   p.K /= 2;
   p.lda /= 2;
   p.ldb /= 2;
@@ -1684,7 +1683,7 @@ void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const b
   p.rd_seq = rd_seq;
   if (epi == E2_STORE_RDOT && (rd == nullptr || rd_seq <= 0 || M % rd_seq || N % 64)) abort();
   p.diag = g_diag;
-  p.nt_store = HSD_KNOB("HSD_G2_NT", 1);
+  p.nt_store = 1;  // non-temporal epilogue stores (profiles/store_policy_r3.log)
   p.A = A; p.lda = lda; p.B = B; p.ldb = ldb; p.M = M; p.N = N; p.K = K; p.C = C; p.ldc = ldc;
   p.bias = bias; p.aux = aux; p.ldaux = ldaux; p.C2 = C2;
   p.dp = make_dropout(p_drop, seed);

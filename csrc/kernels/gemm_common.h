@@ -42,7 +42,7 @@ struct G2Params {
   int tiles_n;
   int ntiles;    // tiles_m * tiles_n
   float* dbias;  // E2_DGELU: optional fp32 column sums of the output (the bias gradient), BN 256 only
-  int nt_store;  // bf16 epilogues: non-temporal stores (default; HSD_G2_NT=0 turns them off)
+  int nt_store;  // bf16 epilogues: non-temporal stores (always 1 in the step; plain stores measured slower)
   unsigned long long* diag;  // persistent NT kernel, diagnostic: per-workgroup seam timestamps (gemm2_set_diag)
   // optional fp8 copy of the bf16 output (C2 for two-output epilogues, else C) for the next fp8 GEMM: q8 [M][ldc]
   // bytes, format q8_fmt, delayed scaling from *q8_amax; 1/scale into *q8_sinv, this output's amax into *q8_track
@@ -192,20 +192,26 @@ __device__ __forceinline__ void epi_chunk(u32x4& o, u32x4& o2, const u32x4& x, i
   } else if constexpr (EPI == E2_BIAS_DROP_RES) {
     // z = bf16(y · keep · scale + residual), y = bf16(acc + bias): one rounding of the sum (the dropped value is not
     // rounded to bf16 on its own -- a pack / unpack pair per element less, and no less accurate)
+    // rounded once, as fma(y, keep ? scale : 0, residual) -- the same expression as gemm.hip's epi_block, so a site gives
+    // the same bits on every kernel path
     float v[8] = {lo_bf(o.x), hi_bf(o.x), lo_bf(o.y), hi_bf(o.y), lo_bf(o.z), hi_bf(o.z), lo_bf(o.w), hi_bf(o.w)};
+    const float r[8] = {lo_bf(x.x), hi_bf(x.x), lo_bf(x.y), hi_bf(x.y), lo_bf(x.z), hi_bf(x.z), lo_bf(x.w), hi_bf(x.w)};
     if (p.dp.enabled) {
       // mask row m (width N), pairs n / 2 + e = n / 2 ^ e (n % 8 == 0)
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const uint32_t b = drop_fin(xw ^ drop_col((uint32_t)e));
-        v[2 * e] = keep_lo(b, p.dp.thr) ? v[2 * e] * p.dp.scale : 0.f;
-        v[2 * e + 1] = keep_hi(b, p.dp.thr) ? v[2 * e + 1] * p.dp.scale : 0.f;
+        v[2 * e] = __builtin_fmaf(v[2 * e], keep_lo(b, p.dp.thr) ? p.dp.scale : 0.f, r[2 * e]);
+        v[2 * e + 1] = __builtin_fmaf(v[2 * e + 1], keep_hi(b, p.dp.thr) ? p.dp.scale : 0.f, r[2 * e + 1]);
       }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] += r[e];
     }
-    o.x = pack_bf2(v[0] + lo_bf(x.x), v[1] + hi_bf(x.x));
-    o.y = pack_bf2(v[2] + lo_bf(x.y), v[3] + hi_bf(x.y));
-    o.z = pack_bf2(v[4] + lo_bf(x.z), v[5] + hi_bf(x.z));
-    o.w = pack_bf2(v[6] + lo_bf(x.w), v[7] + hi_bf(x.w));
+    o.x = pack_bf2(v[0], v[1]);
+    o.y = pack_bf2(v[2], v[3]);
+    o.z = pack_bf2(v[4], v[5]);
+    o.w = pack_bf2(v[6], v[7]);
   } else if constexpr (EPI == E2_RES) {
     o.x = pack_bf2(lo_bf(o.x) + lo_bf(x.x), hi_bf(o.x) + hi_bf(x.x));
     o.y = pack_bf2(lo_bf(o.y) + lo_bf(x.y), hi_bf(o.y) + hi_bf(x.y));
@@ -319,7 +325,7 @@ __device__ __forceinline__ void epilogue_bf16(f32x4 (&acc)[MB][BN / 64], const G
     epi_bias_regs<EPI, BN>(bv, p, lane, nw);
   }
   bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
-  // stores: non-temporal buffer stores off the wave's first row (st16nt); p.nt_store = 0 (HSD_G2_NT=0): plain
+  // stores: non-temporal buffer stores off the wave's first row (st16nt); p.nt_store = 0: plain
   const __amdgpu_buffer_rsrc_t rc = wave_rsrc(C + (int64_t)mw * p.ldc);
   const __amdgpu_buffer_rsrc_t rc2 = wave_rsrc(epi_two_out(EPI) ? p.C2 + (int64_t)mw * p.ldc : C);
   constexpr bool kColsum = (EPI == E2_DGELU || EPI == E2_MUL) && CPR == 8;

@@ -151,6 +151,7 @@ void launch_fp8_quant(const bf16_t* x, int64_t n, float* amax, uint8_t* q, float
 void launch_fp8_quant_many(const int64_t* amax_desc, int n_amax, int amax_blocks, const int64_t* quant_desc,
                            int n_quant, int quant_blocks_total, float* amax, float* sinv, int fmt, hipStream_t st);
 int fp8_elems_per_block();
+void attn_set_force_generic(bool on);  // tests: every S on the tiled generic attention kernels
 void attn128_set_diag(void* p);  // diagnostic phase stamps of the S=128 attention backward ([B*heads][8] u64)
 void gemm2_set_diag(void* p);  // diagnostic timestamps of the persistent NT kernel ([grid][64][4] u64), nullptr = off
 void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, int M, int N,

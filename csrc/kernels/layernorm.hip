@@ -228,109 +228,10 @@ __device__ __forceinline__ void ln_bwd_row(const u32x2 (&zw)[NCH], const u32x2 (
   }
 }
 
-// Pass 1: one wave per row, 4 rows per block (high occupancy, like ln_fwd): dz (+dres_add) and dy.
-template <int NCH>
-__global__ __launch_bounds__(256) void ln_bwd_rows_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ z,
-                                                          const float* __restrict__ mean_in,
-                                                          const float* __restrict__ rstd_in,
-                                                          const bf16_t* __restrict__ gamma, bf16_t* __restrict__ dz_out,
-                                                          bf16_t* __restrict__ dy_out,
-                                                          const bf16_t* __restrict__ dres_add, int rows, int H,
-                                                          DropoutParams dp) {
-  dp = resolve_seed(dp);
-  const int lane = threadIdx.x & 63;
-  const int row = blockIdx.x * kLnWaves + (threadIdx.x >> 6);
-  if (row >= rows) return;
-  const int nq = H >> 2;
-  float gam[NCH][4], dummy_g[NCH][4], dummy_b[NCH][4], dummy_db[NCH][4];
-#pragma unroll
-  for (int i = 0; i < NCH; ++i) {
-    const int c = lane + 64 * i;
-#pragma unroll
-    for (int k = 0; k < 4; ++k) gam[i][k] = dummy_g[i][k] = dummy_b[i][k] = dummy_db[i][k] = 0.f;
-    if (c < nq) {
-      u32x2 gw = *reinterpret_cast<const u32x2*>(gamma + 4 * c);
-      gam[i][0] = lo_bf(gw.x); gam[i][1] = hi_bf(gw.x); gam[i][2] = lo_bf(gw.y); gam[i][3] = hi_bf(gw.y);
-    }
-  }
-  u32x2 za[NCH], da[NCH];
-  ln_bwd_load<NCH>(dout, z, row, H, lane, za, da);
-  // the accumulators are dead here (column sums are pass 2); the compiler drops them
-  ln_bwd_row<NCH>(za, da, mean_in[row], rstd_in[row], gam, row, H, lane, dz_out, dy_out, dres_add, dp, dummy_g,
-                  dummy_b, dummy_db);
-}
-
-// Pass 2: column sums dgamma += Σ dout·xhat, dbeta += Σ dout, dbias += Σ dy. Block = 64 column chunks
-// (8 columns) x 4 row groups, 4 rows' loads in flight per thread, LDS reduction, one atomic per column.
-__global__ __launch_bounds__(256) void ln_bwd_cols_kernel(const bf16_t* __restrict__ dout, const bf16_t* __restrict__ z,
-                                                          const float* __restrict__ mean_in,
-                                                          const float* __restrict__ rstd_in,
-                                                          const bf16_t* __restrict__ dy, float* __restrict__ dgamma,
-                                                          float* __restrict__ dbeta, float* __restrict__ dbias,
-                                                          int rows, int H, int rows_per_block) {
-  __shared__ float red[3][4][512 + 4];
-  const int cc = threadIdx.x & 63, rg = threadIdx.x >> 6;
-  const int col = blockIdx.x * 512 + cc * 8;
-  const bool active = col < H;
-  const int r0 = blockIdx.y * rows_per_block;
-  const int r1 = min(rows, r0 + rows_per_block);
-  float ag[8], ab[8], ad[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) ag[k] = ab[k] = ad[k] = 0.f;
-  if (active) {
-    for (int rb = r0 + rg; rb < r1; rb += 16) {
-      u32x4 dw[4], zw[4], yw[4];
-      float mu[4], rs[4];
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        const int r = rb + 4 * u;
-        if (r < r1) {
-          const size_t off = (size_t)r * H + col;
-          dw[u] = *reinterpret_cast<const u32x4*>(dout + off);
-          zw[u] = *reinterpret_cast<const u32x4*>(z + off);
-          if (dbias) yw[u] = *reinterpret_cast<const u32x4*>(dy + off);
-          mu[u] = mean_in[r];
-          rs[u] = rstd_in[r];
-        }
-      }
-#pragma unroll
-      for (int u = 0; u < 4; ++u) {
-        if (rb + 4 * u >= r1) continue;
-#pragma unroll
-        for (int k = 0; k < 4; ++k) {
-          const float d0 = lo_bf(dw[u][k]), d1 = hi_bf(dw[u][k]);
-          ag[2 * k] += d0 * (lo_bf(zw[u][k]) - mu[u]) * rs[u];
-          ag[2 * k + 1] += d1 * (hi_bf(zw[u][k]) - mu[u]) * rs[u];
-          ab[2 * k] += d0;
-          ab[2 * k + 1] += d1;
-          if (dbias) {
-            ad[2 * k] += lo_bf(yw[u][k]);
-            ad[2 * k + 1] += hi_bf(yw[u][k]);
-          }
-        }
-      }
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    red[0][rg][cc * 8 + k] = ag[k];
-    red[1][rg][cc * 8 + k] = ab[k];
-    red[2][rg][cc * 8 + k] = ad[k];
-  }
-  __syncthreads();
-  for (int c = threadIdx.x; c < 512; c += 256) {
-    const int gc = blockIdx.x * 512 + c;
-    if (gc >= H) continue;
-    atomicAdd(dgamma + gc, red[0][0][c] + red[0][1][c] + red[0][2][c] + red[0][3][c]);
-    atomicAdd(dbeta + gc, red[1][0][c] + red[1][1][c] + red[1][2][c] + red[1][3][c]);
-    if (dbias) atomicAdd(dbias + gc, red[2][0][c] + red[2][1][c] + red[2][2][c] + red[2][3][c]);
-  }
-}
-
 // Single pass: every wave walks `rpw` consecutive rows (next row's loads in flight while the current
 // row reduces), keeps dgamma / dbeta / dbias column partials in registers, and the block reduces its 4
 // waves' partials through LDS into one fp32 atomic per column per block. Reads dout, z once; writes
-// dz, dy once (the split rows + cols passes read dout / z twice).
+// dz, dy once (the round-1 split rows + columns passes read dout / z twice: 170 -> ~120 us at the headline shape).
 template <int NCH, int QF>
 __global__ __launch_bounds__(256) void ln_bwd_fused_kernel(const bf16_t* __restrict__ dout,
                                                            const bf16_t* __restrict__ z,
@@ -410,12 +311,11 @@ template <int NCH>
 static void ln_fwd_t(const bf16_t* y, const bf16_t* res, const bf16_t* gamma, const bf16_t* beta, bf16_t* z,
                      bf16_t* out, float* mean, float* rstd, int rows, int H, float eps, const DropoutParams& dp,
                      hipStream_t st) {
-  const int mode = HSD_KNOB("HSD_LN_FWD_RPW", 0);  // A/B: 1 = the one-row kernel; > 1 = rows per wave
-  if (mode != 1 && res == nullptr && z == nullptr && !dp.enabled && H % 8 == 0 && H <= 1024) {
+  if (res == nullptr && z == nullptr && !dp.enabled && H % 8 == 0 && H <= 1024) {
     // 2 rows per wave (the next row's loads in flight while one reduces): best at the HBM-bound headline shape
     // (131072 x 768: 75 us vs 81 us at 16 rows per wave); every setting is equal once the tensors fit the MALL
     // (tools/bench_ln_rpw.py, profiles/bench_ln_rpw_r2.jsonl)
-    const int rpw = mode > 1 ? mode : 2;
+    const int rpw = 2;
     const int waves = (rows + rpw - 1) / rpw;
     const int blocks = (waves + kLnWaves - 1) / kLnWaves;
     if (H <= 512)
@@ -450,39 +350,25 @@ static void ln_bwd_t(const bf16_t* dout, const bf16_t* z, const float* mean, con
                      bf16_t* dz, bf16_t* dy, const bf16_t* dres_add, float* dgamma, float* dbeta, float* dbias,
                      int rows, int H, const DropoutParams& dp, hipStream_t st, const Q8Out& q8o = Q8Out{},
                      int qfmt = -1) {
-  if (qfmt >= 0 || !HSD_KNOB("HSD_LN_SPLIT", 0)) {
-    // ~16 rows per wave at the headline's 131072 rows: 2048 waves = 8 per CU, a few thousand column atomics per
-    // block; at least 4 rows per wave (a floor of 2 for small row counts, twice the waves and the column atomics,
-    // measured 1-2 % slower end to end at bert-large B = 8 and bert-base B = 32: profiles/small_tiles_r2.log;
-    // HSD_LN_BWD_MIN_RPW overrides the floor)
-    const int min_rpw = std::max(1, HSD_KNOB("HSD_LN_BWD_MIN_RPW", 4));
-    const int rpw = std::max(min_rpw, (rows + 2047) / 2048);
-    const int waves = (rows + rpw - 1) / rpw;
-    const int blocks = (waves + kLnWaves - 1) / kLnWaves;
-    // dbias sums the gradient that enters the GEMM: dy (or dz, which equals dy when there is no dropout)
-    bf16_t* ysink = dy ? dy : nullptr;
-    if (qfmt == 0)
-      hipLaunchKernelGGL((ln_bwd_fused_kernel<NCH, 0>), dim3(blocks), dim3(256), 0, st, dout, z, mean, rstd, gamma, dz,
-                         ysink, dres_add, dgamma, dbeta, dbias, rows, H, rpw, dp, q8o);
-    else if (qfmt == 1)
-      hipLaunchKernelGGL((ln_bwd_fused_kernel<NCH, 1>), dim3(blocks), dim3(256), 0, st, dout, z, mean, rstd, gamma, dz,
-                         ysink, dres_add, dgamma, dbeta, dbias, rows, H, rpw, dp, q8o);
-    else
-      hipLaunchKernelGGL((ln_bwd_fused_kernel<NCH, -1>), dim3(blocks), dim3(256), 0, st, dout, z, mean, rstd, gamma, dz,
-                         ysink, dres_add, dgamma, dbeta, dbias, rows, H, rpw, dp, q8o);
-    return;
-  }
-  hipLaunchKernelGGL((ln_bwd_rows_kernel<NCH>), dim3((rows + kLnWaves - 1) / kLnWaves), dim3(256), 0, st, dout, z,
-                     mean, rstd, gamma, dz, dy, dres_add, rows, H, dp);
-  const int gx = (H + 511) / 512;
-  int want_y = max(1, 2048 / gx);
-  int rpb = max(16, (rows + want_y - 1) / want_y);
-  rpb = (rpb + 15) / 16 * 16;
-  const int gy = (rows + rpb - 1) / rpb;
-  // dbias sums the gradient that enters the GEMM (dy, or dz when dy is not materialised separately)
-  const bf16_t* ysrc = dy ? dy : dz;
-  hipLaunchKernelGGL(ln_bwd_cols_kernel, dim3(gx, gy), dim3(256), 0, st, dout, z, mean, rstd, ysrc, dgamma, dbeta,
-                     ysrc ? dbias : nullptr, rows, H, rpb);
+  // ~16 rows per wave at the headline's 131072 rows: 2048 waves = 8 per CU, a few thousand column atomics per
+  // block; at least 4 rows per wave (a floor of 2 for small row counts, twice the waves and the column atomics,
+  // measured 1-2 % slower end to end at bert-large B = 8 and bert-base B = 32: profiles/small_tiles_r2.log; other
+  // floors: profiles/ln_bwd_rpw_r5.log)
+  const int min_rpw = 4;
+  const int rpw = std::max(min_rpw, (rows + 2047) / 2048);
+  const int waves = (rows + rpw - 1) / rpw;
+  const int blocks = (waves + kLnWaves - 1) / kLnWaves;
+  // dbias sums the gradient that enters the GEMM: dy (or dz, which equals dy when there is no dropout)
+  bf16_t* ysink = dy ? dy : nullptr;
+  if (qfmt == 0)
+    hipLaunchKernelGGL((ln_bwd_fused_kernel<NCH, 0>), dim3(blocks), dim3(256), 0, st, dout, z, mean, rstd, gamma, dz,
+                       ysink, dres_add, dgamma, dbeta, dbias, rows, H, rpw, dp, q8o);
+  else if (qfmt == 1)
+    hipLaunchKernelGGL((ln_bwd_fused_kernel<NCH, 1>), dim3(blocks), dim3(256), 0, st, dout, z, mean, rstd, gamma, dz,
+                       ysink, dres_add, dgamma, dbeta, dbias, rows, H, rpw, dp, q8o);
+  else
+    hipLaunchKernelGGL((ln_bwd_fused_kernel<NCH, -1>), dim3(blocks), dim3(256), 0, st, dout, z, mean, rstd, gamma, dz,
+                       ysink, dres_add, dgamma, dbeta, dbias, rows, H, rpw, dp, q8o);
 }
 
 // LayerNorm forward (no residual / dropout) that also writes the output's fp8 e4m3 copy for the next fp8 GEMM

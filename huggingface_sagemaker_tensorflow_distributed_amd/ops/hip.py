@@ -66,22 +66,17 @@ import os as _os
 
 _WGRAD_MODE = _os.environ.get("HSD_WGRAD_STREAM", "auto").strip().lower()
 _WGRAD_AUTO_MAX_TOKENS = int(_os.environ.get("HSD_WGRAD_STREAM_MAX_TOKENS", "131072"))
-# HSD_WGRAD_STASH=1 (default): instead of record_stream, the side stream's operands stay referenced until the
-# next join_side_streams() (the compute stream has then waited for the side stream, so their blocks go back to
-# the compute stream's pool with no cross-stream event bookkeeping in the allocator; record_stream collapsed
-# throughput 7x at B = 256-1024). Costs the operands' memory until the end of the backward.
-_WGRAD_STASH = _os.environ.get("HSD_WGRAD_STASH", "1") == "1"
-# HSD_WGRAD_CXX=0: fork to the side stream through torch's Python stream objects (the round-2 path) instead of the
-# extension's stream_wait + gemm2_on
-_WGRAD_CXX = _os.environ.get("HSD_WGRAD_CXX", "1") == "1"
+# The side stream's operands stay referenced until the next join_side_streams() instead of record_stream (the compute
+# stream has then waited for the side stream, so their blocks go back to the compute stream's pool with no cross-stream
+# event bookkeeping in the allocator; record_stream collapsed throughput 7x at B = 256-1024). Costs the operands' memory
+# until the end of the backward. The fork is the extension's stream_wait + gemm2_on (no Python stream plumbing).
 _SIDE = {}
 _STASH = []
 _JOIN_QUEUED = [False]
 # HIP-graph capture (train/graph.py): the capture stream the side stream forks from and joins back to (autograd's
 # end-of-backward callback runs with the device's default stream current, not the capture stream), and whether this
-# capture forked it. HSD_GRAPH_SIDE=0: captured steps keep every weight gradient on the capture stream (round 3).
+# capture forked it.
 _CAPTURE = {"parent": None, "forked": False}
-_GRAPH_SIDE = _os.environ.get("HSD_GRAPH_SIDE", "1") == "1"
 # HSD_TEST_SIDE_DELAY_US: test-only stall queued on the side stream before each backward's first weight gradient
 _SIDE_DELAY_US = float(_os.environ.get("HSD_TEST_SIDE_DELAY_US", "0"))
 
@@ -121,9 +116,6 @@ def side_stream_waitable() -> bool:
 def stream_wait(dst, src) -> None:
     """``dst`` waits for everything queued on ``src`` so far (``dst.wait_stream(src)`` with an event from the
     extension's per-thread ring). Streams or raw handles; ``None`` / 0 = the current stream."""
-    if not _WGRAD_CXX and hasattr(dst, "wait_stream") and hasattr(src, "cuda_stream"):
-        dst.wait_stream(src)
-        return
     _C.stream_wait(dst.cuda_stream if hasattr(dst, "cuda_stream") else int(dst or 0),
                    src.cuda_stream if hasattr(src, "cuda_stream") else int(src or 0))
 
@@ -143,7 +135,7 @@ def side_stream(device) -> Optional[torch.cuda.Stream]:
 def _use_side_stream(tokens: int) -> bool:
     if _WGRAD_MODE in ("0", "off", "false"):
         return False
-    if torch.cuda.is_current_stream_capturing() and (_CAPTURE["parent"] is None or not _GRAPH_SIDE):
+    if torch.cuda.is_current_stream_capturing() and _CAPTURE["parent"] is None:
         return False
     return _WGRAD_MODE in ("1", "on", "true") or tokens <= _WGRAD_AUTO_MAX_TOKENS
 
@@ -222,12 +214,7 @@ def wgrad_done(g: "_Grad", dy: torch.Tensor, x: torch.Tensor, dyq=None, xq=None)
             _C.stream_wait(s.cuda_stream, src)
             with torch.cuda.stream(s):
                 _C.cu_hog(1, _SIDE_DELAY_US)
-    if not _WGRAD_CXX and parent is None:
-        s.wait_stream(torch.cuda.current_stream())
-        with torch.cuda.stream(s):
-            gemm_wgrad_(g, dy, x)
-            r = g.done()
-    elif g.buf is g.mg and _wgrad8_ok(dyq, xq, N, K, T):
+    if g.buf is g.mg and _wgrad8_ok(dyq, xq, N, K, T):
         _C.stream_wait(s.cuda_stream, src)
         _wgrad8(g.buf, dyq, xq, N, K, T, s)
         r = None
@@ -243,11 +230,7 @@ def wgrad_done(g: "_Grad", dy: torch.Tensor, x: torch.Tensor, dyq=None, xq=None)
         with torch.cuda.stream(s):
             gemm_wgrad_(g, dy, x, dyq, xq)
             r = g.done()
-    if _WGRAD_STASH:
-        _STASH.append((dy, x, dyq, xq))
-    else:
-        for t in (dy, x, *(dyq or ()), *(xq or ())):
-            t.record_stream(s)
+    _STASH.append((dy, x, dyq, xq))
     return r
 
 
@@ -506,7 +489,7 @@ def _keep_mask(B, S, heads, p, device):
     (query, key) pair (attention128.hip, attentionS.hip headers): S^2/8 B per (batch, head) (25 MB per bert-base
     layer at B = 1024, S = 128; 4 MB per bert-large layer at B = 8, S = 512). None without dropout or where the
     kernels do not support it."""
-    if p > 0 and _os.environ.get("HSD_ATTN_KMASK", "1") != "0":  # HSD_ATTN_KMASK=0: re-hash in the backward (A/B)
+    if p > 0:
         n = _C.attn_keep_mask_numel(B, S, heads)
         if n > 0:
             return torch.empty(n, dtype=torch.int32, device=device)
@@ -558,8 +541,6 @@ def attention(qkv, mask_bias, batch, seq, heads, p, seed):
 # ------------------------------------------------------------------------------------------ GEMM helpers
 EPI_STORE, EPI_BIAS, EPI_BIAS_GELU, EPI_BIAS_DROP_RES, EPI_RES, EPI_DGELU, EPI_F32_ATOMIC = range(7)
 EPI_F32_SLAB, EPI_BIAS_GELU_D, EPI_MUL, EPI_STORE_RDOT = 7, 8, 9, 10  # gemm2 only
-# HSD_ATTN_DELTA_EPI=0: the streaming attention backward computes its delta rows in its own pass (A/B)
-_DELTA_EPI = _os.environ.get("HSD_ATTN_DELTA_EPI", "1") != "0"
 
 # split-K factors for the wgrad GEMM (fp32 atomic epilogue), measured with tools/bench_gemm.py at
 # T = 32768 tokens; key = (out_features, in_features)
@@ -744,7 +725,7 @@ def gemm_dgrad_rd(dy, w, o, rd, seq, dyq=None):
     ``(gemm_dgrad(dy, w, dyq=dyq), False)`` when no kernel path takes the shape (N % 256)."""
     M, N, K = dy.shape[0], w.shape[1], dy.shape[1]
     wqt = _fp8_w(w, "_hsd_qt")
-    if _DELTA_EPI and wqt is not None and o.is_contiguous() and o.shape == (M, N) and \
+    if wqt is not None and o.is_contiguous() and o.shape == (M, N) and \
             _C.gemm8_supported(EPI_STORE_RDOT, M, N, K):
         fmt = _FP8["grad_fmt"]
         qdy, sdy = dyq if dyq is not None else quant_fp8(dy, fmt, getattr(w, "_hsd_fp8_g", None))
@@ -752,7 +733,7 @@ def gemm_dgrad_rd(dy, w, o, rd, seq, dyq=None):
         _C.gemm8(qdy, fmt, sdy, wqt, FP8_E4M3, w._hsd_qs, dx, EPI_STORE_RDOT, None, o, None, 0.0, 0, None, rd=rd,
                  rd_seq=seq)
         return dx, True
-    if _DELTA_EPI and wqt is None and o.is_contiguous() and o.shape == (M, N):
+    if wqt is None and o.is_contiguous() and o.shape == (M, N):
         wt = getattr(w, "_hsd_wt", None)
         if wt is not None and (wt.shape[0] != N or wt.shape[1] != K):
             wt = None

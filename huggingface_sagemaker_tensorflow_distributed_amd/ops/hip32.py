@@ -48,14 +48,13 @@ def _split(x: torch.Tensor, pat: int, rows: bool = False, pad_rows: int = 0) -> 
     return out
 
 
-# HSD_F32_DUAL_SPLIT=1 (default): a linear layer's incoming gradient is split ONCE into both layouts its backward
-# needs (column blocks for the dgrad, row blocks for the weight gradient): one read of dy and one launch instead of two
-_DUAL = os.environ.get("HSD_F32_DUAL_SPLIT", "1") == "1"
+# A linear layer's incoming gradient is split ONCE into both layouts its backward needs (column blocks for the dgrad,
+# row blocks for the weight gradient): one read of dy and one launch instead of two (profiles/fp32_dual_split_ab_r5.log)
 
 
 def _split_grad(dy: torch.Tensor, need_dgrad: bool):
     """(column-block split for :func:`mm_dgrad` or None, row-block split for :func:`wgrad_` or None) of ``dy``."""
-    if not (_DUAL and need_dgrad and dy.dim() == 2 and dy.shape[0] % 64 == 0 and dy.shape[1] % 4 == 0):
+    if not (need_dgrad and dy.dim() == 2 and dy.shape[0] % 64 == 0 and dy.shape[1] % 4 == 0):
         return None, None
     dy = dy.contiguous()
     R, C = dy.shape
@@ -370,10 +369,9 @@ class _Attention32M(torch.autograd.Function):
         return dqkv, None, None, None, None, None, None
 
 
-import os as _os
-
-# HSD_ATTN32M=0: the round-4 fp32 attention on the vector ALUs (exact fp32 FMAs) instead of the split MFMA products
-_ATTN32M = _os.environ.get("HSD_ATTN32M", "1") != "0"
+# the split-product MFMA attention wherever it takes the sequence length; the vector-ALU fp32 kernels (exact fp32 FMAs)
+# serve the rest. Module attribute, not an env knob: tests/test_gpu_fp32.py flips it to cover the fallback.
+_ATTN32M = True
 
 
 def attention_ok(qkv, seq, heads) -> bool:

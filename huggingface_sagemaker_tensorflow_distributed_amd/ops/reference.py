@@ -46,7 +46,13 @@ def linear_gelu(x, w, b):
 
 
 def linear_dropout_residual(x, w, b, residual, p: float, seed: int, training: bool):
-    return dropout(F.linear(x, w, b), p, seed, training) + residual
+    """``dropout(x Wᵀ + b) + residual`` rounded ONCE to the output dtype (fp32 product and sum), as the HIP epilogues
+    compute it (gemm_common.h / gemm.hip: bf16(fma(y, keep · scale, residual)) with y = bf16(x Wᵀ + b))."""
+    y = F.linear(x, w, b)
+    if not training or p <= 0.0:
+        return y + residual
+    k = keep_mask(seed, y.shape, p, device=y.device).to(torch.float32) * (1.0 / (1.0 - p))
+    return torch.addcmul(residual.float(), y.float(), k).to(y.dtype)
 
 
 def layer_norm(x, w, b, eps: float):

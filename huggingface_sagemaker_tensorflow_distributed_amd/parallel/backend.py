@@ -41,20 +41,6 @@ def _want_cuda(device: Optional[str]) -> bool:
     return torch.cuda.is_available()
 
 
-_MAIN_STREAM = [None]
-
-
-def _main_stream(dev) -> None:
-    """HSD_MAIN_STREAM_PRIORITY=<p> (A/B): run the step on a stream of that priority (lower = higher) instead of the
-    device's default stream, so its kernels are dispatched ahead of the weight-gradient / optimizer side streams'."""
-    pr = os.environ.get("HSD_MAIN_STREAM_PRIORITY")
-    if pr is None or _MAIN_STREAM[0] is not None:
-        return
-    _MAIN_STREAM[0] = torch.cuda.Stream(device=dev, priority=int(pr))
-    torch.cuda.set_stream(_MAIN_STREAM[0])
-    logger.info("main stream priority %s (range %s)", pr, torch.cuda.Stream.priority_range())
-
-
 def init(device: Optional[str] = None, timeout_s: float = 1800.0, backend: Optional[str] = None) -> DistState:
     """Initialise (idempotent). Reads RANK/WORLD_SIZE/LOCAL_RANK/MASTER_* (or MPI/Horovod vars)."""
     global _STATE
@@ -67,7 +53,6 @@ def init(device: Optional[str] = None, timeout_s: float = 1800.0, backend: Optio
     if use_cuda:
         torch.cuda.set_device(env["local_rank"] % max(1, torch.cuda.device_count()))
         dev = torch.device("cuda", torch.cuda.current_device())
-        _main_stream(dev)
     else:
         dev = torch.device("cpu")
     # HSD_DIST_BACKEND=gloo: force the CPU-transport backend (e.g. several ranks sharing one GPU in a test)

@@ -39,25 +39,44 @@ DEFAULT_BUCKET_MB = float(os.environ.get("HSD_BUCKET_MB", "64"))
 COMPRESSION = {"none": (0, None), "bf16": (1, torch.bfloat16), "fp16": (2, torch.float16)}
 
 # Gradient wire format policy (``--grad_compression auto``, the default). bf16 on the wire halves the all-reduce bytes
-# (bert-base 418 -> 209 MiB, bert-large 1,278 -> 639 MiB per step) for two fused casts on the comm
-# stream, measured on one MI355X (tools/wire_cast_cost.py, profiles/wire_cast_r5.jsonl): 0.247 ms per step for
-# bert-base's 109.5M gradients, 0.764 ms for bert-large's 335M -- 2.26 ns per parameter, whatever the step size --
-# while the backward costs ~3.5e-15 s per token x parameter (bert-base B=1024 S=128: ~51 ms). The casts' share of the
-# backward is therefore ~6.4e5 / tokens: 0.5 % at the headline's 131,072 tokens per rank, 16 % at the reference's
-# bert-large B=8 S=512 (4,096 tokens). ``auto`` takes bf16 from WIRE_BF16_MIN_TOKENS tokens per rank and optimizer
-# step (casts <= 2 % of the backward) and keeps fp32 below, where the casts would cost more than the halved bytes
-# save under the overlapped backward. Explicit ``none`` / ``bf16`` / ``fp16`` are kept as given.
-WIRE_BF16_MIN_TOKENS = int(os.environ.get("HSD_WIRE_BF16_MIN_TOKENS", "32768"))
+# (bert-base 418 -> 209 MiB, bert-large 1,278 -> 639 MiB per step) at the price of two fused casts
+# (fp32 -> bf16 before the all-reduce, back after it). Both the casts and the transfer run on the comm stream
+# (csrc/comm/comm_engine.cpp launch_wire_cast, then ncclAllReduce), so the casts are weighed against the transfer time
+# they save -- not against the backward they overlap with:
+#
+#   casts       CAST_S_PER_PARAM = 2.28e-12 s per parameter and step, measured on one MI355X (tools/wire_cast_cost.py,
+#               profiles/wire_cast_r5.jsonl: 0.247 ms for bert-base's 109.5M gradients, 0.764 ms for bert-large's 335M)
+#   transfer    a ring all-reduce moves 2(N-1)/N x S bytes per rank over the xGMI links RCCL's rings
+#               can use: min(N-1, 7) point-to-point links of LINK_BPS = 153 GB/s (1 link at N = 2, 3 at N = 4, 7 at N = 8)
+#   saved       2(N-1)/N x 2 bytes per parameter / (links x LINK_BPS): 13.1 ps at N = 2, 6.5 ps at N = 4, 3.3 ps at N = 8
+#
+# So bf16 wins at every N >= 2 whatever the step size, including the reference's own bert-large B = 8 S = 512 (N = 8:
+# 1.10 ms of transfer saved for 0.76 ms of casts; N = 2: 4.4 ms saved), where the round-5 rule (casts vs 16 % of the
+# backward) picked fp32. ``auto`` = bf16 for bf16 / fp8 runs on GPUs at N >= 2 when the model says it saves time, and
+# fp32 on the wire for ``--dtype fp32`` -- the reference's precision and Horovod's uncompressed fp32 all-reduce
+# (scripts/train.py:114; docs/PARITY.md 'gradient wire format'). Explicit ``none`` / ``bf16`` / ``fp16`` are kept.
+CAST_S_PER_PARAM = 2.28e-12
+LINK_BPS = 153e9
+MAX_XGMI_LINKS = 7
 
 
-def resolve_compression(requested: str, world: int, on_gpu: bool, tokens_per_step: int | None) -> str:
-    """The wire format of a data-parallel job: ``requested`` unless it is ``auto`` (see WIRE_BF16_MIN_TOKENS).
-    ``tokens_per_step``: tokens per rank and optimizer step (micro-batch x seq x accumulation), None = unknown."""
+def wire_times(world: int, n_params: int = 1) -> dict:
+    """Comm-stream seconds for ``n_params`` fp32 gradients at ``world`` ranks: fp32 wire vs bf16 wire (+ casts)."""
+    links = max(1, min(world - 1, MAX_XGMI_LINKS))
+    ring = 2.0 * (world - 1) / world / (links * LINK_BPS)  # seconds per byte of payload per rank
+    fp32 = 4 * n_params * ring
+    bf16 = 2 * n_params * ring + CAST_S_PER_PARAM * n_params
+    return {"links": links, "fp32_s": fp32, "bf16_s": bf16, "saved_s": fp32 - bf16}
+
+
+def resolve_compression(requested: str, world: int, on_gpu: bool, dtype: str = "bf16") -> str:
+    """The gradient wire format of a data-parallel job: ``requested`` unless it is ``auto`` (see the model above).
+    ``dtype``: the run's compute dtype (``fp32`` keeps fp32 on the wire, the reference's numerics)."""
     if requested != "auto":
         return requested
-    if world <= 1 or not on_gpu or tokens_per_step is None:
+    if world <= 1 or not on_gpu or dtype == "fp32":
         return "none"
-    return "bf16" if tokens_per_step >= WIRE_BF16_MIN_TOKENS else "none"
+    return "bf16" if wire_times(world)["saved_s"] > 0 else "none"
 
 
 def overlap_from_timeline(backward_ms: float, buckets) -> dict:

@@ -173,8 +173,8 @@ class FlatParamStore:
         self.fp8_wt = torch.empty(total, dtype=torch.uint8, device=self.device)
         # one 128-B line per weight for its amax / scale: every block of the amax pass ends with an atomic on its
         # weight's slot, and packed slots put all ~18k of them on one L2 line (roberta-large: 514 us for a 604 MB
-        # read, 1.2 TB/s; profiles/fp8_refresh_r5.log). HSD_FP8_SLOT = floats per slot (1 = packed).
-        slot = max(1, int(os.environ.get("HSD_FP8_SLOT", "32")))
+        # read, 1.2 TB/s; profiles/fp8_refresh_r5.log): 32 floats per slot.
+        slot = 32
         self.fp8_amax = torch.zeros(len(idx) * slot, dtype=torch.float32, device=self.device)
         self.fp8_sinv = torch.ones(len(idx) * slot, dtype=torch.float32, device=self.device)
         # delayed-scaling history of the two activation-side quantisation sites of each weight:

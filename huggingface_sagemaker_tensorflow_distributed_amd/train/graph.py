@@ -134,6 +134,38 @@ class CapturedStep:
         return self.loss, self.logits
 
 
+class CapturedEval:
+    """The eval-mode forward + loss + fused metric counts of ``trainer`` for batches shaped like ``example``, as one
+    graph: the reference's ``model.evaluate`` at ``eval_batch_size`` 2 (``launch.py:16``, ``scripts/train.py:170``) is
+    12,500 forwards of 2 sequences, each a few hundred short kernels -- launch-bound when issued one by one. No dropout
+    (eval mode: no seeds), no autograd (``no_grad``): nothing but the static inputs changes between replays."""
+
+    def __init__(self, trainer, example: Dict[str, torch.Tensor], warmup: int = 1):
+        self.trainer = trainer
+        self.static = {k: v.clone() for k, v in example.items() if torch.is_tensor(v)}
+        model = trainer.model
+        model.eval()
+        dev = trainer.device
+        s = torch.cuda.Stream(device=dev)
+        s.wait_stream(torch.cuda.current_stream(dev))
+        with torch.no_grad(), torch.cuda.stream(s):
+            for _ in range(warmup):  # first-use workspaces / lazy caches, outside the capture
+                trainer._forward_loss(self.static)
+        torch.cuda.current_stream(dev).wait_stream(s)
+        torch.cuda.synchronize(dev)
+        self.graph = torch.cuda.CUDAGraph()
+        with torch.no_grad(), torch.cuda.graph(self.graph, capture_error_mode="thread_local"), _NoGC():
+            self.loss, self.logits = trainer._forward_loss(self.static)
+        torch.cuda.synchronize(dev)
+        logger.info("captured eval forward graph for batch shape %s", tuple(example["input_ids"].shape))
+
+    def run(self, batch: Dict[str, torch.Tensor]):
+        for k, v in self.static.items():
+            v.copy_(batch[k], non_blocking=True)
+        self.graph.replay()
+        return self.loss, self.logits
+
+
 class CapturedTrainStep:
     """The WHOLE training step as one graph: gradient zeroing, forward, loss, backward, the optimizer slices stepped
     under backward (one process: optim/adam.py LocalOverlap, a side-stream branch of the graph per slice, forked when

@@ -136,7 +136,7 @@ def build(args, mode: str):
         batch_plan = batch_planner.plan(model, store, max_len, dev, headroom=args.auto_batch_headroom,
                                         max_tokens=args.auto_batch_max_tokens or None,
                                         compression=resolve_compression(getattr(args, "grad_compression", "none"),
-                                                                        world, on_gpu, 1 << 30))
+                                                                        world, on_gpu, dtype_name))
         per_gpu = batch_planner.agree_min(batch_plan.per_gpu_batch, dev)
         batch_plan.per_gpu_batch = per_gpu
         args.train_batch_size = per_gpu if mode == "train" else per_gpu * world
@@ -145,8 +145,7 @@ def build(args, mode: str):
                     batch_plan.per_seq_bytes / 2**20, batch_plan.fixed_bytes / 2**30, batch_plan.budget_bytes / 2**30,
                     batch_plan.total_bytes / 2**30, batch_plan.capped_by, args.train_batch_size)
     per_rank = int(args.train_batch_size) // (1 if mode == "train" else world)
-    wire = resolve_compression(getattr(args, "grad_compression", "none"), world, on_gpu,
-                               per_rank * max_len * max(1, args.gradient_accumulation_steps))
+    wire = resolve_compression(getattr(args, "grad_compression", "none"), world, on_gpu, dtype_name)
     if world > 1:
         logger.info("gradient wire format: %s (--grad_compression %s)", wire, getattr(args, "grad_compression", "none"))
     bucketer = GradBucketer(store, bucket_mb=args.bucket_mb, compression=wire) if world > 1 else None
@@ -155,7 +154,8 @@ def build(args, mode: str):
                       lr_warmup_steps=getattr(args, "lr_warmup_steps", 0),
                       check_sync=args.check_sync, log_every=args.log_every, step_watchdog=args.step_watchdog,
                       hip_graph=resolve_hip_graph(getattr(args, "hip_graph", False), on_gpu, world,
-                                                  per_rank * max_len, args.gradient_accumulation_steps))
+                                                  per_rank * max_len, args.gradient_accumulation_steps),
+                      eval_hip_graph=getattr(args, "eval_hip_graph", "auto"))
     initial_epoch = 0
     if args.resume_from:
         initial_epoch = int(load_checkpoint(args.resume_from, trainer).get("epoch", 0))
@@ -202,6 +202,16 @@ def run(argv: Optional[Sequence[str]] = None, mode: str = "train") -> dict:
             raise ValueError(f"global train_batch_size {args.train_batch_size} not divisible by {world} replicas")
         per_rank_train = args.train_batch_size // world
     per_rank_eval = args.eval_batch_size if mode == "train" else max(1, args.eval_batch_size // world)
+    # eval batch coalescing: evaluation has no dropout and no cross-example math (no batch statistics), so each
+    # example's logits and loss do not depend on which examples share its forward, and the metrics are per-example
+    # means (Keras evaluate with SUM_OVER_BATCH_SIZE over equal batches). Consecutive eval batches are therefore run
+    # k at a time, up to --eval_coalesce_tokens tokens per forward: the reference's eval_batch_size 2 at S = 512
+    # (launch.py:16) is 1,024-token forwards that leave most of the GPU idle. 0 = one forward per eval batch.
+    coalesce = max(1, int(getattr(args, "eval_coalesce_tokens", 0) or 0) // max(1, per_rank_eval * max_len))
+    per_rank_eval_fwd = per_rank_eval * coalesce
+    if coalesce > 1:
+        logger.info("evaluate: eval_batch_size %d per rank, %d batches per forward (%d sequences; "
+                    "--eval_coalesce_tokens %d)", per_rank_eval, coalesce, per_rank_eval_fwd, args.eval_coalesce_tokens)
 
     train_loader = hdata.BatchLoader(train_ds, ShardSampler(len(train_ds), rank, world, shuffle=False, seed=args.seed,
                                                              batch_size=per_rank_train), dev)
@@ -209,7 +219,7 @@ def run(argv: Optional[Sequence[str]] = None, mode: str = "train") -> dict:
     # ignored rows, the last partial batch kept
     test_loader = hdata.BatchLoader(test_ds, ShardSampler(len(test_ds), rank, world, shuffle=False, seed=args.seed,
                                                            drop_last=False, mark_padding=True,
-                                                           batch_size=per_rank_eval), dev)
+                                                           batch_size=per_rank_eval_fwd), dev)
     _provenance(args, model, rank, len(train_ds), len(test_ds), parts["batch_plan"])
     out = {"args": args}
     callbacks = [FaultInjection()]
@@ -244,10 +254,22 @@ def run(argv: Optional[Sequence[str]] = None, mode: str = "train") -> dict:
 
     if args.do_eval:
         logger.info("*** Evaluate ***")
-        result = trainer.evaluate(test_loader)
+        start = time.time()
+        result = trainer.evaluate(test_loader)  # the meter's global all-reduce syncs the device
+        eval_runtime = round(time.time() - start, 4)
+        # not in eval_results.txt (the reference's writer holds the metrics only, scripts/train.py:172-179): the log line
+        # and run_provenance-style JSON beside it time the reference's other measured phase, model.evaluate (:170)
+        eval_speed = {"eval_runtime": eval_runtime, "eval_samples": len(test_ds),
+                      "eval_samples_per_second": round(len(test_ds) / max(eval_runtime, 1e-9), 2),
+                      "eval_batch_size": per_rank_eval, "eval_sequences_per_forward": per_rank_eval_fwd,
+                      "eval_hip_graph": trainer.eval_graph_active}
+        logger.info(f"eval_runtime = {eval_speed}")
         if rank == 0:
             write_eval_results(args.output_data_dir, result)
+            with open(os.path.join(args.output_data_dir, "eval_speed.json"), "w") as f:
+                json.dump(eval_speed, f, indent=1)
         out["eval"] = result
+        out["eval_speed"] = eval_speed
 
     # Q5: rank-0-only save, then barrier
     if rank == 0:

@@ -101,7 +101,7 @@ class _Meter:
 class Trainer:
     def __init__(self, model, store, optimizer, bucketer=None, device=None, grad_accum: int = 1,
                  check_sync: int = 0, log_every: int = 50, step_watchdog: float = 0.0, hip_graph: bool = False,
-                 lr_schedule: str = "constant", lr_warmup_steps: int = 0):
+                 lr_schedule: str = "constant", lr_warmup_steps: int = 0, eval_hip_graph="auto"):
         self.model = model
         self.store = store
         self.optimizer = optimizer
@@ -117,6 +117,9 @@ class Trainer:
         self.world = backend.size()
         self.rank = backend.rank()
         self._graphs = {}
+        self.eval_hip_graph = eval_hip_graph
+        self._eval_graphs = {}
+        self.eval_graph_active = False  # whether the last evaluate() replayed a captured forward
         self._seed = None
         self._graph_replay = True  # tests: False = graph-mode seeding with eager kernels
         self._opt_overlap = None  # LocalOverlap (one process) | "engine" (DP ranks) | None
@@ -404,15 +407,51 @@ class Trainer:
                 cb.on_epoch_end(self, epoch, logs)
 
     # -------------------------------------------------------------------------- evaluate
+    def _eval_graph_wanted(self, tokens: int) -> bool:
+        """``eval_hip_graph``: True / False as given; ``auto`` = replay captured eval forwards for batches of at most
+        HSD_EVAL_GRAPH_MAX_TOKENS (16,384) tokens on the GPU, where one forward is a few hundred short launches."""
+        flag = self.eval_hip_graph
+        if self.device.type != "cuda" or not getattr(self.model, "graph_safe", True) or not ops.hip_active(self.device):
+            return False
+        if flag != "auto":
+            return bool(flag)
+        return tokens <= int(os.environ.get("HSD_EVAL_GRAPH_MAX_TOKENS", "16384"))
+
+    def _eval_forward(self, b):
+        """(loss, logits, static): a captured replay when the eval graph is on for this shape, else eager."""
+        ids = b["input_ids"]
+        if self._eval_graph_wanted(ids.numel()):
+            key = tuple((k, tuple(v.shape), v.dtype) for k, v in sorted(b.items()) if torch.is_tensor(v))
+            g = self._eval_graphs.get(key)
+            if g is None and key not in self._eval_graphs:
+                from .graph import CapturedEval
+
+                try:
+                    g = CapturedEval(self, b)
+                except Exception as e:  # an op that cannot be captured: this shape stays eager (loudly)
+                    logger.warning("eval graph capture failed for shape %s (%s): eager forward", tuple(ids.shape), e)
+                    g = None
+                self._eval_graphs[key] = g
+            if g is not None:
+                self.eval_graph_active = True
+                loss, logits = g.run(b)
+                return loss, logits, True
+        loss, logits = self._forward_loss(b)
+        return loss, logits, False
+
     @torch.no_grad()
     def evaluate(self, loader, max_steps: Optional[int] = None) -> Dict[str, float]:
         self.model.eval()
+        self.eval_graph_active = False
         meter = _Meter(self.device)
         for i, b in enumerate(loader):
             if max_steps and i >= max_steps:
                 continue  # drain
             if b.get("num_valid", 1) == 0:
                 continue  # a shard's tail made only of padding rows
-            loss, logits = self._forward_loss(b)
-            meter.update(loss, logits, b["labels"])
+            loss, logits, static = self._eval_forward(b)
+            meter.update(loss, logits, b["labels"], static=static)
+            if self.rank == 0 and self.log_every and (i + 1) % (self.log_every * 20) == 0:
+                # progress only (Keras' evaluate progress bar): host-side count, no device sync
+                logger.info("evaluate: %d/%d batches issued", i + 1, len(loader))
         return meter.result(global_=True)

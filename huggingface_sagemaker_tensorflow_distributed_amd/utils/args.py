@@ -85,7 +85,9 @@ def _add_framework_flags(p: argparse.ArgumentParser) -> None:
     g.add_argument("--grad_dtype", choices=["fp32", "bf16"], default=None)
     g.add_argument("--grad_compression", choices=["auto", "none", "bf16", "fp16"], default="auto",
                    help="dtype fp32 gradient buckets are all-reduced in (Horovod's hvd.Compression.fp16); auto: bf16 "
-                        "from 32,768 tokens per rank and step on GPUs, fp32 below (parallel/ddp.py resolve_compression)")
+                        "for bf16 / fp8 runs on GPUs at N >= 2 (the casts cost less than the transfer time they save "
+                        "over xGMI, parallel/ddp.py resolve_compression), fp32 for --dtype fp32; none = fp32 always "
+                        "(the reference's Horovod all-reduce)")
     g.add_argument("--optimizer", choices=["adam", "adamw"], default="adam")
     g.add_argument("--weight_decay", type=float, default=0.0)
     g.add_argument("--adam_eps_mode", choices=["keras", "torch"], default="keras")
@@ -97,10 +99,17 @@ def _add_framework_flags(p: argparse.ArgumentParser) -> None:
     g.add_argument("--benchmark", type=str2bool, default=False)
     g.add_argument("--warmup_steps", type=int, default=3, help="benchmark warmup steps")
     g.add_argument("--profile", type=str2bool, default=False)
-    g.add_argument("--hip_graph", type=bool_or_auto, default=False,
-                   help="replay the whole step from a captured HIP graph (single-process GPU runs); auto = on for "
-                        "launch-bound steps of <= HSD_GRAPH_AUTO_MAX_TOKENS (2,048) tokens, one micro-step, one "
+    g.add_argument("--hip_graph", type=bool_or_auto, default="auto",
+                   help="replay the whole step from a captured HIP graph (single-process GPU runs); auto (default) = "
+                        "on for launch-bound steps of <= HSD_GRAPH_AUTO_MAX_TOKENS (2,048) tokens, one micro-step, one "
                         "process (bert-base S=128 B=1-16: 1.04-1.5x eager; B>=32: eager faster)")
+    g.add_argument("--eval_hip_graph", type=bool_or_auto, default="auto",
+                   help="evaluate by replaying a captured forward graph per batch shape; auto = for eval batches of <= "
+                        "HSD_EVAL_GRAPH_MAX_TOKENS (16,384) tokens on the GPU (the reference's eval_batch_size 2: "
+                        "launch-bound forwards)")
+    g.add_argument("--eval_coalesce_tokens", type=int, default=16384,
+                   help="run consecutive eval batches together, up to this many tokens per forward (metrics are "
+                        "per-example: unchanged); 0 = one forward per --eval_batch_size batch")
     g.add_argument("--save_every_epoch", type=str2bool, default=False)
     g.add_argument("--resume_from", type=str, default=None)
     g.add_argument("--check_sync", type=int, default=0, help="verify cross-rank param hash every N steps")

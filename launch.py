@@ -23,6 +23,11 @@ hyperparameters = {
     "max_steps": int(os.environ.get("HSD_MAX_STEPS", "20")),
     "num_train_examples": int(os.environ.get("HSD_NUM_TRAIN", "2048")),
     "num_eval_examples": int(os.environ.get("HSD_NUM_EVAL", "256")),
+    # None = the CLI default (bf16 on a GPU); "fp32" = the reference's own precision
+    "dtype": os.environ.get("HSD_DTYPE"),
+    "eval_hip_graph": os.environ.get("HSD_EVAL_HIP_GRAPH"),  # None = auto (captured forwards at eval batch 2)
+    "do_train": os.environ.get("HSD_DO_TRAIN"),
+    "eval_coalesce_tokens": os.environ.get("HSD_EVAL_COALESCE_TOKENS"),  # None = 16,384 tokens per eval forward
 }
 # configuration for running training on smdistributed Data Parallel -> RCCL DP engine
 # distribution = {'smdistributed': {'dataparallel': {'enabled': True}}}

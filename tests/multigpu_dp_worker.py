@@ -55,11 +55,20 @@ def main(out):
     torch.cuda.synchronize()
     in_sync = params_in_sync(store)
     engine = getattr(buck, "engine", None)
+    master = store.master.float().cpu()
+    overlap = None
+    if buck is not None and os.environ.get("HSD_MGPU_OVERLAP") == "1" and buck.set_timing(True):
+        # one more step with the engine's per-bucket HIP events on (after the compared state was taken): the
+        # comm / compute overlap report bench.py prints for N > 1
+        tr.train_step([batch])
+        torch.cuda.synchronize()
+        overlap = buck.overlap_report()
+        buck.set_timing(False)
     if rank == 0:
-        torch.save({"grad0": first_grad, "master": store.master.float().cpu(), "in_sync": in_sync, "world": world,
+        torch.save({"grad0": first_grad, "master": master, "in_sync": in_sync, "world": world,
                     "graphs": len(getattr(tr, "_graphs", {}) or {}), "compression": comp,
                     "rccl_world": int(engine.world) if engine is not None else None,
-                    "n_buckets": len(buck.buckets) if buck is not None else 0}, out)
+                    "n_buckets": len(buck.buckets) if buck is not None else 0, "overlap": overlap}, out)
     backend.shutdown()
 
 

@@ -61,3 +61,13 @@ def test_bench_exits_nonzero_when_ranks_diverge():
     assert r.returncode != 0
     lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1 and json.loads(lines[0])["validation"]["ranks_in_sync"] is False
+
+
+def test_bench_refuses_gpus_world_mismatch():
+    """``--gpus N`` without N ranks (WORLD_SIZE unset = 1) exits non-zero instead of printing a world-1 number."""
+    env = dict(os.environ, HSD_DEVICE="cpu")
+    env.pop("WORLD_SIZE", None)
+    r = subprocess.run([sys.executable, "bench.py", "--gpus", "2", "--steps", "1", "--warmup", "0"], cwd=ROOT, env=env,
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 2 and "WORLD_SIZE=1" in r.stderr, (r.returncode, r.stderr[-500:])
+    assert r.stdout.strip() == ""

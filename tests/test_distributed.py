@@ -461,30 +461,39 @@ def _worker_compression(rank, world, port, mode):
 def test_gradient_wire_compression_world2(mode):
     """Horovod's ``hvd.Compression.fp16`` (``--grad_compression``): fp32 gradient buckets all-reduced in 16 bits,
     cast back to fp32, identical on every rank, within 16-bit rounding of the fp32 sum (gloo world 2). ``auto`` is the
-    default's resolution for the headline job (GPU ranks, 131,072 tokens per rank and step): bf16 on the wire."""
+    default's resolution for a bf16 job on GPU ranks: bf16 on the wire."""
     from huggingface_sagemaker_tensorflow_distributed_amd.parallel.ddp import resolve_compression
 
     if mode == "auto":
-        mode = resolve_compression("auto", 2, True, 1024 * 128)
+        mode = resolve_compression("auto", 2, True, "bf16")
         assert mode == "bf16"
     mp.spawn(_worker_compression, args=(2, _port(), mode), nprocs=2, join=True)
 
 
 def test_wire_policy_auto():
-    """``--grad_compression auto`` (default): bf16 from 32,768 tokens per rank and optimizer step on GPUs (the two
-    casts <= 2 % of the backward, profiles/wire_cast_r5.jsonl), fp32 below, on CPUs and for one rank; explicit choices
-    are kept."""
-    from huggingface_sagemaker_tensorflow_distributed_amd.parallel.ddp import resolve_compression
+    """``--grad_compression auto`` (default) weighs the two casts (comm stream) against the ring transfer time they
+    save over min(N-1, 7) xGMI links (parallel/ddp.py): bf16 for bf16 / fp8 runs at every N >= 2 -- including the
+    reference's own bert-large B=8 S=512 job at N = 8, whatever the tokens per step --, fp32 for ``--dtype fp32`` (the
+    reference's precision), on CPUs and for one rank; explicit choices are kept."""
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel.ddp import resolve_compression, wire_times
     from huggingface_sagemaker_tensorflow_distributed_amd.utils.args import build_parser
 
     assert build_parser("train").parse_known_args([])[0].grad_compression == "auto"
-    assert resolve_compression("auto", 8, True, 1024 * 128) == "bf16"      # headline bert-base B=1024 S=128
-    assert resolve_compression("auto", 8, True, 8 * 512) == "none"         # the reference's bert-large B=8 S=512
-    assert resolve_compression("auto", 8, True, 8 * 512 * 8) == "bf16"     # ... with 8 accumulation micro-steps
-    assert resolve_compression("auto", 1, True, 1 << 20) == "none"
-    assert resolve_compression("auto", 2, False, 1 << 20) == "none"
-    assert resolve_compression("fp16", 2, True, 16) == "fp16"
-    assert resolve_compression("none", 8, True, 1 << 20) == "none"
+    for n in (2, 3, 4, 8):
+        assert resolve_compression("auto", n, True, "bf16") == "bf16"
+        assert resolve_compression("auto", n, True, "fp8") == "bf16"
+        assert resolve_compression("auto", n, True, "fp32") == "none"
+    # the numbers the docstring cites: bert-large (335.1M gradients) at N = 8 saves ~1.1 ms of transfer for ~0.76 ms
+    # of casts; at N = 2 (one link) the transfer alone drops by ~4.4 ms
+    t8 = wire_times(8, 335_143_938)
+    assert t8["links"] == 7 and abs((t8["fp32_s"] - t8["bf16_s"] + 0.764e-3) - 1.10e-3) < 0.05e-3
+    t2 = wire_times(2, 335_143_938)
+    assert t2["links"] == 1 and abs(t2["fp32_s"] / 2 - 4.38e-3) < 0.05e-3
+    assert wire_times(4)["links"] == 3
+    assert resolve_compression("auto", 1, True, "bf16") == "none"
+    assert resolve_compression("auto", 2, False, "bf16") == "none"
+    assert resolve_compression("fp16", 2, True, "fp32") == "fp16"
+    assert resolve_compression("none", 8, True, "bf16") == "none"
 
 
 def _worker_fp16_range(rank, world, port):

@@ -105,10 +105,41 @@ def test_gemm_bias_dropout_residual(gpu, p):
     A, B = _mk((M, K), gpu), _mk((N, K), gpu, 0.05)
     bias, res = _mk((N,), gpu), _mk((M, N), gpu)
     y = (_ref(A, B, 0, 0) + bias.float()).bfloat16()
-    ref = dropout(y, p, 4242, True).float() + res.float()
+    ref = dropout(y.float(), p, 4242, True) + res.float()  # one rounding, as the kernels
     C = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
     _C().gemm(A, B, C, 0, 0, EPI_BIAS_DROP_RES, bias, res, None, p, 4242, 1)
     _check(C, ref, mag=2 * y.float().abs() + res.float().abs() + ref.abs(), acc=2 * _absmm(A, B, 0, 0))
+
+
+@pytest.mark.parametrize("M", [96, 512])
+@pytest.mark.parametrize("p", [0.0, 0.1])
+def test_dropout_residual_site_same_bits_on_every_gemm_path(gpu, M, p):
+    """the dropout + residual epilogue rounds once, bf16(fma(y, keep·scale, residual)), on every kernel that
+    serves the site -- gemm2 (the NT fast path), gemm.hip's LDS-DMA kernel (M >= 128) and its register-staged kernel
+    (M < 128), the fallbacks `gemm_fwd` takes when `_nt_ok` fails. Small-integer operands make the fp32 accumulation
+    exact in any order, so y = bf16(acc + b) is the same on every path and the outputs must match bit for bit."""
+    torch.manual_seed(5)
+    N, K = 768, 128
+    A = torch.randint(-1, 2, (M, K), device=gpu).bfloat16()
+    B = torch.randint(-1, 2, (N, K), device=gpu).bfloat16()
+    bias = torch.randint(-2, 3, (N,), device=gpu).bfloat16()
+    res = _mk((M, N), gpu)
+    outs = []
+    for kernel in ("gemm", "gemm2"):
+        C = torch.empty(M, N, device=gpu, dtype=torch.bfloat16)
+        if kernel == "gemm":
+            _C().gemm(A, B, C, 0, 0, EPI_BIAS_DROP_RES, bias, res, None, p, 777, 1)
+        else:
+            _C().gemm2(A, B, C, 0, 0, EPI_BIAS_DROP_RES, bias, res, None, p, 777, 1, None, None)
+        outs.append(C)
+    assert torch.equal(outs[0], outs[1]), int((outs[0] != outs[1]).sum())
+    from huggingface_sagemaker_tensorflow_distributed_amd.ops.reference import keep_mask
+
+    y = (A.float() @ B.float().t() + bias.float()).bfloat16().float()
+    k = keep_mask(777, (M, N), p, device=gpu).float() * (1.0 / (1.0 - p)) if p > 0 else torch.ones_like(y)
+    ref = torch.addcmul(res.float(), y, k).bfloat16()
+    # fp32 fma vs torch's product-then-sum: the same bf16 value except on a rare fp32 tie
+    assert float((outs[0].float() != ref.float()).float().mean()) < 1e-3
 
 
 def test_gemm_dgrad_epilogues(gpu):
@@ -165,7 +196,7 @@ def test_gemm2_nt_epilogues(gpu, M, N, K, epi):
     if epi == 3:
         y = acc.bfloat16().float()
         keep = ref.dropout(torch.ones(M, N, device=gpu), p, 99, True)
-        acc = (y * keep).bfloat16().float() + aux.float()
+        acc = y * keep + aux.float()  # one rounding (gemm_common.h E2_BIAS_DROP_RES)
         mag = 2 * (y * keep).abs() + aux.float().abs() + acc.abs()
     elif epi == 4:
         acc = acc.bfloat16().float() + aux.float()

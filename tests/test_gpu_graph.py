@@ -104,3 +104,36 @@ def test_graph_accumulation_and_metrics_match_eager(gpu, monkeypatch):
         tr._seed.close()
     for k in res[False]:
         assert abs(res[False][k] - res[True][k]) <= 2e-3 * max(1.0, abs(res[False][k])), res
+
+
+def test_eval_graph_and_coalescing_match_eager(gpu):
+    """``Trainer.evaluate`` by captured-forward replays (``eval_hip_graph``, one graph per batch shape) == the eager
+    forwards, and coalesced eval batches (runner ``--eval_coalesce_tokens``: k batches of 2 per forward) give the same
+    per-example metrics as one forward per batch of 2 -- the reference's eval_batch_size 2 (launch.py:16)."""
+    from huggingface_sagemaker_tensorflow_distributed_amd.train.graph import CapturedEval  # noqa: F401
+
+    g = torch.Generator().manual_seed(3)
+    n, S = 24, 128
+    ids = torch.randint(1000, 30000, (n, S), generator=g)
+    am = torch.ones(n, S, dtype=torch.long)
+    am[5, 60:] = 0
+    am[17, 90:] = 0
+    labels = torch.randint(0, 2, (n,), generator=g)
+
+    def batches(bs):
+        return [{"input_ids": ids[i:i + bs].to(gpu), "attention_mask": am[i:i + bs].to(gpu),
+                 "labels": labels[i:i + bs].to(gpu)} for i in range(0, n, bs)]
+
+    tr = _trainer(gpu, True)
+    tr._seed.close()
+    res = {}
+    for flag in (False, True):
+        tr.eval_hip_graph = flag
+        res[flag] = tr.evaluate(batches(2))
+        assert tr.eval_graph_active == flag
+    assert len(tr._eval_graphs) == 1  # one shape, captured once
+    assert res[False] == res[True], res  # the same kernels replayed: identical sums
+    tr.eval_hip_graph = True
+    big = tr.evaluate(batches(8))  # 4 batches of 2 per forward
+    assert abs(big["loss"] - res[True]["loss"]) <= 1e-3 * abs(res[True]["loss"]), (big, res[True])
+    assert abs(big["sparse_categorical_accuracy"] - res[True]["sparse_categorical_accuracy"]) <= 1.0 / n + 1e-9

@@ -264,13 +264,15 @@ def test_attention_fast_paths_match_generic_kernel(gpu, p, S, monkeypatch):
     mb = ref.key_mask_bias(am)
     d = torch.randn(B * S, H, device=gpu, dtype=torch.bfloat16)
     outs = []
-    for generic in (False, True):
-        if generic:
-            monkeypatch.setenv("HSD_ATTN_GENERIC", "1")
-        x = qkv.clone().requires_grad_()
-        o = hip.attention(x, mb, B, S, heads, p, 4242)
-        o.backward(d)
-        outs.append((o.float(), x.grad.float()))
+    try:
+        for generic in (False, True):
+            hip._C.attn_set_force_generic(generic)
+            x = qkv.clone().requires_grad_()
+            o = hip.attention(x, mb, B, S, heads, p, 4242)
+            o.backward(d)
+            outs.append((o.float(), x.grad.float()))
+    finally:
+        hip._C.attn_set_force_generic(False)
     _close(outs[0][0], outs[1][0], 1e-2, 1e-2, "fwd")
     _close(outs[0][1], outs[1][1], 2e-2, 2e-2, "bwd")
 
