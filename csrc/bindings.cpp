@@ -43,7 +43,7 @@ void stream_wait(int64_t dst_ptr, int64_t src_ptr) {
 
 void adam_step(torch::Tensor p, torch::Tensor m, torch::Tensor v, torch::Tensor g, c10::optional<torch::Tensor> out,
                c10::optional<torch::Tensor> decay, double step, double eps, double b1, double b2, double gscale,
-               double lr_wd, c10::optional<torch::Tensor> coef) {
+               double lr_wd, c10::optional<torch::Tensor> coef, c10::optional<torch::Tensor> out_lo) {
   CHECK_CUDA(p); CHECK_CONTIG(p); CHECK_DTYPE(p, torch::kFloat32);
   CHECK_DTYPE(m, torch::kFloat32); CHECK_DTYPE(v, torch::kFloat32);
   TORCH_CHECK(p.numel() == m.numel() && p.numel() == v.numel() && p.numel() == g.numel(), "size mismatch");
@@ -67,9 +67,15 @@ void adam_step(torch::Tensor p, torch::Tensor m, torch::Tensor v, torch::Tensor 
     TORCH_CHECK(coef->numel() >= 4, "coef: fp32 [4]");
     dcoef = coef->data_ptr<float>();
   }
+  hsd::bf16_t* lo = nullptr;  // fp32 compute: `out` / `out_lo` = the bf16 hi / lo halves of the updated weights
+  if (out_lo.has_value()) {
+    CHECK_DTYPE(*out_lo, torch::kBFloat16);
+    TORCH_CHECK(o != nullptr && out_lo->numel() == p.numel() && out_lo->is_contiguous(), "out_lo needs out, same size");
+    lo = BF(*out_lo);
+  }
   hsd::launch_adam(p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), g.data_ptr(), gbf, o, dm,
                    p.numel(), (float)step, (float)eps, (float)b1, (float)b2, (float)gscale, (float)lr_wd,
-                   dcoef, cur_stream());
+                   dcoef, cur_stream(), lo);
 }
 
 #define OPT_BF(o) ((o).has_value() ? reinterpret_cast<hsd::bf16_t*>((o)->data_ptr()) : nullptr)
@@ -588,6 +594,42 @@ void gemm2_f32nt(torch::Tensor A, torch::Tensor B, torch::Tensor C, int64_t lb) 
                     nullptr, cur_stream());
 }
 
+// Segmented-K split-product GEMM (gemm2.hip launch_gemm2_seg): C = Σ_s A[s] · B[s] over three K segments of the bf16
+// hi / lo halves (same shapes and strides within A and within B). la = 0: NT, A [M][K], B [N][K] (lb 0) or [K][N]
+// (lb 1), C [M][N] fp32 written; la = lb = 1: TT weight gradient, A [T][M], B [T][N], C [M][N] fp32 accumulated.
+void gemm2_seg(std::vector<torch::Tensor> A, std::vector<torch::Tensor> B, torch::Tensor C, int64_t la, int64_t lb,
+               bool accumulate) {
+  TORCH_CHECK(A.size() == 3 && B.size() == 3, "gemm2_seg: three A and three B segments");
+  for (int s = 0; s < 3; ++s) {
+    TORCH_CHECK(A[s].is_cuda() && B[s].is_cuda() && A[s].scalar_type() == torch::kBFloat16 &&
+                B[s].scalar_type() == torch::kBFloat16 && A[s].dim() == 2 && B[s].dim() == 2 &&
+                A[s].stride(1) == 1 && B[s].stride(1) == 1, "gemm2_seg: 2-D bf16 GPU segments, unit inner stride");
+    TORCH_CHECK(A[s].sizes() == A[0].sizes() && A[s].stride(0) == A[0].stride(0) && B[s].sizes() == B[0].sizes() &&
+                B[s].stride(0) == B[0].stride(0), "gemm2_seg: segments of one operand share shape and stride");
+  }
+  check_f32(C, "C");
+  TORCH_CHECK(C.dim() == 2 && (la == 0 ? (lb == 0 || lb == 1) : lb == 1), "gemm2_seg layouts: (0,0), (0,1), (1,1)");
+  const int64_t M = la == 0 ? A[0].size(0) : A[0].size(1);
+  const int64_t Kseg = la == 0 ? A[0].size(1) : A[0].size(0);
+  const int64_t N = lb == 0 ? B[0].size(0) : B[0].size(1);
+  const int64_t KB = lb == 0 ? B[0].size(1) : B[0].size(0);
+  TORCH_CHECK(Kseg == KB && C.size(0) == M && C.size(1) == N, "gemm2_seg shapes");
+  TORCH_CHECK(hsd::gemm2_seg_supported((int)la, (int)lb, (int)M, (int)N, (int)Kseg), "gemm2_seg: unsupported shape");
+  TORCH_CHECK(A[0].stride(0) % 8 == 0 && B[0].stride(0) % 8 == 0, "gemm2_seg leading dims alignment");
+  const int64_t wsn = hsd::gemm2_seg_ws_numel((int)la, (int)lb, (int)M, (int)N, (int)Kseg);
+  torch::Tensor ws;
+  if (wsn > 0) ws = torch::empty({wsn}, C.options());  // K-split slabs (stream-ordered pool)
+  const hsd::bf16_t* a[3] = {CBF(A[0]), CBF(A[1]), CBF(A[2])};
+  const hsd::bf16_t* b[3] = {CBF(B[0]), CBF(B[1]), CBF(B[2])};
+  hsd::launch_gemm2_seg((int)la, (int)lb, a, A[0].stride(0), b, B[0].stride(0), (int)M, (int)N, (int)Kseg,
+                        C.data_ptr<float>(), C.stride(0), wsn > 0 ? ws.data_ptr<float>() : nullptr, cur_stream(),
+                        accumulate);
+}
+
+bool gemm2_seg_supported(int64_t la, int64_t lb, int64_t M, int64_t N, int64_t Kseg) {
+  return hsd::gemm2_seg_supported((int)la, (int)lb, (int)M, (int)N, (int)Kseg);
+}
+
 void split3(torch::Tensor x, torch::Tensor out, int64_t pat, bool rows) {
   check_f32(x, "x"); check_bf16(out, "out");
   TORCH_CHECK(x.dim() == 2 && x.size(1) % 4 == 0 && out.numel() == 3 * x.numel(), "split3 shapes");
@@ -926,6 +968,9 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("cu_hog", [](int64_t blocks, double usec) { hsd::launch_cu_hog((int)blocks, usec, cur_stream()); },
         "contention emulation: hold `blocks` whole CUs for `usec` us on the current stream");
   m.def("gemm2_f32nt", &gemm2_f32nt);
+  m.def("gemm2_seg", &gemm2_seg, py::arg("A"), py::arg("B"), py::arg("C"), py::arg("la"), py::arg("lb"),
+        py::arg("accumulate") = false);
+  m.def("gemm2_seg_supported", &gemm2_seg_supported);
   m.def("split3", &split3);
   m.def("split3_dual", &split3_dual);
   m.def("epi32", &epi32);

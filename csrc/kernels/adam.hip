@@ -23,15 +23,19 @@ __device__ __forceinline__ f32x4 load_grad(const void* __restrict__ g_, int64_t 
   }
 }
 
+// kLo (fp32 compute, ops/hip32.py): `out` / `out_lo` receive the bf16 hi / lo halves of the updated weight (hi =
+// bf16(θ), lo = bf16(θ - hi), exactly split2's), which the split-product GEMMs read directly -- the weights are split
+// once per optimizer step instead of at every use in forward and backward.
 // U chunks of 4 elements per thread per trip, all U x 4 loads issued before the first use (a one-chunk trip
 // leaves ~4 loads in flight per thread, too few to cover HBM latency at the occupancy a CU holds). Every
 // byte is touched once per step, so loads and stores are non-temporal (no L2 / MALL pollution).
-template <bool kGradBf16, bool kWriteBf16, int U>
+template <bool kGradBf16, bool kWriteBf16, int U, bool kLo = false>
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float* __restrict__ m,
                                                    float* __restrict__ v, const void* __restrict__ g_,
                                                    bf16_t* __restrict__ out, const uint8_t* __restrict__ decay,
                                                    int64_t n4, float step, float eps, float b1, float b2,
-                                                   float gscale, float lr_wd, const float* __restrict__ coef) {
+                                                   float gscale, float lr_wd, const float* __restrict__ coef,
+                                                   bf16_t* __restrict__ out_lo) {
   if (coef != nullptr) {  // HIP-graph replays: this step's scalars live on the device (train/graph.py)
     step = coef[0];
     eps = coef[1];
@@ -72,6 +76,12 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
         o.x = pack_bf2(pp[u][0], pp[u][1]);
         o.y = pack_bf2(pp[u][2], pp[u][3]);
         reinterpret_cast<u32x2*>(out)[i] = o;
+        if constexpr (kLo) {
+          u32x2 l;
+          l.x = pack_bf2(pp[u][0] - lo_bf(o.x), pp[u][1] - hi_bf(o.x));
+          l.y = pack_bf2(pp[u][2] - lo_bf(o.y), pp[u][3] - hi_bf(o.y));
+          reinterpret_cast<u32x2*>(out_lo)[i] = l;
+        }
       }
     }
   }
@@ -79,15 +89,26 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
 
 void launch_adam(float* p, float* m, float* v, const void* g, bool grad_bf16, bf16_t* out_bf16,
                  const uint8_t* decay, int64_t n, float step, float eps, float b1, float b2, float gscale,
-                 float lr_wd, const float* coef, hipStream_t stream) {
+                 float lr_wd, const float* coef, hipStream_t stream, bf16_t* out_lo) {
   int64_t n4 = n / 4;  // n is a multiple of 1024 (FlatParamStore)
   int threads = 256;
   int64_t blocks = (n4 + threads - 1) / threads;
   if (blocks > 256 * 8) blocks = 256 * 8;  // grid-stride: 8 blocks (32 waves) per CU over 256 CUs
   // two 16-B chunks per thread per trip (1 and 4 measured slower: profiles/bench_adam_r2.json)
-#define HSD_ADAM(GB, WB)                                                                                       \
-  hipLaunchKernelGGL((adam_kernel<GB, WB, 2>), dim3((unsigned)blocks), dim3(threads), 0, stream, p, m, v, g, \
-                     out_bf16, decay, n4, step, eps, b1, b2, gscale, lr_wd, coef)
+#define HSD_ADAM(GB, WB)                                                                                            \
+  hipLaunchKernelGGL((adam_kernel<GB, WB, 2>), dim3((unsigned)blocks), dim3(threads), 0, stream, p, m, v, g,      \
+                     out_bf16, decay, n4, step, eps, b1, b2, gscale, lr_wd, coef, nullptr)
+  if (out_lo != nullptr) {
+    if (out_bf16 == nullptr) abort();
+    if (grad_bf16)
+      hipLaunchKernelGGL((adam_kernel<true, true, 2, true>), dim3((unsigned)blocks), dim3(threads), 0, stream, p, m, v,
+                         g, out_bf16, decay, n4, step, eps, b1, b2, gscale, lr_wd, coef, out_lo);
+    else
+      hipLaunchKernelGGL((adam_kernel<false, true, 2, true>), dim3((unsigned)blocks), dim3(threads), 0, stream, p, m,
+                         v, g, out_bf16, decay, n4, step, eps, b1, b2, gscale, lr_wd, coef, out_lo);
+    HSD_CHECK_LAUNCH();
+    return;
+  }
   if (grad_bf16) {
     if (out_bf16) HSD_ADAM(true, true); else HSD_ADAM(true, false);
   } else {

@@ -134,7 +134,11 @@ __device__ __forceinline__ float wave_max(float v) {
 // Per element pair that is one XOR, one multiply and one XOR (the round-4 hash was two lowbias32 multiplies, three
 // xor-shifts and the pair-index arithmetic per pair). Statistics (tools/rng_quality.py, tests/test_rng.py): keep rate
 // within 3 sigma of 1 - p over 1e8 draws, no correlation between neighbouring rows / columns / pair halves / strides, 2x2
-// block patterns chi-square consistent with independence.
+// block patterns chi-square consistent with independence. Trade-off of the linear column word: two rows whose row
+// words differ by C(d) (0 < d < W/2) carry the same mask with the column pairs permuted by XOR d; a row pair hits one of
+// those W/2 - 1 differences with probability (W/2 - 1) / 2^32, the rate of a random function
+// (tests/test_rng.py::test_cross_row_twin_masks_occur_at_the_random_function_rate), and a twin keeps exactly as many
+// elements as its partner.
 __host__ __device__ __forceinline__ uint32_t mix32(uint32_t x) {
   x ^= x >> 16;
   x *= 0x7FEB352Du;

@@ -159,7 +159,7 @@ __device__ __forceinline__ void mainloop_staggered(f32x4 (&acc)[8][BN / 64], bf1
 #undef G2_LGKM0
 }
 
-template <int LA, int LB, int EPI, int BN, int SYNC>
+template <int LA, int LB, int EPI, int BN, int SYNC, bool SEG = false>
 __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
   p.dp = resolve_seed(p.dp);
   constexpr int WN = BN / 4;       // wave tile columns
@@ -209,13 +209,16 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
   // LDS byte address of smem (one generic -> LDS conversion; stage / slot offsets are plain integer adds)
   const uint32_t smem_lds = (uint32_t)(size_t)(__attribute__((address_space(3))) bf16_t*)smem;
   auto dma_slot = [&](int q, bf16_t* stage, int k0) {
+    const bf16_t* Ap;
+    const bf16_t* Bp;
+    const int kk = seg_k<SEG>(p, k0, Ap, Bp);
     if constexpr (ASM) {
       const uint32_t st = smem_lds + (uint32_t)(stage - smem) * 2u;
-      if (q < GA) dma_lds_asm(asm_base<LA>(p.A, p.lda, m0, k0), aoff[q], st + (wave * GA + q) * 1024u);
-      else dma_lds_asm(asm_base<LB>(p.B, p.ldb, n0, k0), aoff[q], st + (TA + (wave * GB + (q - GA)) * 512) * 2u);
+      if (q < GA) dma_lds_asm(asm_base<LA>(Ap, p.lda, m0, kk), aoff[q], st + (wave * GA + q) * 1024u);
+      else dma_lds_asm(asm_base<LB>(Bp, p.ldb, n0, kk), aoff[q], st + (TA + (wave * GB + (q - GA)) * 512) * 2u);
     } else {
-      if (q < GA) dma<LA, BM>(stage, p.A, p.lda, m0, p.M, k0, wave * GA + q, lane);
-      else dma<LB, BN>(stage + TA, p.B, p.ldb, n0, p.N, k0, wave * GB + (q - GA), lane);
+      if (q < GA) dma<LA, BM>(stage, Ap, p.lda, m0, p.M, kk, wave * GA + q, lane);
+      else dma<LB, BN>(stage + TA, Bp, p.ldb, n0, p.N, kk, wave * GB + (q - GA), lane);
     }
   };
 
@@ -1123,7 +1126,7 @@ __device__ __forceinline__ void wait_tiles(int left) {
 // 2 x 2 arrangement of 64 x 64 wave tiles (a K-split inside the workgroup), so on each SIMD one wave's MFMAs run
 // while the other's LDS reads are in flight; group 1 hands its partial tile to group 0 through LDS (64 KiB after
 // the 32 KiB epilogue staging: NSTG 3 or 4) and group 0 runs the epilogue. KW = 1: 4 waves, one per SIMD.
-template <int LA, int LB, int EPI, int NSTG, int KW = 1>
+template <int LA, int LB, int EPI, int NSTG, int KW = 1, bool SEG = false>
 __global__ __launch_bounds__(256 * KW, (NSTG <= 2 && KW == 1) ? 2 : 1) void gemm2s_kernel(G2Params p) {
   static_assert(NSTG >= 2 && NSTG <= 4, "2-4 stages");
   static_assert(KW == 1 || (KW == 2 && NSTG >= 3), "the in-workgroup K-split needs the 3rd stage's LDS for its handoff");
@@ -1151,10 +1154,13 @@ __global__ __launch_bounds__(256 * KW, (NSTG <= 2 && KW == 1) ? 2 : 1) void gemm
   // 16 DMA wave-instructions per operand image per stage, DW + DW per wave
   constexpr int DW = 4 / KW;
   auto dma_tile = [&](bf16_t* stage, int k0) {
+    const bf16_t* Ap;
+    const bf16_t* Bp;
+    const int kk = seg_k<SEG>(p, k0, Ap, Bp);
 #pragma unroll
-    for (int q = 0; q < DW; ++q) dma_asm<LA>(stage, p.A, p.lda, m0, p.M, k0, wave * DW + q, lane);
+    for (int q = 0; q < DW; ++q) dma_asm<LA>(stage, Ap, p.lda, m0, p.M, kk, wave * DW + q, lane);
 #pragma unroll
-    for (int q = 0; q < DW; ++q) dma_asm<LB>(stage + TA, p.B, p.ldb, n0, p.N, k0, wave * DW + q, lane);
+    for (int q = 0; q < DW; ++q) dma_asm<LB>(stage + TA, Bp, p.ldb, n0, p.N, kk, wave * DW + q, lane);
   };
 
   f32x4 acc[4][4];
@@ -1253,7 +1259,7 @@ static int g2_sync_mode(int la, int K) {
   return e != kKnobUnset ? e : 4;
 }
 
-template <int LA, int LB, int EPI, int BN>
+template <int LA, int LB, int EPI, int BN, bool SEG = false>
 static void g2_launch(const G2Params& p0, int splits, hipStream_t st) {
   G2Params p = p0;
   const int tiles_m = (p.M + g2::BM - 1) / g2::BM;
@@ -1265,6 +1271,11 @@ static void g2_launch(const G2Params& p0, int splits, hipStream_t st) {
   p.kps = kps;
   p.ntiles = tiles_m * p.tiles_n;
   dim3 grid(p.ntiles * splits);
+  if constexpr (SEG) {
+    hipLaunchKernelGGL((g2::gemm2_kernel<LA, LB, EPI, BN, 4, true>), grid, dim3(512), 0, st, p);
+    HSD_CHECK_LAUNCH();
+    return;
+  }
   const int mode = g2_sync_mode(LA, p.K);
   if (mode == 1) hipLaunchKernelGGL((g2::gemm2_kernel<LA, LB, EPI, BN, 1>), grid, dim3(512), 0, st, p);
   else if (mode == 2) hipLaunchKernelGGL((g2::gemm2_kernel<LA, LB, EPI, BN, 2>), grid, dim3(512), 0, st, p);
@@ -1293,9 +1304,9 @@ static int g2_num_cus() {
 // Tile-queue ring of the persistent kernels (gemm_common.h tq_*): one 9-counter slot per launch, 256 slots per device,
 // zeroed once; every launch leaves its slot zeroed (the last workgroup resets it). Launches on one stream reuse a slot
 // only 256 launches later; persistent GEMMs run on the compute stream only (the weight-gradient side stream runs the
-// TT kernels), so no two co-running launches share a slot. HSD_G2_DYN=0: static tile walk (A/B).
+// TT kernels), so no two co-running launches share a slot. (The static tile walk, p.tq = nullptr, measured 71-78 %
+// slower on the QKV forward with CUs held by a co-running kernel: profiles/contention_ab_r4.jsonl.)
 static int* g2_tq_slot(hipStream_t st) {
-  if (!HSD_KNOB("HSD_G2_DYN", 1)) return nullptr;
   constexpr int kSlots = 256;
   static int* base[64] = {};
   static unsigned next = 0;
@@ -1452,7 +1463,7 @@ bool gemm2s_use(int M, int N, int K) {
 // count, by a cost model fitted to tools/wgrad_ab.py on MI355X (24 BERT shapes x T = 4096 / 8192 / 16384; it
 // picks the faster path on all 24, profiles/wgrad_ab_r2.json): us = rounds x (a·K-tiles per split + b) + c·MB of
 // slab / C traffic, rounds = ceil(workgroups / 256) (one workgroup per CU on both). HSD_G2_SMALL_TT=0 / 1 forces
-// the tile size (the split count is still chosen by the model); HSD_WGRAD_MIN_KT sets the minimum K-tiles per split.
+// the tile size (the split count is still chosen by the model); >= 2 K-tiles per split.
 struct WgradPlan {
   bool small;
   int splits;
@@ -1486,7 +1497,7 @@ static WgradPlan wgrad_plan(int M, int N, int K) {
     while (tiles * sp < min_grid && sp < 32 && (K / 64) / (sp + 1) >= 2) ++sp;
     return WgradPlan{true, sp};
   }
-  const int min_kt = std::max(1, HSD_KNOB("HSD_WGRAD_MIN_KT", 2));
+  const int min_kt = 2;
   const int kt_all = K / 64;
   WgradPlan best{can_small && !can_big, 1};
   double best_cost = 1e30;
@@ -1522,9 +1533,15 @@ static int g2s_kw(int grid) {
   return 2;
 }
 
-template <int LA, int LB, int EPI>
+template <int LA, int LB, int EPI, bool SEG = false>
 static void g2s_launch(const G2Params& q, int grid, hipStream_t st) {
   const int ns = g2s_stages(grid);
+  if constexpr (SEG) {
+    if (ns == 2) hipLaunchKernelGGL((g2::gemm2s_kernel<LA, LB, EPI, 2, 1, true>), dim3(grid), dim3(256), 0, st, q);
+    else hipLaunchKernelGGL((g2::gemm2s_kernel<LA, LB, EPI, 3, 2, true>), dim3(grid), dim3(512), 0, st, q);
+    HSD_CHECK_LAUNCH();
+    return;
+  }
   if (ns == 2) hipLaunchKernelGGL((g2::gemm2s_kernel<LA, LB, EPI, 2>), dim3(grid), dim3(256), 0, st, q);
   else if (ns == 3 && g2s_kw(grid) == 2)
     hipLaunchKernelGGL((g2::gemm2s_kernel<LA, LB, EPI, 3, 2>), dim3(grid), dim3(512), 0, st, q);
@@ -1756,14 +1773,88 @@ void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const b
   }
 }
 
+// ---- segmented-K fp32-output GEMMs (the fp32 step's split products) ------------------------------------------------
+// C[M][N] (fp32) = Σ_{s<3} A_s · B_s over segments of Kseg (G2Params seg): la = 0, lb = 0 / 1: the NT forward / dgrad
+// (C written, or C += with `accumulate`: the fp32 blocks' residual gradient + dgrad in place; split-K slabs + one reduce
+// for small grids, gemm2_f32nt_splits), la = lb = 1: the TT weight gradient (C += ..., wgrad_plan's tile size and
+// K-splits). Kseg % 64 == 0.
+bool gemm2_seg_supported(int la, int lb, int M, int N, int Kseg) {
+  if (Kseg % 64 || Kseg <= 0) return false;
+  if (la == 0) return (lb == 0 || lb == 1) && gemm2_supported(0, lb, E2_F32_SLAB, M, N, 3 * Kseg);
+  return la == 1 && lb == 1 && gemm2_supported(1, 1, E2_F32_SLAB, M, N, 3 * Kseg);
+}
+
+int64_t gemm2_seg_ws_numel(int la, int lb, int M, int N, int Kseg) {
+  const int K = 3 * Kseg;
+  int sp = la == 0 ? gemm2_f32nt_splits(M, N, K) : wgrad_plan(M, N, K).splits;
+  if (sp <= 1) return 0;
+  int kps = (K + sp - 1) / sp;
+  kps = (kps + 63) / 64 * 64;
+  return (int64_t)((K + kps - 1) / kps) * M * N;
+}
+
+void launch_gemm2_seg(int la, int lb, const bf16_t* const A[3], int64_t lda, const bf16_t* const B[3], int64_t ldb,
+                      int M, int N, int Kseg, float* C, int64_t ldc, float* ws, hipStream_t st, bool accumulate) {
+  if (!gemm2_seg_supported(la, lb, M, N, Kseg) || ldc % 4) abort();
+  G2Params p{};
+  p.nt_store = 1;
+  p.A = A[0]; p.lda = lda; p.B = B[0]; p.ldb = ldb; p.M = M; p.N = N; p.K = 3 * Kseg; p.C = C; p.ldc = ldc;
+  p.seg = Kseg;
+  for (int s = 0; s < 3; ++s) {
+    p.segA[s] = A[s];
+    p.segB[s] = B[s];
+  }
+  const int K = 3 * Kseg;
+  auto reduce = [&](int real, int assign) {
+    const int64_t n4 = (int64_t)M * N / 4;
+    const int blocks = (int)std::min<int64_t>((n4 + 255) / 256, 2048);
+    hipLaunchKernelGGL(g2::slab_reduce_kernel, dim3(blocks), dim3(256), 0, st, ws, C, ldc, M, N, real, assign);
+    HSD_CHECK_LAUNCH();
+  };
+  auto real_of = [&](int sp) {
+    int kps = (K + sp - 1) / sp;
+    kps = (kps + 63) / 64 * 64;
+    return (K + kps - 1) / kps;
+  };
+  if (la == 0) {
+    if (ldc != N) abort();
+    const int sp = gemm2_f32nt_splits(M, N, K);
+    if (sp > 1 && ws == nullptr) abort();
+    G2Params q = p;
+    if (sp > 1) q.C = ws;
+    else q.accum_direct = accumulate ? 1 : 0;  // one split: each element has one owner (C += acc in place)
+    if (lb == 0) g2_launch<0, 0, E2_F32_SLAB, 256, true>(q, sp, st);
+    else g2_launch<0, 1, E2_F32_SLAB, 256, true>(q, sp, st);
+    if (sp > 1) reduce(real_of(sp), accumulate ? 0 : 1);
+    return;
+  }
+  const WgradPlan plan = wgrad_plan(M, N, K);
+  const int real = real_of(plan.splits);
+  if (real > 1 && ws == nullptr) abort();
+  G2Params q = p;
+  if (plan.small) {
+    q.tiles_n = N / g2::SBN;
+    q.ntiles = ((M + g2::SBM - 1) / g2::SBM) * q.tiles_n;
+    int kps = (K + plan.splits - 1) / plan.splits;
+    q.kps = (kps + 63) / 64 * 64;
+    if (real > 1) q.C = ws;  // one split: the kernel accumulates into C (unique owner per element)
+    g2s_launch<1, 1, E2_F32_SLAB, true>(q, q.ntiles * real, st);
+  } else if (real > 1) {
+    q.C = ws;
+    g2_launch<1, 1, E2_F32_SLAB, 256, true>(q, plan.splits, st);
+  } else {
+    q.accum_direct = 1;
+    g2_launch<1, 1, E2_F32_SLAB, 256, true>(q, 1, st);
+  }
+  if (real > 1) reduce(real, 0);
+}
+
 // ---- fp8 TT weight gradient (g2::gemm8tt_kernel) ----------------------------------------------------------------------
 bool gemm8_wgrad_supported(int M, int N, int T) { return M % 256 == 0 && N % 256 == 0 && T % 128 == 0 && T >= 128; }
 
 // K-splits: wgrad_plan's cost model for the 256-tile kernel with one fp8 K-tile (128 tokens: the bytes and MFMA cycles
 // of one bf16 K-tile of 64) per bf16 K-tile
 int gemm8_wgrad_splits(int M, int N, int T) {
-  const int env = HSD_KNOB("HSD_G8_WGRAD_SPLITS", 0);
-  if (env > 0) return env;
   const int kt_all = T / 128;
   int best = 1;
   double best_cost = 1e30;

@@ -58,7 +58,29 @@ struct G2Params {
   // E2_STORE_RDOT: fp32 [M / rd_seq · N / 64][rd_seq] row dots (rd_seq = the attention's sequence length)
   float* rd;
   int rd_seq;
+  // segmented K (SEG kernels; the fp32 step's split products, ops/hip32.py): K = 3 · seg, and a K-tile at k0 of segment
+  // s = k0 / seg reads segA[s] / segB[s] at k0 - s · seg (the leading dimensions lda / ldb are shared), so
+  // [xh | xh | xl] · [wh | wl | wh]ᵀ runs over the bf16 hi / lo halves of each operand as they are stored -- no
+  // concatenated three-block copies (seg % 64 == 0: a K-tile never straddles two segments)
+  int seg;
+  const bf16_t* segA[3];
+  const bf16_t* segB[3];
 };
+
+// operand bases and the segment-local k0 of a K-tile (SEG = false: p.A / p.B, k0 unchanged)
+template <bool SEG>
+__device__ __forceinline__ int seg_k(const G2Params& p, int k0, const bf16_t*& A, const bf16_t*& B) {
+  if constexpr (!SEG) {
+    A = p.A;
+    B = p.B;
+    return k0;
+  } else {
+    const int s = (k0 >= p.seg) + (k0 >= 2 * p.seg);
+    A = s == 0 ? p.segA[0] : (s == 1 ? p.segA[1] : p.segA[2]);
+    B = s == 0 ? p.segB[0] : (s == 1 ? p.segB[1] : p.segB[2]);
+    return k0 - s * p.seg;
+  }
+}
 
 // E2_STORE_RDOT: the 8 lanes holding the 8 chunks (64 columns = one head) of row m reduce their chunk dots; the first
 // writes the head's delta. Called by every lane of the group (DPP), `store` false for rows past M.

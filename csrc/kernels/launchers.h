@@ -11,7 +11,8 @@ struct DropoutParams;
 // adam.hip
 void launch_adam(float* p, float* m, float* v, const void* g, bool grad_bf16, bf16_t* out_bf16,
                  const uint8_t* decay, int64_t n, float step, float eps, float b1, float b2, float gscale,
-                 float lr_wd, const float* coef, hipStream_t stream);
+                 float lr_wd, const float* coef, hipStream_t stream,
+                 bf16_t* out_lo = nullptr);
 
 }  // namespace hsd
 
@@ -151,7 +152,12 @@ void launch_fp8_quant(const bf16_t* x, int64_t n, float* amax, uint8_t* q, float
 void launch_fp8_quant_many(const int64_t* amax_desc, int n_amax, int amax_blocks, const int64_t* quant_desc,
                            int n_quant, int quant_blocks_total, float* amax, float* sinv, int fmt, hipStream_t st);
 int fp8_elems_per_block();
-void attn_set_force_generic(bool on);  // tests: every S on the tiled generic attention kernels
+void attn_set_force_generic(bool on);
+// gemm2.hip: segmented-K fp32-output GEMMs over bf16 hi / lo operand halves (the fp32 step's split products)
+bool gemm2_seg_supported(int la, int lb, int M, int N, int Kseg);
+int64_t gemm2_seg_ws_numel(int la, int lb, int M, int N, int Kseg);
+void launch_gemm2_seg(int la, int lb, const bf16_t* const A[3], int64_t lda, const bf16_t* const B[3], int64_t ldb,
+                      int M, int N, int Kseg, float* C, int64_t ldc, float* ws, hipStream_t st, bool accumulate = false);  // tests: every S on the tiled generic attention kernels
 void attn128_set_diag(void* p);  // diagnostic phase stamps of the S=128 attention backward ([B*heads][8] u64)
 void gemm2_set_diag(void* p);  // diagnostic timestamps of the persistent NT kernel ([grid][64][4] u64), nullptr = off
 void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const bf16_t* B, int64_t ldb, int M, int N,

@@ -115,6 +115,9 @@ def attn_block(h, qkv_w, qkv_b, out_w, out_b, ln_w, ln_b, eps, mask_bias, batch,
     if _hip(h) and h.dtype == torch.bfloat16 and qkv_w.shape[0] == 3 * heads * 64:
         return _hipmod().attn_block(h, qkv_w, qkv_b, out_w, out_b, ln_w, ln_b, eps, mask_bias, batch, seq, heads,
                                     p_attn, seed_attn, p_hidden, seed_hidden, q8_next)
+    if _hip32(h) and _hip32mod().attn_block_ok(h, qkv_w, seq, heads):
+        return _hip32mod().attn_block(h, qkv_w, qkv_b, out_w, out_b, ln_w, ln_b, eps, mask_bias, batch, seq, heads,
+                                      p_attn, seed_attn, p_hidden, seed_hidden)
     qkv = linear(h, qkv_w, qkv_b)
     ctx = attention(qkv, mask_bias, batch, seq, heads, p_attn, seed_attn)
     return dense_residual_ln(ctx, out_w, out_b, h, ln_w, ln_b, eps, p_hidden, seed_hidden)
@@ -124,6 +127,8 @@ def ffn_block(h, w1, b1, w2, b2, ln_w, ln_b, eps, p, seed, q8_next=None):
     """Feed-forward sub-block: ``LN(dropout(gelu(h W1ᵀ + b1) W2ᵀ + b2) + h)``."""
     if _hip(h) and h.dtype == torch.bfloat16:
         return _hipmod().ffn_block(h, w1, b1, w2, b2, ln_w, ln_b, eps, p, seed, q8_next)
+    if _hip32(h) and _hip32mod().ffn_block_ok(h, w1):
+        return _hip32mod().ffn_block(h, w1, b1, w2, b2, ln_w, ln_b, eps, p, seed)
     a = linear_gelu(h, w1, b1)
     return dense_residual_ln(a, w2, b2, h, ln_w, ln_b, eps, p, seed)
 

@@ -244,10 +244,11 @@ def _empty(shape, like, dtype=None):
 
 
 # ------------------------------------------------------------------------------------------ optimizer
-def adam_step(p, m, v, g, out, decay, step, eps, b1, b2, gscale, lr_wd, coef=None):
+def adam_step(p, m, v, g, out, decay, step, eps, b1, b2, gscale, lr_wd, coef=None, out_lo=None):
     """``coef``: optional fp32 [4] device tensor (step, eps, grad_scale, lr*wd) read by the kernel instead of the
-    host scalars (captured HIP-graph steps, train/graph.py)."""
-    _C.adam_step(p, m, v, g, out, decay, step, eps, b1, b2, gscale, lr_wd, coef)
+    host scalars (captured HIP-graph steps, train/graph.py). ``out_lo``: with ``out``, the kernel writes the updated
+    weights' bf16 hi / lo halves (fp32 compute: the split-product GEMMs' operands, ops/hip32.py)."""
+    _C.adam_step(p, m, v, g, out, decay, step, eps, b1, b2, gscale, lr_wd, coef, out_lo)
 
 
 # ------------------------------------------------------------------------------------------ linear

@@ -7,10 +7,14 @@ multiples of 256):
 
 * GEMMs: the bf16 MFMA kernels (``csrc/kernels/gemm2.hip``) on 3-term split products. ``x = hi + lo`` with
   ``hi = bf16(x)``, ``lo = bf16(x - hi)`` (``|x - hi - lo| <= 2^-17 |x|``), and ``x·wᵀ ≈ xh·whᵀ + xh·wlᵀ + xl·whᵀ``
-  (the dropped ``xl·wlᵀ`` is ``<= 2^-16`` of each product), summed in fp32 by ONE GEMM over the concatenated K:
-  ``[xh|xh|xl] · [wh|wl|wh]ᵀ`` (``fp32.hip`` ``split3``). Forward and dgrad are NT with fp32 output, the weight
-  gradient is the TT kernel accumulating into the fp32 ``main_grad`` with the three blocks stacked along the tokens.
-  Relative error per output ~1e-5 of Σ|products| (vs ~4e-3 for one bf16 product).
+  (the dropped ``xl·wlᵀ`` is ``<= 2^-16`` of each product), summed in fp32 by ONE GEMM over a segmented K
+  (``gemm2_seg``: K-tiles of segment s read the s-th (A, B) pair of hi / lo halves as they are stored, so the operands
+  are never copied into three-block concatenations). Forward and dgrad are NT with fp32 output, the weight gradient is
+  the TT kernel accumulating into the fp32 ``main_grad`` with the segments along the tokens. Relative error per output
+  ~1e-5 of Σ|products| (vs ~4e-3 for one bf16 product).
+* Splits: weights are split ONCE per optimizer step -- the fused Adam writes each updated weight's hi / lo halves
+  (``FlatParamStore`` fp32 split buffers, ``p._hsd_split``); an activation is split once in the forward and its halves
+  saved for the weight gradient; an incoming gradient is split once for both of its GEMMs.
 * bias / GELU / dropout + residual epilogues, LayerNorm, embeddings, streaming attention (online softmax, exact fp32
   FMAs) and the classification head: ``csrc/kernels/fp32.hip``.
 
@@ -52,8 +56,16 @@ def _split(x: torch.Tensor, pat: int, rows: bool = False, pad_rows: int = 0) -> 
 # row blocks for the weight gradient): one read of dy and one launch instead of two (profiles/fp32_dual_split_ab_r5.log)
 
 
-def _split_grad(dy: torch.Tensor, need_dgrad: bool):
-    """(column-block split for :func:`mm_dgrad` or None, row-block split for :func:`wgrad_` or None) of ``dy``."""
+def _split_grad(dy: torch.Tensor, need_dgrad: bool, w: Optional[torch.Tensor] = None):
+    """``dy``'s split for both of its GEMMs: ((hi, lo), (hi, lo)) when the segmented GEMMs take the layer's shapes
+    (``w`` given), else (column-block split for :func:`mm_dgrad` or None, row-block split for :func:`wgrad_` or
+    None)."""
+    if w is not None and dy.dim() == 2 and dy.shape[1] % 4 == 0:
+        T, N = dy.shape
+        K = w.shape[1]
+        if _seg_ok(1, 1, N, K, T) and (not need_dgrad or _seg_ok(0, 1, T, K, N)):
+            hl = _split2(dy.contiguous())
+            return (hl if need_dgrad else None), hl
     if not (need_dgrad and dy.dim() == 2 and dy.shape[0] % 64 == 0 and dy.shape[1] % 4 == 0):
         return None, None
     dy = dy.contiguous()
@@ -64,14 +76,44 @@ def _split_grad(dy: torch.Tensor, need_dgrad: bool):
     return cols, rows
 
 
+def _split2(x: torch.Tensor):
+    hi = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+    lo = torch.empty_like(hi)
+    _C.split2(x, hi, lo)
+    return hi, lo
+
+
+def weight_split(w: torch.Tensor):
+    """(hi, lo) of weight ``w``: the halves the optimizer step wrote (``FlatParamStore`` split buffers) while they are
+    current, else split here. Current = no in-place change since the store last wrote them: the store's master buffer
+    and the parameter itself carry the versions recorded at that refresh (the fused Adam writes master and halves in
+    one kernel, so an optimizer step keeps them current)."""
+    sp = getattr(w, "_hsd_split", None)
+    if sp is not None:
+        hi, lo, store, ver = sp
+        if store.splits_current() and w._version == ver:
+            return hi, lo
+    return _split2(w.contiguous())
+
+
+def _seg_ok(la: int, lb: int, M: int, N: int, Kseg: int) -> bool:
+    return Kseg % 64 == 0 and _C.gemm2_seg_supported(la, lb, M, N, Kseg)
+
+
 def _nt_ok(M: int, N: int, K: int) -> bool:
     return N % 256 == 0 and (3 * K) % 64 == 0 and K % 4 == 0 and _C.gemm2_supported(0, 0, 7, M, N, 3 * K)
 
 
-def mm_nt(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
-    """x [M, K] · w [N, K]ᵀ -> [M, N] fp32 (split-product MFMA GEMM)."""
+def mm_nt(x: torch.Tensor, w: torch.Tensor, xs=None) -> torch.Tensor:
+    """x [M, K] · w [N, K]ᵀ -> [M, N] fp32 (split-product MFMA GEMM). ``xs``: x's (hi, lo), already made."""
     M, K = x.shape
     N = w.shape[0]
+    if _seg_ok(0, 0, M, N, K):
+        xh, xl = xs if xs is not None else _split2(x)
+        wh, wl = weight_split(w)
+        y = torch.empty((M, N), dtype=torch.float32, device=x.device)
+        _C.gemm2_seg([xh, xh, xl], [wh, wl, wh], y, 0, 0)
+        return y
     if not _nt_ok(M, N, K):
         return x @ w.t()  # odd widths only (not on the BERT-family shapes)
     y = torch.empty((M, N), dtype=torch.float32, device=x.device)
@@ -79,11 +121,22 @@ def mm_nt(x: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
     return y
 
 
-def mm_dgrad(dy: torch.Tensor, w: torch.Tensor, dys: Optional[torch.Tensor] = None) -> torch.Tensor:
+def mm_dgrad(dy: torch.Tensor, w: torch.Tensor, dys: Optional[torch.Tensor] = None,
+             acc: Optional[torch.Tensor] = None) -> torch.Tensor:
     """dy [M, N] · w [N, K] -> [M, K] fp32: NT with W read k-strided (layout (0, 1)), the split blocks of W stacked
-    along its rows (= the product's K). ``dys``: dy's column-block split, already made (:func:`_split_grad`)."""
+    along its rows (= the product's K). ``dys``: dy's split, already made (:func:`_split_grad`). ``acc`` (fp32 [M, K],
+    segmented GEMM only): the product is added to it in place and it is returned (a residual gradient + the dgrad
+    in one pass: the fused fp32 blocks below)."""
     M, N = dy.shape
     K = w.shape[1]
+    if isinstance(dys, tuple) or (dys is None and _seg_ok(0, 1, M, K, N)):
+        dh, dl = dys if dys is not None else _split2(dy.contiguous())
+        wh, wl = weight_split(w)
+        dx = acc if acc is not None else torch.empty((M, K), dtype=torch.float32, device=dy.device)
+        _C.gemm2_seg([dh, dh, dl], [wh, wl, wh], dx, 0, 1, acc is not None)
+        return dx
+    if acc is not None:
+        return acc.add_(mm_dgrad(dy, w, dys))
     if not (K % 256 == 0 and (3 * N) % 64 == 0 and N % 4 == 0 and _C.gemm2_supported(0, 1, 7, M, K, 3 * N)):
         return dy @ w
     dx = torch.empty((M, K), dtype=torch.float32, device=dy.device)
@@ -91,10 +144,17 @@ def mm_dgrad(dy: torch.Tensor, w: torch.Tensor, dys: Optional[torch.Tensor] = No
     return dx
 
 
-def wgrad_(g: _Grad, dy: torch.Tensor, x: torch.Tensor, dys: Optional[torch.Tensor] = None) -> None:
+def wgrad_(g: _Grad, dy: torch.Tensor, x: torch.Tensor, dys=None, xs=None) -> None:
     """g.buf [N, K] += dyᵀ [N, T] · x [T, K] in fp32 (TT kernel, split blocks stacked along the tokens, padded to
-    64-token K-tiles). ``dys``: dy's row-block split (T % 64 == 0), already made (:func:`_split_grad`)."""
-    N, K, T = dy.shape[1], x.shape[1], dy.shape[0]
+    64-token K-tiles). ``dys``: dy's split made by :func:`_split_grad` -- (hi, lo) on the segmented GEMM, else the
+    row-block split (T % 64 == 0); ``xs``: x's (hi, lo) saved by the forward."""
+    N, K, T = dy.shape[1], (x if x is not None else xs[0]).shape[1], dy.shape[0]
+    if xs is not None or isinstance(dys, tuple) or (dys is None and _seg_ok(1, 1, N, K, T)):
+        # (xs is only made where this segmented GEMM takes the shape: _x_split)
+        dh, dl = dys if isinstance(dys, tuple) else _split2(dy.contiguous())
+        xh, xl = xs if xs is not None else _split2(x.contiguous())
+        _C.gemm2_seg([dh, dh, dl], [xh, xl, xh], g.buf, 1, 1)
+        return
     Tp = -(-T // 64) * 64
     if not (N % 8 == 0 and K % 256 == 0 and N % 4 == 0 and K % 4 == 0 and _C.gemm2_supported(1, 1, 7, N, K, 3 * Tp)):
         g.buf.add_(dy.t() @ x)
@@ -111,24 +171,51 @@ def _colsum_(g: _Grad, x: torch.Tensor) -> None:
 
 
 # ------------------------------------------------------------------------------------------ linear layers
+def _x_split(x2: torch.Tensor, w: torch.Tensor):
+    """x's (hi, lo) when the segmented GEMMs take the layer (forward NT and the weight gradient reuse them), else None."""
+    M, K = x2.shape
+    if _seg_ok(0, 0, M, w.shape[0], K) and _seg_ok(1, 1, w.shape[0], K, M):
+        return _split2(x2)
+    return None
+
+
+def _save_x(ctx, x2, xs, *rest):
+    """Keep x's halves for the weight gradient instead of x itself (the same bytes, no re-split in backward)."""
+    if xs is not None:
+        ctx.save_for_backward(xs[0], xs[1], *rest)
+        ctx.x_split = True
+    else:
+        ctx.save_for_backward(x2, *rest)
+        ctx.x_split = False
+
+
+def _saved_x(ctx):
+    """(x2 or None, xs or None, *rest) from :func:`_save_x`."""
+    t = ctx.saved_tensors
+    if ctx.x_split:
+        return (None, (t[0], t[1])) + tuple(t[2:])
+    return (t[0], None) + tuple(t[1:])
+
+
 class _Linear32(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
         x2 = x.reshape(-1, x.shape[-1]).contiguous()
-        y = mm_nt(x2, w)
+        xs = _x_split(x2, w)
+        y = mm_nt(x2, w, xs)
         _C.epi32(y, b, None, y, 0, 0.0, 0)
-        ctx.save_for_backward(x2, w, b)
+        _save_x(ctx, x2, xs, w, b)
         ctx.xshape = x.shape
         return y.view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
     def backward(ctx, dy):
-        x2, w, b = ctx.saved_tensors
+        x2, xs, w, b = _saved_x(ctx)
         dy2 = dy.reshape(-1, w.shape[0]).contiguous()
-        sc, sr = _split_grad(dy2, ctx.needs_input_grad[0])
+        sc, sr = _split_grad(dy2, ctx.needs_input_grad[0], w)
         dx = mm_dgrad(dy2, w, sc).view(ctx.xshape) if ctx.needs_input_grad[0] else None
         gw, gb = _Grad(w), _Grad(b)
-        wgrad_(gw, dy2, x2, sr)
+        wgrad_(gw, dy2, x2, sr, xs)
         _colsum_(gb, dy2)
         return dx, gw.done(), gb.done()
 
@@ -141,23 +228,24 @@ class _LinearGelu32(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b):
         x2 = x.reshape(-1, x.shape[-1]).contiguous()
-        y = mm_nt(x2, w)  # becomes the pre-activation (bias added in place)
+        xs = _x_split(x2, w)
+        y = mm_nt(x2, w, xs)  # becomes the pre-activation (bias added in place)
         g = torch.empty_like(y)
         _C.epi32(y, b, None, g, 1, 0.0, 0)
-        ctx.save_for_backward(x2, w, b, y)
+        _save_x(ctx, x2, xs, w, b, y)
         ctx.xshape = x.shape
         return g.view(*x.shape[:-1], w.shape[0])
 
     @staticmethod
     def backward(ctx, dg):
-        x2, w, b, y = ctx.saved_tensors
+        x2, xs, w, b, y = _saved_x(ctx)
         da = torch.empty_like(y)
         _C.epi32(dg.reshape(y.shape).contiguous(), None, y, da, 4, 0.0, 0)
         gw, gb = _Grad(w), _Grad(b)
         _colsum_(gb, da)
-        sc, sr = _split_grad(da, ctx.needs_input_grad[0])
+        sc, sr = _split_grad(da, ctx.needs_input_grad[0], w)
         dx = mm_dgrad(da, w, sc).view(ctx.xshape) if ctx.needs_input_grad[0] else None
-        wgrad_(gw, da, x2, sr)
+        wgrad_(gw, da, x2, sr, xs)
         return dx, gw.done(), gb.done()
 
 
@@ -171,7 +259,8 @@ class _DenseResidualLN32(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, w, b, res, ln_w, ln_b, eps, p, seed):
         x2 = x.reshape(-1, x.shape[-1]).contiguous()
-        y = mm_nt(x2, w)
+        xs = _x_split(x2, w)
+        y = mm_nt(x2, w, xs)
         rows, H = y.shape
         z = torch.empty_like(y)
         _C.epi32(y, b, res.reshape(rows, H).contiguous(), z, 2, float(p), _s64(seed))
@@ -179,13 +268,13 @@ class _DenseResidualLN32(torch.autograd.Function):
         mean = torch.empty(rows, dtype=torch.float32, device=y.device)
         rstd = torch.empty_like(mean)
         _C.ln32_fwd(z, ln_w, ln_b, out, mean, rstd, float(eps))
-        ctx.save_for_backward(x2, w, b, z, mean, rstd, ln_w, ln_b)
+        _save_x(ctx, x2, xs, w, b, z, mean, rstd, ln_w, ln_b)
         ctx.p, ctx.seed, ctx.xshape = float(p), seed, x.shape
         return out.view(res.shape)
 
     @staticmethod
     def backward(ctx, dout):
-        x2, w, b, z, mean, rstd, ln_w, ln_b = ctx.saved_tensors
+        x2, xs, w, b, z, mean, rstd, ln_w, ln_b = _saved_x(ctx)
         gw, gb, gg, gbe = _Grad(w), _Grad(b), _Grad(ln_w), _Grad(ln_b)
         dz = torch.empty_like(z)
         _C.ln32_bwd(dout.reshape(z.shape).contiguous(), z, mean, rstd, ln_w, dz, gg.buf, gbe.buf)
@@ -194,9 +283,9 @@ class _DenseResidualLN32(torch.autograd.Function):
             dy = torch.empty_like(dz)
             _C.dropout32(dz, dy, ctx.p, _s64(ctx.seed))
         _colsum_(gb, dy)
-        sc, sr = _split_grad(dy, ctx.needs_input_grad[0])
+        sc, sr = _split_grad(dy, ctx.needs_input_grad[0], w)
         dx = mm_dgrad(dy, w, sc).view(ctx.xshape) if ctx.needs_input_grad[0] else None
-        wgrad_(gw, dy, x2, sr)
+        wgrad_(gw, dy, x2, sr, xs)
         return dx, gw.done(), gb.done(), dz.view(dout.shape), gg.done(), gbe.done(), None, None, None
 
 
@@ -331,13 +420,6 @@ class _Attention32(torch.autograd.Function):
         return dqkv, None, None, None, None, None, None
 
 
-def _split2(x: torch.Tensor):
-    hi = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
-    lo = torch.empty_like(hi)
-    _C.split2(x, hi, lo)
-    return hi, lo
-
-
 class _Attention32M(torch.autograd.Function):
     """fp32 attention on the bf16 matrix cores (attention32m.hip): qkv and dout carried as hi + lo bf16 pairs, every
     product the three-term split product, softmax / dropout / accumulation fp32. S a multiple of 128 up to 1024."""
@@ -386,6 +468,164 @@ def attention(qkv, mask_bias, batch, seq, heads, p, seed):
     if _ATTN32M and _C.attn32m_supported(seq):
         return _Attention32M.apply(qkv, mask_bias, batch, seq, heads, p, seed)
     return _Attention32.apply(qkv, mask_bias, batch, seq, heads, p, seed)
+
+
+# ------------------------------------------------------------------------------------------ fused encoder blocks
+# The post-LN residual of a block, LN(dropout(f(h) Wᵀ + b) + h), gives h two consumers; as separate autograd ops
+# the two gradients of h are summed by an ATen add (2 per layer, ~0.5 ms of a bert-large B = 8 step). The fused
+# blocks add the block's first dgrad straight into the residual gradient the LayerNorm backward produced
+# (mm_dgrad(acc=)): the segmented GEMM accumulates in place, one pass. Every kernel is the unfused ops' kernel, in the
+# same order, and the residual add is the same single fp32 add: outputs and gradients match the unfused ops bit for bit
+# (tests/test_gpu_fp32.py::test_fused_fp32_blocks_match_unfused_ops).
+def _ln_tail_bwd(dout, z, mean, rstd, ln_w, ln_b, p, seed, gb):
+    """LN backward of the block tail: (dz = the residual gradient, dy = the GEMM-output gradient), with the LN and the
+    GEMM bias gradients accumulated."""
+    gg, gbe = _Grad(ln_w), _Grad(ln_b)
+    dz = torch.empty_like(z)
+    _C.ln32_bwd(dout.reshape(z.shape).contiguous(), z, mean, rstd, ln_w, dz, gg.buf, gbe.buf)
+    dy = dz
+    if p > 0:
+        dy = torch.empty_like(dz)
+        _C.dropout32(dz, dy, p, _s64(seed))
+    _colsum_(gb, dy)
+    return dz, dy, gg, gbe
+
+
+def _ln_tail_fwd(y, b, res2d, ln_w, ln_b, eps, p, seed):
+    rows, H = y.shape
+    z = torch.empty_like(y)
+    _C.epi32(y, b, res2d, z, 2, float(p), _s64(seed))
+    out = torch.empty_like(z)
+    mean = torch.empty(rows, dtype=torch.float32, device=y.device)
+    rstd = torch.empty_like(mean)
+    _C.ln32_fwd(z, ln_w, ln_b, out, mean, rstd, float(eps))
+    return z, out, mean, rstd
+
+
+class _AttnBlock32(torch.autograd.Function):
+    """LN(dropout(attn(h Wqkvᵀ + bqkv) Woᵀ + bo) + h): QKV split-product GEMM, the split-product MFMA attention
+    (attention32m.hip), out-projection, dropout + residual, LayerNorm."""
+
+    @staticmethod
+    def forward(ctx, h, qkv_w, qkv_b, out_w, out_b, ln_w, ln_b, eps, mask_bias, B, S, heads, p_a, seed_a, p_h, seed_h):
+        h2d = h.reshape(-1, h.shape[-1]).contiguous()
+        hs = _x_split(h2d, qkv_w)
+        qkv = mm_nt(h2d, qkv_w, hs)
+        _C.epi32(qkv, qkv_b, None, qkv, 0, 0.0, 0)
+        qh, ql = _split2(qkv)
+        H = out_w.shape[1]
+        att = torch.empty((h2d.shape[0], H), dtype=torch.float32, device=h.device)
+        lse = torch.empty(B * heads * S, dtype=torch.float32, device=h.device)
+        mb = mask_bias.contiguous().float() if mask_bias is not None else None
+        _C.attn32m_fwd(qh, ql, mb, att, lse, B, S, heads, float(p_a), _s64(seed_a))
+        as_ = _x_split(att, out_w)
+        y = mm_nt(att, out_w, as_)
+        z, out, mean, rstd = _ln_tail_fwd(y, out_b, h2d, ln_w, ln_b, eps, p_h, seed_h)
+        ctx.save_for_backward(*(hs if hs is not None else (h2d,)), qkv_w, qkv_b, qh, ql, att, lse,
+                              mb if mb is not None else lse, *(as_ if as_ is not None else ()), out_w, out_b, z, mean,
+                              rstd, ln_w, ln_b)
+        ctx.cfg = (B, S, heads, float(p_a), seed_a, float(p_h), seed_h, mb is not None, hs is not None,
+                   as_ is not None)
+        return out.view(h.shape)
+
+    @staticmethod
+    def backward(ctx, dout):
+        B, S, heads, p_a, seed_a, p_h, seed_h, has_mask, h_split, a_split = ctx.cfg
+        t = list(ctx.saved_tensors)
+        hs = (t.pop(0), t.pop(0)) if h_split else None
+        h2d = None if h_split else t.pop(0)
+        qkv_w, qkv_b, qh, ql, att, lse, mb = t[:7]
+        t = t[7:]
+        as_ = (t.pop(0), t.pop(0)) if a_split else None
+        out_w, out_b, z, mean, rstd, ln_w, ln_b = t
+        g_ow, g_ob, g_qw, g_qb = _Grad(out_w), _Grad(out_b), _Grad(qkv_w), _Grad(qkv_b)
+        dz, dy, gg, gbe = _ln_tail_bwd(dout, z, mean, rstd, ln_w, ln_b, p_h, seed_h, g_ob)
+        sc, sr = _split_grad(dy, True, out_w)
+        datt = mm_dgrad(dy, out_w, sc)
+        wgrad_(g_ow, dy, None if a_split else att, sr, as_)
+        dh_, dl_ = _split2(datt)
+        dqkv = torch.empty(qh.shape, dtype=torch.float32, device=qh.device)
+        delta = torch.empty(B * heads * S, dtype=torch.float32, device=qh.device)
+        _C.attn32m_bwd(qh, ql, dh_, dl_, mb if has_mask else None, att, datt, lse, dqkv, delta, B, S, heads, p_a,
+                       _s64(seed_a))
+        _colsum_(g_qb, dqkv)
+        sc, sr = _split_grad(dqkv, ctx.needs_input_grad[0], qkv_w)
+        dh = mm_dgrad(dqkv, qkv_w, sc, acc=dz) if ctx.needs_input_grad[0] else None
+        wgrad_(g_qw, dqkv, h2d, sr, hs)
+        return (dh.view(dout.shape) if dh is not None else None, g_qw.done(), g_qb.done(), g_ow.done(), g_ob.done(),
+                gg.done(), gbe.done(), None, None, None, None, None, None, None, None, None)
+
+
+class _FFNBlock32(torch.autograd.Function):
+    """LN(dropout(gelu(h W1ᵀ + b1) W2ᵀ + b2) + h)."""
+
+    @staticmethod
+    def forward(ctx, h, w1, b1, w2, b2, ln_w, ln_b, eps, p, seed):
+        h2d = h.reshape(-1, h.shape[-1]).contiguous()
+        hs = _x_split(h2d, w1)
+        pre = mm_nt(h2d, w1, hs)  # becomes the pre-activation (bias added in place)
+        g = torch.empty_like(pre)
+        _C.epi32(pre, b1, None, g, 1, 0.0, 0)
+        gs = _x_split(g, w2)
+        y = mm_nt(g, w2, gs)
+        z, out, mean, rstd = _ln_tail_fwd(y, b2, h2d, ln_w, ln_b, eps, p, seed)
+        ctx.save_for_backward(*(hs if hs is not None else (h2d,)), w1, b1, pre, *(gs if gs is not None else (g,)), w2,
+                              b2, z, mean, rstd, ln_w, ln_b)
+        ctx.cfg = (float(p), seed, hs is not None, gs is not None)
+        return out.view(h.shape)
+
+    @staticmethod
+    def backward(ctx, dout):
+        p, seed, h_split, g_split = ctx.cfg
+        t = list(ctx.saved_tensors)
+        hs = (t.pop(0), t.pop(0)) if h_split else None
+        h2d = None if h_split else t.pop(0)
+        w1, b1, pre = t[:3]
+        t = t[3:]
+        gs = (t.pop(0), t.pop(0)) if g_split else None
+        g = None if g_split else t.pop(0)
+        w2, b2, z, mean, rstd, ln_w, ln_b = t
+        g_w1, g_b1, g_w2, g_b2 = _Grad(w1), _Grad(b1), _Grad(w2), _Grad(b2)
+        dz, dy, gg, gbe = _ln_tail_bwd(dout, z, mean, rstd, ln_w, ln_b, p, seed, g_b2)
+        sc, sr = _split_grad(dy, True, w2)
+        dg = mm_dgrad(dy, w2, sc)
+        wgrad_(g_w2, dy, g, sr, gs)
+        da = torch.empty_like(pre)
+        _C.epi32(dg, None, pre, da, 4, 0.0, 0)
+        _colsum_(g_b1, da)
+        sc, sr = _split_grad(da, ctx.needs_input_grad[0], w1)
+        dh = mm_dgrad(da, w1, sc, acc=dz) if ctx.needs_input_grad[0] else None
+        wgrad_(g_w1, da, h2d, sr, hs)
+        return (dh.view(dout.shape) if dh is not None else None, g_w1.done(), g_b1.done(), g_w2.done(), g_b2.done(),
+                gg.done(), gbe.done(), None, None, None)
+
+
+def _blocks_ok(h, H: int, inner: int) -> bool:
+    """The fused blocks' segmented GEMMs and fp32 LayerNorm take these shapes (else the unfused ops run)."""
+    T = h.numel() // H
+    return (H % 4 == 0 and H <= 1024 and T % 64 == 0 and _seg_ok(0, 0, T, inner, H) and _seg_ok(0, 1, T, H, inner)
+            and _seg_ok(0, 0, T, H, inner) and _seg_ok(0, 1, T, inner, H))
+
+
+def attn_block_ok(h, qkv_w, S: int, heads: int) -> bool:
+    H = h.shape[-1]
+    return (qkv_w.shape[0] == 3 * heads * 64 and _ATTN32M and _C.attn32m_supported(S) and _blocks_ok(h, H, 3 * H)
+            and _seg_ok(1, 1, 3 * H, H, h.numel() // H) and _seg_ok(1, 1, H, H, h.numel() // H))
+
+
+def ffn_block_ok(h, w1) -> bool:
+    H, inner = h.shape[-1], w1.shape[0]
+    T = h.numel() // H
+    return _blocks_ok(h, H, inner) and _seg_ok(1, 1, inner, H, T) and _seg_ok(1, 1, H, inner, T)
+
+
+def attn_block(h, qkv_w, qkv_b, out_w, out_b, ln_w, ln_b, eps, mask_bias, B, S, heads, p_a, seed_a, p_h, seed_h):
+    return _AttnBlock32.apply(h, qkv_w, qkv_b, out_w, out_b, ln_w, ln_b, eps, mask_bias, B, S, heads, p_a, seed_a,
+                              p_h, seed_h)
+
+
+def ffn_block(h, w1, b1, w2, b2, ln_w, ln_b, eps, p, seed):
+    return _FFNBlock32.apply(h, w1, b1, w2, b2, ln_w, ln_b, eps, p, seed)
 
 
 # ------------------------------------------------------------------------------------------ classification head

@@ -156,10 +156,10 @@ class FusedAdam:
         st, e = self._ranges[b]
         s = self.store
         step, eps_eff, gscale = self._coef
-        out = s.compute[st:e] if s.compute is not s.master else None
+        out, out_lo = s.adam_outputs(st, e)
         dm = self._decay_mask[st // ALIGN:(e + ALIGN - 1) // ALIGN] if self._decay_mask is not None else None
         hip.adam_step(s.master[st:e], self.exp_avg[st:e], self.exp_avg_sq[st:e], s.grad[st:e], out, dm, step,
-                      eps_eff, self.beta1, self.beta2, gscale, self.lr * self.weight_decay, self._kernel_coef())
+                      eps_eff, self.beta1, self.beta2, gscale, self.lr * self.weight_decay, self._kernel_coef(), out_lo)
         if self._tsub is not None:
             s.refresh_transposed_subset(self._tsub[b])
         self._done[b] = True
@@ -192,9 +192,10 @@ class FusedAdam:
             from ..ops import hip
 
             hip.join_side_streams()  # weight gradients may still be in flight on the wgrad stream
-            hip.adam_step(s.master, self.exp_avg, self.exp_avg_sq, s.grad, s.compute if write_compute else None,
+            out, out_lo = s.adam_outputs(0, s.numel)
+            hip.adam_step(s.master, self.exp_avg, self.exp_avg_sq, s.grad, out,
                           self._decay_mask, step, eps_eff, self.beta1, self.beta2, float(grad_scale),
-                          self.lr * self.weight_decay, self._kernel_coef())
+                          self.lr * self.weight_decay, self._kernel_coef(), out_lo)
             s.refresh_transposed()
             return
         # reference path (CPU): identical math on flat buffers

@@ -222,8 +222,7 @@ class GradBucketer:
             if self.compression == "fp16":
                 self.engine.set_prescale(self._prescale)
             # inside a capture the engine waits on the wgrad branch only once the capture has forked it (mark_ready)
-            # (HSD_ENGINE_CAPTURE_DEPS=0 drops that edge: only to show the ordering test detects the race)
-            self._capture_deps_pending = self._hip is not None and os.environ.get("HSD_ENGINE_CAPTURE_DEPS", "1") == "1"
+            self._capture_deps_pending = self._hip is not None
             self.engine.begin_step()
             return
         for b in self.buckets:

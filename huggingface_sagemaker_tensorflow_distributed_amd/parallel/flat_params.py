@@ -101,6 +101,7 @@ class FlatParamStore:
             p.grad = None
         self._index: Dict[int, int] = {id(p): i for i, p in enumerate(self.params)}
         self._setup_transposed()
+        self._setup_splits()
         # gradient-ready notification: HIP backward kernels write main_grad directly and return None;
         # torch-autograd gradients (CPU path, small torch-op heads) are folded into main_grad here. Either
         # way autograd runs the post-accumulate hook exactly once per parameter per backward, after every
@@ -129,6 +130,46 @@ class FlatParamStore:
         return hook
 
     # ----------------------------------------------------------------------------------
+    def _setup_splits(self) -> None:
+        """fp32 compute on the GPU (the reference's precision, ops/hip32.py): bf16 hi / lo halves of every parameter
+        (hi = bf16(θ), lo = bf16(θ - hi)) for the split-product GEMMs, written by the fused Adam in the same pass as
+        the update -- the weights are split once per optimizer step, not at every forward / backward use."""
+        self.split_hi = self.split_lo = None
+        self._split_version = None
+        if self.device.type != "cuda" or self.compute_dtype != torch.float32 or not hip_kernels_active():
+            return
+        self.split_hi = torch.empty(self.numel, dtype=torch.bfloat16, device=self.device)
+        self.split_lo = torch.empty_like(self.split_hi)
+        for seg, p in zip(self.segments, self.params):
+            p._hsd_split = [self.split_hi[seg.offset:seg.offset + seg.numel].view(seg.shape),
+                            self.split_lo[seg.offset:seg.offset + seg.numel].view(seg.shape), self, p._version]
+        self.refresh_splits()
+
+    @torch.no_grad()
+    def refresh_splits(self) -> None:
+        """Re-split every parameter (after anything other than the optimizer step changed the weights) and record the
+        versions the halves are current for (ops/hip32.py weight_split re-splits a weight changed in place since)."""
+        if self.split_hi is None:
+            return
+        from ..ops import hip
+
+        hip._C.split2(self.master, self.split_hi, self.split_lo)
+        self._split_version = self.master._version
+        for p in self.params:
+            p._hsd_split[3] = p._version
+
+    def splits_current(self) -> bool:
+        return self._split_version is not None and self.master._version == self._split_version
+
+    def adam_outputs(self, start: int, end: int):
+        """(out, out_lo) for the fused Adam on flat slice [start, end): the bf16 compute copy (bf16 / fp8 runs), or the
+        fp32 run's hi / lo halves, or (None, None)."""
+        if self.split_hi is not None:
+            return self.split_hi[start:end], self.split_lo[start:end]
+        if self.compute is not self.master:
+            return self.compute[start:end], None
+        return None, None
+
     def _setup_transposed(self) -> None:
         """bf16 Wᵀ copies (one flat buffer) for the dgrad GEMMs, refreshed by ONE batched transpose launch
         after every optimizer step instead of a transpose per GEMM per step."""
@@ -272,6 +313,7 @@ class FlatParamStore:
         if self.compute is not self.master:
             self.compute.copy_(self.master)
         self.refresh_transposed()
+        self.refresh_splits()
 
     def decay_block_mask(self, block: int) -> torch.Tensor:
         """uint8 per ``block`` elements: 1 = apply weight decay. Segments are ALIGN-aligned."""

@@ -64,7 +64,7 @@ def test_hip_backward_through_native_engine(gpu):
 
     args, _ = build_parser("train").parse_known_args(
         ["--model_name_or_path", "bert-base-uncased", "--train_batch_size", "16", "--dtype", "bf16",
-         "--log_every", "0"])
+         "--log_every", "0", "--hip_graph", "false"])
     parts = build(args, "train")
     model, store = parts["model"], parts["trainer"].store
     ds = hdata.synthetic_classification(16, 128, 30522, seed=0, full_length=True)
@@ -120,7 +120,7 @@ def test_optimizer_overlap_on_engine_stream(gpu, monkeypatch):
     monkeypatch.setenv("HSD_OPT_OVERLAP", "1")
     args, _ = build_parser("train").parse_known_args(
         ["--model_name_or_path", "bert-base-uncased", "--train_batch_size", "8", "--dtype", "bf16",
-         "--learning_rate", "1e-4", "--log_every", "0"])
+         "--learning_rate", "1e-4", "--log_every", "0", "--hip_graph", "false"])
     parts = build(args, "train")
     model, store, opt = parts["model"], parts["store"], parts["optimizer"]
     C = _C()
@@ -189,7 +189,7 @@ def test_whole_step_graph_with_native_engine(gpu, monkeypatch):
     for replay in (False, True):
         args, _ = build_parser("train").parse_known_args(
             ["--model_name_or_path", "bert-base-uncased", "--train_batch_size", "16", "--dtype", "bf16",
-             "--learning_rate", "1e-4", "--log_every", "0", "--seed", "3"])
+             "--learning_rate", "1e-4", "--log_every", "0", "--hip_graph", "false", "--seed", "3"])
         parts = build(args, "train")
         model, store, opt = parts["model"], parts["store"], parts["optimizer"]
         model.cfg  # noqa: B018
@@ -238,7 +238,7 @@ def test_whole_step_graph_waits_for_delayed_wgrad_branch(gpu, monkeypatch):
     for replay in (False, True):
         args, _ = build_parser("train").parse_known_args(
             ["--model_name_or_path", "bert-base-uncased", "--train_batch_size", "16", "--dtype", "bf16",
-             "--learning_rate", "1e-4", "--log_every", "0", "--seed", "5"])
+             "--learning_rate", "1e-4", "--log_every", "0", "--hip_graph", "false", "--seed", "5"])
         parts = build(args, "train")
         model, store, opt = parts["model"], parts["store"], parts["optimizer"]
         eng = C.CommEngine(0, 1, C.CommEngine.unique_id(), gpu.index, True)

@@ -50,7 +50,7 @@ def test_bert_base_train_steps_loss_decreases(gpu):
 
     args, _ = build_parser("train").parse_known_args(
         ["--model_name_or_path", "bert-base-uncased", "--train_batch_size", "32", "--learning_rate", "5e-5",
-         "--dtype", "bf16", "--log_every", "0"])
+         "--dtype", "bf16", "--log_every", "0", "--hip_graph", "false"])
     parts = build(args, "train")
     tr = parts["trainer"]
     ds = hdata.synthetic_classification(32 * 4, 128, 30522, seed=0)
@@ -136,7 +136,7 @@ def test_optimizer_overlapped_with_backward_uses_final_gradients(gpu, monkeypatc
     monkeypatch.setenv("HSD_WT", "1")  # keep the Wᵀ copies at this small step (their per-slice refresh is checked)
     args, _ = build_parser("train").parse_known_args(
         ["--model_name_or_path", "bert-base-uncased", "--train_batch_size", "8", "--learning_rate", "1e-4",
-         "--dtype", "bf16", "--log_every", "0", "--seed", "3"])
+         "--dtype", "bf16", "--log_every", "0", "--hip_graph", "false", "--seed", "3"])
     parts = build(args, "train")
     tr, st, opt = parts["trainer"], parts["store"], parts["optimizer"]
     assert tr._opt_overlap is not None and len(opt._ranges) > 10
@@ -175,7 +175,7 @@ def test_two_layer_bert_learns_the_marker_task(gpu, tmp_path):
     (tmp_path / "config.json").write_text(json.dumps(cfg))
     args, _ = build_parser("train").parse_known_args(
         ["--model_name_or_path", str(tmp_path), "--train_batch_size", "32", "--learning_rate", "1e-4",
-         "--dtype", "bf16", "--log_every", "0", "--seed", "7"])
+         "--dtype", "bf16", "--log_every", "0", "--hip_graph", "false", "--seed", "7"])
     parts = build(args, "train")
     tr = parts["trainer"]
     ds = hdata.synthetic_classification(32 * 300, 128, 30522, seed=1)
@@ -235,7 +235,7 @@ def test_fp32_mode_on_gpu_matches_cpu_fp32(gpu, tmp_path):
         cmd = [sys.executable, os.path.join(root, "scripts", "train.py"), "--epochs", "1", "--train_batch_size", "8",
                "--eval_batch_size", "8", "--model_name_or_path", "hsd-tiny-bert", "--max_seq_length", "64",
                "--num_train_examples", "64", "--num_eval_examples", "32", "--dtype", "fp32", "--device", device,
-               "--log_every", "0"]
+               "--log_every", "0", "--hip_graph", "false"]
         r = subprocess.run(cmd, env=env, capture_output=True, text=True, timeout=600)
         assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
         ev = dict(line.split(" = ") for line in (d / "data" / "eval_results.txt").read_text().splitlines())

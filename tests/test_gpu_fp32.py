@@ -198,3 +198,106 @@ def test_fp32_bert_step_on_kernels_matches_cpu(gpu):
     assert set(gc) == set(gg)
     worst = max((_rel(gg[k], gc[k]), k) for k in gc if gc[k].norm() > 0)
     assert worst[0] < 1e-3, worst
+
+
+@pytest.mark.parametrize("M,K,N", [(4096, 1024, 1024), (4096, 1024, 4096), (4096, 4096, 1024), (512, 768, 3072)])
+def test_segmented_gemm_equals_concatenated_split_gemm(gpu, M, K, N):
+    """gemm2_seg over the hi / lo halves == the GEMM over the three-block concatenations (split3) bit for bit: the same
+    K order, tiles and K-splits, only the operand addresses differ (forward NT, dgrad with W read k-strided, TT weight
+    gradient accumulating into C)."""
+    h = _h32()
+    C_ = h._C
+    torch.manual_seed(K + N)
+    x, w, dy = torch.randn(M, K, device=gpu), torch.randn(N, K, device=gpu) * 0.05, torch.randn(M, N, device=gpu)
+    xh, xl = h._split2(x)
+    wh, wl = h._split2(w)
+    dh, dl = h._split2(dy)
+    y_seg = torch.empty(M, N, device=gpu)
+    C_.gemm2_seg([xh, xh, xl], [wh, wl, wh], y_seg, 0, 0)
+    y_cat = torch.empty(M, N, device=gpu)
+    C_.gemm2_f32nt(h._split(x, h.PAT_A), h._split(w, h.PAT_B), y_cat, 0)
+    assert torch.equal(y_seg, y_cat)
+    dx_seg = torch.empty(M, K, device=gpu)
+    C_.gemm2_seg([dh, dh, dl], [wh, wl, wh], dx_seg, 0, 1)
+    dx_cat = torch.empty(M, K, device=gpu)
+    C_.gemm2_f32nt(h._split(dy, h.PAT_A), h._split(w, h.PAT_B, rows=True), dx_cat, 1)
+    assert torch.equal(dx_seg, dx_cat)
+    g0 = torch.randn(N, K, device=gpu)
+    g_seg = g0.clone()
+    C_.gemm2_seg([dh, dh, dl], [xh, xl, xh], g_seg, 1, 1)
+    g_cat = g0.clone()
+    sp = C_.gemm2_splits(N, K, 3 * M)
+    ws = torch.empty(max(1, sp) * N * K, device=gpu)
+    C_.gemm2(h._split(dy, h.PAT_A, rows=True), h._split(x, h.PAT_B, rows=True), g_cat, 1, 1, 7, None, None, None,
+             0.0, 0, sp, ws, None, None, 0)
+    assert torch.equal(g_seg, g_cat)
+
+
+def test_adam_writes_weight_halves_and_stale_halves_are_resplit(gpu):
+    """fp32 store: the fused Adam writes every updated weight's bf16 hi / lo halves (= split2 of the new master) in the
+    same pass, and a weight changed in place outside the optimizer is split again at use (weight_split)."""
+    from huggingface_sagemaker_tensorflow_distributed_amd.optim import FusedAdam
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel import FlatParamStore
+
+    h = _h32()
+    model = _bert2().to(gpu)
+    store = FlatParamStore(model, gpu, compute_dtype=torch.float32)
+    assert store.split_hi is not None and store.splits_current()
+    opt = FusedAdam(store, lr=1e-3)
+    store.grad.normal_()
+    opt.step()
+    hi, lo = h._split2(store.master)
+    assert torch.equal(store.split_hi, hi) and torch.equal(store.split_lo, lo)
+    w = model.encoder.layers[0].qkv_weight
+    wh, wl = h.weight_split(w)
+    assert wh.data_ptr() == w._hsd_split[0].data_ptr()  # the store's halves, no split at use
+    with torch.no_grad():
+        w.mul_(2.0)
+    wh2, wl2 = h.weight_split(w)
+    assert wh2.data_ptr() != w._hsd_split[0].data_ptr()
+    rh, rl = h._split2(w.detach().contiguous())
+    assert torch.equal(wh2, rh) and torch.equal(wl2, rl)
+
+
+def test_fused_fp32_blocks_match_unfused_ops(gpu):
+    """_AttnBlock32 / _FFNBlock32 (the block's first dgrad accumulated in place into the residual gradient) == the
+    unfused fp32 ops (linear, attention, dense_residual_ln: autograd adds the two gradients of h): outputs and every
+    gradient bit for bit (the same kernels in the same order; the residual add is the one commutative fp32 add)."""
+    h32 = _h32()
+    torch.manual_seed(5)
+    B, S, H, heads, inner = 2, 512, 1024, 16, 4096
+    h0 = torch.randn(B * S, H, device=gpu)
+    mk = lambda *s: (torch.randn(*s, device=gpu) * 0.03).requires_grad_()  # noqa: E731
+    qkv_w, qkv_b, out_w, out_b = mk(3 * H, H), mk(3 * H), mk(H, H), mk(H)
+    w1, b1, w2, b2 = mk(inner, H), mk(inner), mk(H, inner), mk(H)
+    ln = [(1 + 0.1 * torch.randn(H, device=gpu)).requires_grad_() for _ in range(2)]
+    lb = [(0.1 * torch.randn(H, device=gpu)).requires_grad_() for _ in range(2)]
+    am = torch.ones(B, S, dtype=torch.long, device=gpu)
+    am[1, 300:] = 0
+    from huggingface_sagemaker_tensorflow_distributed_amd.ops import reference as ref
+
+    mb = ref.key_mask_bias(am)
+    params = [qkv_w, qkv_b, out_w, out_b, w1, b1, w2, b2] + ln + lb
+    assert h32.attn_block_ok(h0, qkv_w, S, heads) and h32.ffn_block_ok(h0, w1)
+    d = torch.randn(B * S, H, device=gpu)
+    res = []
+    for fused in (True, False):
+        h = h0.clone().requires_grad_()
+        for p in params:
+            p.grad = None
+        if fused:
+            x = h32.attn_block(h, qkv_w, qkv_b, out_w, out_b, ln[0], lb[0], 1e-12, mb, B, S, heads, 0.1, 11, 0.1, 12)
+            y = h32.ffn_block(x, w1, b1, w2, b2, ln[1], lb[1], 1e-12, 0.1, 13)
+        else:
+            qkv = h32.linear(h, qkv_w, qkv_b)
+            ctx = h32.attention(qkv, mb, B, S, heads, 0.1, 11)
+            x = h32.dense_residual_ln(ctx, out_w, out_b, h, ln[0], lb[0], 1e-12, 0.1, 12)
+            a = h32.linear_gelu(x, w1, b1)
+            y = h32.dense_residual_ln(a, w2, b2, x, ln[1], lb[1], 1e-12, 0.1, 13)
+        y.backward(d)
+        res.append((y.detach().clone(), h.grad.clone(), [p.grad.clone() for p in params]))
+    (y0, g0, p0), (y1, g1, p1) = res
+    assert torch.equal(y0, y1)
+    assert torch.equal(g0, g1)
+    for a, b in zip(p0, p1):
+        assert torch.equal(a, b)

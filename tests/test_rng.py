@@ -126,3 +126,39 @@ def test_no_neighbour_correlation(W):
     exp = pat.size * q ** ones * (1 - q) ** (4 - ones)
     chi2 = float(((obs - exp) ** 2 / exp).sum())
     assert chi2 < 44.3, chi2
+
+
+@pytest.mark.parametrize("W", [128, 1024])
+def test_cross_row_twin_masks_occur_at_the_random_function_rate(W):
+    """because C is GF(2)-linear, rows r1, r2 whose row words satisfy R(r1) ^ R(r2) = C(d) for some
+    0 < d < W/2 have masks that are the same bits with the column pairs permuted (bits(r1, c) == bits(r2, c ^ d) for
+    every c). This is the documented trade-off of the one-XOR-per-pair column word (common.h): R = lowbias32 of the
+    row is a bijection, so each row pair hits one of the W/2 - 1 forbidden differences with probability
+    (W/2 - 1) / 2^32 -- the same rate as for a random function, no structure beyond it. A twin keeps the same number
+    of elements and a data-independent permutation of them. Here: the count over 2^17 rows (the bert-base B = 1024
+    S = 128 attention site's row count) matches n^2/2 x (W/2 - 1) / 2^32 within 5 sigma (Poisson), and every found
+    pair really is a permuted copy."""
+    n = 1 << 17
+    key = rng.site_key(0x1234567, 0x89ABCDE)
+    R = rng.mix32(torch.arange(n, dtype=torch.int64) ^ key).numpy().astype(np.uint32)
+    order = np.argsort(R)
+    Rs = R[order]
+    found, example = 0, None
+    for d in range(1, W // 2):
+        t = (R ^ np.uint32(rng.drop_col_int(d))).astype(np.uint32)
+        pos = np.searchsorted(Rs, t)
+        pos[pos == n] = 0
+        hit = Rs[pos] == t
+        found += int(hit.sum())
+        if example is None and hit.any():
+            i = int(np.nonzero(hit)[0][0])
+            example = (i, int(order[pos[i]]), d)
+    found //= 2  # each twin pair is seen from both rows
+    expect = n * n / 2 * (W // 2 - 1) / 2.0 ** 32
+    assert abs(found - expect) <= 5 * expect ** 0.5 + 1, (found, expect)
+    if example is not None:
+        r1, r2, d = example
+        cps = torch.arange(W // 2, dtype=torch.int64)
+        b1 = rng.pair_bits(key, torch.full_like(cps, r1), cps)
+        b2 = rng.pair_bits(key, torch.full_like(cps, r2), cps ^ d)
+        assert torch.equal(b1, b2)
