@@ -648,21 +648,37 @@ void split3_dual(torch::Tensor x, torch::Tensor out_cols, int64_t pat_cols, torc
                      BF(out_rows), (int)pat_rows);
 }
 
-void epi32(torch::Tensor y, c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> aux, torch::Tensor out,
-           int64_t kind, double p, int64_t seed) {
-  check_f32(y, "y"); check_f32(out, "out");
-  TORCH_CHECK(y.dim() == 2 && y.sizes() == out.sizes() && y.size(1) % 4 == 0, "epi32 shapes");
-  if (bias.has_value()) { check_f32(*bias, "bias"); TORCH_CHECK(bias->numel() == y.size(1), "epi32 bias"); }
-  if (kind >= 2) { TORCH_CHECK(aux.has_value(), "epi32 aux"); check_f32(*aux, "aux"); TORCH_CHECK(aux->sizes() == y.sizes(), "aux"); }
-  hsd::launch_epi32(y.data_ptr<float>(), OPT_F(bias), OPT_F(aux), out.data_ptr<float>(), y.size(0), (int)y.size(1),
-                    (int)kind, p, (uint64_t)seed, cur_stream());
+// optional bf16 halves of an fp32 output (hi = bf16(v), lo = bf16(v - hi)): both or neither, contiguous, numel n
+static void check_halves(const c10::optional<torch::Tensor>& hi, const c10::optional<torch::Tensor>& lo, int64_t n) {
+  TORCH_CHECK(hi.has_value() == lo.has_value(), "halves: hi and lo together");
+  if (!hi.has_value()) return;
+  check_bf16(*hi, "hi"); check_bf16(*lo, "lo");
+  TORCH_CHECK(hi->numel() == n && lo->numel() == n, "halves: numel");
 }
 
-void dropout32(torch::Tensor x, torch::Tensor out, double p, int64_t seed) {
+// out (optional with halves for kinds 0 / 1: the fp32 output is then not written), hi / lo: out's bf16 halves
+void epi32(torch::Tensor y, c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> aux,
+           c10::optional<torch::Tensor> out, int64_t kind, double p, int64_t seed, c10::optional<torch::Tensor> hi,
+           c10::optional<torch::Tensor> lo) {
+  check_f32(y, "y");
+  if (out.has_value()) { check_f32(*out, "out"); TORCH_CHECK(y.sizes() == out->sizes(), "epi32 out shape"); }
+  TORCH_CHECK(out.has_value() || (hi.has_value() && kind <= 1), "epi32: out needed");
+  TORCH_CHECK(y.dim() == 2 && y.size(1) % 4 == 0, "epi32 shapes");
+  check_halves(hi, lo, y.numel());
+  if (bias.has_value()) { check_f32(*bias, "bias"); TORCH_CHECK(bias->numel() == y.size(1), "epi32 bias"); }
+  if (kind >= 2) { TORCH_CHECK(aux.has_value(), "epi32 aux"); check_f32(*aux, "aux"); TORCH_CHECK(aux->sizes() == y.sizes(), "aux"); }
+  hsd::launch_epi32(y.data_ptr<float>(), OPT_F(bias), OPT_F(aux), OPT_F(out), y.size(0), (int)y.size(1), (int)kind,
+                    p, (uint64_t)seed, cur_stream(), OPT_BF(hi), OPT_BF(lo));
+}
+
+void dropout32(torch::Tensor x, torch::Tensor out, double p, int64_t seed, c10::optional<torch::Tensor> hi,
+               c10::optional<torch::Tensor> lo) {
   check_f32(x, "x"); check_f32(out, "out");
   const int64_t W = x.dim() ? x.size(-1) : 1;
   TORCH_CHECK(x.numel() == out.numel() && W % 4 == 0, "dropout32 sizes");
-  hsd::launch_dropout32(x.data_ptr<float>(), out.data_ptr<float>(), x.numel(), (int)W, p, (uint64_t)seed, cur_stream());
+  check_halves(hi, lo, x.numel());
+  hsd::launch_dropout32(x.data_ptr<float>(), out.data_ptr<float>(), x.numel(), (int)W, p, (uint64_t)seed, cur_stream(),
+                        OPT_BF(hi), OPT_BF(lo));
 }
 
 void colsum32(torch::Tensor x, torch::Tensor dbias) {
@@ -672,14 +688,16 @@ void colsum32(torch::Tensor x, torch::Tensor dbias) {
 }
 
 void ln32_fwd(torch::Tensor x, torch::Tensor g, torch::Tensor b, torch::Tensor out, torch::Tensor mean,
-              torch::Tensor rstd, double eps) {
+              torch::Tensor rstd, double eps, c10::optional<torch::Tensor> hi, c10::optional<torch::Tensor> lo) {
   check_f32(x, "x"); check_f32(g, "g"); check_f32(b, "b"); check_f32(out, "out"); check_f32(mean, "mean");
   check_f32(rstd, "rstd");
   const int64_t R = x.size(0), H = x.size(1);
   TORCH_CHECK(x.dim() == 2 && H % 4 == 0 && H <= 1024 && g.numel() == H && b.numel() == H && mean.numel() == R &&
               rstd.numel() == R && out.sizes() == x.sizes(), "ln32_fwd shapes");
+  check_halves(hi, lo, x.numel());
   hsd::launch_ln32_fwd(x.data_ptr<float>(), g.data_ptr<float>(), b.data_ptr<float>(), out.data_ptr<float>(),
-                       mean.data_ptr<float>(), rstd.data_ptr<float>(), (int)R, (int)H, (float)eps, cur_stream());
+                       mean.data_ptr<float>(), rstd.data_ptr<float>(), (int)R, (int)H, (float)eps, cur_stream(),
+                       OPT_BF(hi), OPT_BF(lo));
 }
 
 void ln32_bwd(torch::Tensor dy, torch::Tensor x, torch::Tensor mean, torch::Tensor rstd, torch::Tensor g,
@@ -973,10 +991,13 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.def("gemm2_seg_supported", &gemm2_seg_supported);
   m.def("split3", &split3);
   m.def("split3_dual", &split3_dual);
-  m.def("epi32", &epi32);
-  m.def("dropout32", &dropout32);
+  m.def("epi32", &epi32, py::arg("y"), py::arg("bias"), py::arg("aux"), py::arg("out"), py::arg("kind"), py::arg("p"),
+        py::arg("seed"), py::arg("hi") = py::none(), py::arg("lo") = py::none());
+  m.def("dropout32", &dropout32, py::arg("x"), py::arg("out"), py::arg("p"), py::arg("seed"),
+        py::arg("hi") = py::none(), py::arg("lo") = py::none());
   m.def("colsum32", &colsum32);
-  m.def("ln32_fwd", &ln32_fwd);
+  m.def("ln32_fwd", &ln32_fwd, py::arg("x"), py::arg("g"), py::arg("b"), py::arg("out"), py::arg("mean"),
+        py::arg("rstd"), py::arg("eps"), py::arg("hi") = py::none(), py::arg("lo") = py::none());
   m.def("ln32_bwd", &ln32_bwd);
   m.def("embed32_gather", &embed32_gather);
   m.def("embed32_scatter", &embed32_scatter);

@@ -464,13 +464,7 @@ __global__ __launch_bounds__(256) void split2_kernel(const float* __restrict__ x
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     const f32x4 v = reinterpret_cast<const f32x4*>(x)[i];
-    u32x2 h, l;
-    h.x = pack_bf2(v[0], v[1]);
-    h.y = pack_bf2(v[2], v[3]);
-    l.x = pack_bf2(v[0] - lo_bf(h.x), v[1] - hi_bf(h.x));
-    l.y = pack_bf2(v[2] - lo_bf(h.y), v[3] - hi_bf(h.y));
-    reinterpret_cast<u32x2*>(hi)[i] = h;
-    reinterpret_cast<u32x2*>(lo)[i] = l;
+    store_halves4(hi, lo, i, v[0], v[1], v[2], v[3]);
   }
 }
 

@@ -59,6 +59,18 @@ __device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
 }
 __device__ __forceinline__ float lo_bf(uint32_t w) { return __uint_as_float(w << 16); }
 __device__ __forceinline__ float hi_bf(uint32_t w) { return __uint_as_float(w & 0xFFFF0000u); }
+// four fp32 values -> their bf16 hi = bf16(v) and lo = bf16(v - hi) halves at group i (8 B each): the split-product
+// GEMMs' operand halves, written by the producing kernel (split2_kernel's arithmetic, bit for bit)
+__device__ __forceinline__ void store_halves4(bf16_t* hi, bf16_t* lo, int64_t i, const float v0, const float v1,
+                                              const float v2, const float v3) {
+  u32x2 h, l;
+  h.x = pack_bf2(v0, v1);
+  h.y = pack_bf2(v2, v3);
+  l.x = pack_bf2(v0 - lo_bf(h.x), v1 - hi_bf(h.x));
+  l.y = pack_bf2(v2 - lo_bf(h.y), v3 - hi_bf(h.y));
+  reinterpret_cast<u32x2*>(hi)[i] = h;
+  reinterpret_cast<u32x2*>(lo)[i] = l;
+}
 
 // ---- lane exchanges inside 8-lane groups on DPP (one VALU op each; __shfl_xor is a ds_bpermute: an LDS round trip
 // whose lgkmcnt wait serialises dependent chains, e.g. the attention backward's per-key-pair dropout hash exchange)

@@ -92,9 +92,12 @@ __global__ __launch_bounds__(256) void split3_kernel(const float* __restrict__ x
 //   2: out = dropout(y + bias) + res          (dropout element index m·N + n)
 //   3: out = y + res                          (dgrad + residual gradient)
 //   4: out = y · gelu'(aux)                   (dgrad through GELU; aux = saved pre-activation)
+// hi / lo (optional): out's bf16 halves for the next split-product GEMM (no split2 pass); out may then be null (the
+// fp32 value is not needed: the QKV projection's output, the GELU output)
 __global__ __launch_bounds__(256) void epi32_kernel(float* __restrict__ y, const float* __restrict__ bias,
                                                     const float* __restrict__ aux, float* __restrict__ out,
-                                                    int64_t M, int N, int kind, DropoutParams dp) {
+                                                    int64_t M, int N, int kind, DropoutParams dp,
+                                                    bf16_t* __restrict__ hi, bf16_t* __restrict__ lo) {
   dp = resolve_seed(dp);
   const int64_t n4 = M * N / 4;
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
@@ -138,7 +141,8 @@ __global__ __launch_bounds__(256) void epi32_kernel(float* __restrict__ y, const
         o[e] = v[e] * (cdf + x * 0.3989422804014327f * expf(-0.5f * x * x));
       }
     }
-    reinterpret_cast<f32x4*>(out)[i] = o;
+    if (out != nullptr) reinterpret_cast<f32x4*>(out)[i] = o;
+    if (hi != nullptr) store_halves4(hi, lo, i, o[0], o[1], o[2], o[3]);
     c4 += sc;
     m += sr;
     if (c4 >= N4) {
@@ -148,9 +152,11 @@ __global__ __launch_bounds__(256) void epi32_kernel(float* __restrict__ y, const
   }
 }
 
-// out = x · keep (mask rows of width W = the last dimension, W % 4 == 0), in place allowed
-__global__ __launch_bounds__(256) void dropout32_kernel(const float* __restrict__ x, float* __restrict__ out,
-                                                        int64_t n4, int W, DropoutParams dp) {
+// out = x · keep (mask rows of width W = the last dimension, W % 4 == 0), in place allowed; hi / lo (optional): out's
+// bf16 halves
+__global__ __launch_bounds__(256) void dropout32_kernel(const float* __restrict__ x, float* out, int64_t n4, int W,
+                                                        DropoutParams dp, bf16_t* __restrict__ hi,
+                                                        bf16_t* __restrict__ lo) {
   dp = resolve_seed(dp);
   const int64_t stride = (int64_t)gridDim.x * blockDim.x;
   const int W4 = W / 4;
@@ -169,6 +175,7 @@ __global__ __launch_bounds__(256) void dropout32_kernel(const float* __restrict_
     v[2] *= keep_factor(b1, 0, dp);
     v[3] *= keep_factor(b1, 1, dp);
     reinterpret_cast<f32x4*>(out)[i] = v;
+    if (hi != nullptr) store_halves4(hi, lo, i, v[0], v[1], v[2], v[3]);
     c4 += sc;
     row += sr;
     if (c4 >= W4) {
@@ -231,7 +238,8 @@ template <int NJ>
 __global__ __launch_bounds__(256) void ln32_fwd_kernel(const float* __restrict__ x, const float* __restrict__ g,
                                                        const float* __restrict__ b, float* __restrict__ out,
                                                        float* __restrict__ mean, float* __restrict__ rstd, int R,
-                                                       int H, float eps) {
+                                                       int H, float eps, bf16_t* __restrict__ hi,
+                                                       bf16_t* __restrict__ lo) {
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= R) return;
@@ -266,6 +274,7 @@ __global__ __launch_bounds__(256) void ln32_fwd_kernel(const float* __restrict__
 #pragma unroll
       for (int e = 0; e < 4; ++e) o[e] = (v[j][e] - mu) * rs * gg[e] + bb[e];
       *reinterpret_cast<f32x4*>(out + (int64_t)row * H + c) = o;
+      if (hi != nullptr) store_halves4(hi, lo, ((int64_t)row * H + c) / 4, o[0], o[1], o[2], o[3]);
     }
   }
   if (lane == 0) {
@@ -795,17 +804,18 @@ void launch_split3(const float* x, bf16_t* out, int64_t R, int64_t C, int pat, b
 }
 
 void launch_epi32(float* y, const float* bias, const float* aux, float* out, int64_t M, int N, int kind, double p,
-                  uint64_t seed, hipStream_t st) {
-  if (N % 4) abort();
+                  uint64_t seed, hipStream_t st, bf16_t* hi, bf16_t* lo) {
+  if (N % 4 || (hi == nullptr) != (lo == nullptr) || (out == nullptr && (hi == nullptr || kind > 1))) abort();
   hipLaunchKernelGGL(f32k::epi32_kernel, dim3(ew_blocks(M * N / 4)), dim3(256), 0, st, y, bias, aux, out, M, N, kind,
-                     make_dropout(kind == 2 ? p : 0.0, seed));
+                     make_dropout(kind == 2 ? p : 0.0, seed), hi, lo);
   HSD_CHECK_LAUNCH();
 }
 
-void launch_dropout32(const float* x, float* out, int64_t n, int W, double p, uint64_t seed, hipStream_t st) {
-  if (n % 4 || W % 4 || W <= 0) abort();
+void launch_dropout32(const float* x, float* out, int64_t n, int W, double p, uint64_t seed, hipStream_t st,
+                      bf16_t* hi, bf16_t* lo) {
+  if (n % 4 || W % 4 || W <= 0 || (hi == nullptr) != (lo == nullptr)) abort();
   hipLaunchKernelGGL(f32k::dropout32_kernel, dim3(ew_blocks(n / 4)), dim3(256), 0, st, x, out, n / 4, W,
-                     make_dropout(p, seed));
+                     make_dropout(p, seed), hi, lo);
   HSD_CHECK_LAUNCH();
 }
 
@@ -828,12 +838,15 @@ void launch_colsum32(const float* x, float* dbias, int M, int N, hipStream_t st)
 }
 
 void launch_ln32_fwd(const float* x, const float* g, const float* b, float* out, float* mean, float* rstd, int R,
-                     int H, float eps, hipStream_t st) {
-  if (H % 4 || H > 1024) abort();
+                     int H, float eps, hipStream_t st, bf16_t* hi, bf16_t* lo) {
+  if (H % 4 || H > 1024 || (hi == nullptr) != (lo == nullptr)) abort();
   const dim3 grid((R + 3) / 4);
-  if (H <= 256) hipLaunchKernelGGL(f32k::ln32_fwd_kernel<1>, grid, dim3(256), 0, st, x, g, b, out, mean, rstd, R, H, eps);
-  else if (H <= 512) hipLaunchKernelGGL(f32k::ln32_fwd_kernel<2>, grid, dim3(256), 0, st, x, g, b, out, mean, rstd, R, H, eps);
-  else hipLaunchKernelGGL(f32k::ln32_fwd_kernel<4>, grid, dim3(256), 0, st, x, g, b, out, mean, rstd, R, H, eps);
+#define LN32F(NJ) \
+  hipLaunchKernelGGL(f32k::ln32_fwd_kernel<NJ>, grid, dim3(256), 0, st, x, g, b, out, mean, rstd, R, H, eps, hi, lo)
+  if (H <= 256) LN32F(1);
+  else if (H <= 512) LN32F(2);
+  else LN32F(4);
+#undef LN32F
   HSD_CHECK_LAUNCH();
 }
 

@@ -208,10 +208,11 @@ __global__ __launch_bounds__(512, 1) void gemm2_kernel(G2Params p) {
   }
   // LDS byte address of smem (one generic -> LDS conversion; stage / slot offsets are plain integer adds)
   const uint32_t smem_lds = (uint32_t)(size_t)(__attribute__((address_space(3))) bf16_t*)smem;
+  const SegSel<SEG> segsel(p);
   auto dma_slot = [&](int q, bf16_t* stage, int k0) {
     const bf16_t* Ap;
     const bf16_t* Bp;
-    const int kk = seg_k<SEG>(p, k0, Ap, Bp);
+    const int kk = segsel.map(k0, Ap, Bp);
     if constexpr (ASM) {
       const uint32_t st = smem_lds + (uint32_t)(stage - smem) * 2u;
       if (q < GA) dma_lds_asm(asm_base<LA>(Ap, p.lda, m0, kk), aoff[q], st + (wave * GA + q) * 1024u);
@@ -674,14 +675,17 @@ __global__ __launch_bounds__(512, 1) void gemm2pk_kernel(G2Params p) {
 // epilogues. Per K-tile a wave issues 32 MFMAs of 32 cycles (bf16: 64 of 16) and reads 24 x 16 B per lane (same).
 typedef __attribute__((ext_vector_type(8))) int i32x8;
 
-// 16x16x128 fragment: lane l holds row rbase + (l&15), k = 32(l>>4) .. +31 (chunks 2(l>>4), 2(l>>4)+1); A and B use
-// the same k assignment, so the product does not depend on the instruction's internal k order
+// 16x16x128 fragment: lane l holds row rbase + (l&15) and the 16-B chunks (l>>4) and (l>>4)+4 of the 128-B K-tile
+// row as its instruction k slots 32(l>>4) .. +31. A and B use the same chunk -> slot assignment, so the product is the
+// same sum. Chunks (g, g+4) rather than the contiguous (2g, 2g+1): with the f1 swizzle the contiguous pair put two
+// lanes of every ds_read_b128 lane group on the same banks (2-way, 43-48 % SQ_LDS_BANK_CONFLICT per
+// profiles/r6/pmc_gemm8_r6.tsv); (g, g+4) is conflict-free in the gfx950 lane-group model (tools/lds_banks.py)
 __device__ __forceinline__ i32x8 frag8(const bf16_t* img, int rbase, int lane) {
   const int row = rbase + (lane & 15);
-  const int c0 = 2 * (lane >> 4);
+  const int c0 = lane >> 4;
   const bf16_t* r = img + row * 64;
   const u32x4 lo = *reinterpret_cast<const u32x4*>(r + ((c0 ^ f1(row)) << 3));
-  const u32x4 hi = *reinterpret_cast<const u32x4*>(r + (((c0 + 1) ^ f1(row)) << 3));
+  const u32x4 hi = *reinterpret_cast<const u32x4*>(r + (((c0 + 4) ^ f1(row)) << 3));
   i32x8 v;
   v[0] = (int)lo[0]; v[1] = (int)lo[1]; v[2] = (int)lo[2]; v[3] = (int)lo[3];
   v[4] = (int)hi[0]; v[5] = (int)hi[1]; v[6] = (int)hi[2]; v[7] = (int)hi[3];
@@ -1153,10 +1157,11 @@ __global__ __launch_bounds__(256 * KW, (NSTG <= 2 && KW == 1) ? 2 : 1) void gemm
 
   // 16 DMA wave-instructions per operand image per stage, DW + DW per wave
   constexpr int DW = 4 / KW;
+  const SegSel<SEG> segsel(p);
   auto dma_tile = [&](bf16_t* stage, int k0) {
     const bf16_t* Ap;
     const bf16_t* Bp;
-    const int kk = seg_k<SEG>(p, k0, Ap, Bp);
+    const int kk = segsel.map(k0, Ap, Bp);
 #pragma unroll
     for (int q = 0; q < DW; ++q) dma_asm<LA>(stage, Ap, p.lda, m0, p.M, kk, wave * DW + q, lane);
 #pragma unroll
@@ -1218,9 +1223,10 @@ __global__ __launch_bounds__(256 * KW, (NSTG <= 2 && KW == 1) ? 2 : 1) void gemm
   }
   const int mw = m0 + arow, nw = n0 + bcol;
   if constexpr (EPI == E2_F32_SLAB) {
-    // acc[i][j]: lane l holds m = 16i + (l&15), n = 16j + 4(l>>4) + r. One TT split accumulates into C; NT always
-    // writes its slab (splitk_epi_kernel reduces and runs the bf16 epilogue).
-    const bool direct = LA == 1 && nwg == p.ntiles;
+    // acc[i][j]: lane l holds m = 16i + (l&15), n = 16j + 4(l>>4) + r. One TT split (or one NT split with
+    // accum_direct: the fp32 step's dgrad into the residual gradient) accumulates into C; NT otherwise writes its slab
+    // (split 0 of one split: C itself, ldc == N).
+    const bool direct = (LA == 1 || p.accum_direct) && nwg == p.ntiles;
     const int q4 = lane >> 4, lr = lane & 15;
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -1778,6 +1784,15 @@ void launch_gemm2(int la, int lb, int epi, const bf16_t* A, int64_t lda, const b
 // (C written, or C += with `accumulate`: the fp32 blocks' residual gradient + dgrad in place; split-K slabs + one reduce
 // for small grids, gemm2_f32nt_splits), la = lb = 1: the TT weight gradient (C += ..., wgrad_plan's tile size and
 // K-splits). Kseg % 64 == 0.
+// the fp32 forward / dgrad on 128 x 128 tiles (gemm2s, one K-split) for grids that 256 x 256 tiles leave mostly idle
+// (gemm2s_use) and K < 6,144, instead of 256 x 256 tiles split over K into slabs plus a reduce pass. bert-large T = 4,096
+// (tools/seg_vs_cat.py, profiles/r6/seg_vs_cat_r6e.log): N 1,024 at K 3 x 1,024: 32.4 / 34.8 us (fwd / dgrad) vs 44.4 /
+// 45.2 on slabs; at K 3 x 3,072 and 3 x 4,096 the slabs win (81.6 vs 91.2, 96.6 vs 111.8, 99.3 vs 124.5 us).
+// HSD_SEG_NT_SMALL=0: always the slabs.
+static bool seg_nt_small(int M, int N, int K) {
+  return HSD_KNOB("HSD_SEG_NT_SMALL", 1) && K < 6144 && gemm2s_use(M, N, K);
+}
+
 bool gemm2_seg_supported(int la, int lb, int M, int N, int Kseg) {
   if (Kseg % 64 || Kseg <= 0) return false;
   if (la == 0) return (lb == 0 || lb == 1) && gemm2_supported(0, lb, E2_F32_SLAB, M, N, 3 * Kseg);
@@ -1786,6 +1801,7 @@ bool gemm2_seg_supported(int la, int lb, int M, int N, int Kseg) {
 
 int64_t gemm2_seg_ws_numel(int la, int lb, int M, int N, int Kseg) {
   const int K = 3 * Kseg;
+  if (la == 0 && seg_nt_small(M, N, K)) return 0;
   int sp = la == 0 ? gemm2_f32nt_splits(M, N, K) : wgrad_plan(M, N, K).splits;
   if (sp <= 1) return 0;
   int kps = (K + sp - 1) / sp;
@@ -1818,6 +1834,18 @@ void launch_gemm2_seg(int la, int lb, const bf16_t* const A[3], int64_t lda, con
   };
   if (la == 0) {
     if (ldc != N) abort();
+    if (seg_nt_small(M, N, K)) {
+      // 128 x 128 tiles, one K-split: the grid fills the CUs without slabs or a reduce pass; each output element has
+      // one owner (written, or C += acc with `accumulate`)
+      G2Params q = p;
+      q.tiles_n = N / g2::SBN;
+      q.ntiles = ((M + g2::SBM - 1) / g2::SBM) * q.tiles_n;
+      q.kps = K;
+      q.accum_direct = accumulate ? 1 : 0;
+      if (lb == 0) g2s_launch<0, 0, E2_F32_SLAB, true>(q, q.ntiles, st);
+      else g2s_launch<0, 1, E2_F32_SLAB, true>(q, q.ntiles, st);
+      return;
+    }
     const int sp = gemm2_f32nt_splits(M, N, K);
     if (sp > 1 && ws == nullptr) abort();
     G2Params q = p;

@@ -67,20 +67,51 @@ struct G2Params {
   const bf16_t* segB[3];
 };
 
-// operand bases and the segment-local k0 of a K-tile (SEG = false: p.A / p.B, k0 unchanged)
-template <bool SEG>
-__device__ __forceinline__ int seg_k(const G2Params& p, int k0, const bf16_t*& A, const bf16_t*& B) {
-  if constexpr (!SEG) {
-    A = p.A;
-    B = p.B;
-    return k0;
-  } else {
-    const int s = (k0 >= p.seg) + (k0 >= 2 * p.seg);
-    A = s == 0 ? p.segA[0] : (s == 1 ? p.segA[1] : p.segA[2]);
-    B = s == 0 ? p.segB[0] : (s == 1 ? p.segB[1] : p.segB[2]);
-    return k0 - s * p.seg;
-  }
+// wave-uniform copy of a kernel-argument pointer (readfirstlane'd halves: SGPRs, as wave_rsrc below)
+__device__ __forceinline__ const bf16_t* uniform_ptr(const bf16_t* ptr) {
+  const uint64_t a = (uint64_t)ptr;
+  const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+  return reinterpret_cast<const bf16_t*>(((uint64_t)hi << 32) | lo);
 }
+
+// Operand bases and the segment-local k0 of a K-tile. The six segment pointers are copied out of the parameter
+// struct ONCE, into scalar locals: indexing G2Params' arrays inside the main loop made hipcc keep the whole struct in
+// scratch memory and reload it per DMA (a 2.2x slower main loop). SEG = false: p.A / p.B, k0 unchanged.
+template <bool SEG>
+struct SegSel {
+  const bf16_t *a0, *a1, *a2, *b0, *b1, *b2;
+  int seg;
+  __device__ __forceinline__ explicit SegSel(const G2Params& p) {
+    if constexpr (SEG) {
+      a0 = uniform_ptr(p.segA[0]); a1 = uniform_ptr(p.segA[1]); a2 = uniform_ptr(p.segA[2]);
+      b0 = uniform_ptr(p.segB[0]); b1 = uniform_ptr(p.segB[1]); b2 = uniform_ptr(p.segB[2]);
+      seg = __builtin_amdgcn_readfirstlane(p.seg);
+    } else {
+      a0 = a1 = a2 = p.A;
+      b0 = b1 = b2 = p.B;
+      seg = 0;
+    }
+  }
+  __device__ __forceinline__ int map(int k0, const bf16_t*& A, const bf16_t*& B) const {
+    if constexpr (!SEG) {
+      A = a0;
+      B = b0;
+      return k0;
+    } else {
+      // masked adds, not `s == 0 ? a0 : ...`: hipcc turns a select of the six members into a dynamically indexed load
+      // of this object, then promotes the object to LDS (a ds_write of the six pointers in the prologue and a
+      // ds_read_b64 in front of every DMA of the main loop, queued behind the fragment reads: ~45 % slower GEMMs)
+      const bool s1 = k0 >= seg, s2 = k0 >= 2 * seg;
+      const uint64_t m1 = 0 - (uint64_t)(s1 && !s2), m2 = 0 - (uint64_t)s2;
+      A = reinterpret_cast<const bf16_t*>((uint64_t)a0 + ((((uint64_t)a1 - (uint64_t)a0)) & m1) +
+                                          ((((uint64_t)a2 - (uint64_t)a0)) & m2));
+      B = reinterpret_cast<const bf16_t*>((uint64_t)b0 + ((((uint64_t)b1 - (uint64_t)b0)) & m1) +
+                                          ((((uint64_t)b2 - (uint64_t)b0)) & m2));
+      return k0 - ((int)s1 + (int)s2) * seg;
+    }
+  }
+};
 
 // E2_STORE_RDOT: the 8 lanes holding the 8 chunks (64 columns = one head) of row m reduce their chunk dots; the first
 // writes the head's delta. Called by every lane of the group (DPP), `store` false for rows past M.

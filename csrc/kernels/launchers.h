@@ -107,11 +107,12 @@ void refresh_env_knobs();
 void launch_split3(const float* x, bf16_t* out, int64_t R, int64_t C, int pat, bool rows, hipStream_t st,
                    bf16_t* out2 = nullptr, int pat2 = 0);
 void launch_epi32(float* y, const float* bias, const float* aux, float* out, int64_t M, int N, int kind, double p,
-                  uint64_t seed, hipStream_t st);
-void launch_dropout32(const float* x, float* out, int64_t n, int W, double p, uint64_t seed, hipStream_t st);
+                  uint64_t seed, hipStream_t st, bf16_t* hi = nullptr, bf16_t* lo = nullptr);
+void launch_dropout32(const float* x, float* out, int64_t n, int W, double p, uint64_t seed, hipStream_t st,
+                      bf16_t* hi = nullptr, bf16_t* lo = nullptr);
 void launch_colsum32(const float* x, float* dbias, int M, int N, hipStream_t st);
 void launch_ln32_fwd(const float* x, const float* g, const float* b, float* out, float* mean, float* rstd, int R,
-                     int H, float eps, hipStream_t st);
+                     int H, float eps, hipStream_t st, bf16_t* hi = nullptr, bf16_t* lo = nullptr);
 void launch_ln32_bwd(const float* dy, const float* x, const float* mean, const float* rstd, const float* g, float* dx,
                      float* dg, float* db, int R, int H, hipStream_t st);
 void launch_embed32_gather(const int64_t* ids, const int64_t* pids, const int64_t* tids, const float* word,

@@ -56,15 +56,19 @@ def _split(x: torch.Tensor, pat: int, rows: bool = False, pad_rows: int = 0) -> 
 # row blocks for the weight gradient): one read of dy and one launch instead of two (profiles/fp32_dual_split_ab_r5.log)
 
 
-def _split_grad(dy: torch.Tensor, need_dgrad: bool, w: Optional[torch.Tensor] = None):
+def _grad_seg_ok(T: int, N: int, K: int, need_dgrad: bool) -> bool:
+    """A [T, N] gradient of a layer with weight [N, K] goes to the segmented GEMMs (weight gradient, and dgrad)."""
+    return N % 4 == 0 and _seg_ok(1, 1, N, K, T) and (not need_dgrad or _seg_ok(0, 1, T, K, N))
+
+
+def _split_grad(dy: torch.Tensor, need_dgrad: bool, w: Optional[torch.Tensor] = None, halves=None):
     """``dy``'s split for both of its GEMMs: ((hi, lo), (hi, lo)) when the segmented GEMMs take the layer's shapes
-    (``w`` given), else (column-block split for :func:`mm_dgrad` or None, row-block split for :func:`wgrad_` or
-    None)."""
+    (``w`` given; ``halves``: dy's (hi, lo) written by its producer), else (column-block split for :func:`mm_dgrad` or
+    None, row-block split for :func:`wgrad_` or None)."""
     if w is not None and dy.dim() == 2 and dy.shape[1] % 4 == 0:
         T, N = dy.shape
-        K = w.shape[1]
-        if _seg_ok(1, 1, N, K, T) and (not need_dgrad or _seg_ok(0, 1, T, K, N)):
-            hl = _split2(dy.contiguous())
+        if _grad_seg_ok(T, N, w.shape[1], need_dgrad):
+            hl = halves if halves is not None else _split2(dy.contiguous())
             return (hl if need_dgrad else None), hl
     if not (need_dgrad and dy.dim() == 2 and dy.shape[0] % 64 == 0 and dy.shape[1] % 4 == 0):
         return None, None
@@ -81,6 +85,41 @@ def _split2(x: torch.Tensor):
     lo = torch.empty_like(hi)
     _C.split2(x, hi, lo)
     return hi, lo
+
+
+def _halves_like(x: torch.Tensor):
+    return torch.empty(x.shape, dtype=torch.bfloat16, device=x.device), torch.empty(x.shape, dtype=torch.bfloat16,
+                                                                                    device=x.device)
+
+
+# A block's output (its LayerNorm's, or the embeddings') feeds the next block's first GEMM: the producing kernel writes
+# its bf16 halves as well (ln32_fwd / dropout32 hi / lo) and leaves them here; the next block takes them instead of a
+# split2 pass over its input. (tensor, version, hi, lo): the tensor reference keeps the storage from being reused, and
+# the halves are taken only for that storage, unmodified (same data pointer, numel and version counter).
+_next_halves = None
+
+
+def _publish_halves(t: torch.Tensor, hi: torch.Tensor, lo: torch.Tensor) -> None:
+    global _next_halves
+    _next_halves = (t, t._version, hi, lo)
+
+
+def _take_halves(x2: torch.Tensor):
+    global _next_halves
+    c = _next_halves
+    if c is None:
+        return None
+    t, ver, hi, lo = c
+    if (x2.data_ptr() == t.data_ptr() and x2.numel() == t.numel() and x2._version == ver and x2.is_contiguous()
+            and t.is_contiguous()):
+        _next_halves = None
+        return hi.view(x2.shape), lo.view(x2.shape)
+    return None
+
+
+def _halves_wanted(rows: int, H: int) -> bool:
+    """Whether a block output [rows, H] is worth splitting in its producer (the next block's segmented GEMMs read it)."""
+    return rows % 64 == 0 and H % 64 == 0 and H % 256 == 0
 
 
 def weight_split(w: torch.Tensor):
@@ -175,7 +214,8 @@ def _x_split(x2: torch.Tensor, w: torch.Tensor):
     """x's (hi, lo) when the segmented GEMMs take the layer (forward NT and the weight gradient reuse them), else None."""
     M, K = x2.shape
     if _seg_ok(0, 0, M, w.shape[0], K) and _seg_ok(1, 1, w.shape[0], K, M):
-        return _split2(x2)
+        hl = _take_halves(x2)
+        return hl if hl is not None else _split2(x2)
     return None
 
 
@@ -360,9 +400,14 @@ class _EmbedLN32(torch.autograd.Function):
         out = torch.empty_like(x)
         mean = torch.empty(B * S, dtype=torch.float32, device=word.device)
         rstd = torch.empty_like(mean)
-        _C.ln32_fwd(x, ln_w, ln_b, out, mean, rstd, float(eps))
+        hl = _halves_like(out) if _halves_wanted(B * S, H) else None
         if p > 0:
-            _C.dropout32(out, out, float(p), _s64(seed))
+            _C.ln32_fwd(x, ln_w, ln_b, out, mean, rstd, float(eps))
+            _C.dropout32(out, out, float(p), _s64(seed), *(hl or (None, None)))
+        else:
+            _C.ln32_fwd(x, ln_w, ln_b, out, mean, rstd, float(eps), *(hl or (None, None)))
+        if hl is not None:
+            _publish_halves(out, *hl)
         ctx.save_for_backward(ids_c, pos_c, tt_c if tt_c is not None else ids_c, x, mean, rstd, ln_w)
         ctx.tensors = (word, pos, typ, ln_b)
         ctx.has_tt = tt_c is not None
@@ -477,28 +522,34 @@ def attention(qkv, mask_bias, batch, seq, heads, p, seed):
 # (mm_dgrad(acc=)): the segmented GEMM accumulates in place, one pass. Every kernel is the unfused ops' kernel, in the
 # same order, and the residual add is the same single fp32 add: outputs and gradients match the unfused ops bit for bit
 # (tests/test_gpu_fp32.py::test_fused_fp32_blocks_match_unfused_ops).
-def _ln_tail_bwd(dout, z, mean, rstd, ln_w, ln_b, p, seed, gb):
-    """LN backward of the block tail: (dz = the residual gradient, dy = the GEMM-output gradient), with the LN and the
-    GEMM bias gradients accumulated."""
+def _ln_tail_bwd(dout, z, mean, rstd, ln_w, ln_b, p, seed, gb, w):
+    """LN backward of the block tail: (dz = the residual gradient, dy = the GEMM-output gradient, dy's (hi, lo) for the
+    segmented GEMMs of the block's last linear (weight ``w``) or None), with the LN and the GEMM bias gradients
+    accumulated. The dropout pass writes dy's halves (no split2 pass)."""
     gg, gbe = _Grad(ln_w), _Grad(ln_b)
     dz = torch.empty_like(z)
     _C.ln32_bwd(dout.reshape(z.shape).contiguous(), z, mean, rstd, ln_w, dz, gg.buf, gbe.buf)
-    dy = dz
+    dy, dys = dz, None
     if p > 0:
         dy = torch.empty_like(dz)
-        _C.dropout32(dz, dy, p, _s64(seed))
+        dys = _halves_like(dz) if _grad_seg_ok(dz.shape[0], dz.shape[1], w.shape[1], True) else None
+        _C.dropout32(dz, dy, p, _s64(seed), *(dys or (None, None)))
     _colsum_(gb, dy)
-    return dz, dy, gg, gbe
+    return dz, dy, dys, gg, gbe
 
 
 def _ln_tail_fwd(y, b, res2d, ln_w, ln_b, eps, p, seed):
+    """dropout(y + b) + res -> LayerNorm; the output's halves go to the next block (_publish_halves)."""
     rows, H = y.shape
     z = torch.empty_like(y)
     _C.epi32(y, b, res2d, z, 2, float(p), _s64(seed))
     out = torch.empty_like(z)
     mean = torch.empty(rows, dtype=torch.float32, device=y.device)
     rstd = torch.empty_like(mean)
-    _C.ln32_fwd(z, ln_w, ln_b, out, mean, rstd, float(eps))
+    hl = _halves_like(out) if _halves_wanted(rows, H) else None
+    _C.ln32_fwd(z, ln_w, ln_b, out, mean, rstd, float(eps), *(hl or (None, None)))
+    if hl is not None:
+        _publish_halves(out, *hl)
     return z, out, mean, rstd
 
 
@@ -511,8 +562,9 @@ class _AttnBlock32(torch.autograd.Function):
         h2d = h.reshape(-1, h.shape[-1]).contiguous()
         hs = _x_split(h2d, qkv_w)
         qkv = mm_nt(h2d, qkv_w, hs)
-        _C.epi32(qkv, qkv_b, None, qkv, 0, 0.0, 0)
-        qh, ql = _split2(qkv)
+        qh, ql = _halves_like(qkv)
+        _C.epi32(qkv, qkv_b, None, None, 0, 0.0, 0, qh, ql)  # qkv + bias -> its halves only (the fp32 sum is unused)
+        del qkv
         H = out_w.shape[1]
         att = torch.empty((h2d.shape[0], H), dtype=torch.float32, device=h.device)
         lse = torch.empty(B * heads * S, dtype=torch.float32, device=h.device)
@@ -539,8 +591,8 @@ class _AttnBlock32(torch.autograd.Function):
         as_ = (t.pop(0), t.pop(0)) if a_split else None
         out_w, out_b, z, mean, rstd, ln_w, ln_b = t
         g_ow, g_ob, g_qw, g_qb = _Grad(out_w), _Grad(out_b), _Grad(qkv_w), _Grad(qkv_b)
-        dz, dy, gg, gbe = _ln_tail_bwd(dout, z, mean, rstd, ln_w, ln_b, p_h, seed_h, g_ob)
-        sc, sr = _split_grad(dy, True, out_w)
+        dz, dy, dys, gg, gbe = _ln_tail_bwd(dout, z, mean, rstd, ln_w, ln_b, p_h, seed_h, g_ob, out_w)
+        sc, sr = _split_grad(dy, True, out_w, dys)
         datt = mm_dgrad(dy, out_w, sc)
         wgrad_(g_ow, dy, None if a_split else att, sr, as_)
         dh_, dl_ = _split2(datt)
@@ -564,10 +616,15 @@ class _FFNBlock32(torch.autograd.Function):
         h2d = h.reshape(-1, h.shape[-1]).contiguous()
         hs = _x_split(h2d, w1)
         pre = mm_nt(h2d, w1, hs)  # becomes the pre-activation (bias added in place)
-        g = torch.empty_like(pre)
-        _C.epi32(pre, b1, None, g, 1, 0.0, 0)
-        gs = _x_split(g, w2)
-        y = mm_nt(g, w2, gs)
+        T, I = pre.shape
+        if _seg_ok(0, 0, T, w2.shape[0], I) and _seg_ok(1, 1, w2.shape[0], I, T):
+            # GELU output as its halves only: the FFN2 forward and weight gradient read nothing else
+            g, gs = None, _halves_like(pre)
+            _C.epi32(pre, b1, None, None, 1, 0.0, 0, *gs)
+        else:
+            g, gs = torch.empty_like(pre), None
+            _C.epi32(pre, b1, None, g, 1, 0.0, 0)
+        y = mm_nt(g if g is not None else pre, w2, gs)  # (with gs, mm_nt reads only the shape of its first argument)
         z, out, mean, rstd = _ln_tail_fwd(y, b2, h2d, ln_w, ln_b, eps, p, seed)
         ctx.save_for_backward(*(hs if hs is not None else (h2d,)), w1, b1, pre, *(gs if gs is not None else (g,)), w2,
                               b2, z, mean, rstd, ln_w, ln_b)
@@ -586,14 +643,15 @@ class _FFNBlock32(torch.autograd.Function):
         g = None if g_split else t.pop(0)
         w2, b2, z, mean, rstd, ln_w, ln_b = t
         g_w1, g_b1, g_w2, g_b2 = _Grad(w1), _Grad(b1), _Grad(w2), _Grad(b2)
-        dz, dy, gg, gbe = _ln_tail_bwd(dout, z, mean, rstd, ln_w, ln_b, p, seed, g_b2)
-        sc, sr = _split_grad(dy, True, w2)
+        dz, dy, dys, gg, gbe = _ln_tail_bwd(dout, z, mean, rstd, ln_w, ln_b, p, seed, g_b2, w2)
+        sc, sr = _split_grad(dy, True, w2, dys)
         dg = mm_dgrad(dy, w2, sc)
         wgrad_(g_w2, dy, g, sr, gs)
         da = torch.empty_like(pre)
-        _C.epi32(dg, None, pre, da, 4, 0.0, 0)
+        das = _halves_like(da) if _grad_seg_ok(da.shape[0], da.shape[1], w1.shape[1], ctx.needs_input_grad[0]) else None
+        _C.epi32(dg, None, pre, da, 4, 0.0, 0, *(das or (None, None)))
         _colsum_(g_b1, da)
-        sc, sr = _split_grad(da, ctx.needs_input_grad[0], w1)
+        sc, sr = _split_grad(da, ctx.needs_input_grad[0], w1, das)
         dh = mm_dgrad(da, w1, sc, acc=dz) if ctx.needs_input_grad[0] else None
         wgrad_(g_w1, da, h2d, sr, hs)
         return (dh.view(dout.shape) if dh is not None else None, g_w1.done(), g_b1.done(), g_w2.done(), g_b2.done(),

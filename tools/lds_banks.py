@@ -89,3 +89,11 @@ for M in range(1 << 12):
     if best is None or t1 + t2 < best[0]:
         best = (t1 + t2, t1, t2, M)
 print("best dual swizzle", best, [make(best[3])(r) for r in range(16)])
+
+# ---- fp8 NT fragment (gemm2.hip frag8): 16 rows x 2 ds_read_b128 per lane, f1 = (row >> 1) & 7
+def frag8_cycles(chunk_of):
+    f1 = lambda r: (r >> 1) & 7
+    return [cycles([(l & 15) * ROWB + ((chunk_of(l, part) ^ f1(l & 15)) * 16) for l in range(64)], 16, G128)
+            for part in (0, 1)]
+print("frag8 chunks (2g, 2g+1):", frag8_cycles(lambda l, p: 2 * (l >> 4) + p), "(g, g+4):",
+      frag8_cycles(lambda l, p: (l >> 4) + 4 * p), "(ideal 4 each)")
