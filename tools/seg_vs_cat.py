@@ -43,7 +43,16 @@ for K, N in SHAPES:
     g = torch.zeros(N, K, device=dev)
     sp = C_.gemm2_splits(N, K, 3 * T)
     ws = torch.empty(max(1, sp) * N * K, device=dev)
+    # the halves as the two planes of one allocation (hi at +0, lo at +T·K) rather than two allocations
+    one = torch.empty(2, *x.shape, dtype=torch.bfloat16, device=dev)
+    one[0].copy_(xh)
+    one[1].copy_(xl)
+    onew = torch.empty(2, *w.shape, dtype=torch.bfloat16, device=dev)
+    onew[0].copy_(wh)
+    onew[1].copy_(wl)
     cases = {
+        "fwd_seg_1buf": lambda: C_.gemm2_seg([one[0], one[0], one[1]], [onew[0], onew[1], onew[0]], y, 0, 0),
+        "fwd_seg_order": lambda: C_.gemm2_seg([xh, xl, xh], [wh, wh, wl], y, 0, 0),
         "fwd_seg": lambda: C_.gemm2_seg([xh, xh, xl], [wh, wl, wh], y, 0, 0),
         "fwd_cat": lambda: C_.gemm2_f32nt(xc, wc, y, 0),
         "dgrad_seg": lambda: C_.gemm2_seg([dh, dh, dl], [wh, wl, wh], dx, 0, 1),
