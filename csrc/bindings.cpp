@@ -15,14 +15,21 @@ namespace {
 hipStream_t cur_stream() { return c10::hip::getCurrentHIPStream().stream(); }
 
 // ---- host-cheap stream ordering (ops/hip.py weight-gradient side stream, optimizer slices): one event from a
-// per-thread ring per fork, no Python stream objects / context managers on the per-layer backward path
+// per-thread ring per fork, no Python stream objects / context managers on the per-layer backward path.
+// The events order streams of ONE device, so they skip the system-scope fence (hipEventDisableSystemFence): a default
+// event's record made the next kernel on the recording stream wait for a system-scope release, a 6-12 us bubble per
+// fork on a busy stream (bert-large B = 8: ~8 forks per layer, tools/timeline.py). HSD_EVENT_SYSFENCE=1: the old events.
 static hipEvent_t ring_event() {
   constexpr int kRing = 64;
   thread_local hipEvent_t ring[kRing] = {};
   thread_local int next = 0;
   hipEvent_t& e = ring[next];
   next = (next + 1) % kRing;
-  if (e == nullptr) TORCH_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess, "hipEventCreate");
+  if (e == nullptr) {
+    const char* env = getenv("HSD_EVENT_SYSFENCE");
+    const unsigned flags = hipEventDisableTiming | ((env && atoi(env)) ? 0u : (unsigned)hipEventDisableSystemFence);
+    TORCH_CHECK(hipEventCreateWithFlags(&e, flags) == hipSuccess, "hipEventCreate");
+  }
   return e;
 }
 
