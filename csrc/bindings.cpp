@@ -50,8 +50,9 @@ void stream_wait(int64_t dst_ptr, int64_t src_ptr) {
 
 void adam_step(torch::Tensor p, torch::Tensor m, torch::Tensor v, torch::Tensor g, c10::optional<torch::Tensor> out,
                c10::optional<torch::Tensor> decay, double step, double eps, double b1, double b2, double gscale,
-               double lr_wd, c10::optional<torch::Tensor> coef, c10::optional<torch::Tensor> out_lo) {
+               double lr_wd, c10::optional<torch::Tensor> coef, c10::optional<torch::Tensor> out_lo, bool zero_grad) {
   CHECK_CUDA(p); CHECK_CONTIG(p); CHECK_DTYPE(p, torch::kFloat32);
+  TORCH_CHECK(!zero_grad || g.is_contiguous(), "adam zero_grad: contiguous gradient");
   CHECK_DTYPE(m, torch::kFloat32); CHECK_DTYPE(v, torch::kFloat32);
   TORCH_CHECK(p.numel() == m.numel() && p.numel() == v.numel() && p.numel() == g.numel(), "size mismatch");
   TORCH_CHECK(p.numel() % 64 == 0, "flat buffer (or slice) must be a multiple of 64 elements");
@@ -82,7 +83,7 @@ void adam_step(torch::Tensor p, torch::Tensor m, torch::Tensor v, torch::Tensor 
   }
   hsd::launch_adam(p.data_ptr<float>(), m.data_ptr<float>(), v.data_ptr<float>(), g.data_ptr(), gbf, o, dm,
                    p.numel(), (float)step, (float)eps, (float)b1, (float)b2, (float)gscale, (float)lr_wd,
-                   dcoef, cur_stream(), lo);
+                   dcoef, cur_stream(), lo, zero_grad);
 }
 
 #define OPT_BF(o) ((o).has_value() ? reinterpret_cast<hsd::bf16_t*>((o)->data_ptr()) : nullptr)
@@ -156,8 +157,9 @@ void ln_bwd(torch::Tensor dout, torch::Tensor z, torch::Tensor mean, torch::Tens
 void ln_bwd_q8(torch::Tensor dout, torch::Tensor z, torch::Tensor mean, torch::Tensor rstd, torch::Tensor gamma,
                c10::optional<torch::Tensor> dz, torch::Tensor dy, torch::Tensor dgamma, torch::Tensor dbeta,
                c10::optional<torch::Tensor> dbias, double p, int64_t seed, torch::Tensor q8, torch::Tensor amax_in,
-               torch::Tensor sinv, torch::Tensor amax_track, int64_t qfmt) {
+               torch::Tensor sinv, torch::Tensor amax_track, int64_t qfmt, bool q8_only) {
   check_bf16(dout, "dout"); check_bf16(z, "z"); check_bf16(gamma, "gamma"); check_bf16(dy, "dy");
+  TORCH_CHECK(!q8_only || (dz.has_value() && p > 0), "ln_bwd_q8 q8_only: dz must be its own buffer (dropout on)");
   check_f32(mean, "mean"); check_f32(rstd, "rstd"); check_f32(dgamma, "dgamma"); check_f32(dbeta, "dbeta");
   check_f32(amax_in, "amax_in"); check_f32(sinv, "sinv"); check_f32(amax_track, "amax_track");
   CHECK_CUDA(q8); CHECK_CONTIG(q8); CHECK_DTYPE(q8, torch::kUInt8);
@@ -171,7 +173,7 @@ void ln_bwd_q8(torch::Tensor dout, torch::Tensor z, torch::Tensor mean, torch::T
   hsd::launch_ln_bwd_q8(CBF(dout), CBF(z), mean.data_ptr<float>(), rstd.data_ptr<float>(), CBF(gamma), OPT_BF(dz),
                         BF(dy), nullptr, dgamma.data_ptr<float>(), dbeta.data_ptr<float>(), OPT_F(dbias), rows, H, p,
                         (uint64_t)seed, q8.data_ptr<uint8_t>(), amax_in.data_ptr<float>(), sinv.data_ptr<float>(),
-                        amax_track.data_ptr<float>(), (int)qfmt, cur_stream());
+                        amax_track.data_ptr<float>(), (int)qfmt, cur_stream(), q8_only);
 }
 
 void embed_fwd(torch::Tensor ids, torch::Tensor pos_ids, c10::optional<torch::Tensor> type_ids, torch::Tensor word,
@@ -326,7 +328,7 @@ void attn_bwd_q8(torch::Tensor qkv, c10::optional<torch::Tensor> mask, torch::Te
                  torch::Tensor lse2, torch::Tensor dqkv, torch::Tensor ws, int64_t B, int64_t S, int64_t heads, double p,
                  int64_t seed, c10::optional<torch::Tensor> dbias, torch::Tensor q8, torch::Tensor amax_in,
                  torch::Tensor sinv, torch::Tensor amax_track, int64_t qfmt, c10::optional<torch::Tensor> kmask,
-                 bool delta_ready) {
+                 bool delta_ready, bool q8_only) {
   check_bf16(qkv, "qkv"); check_bf16(o, "o"); check_bf16(dout, "dout"); check_bf16(dqkv, "dqkv");
   check_f32(lse2, "lse2"); check_f32(ws, "ws");
   TORCH_CHECK(S > 128 && hsd::attn_streaming((int)S), "attn_bwd_q8: streaming attention (S > 128) only");
@@ -341,7 +343,7 @@ void attn_bwd_q8(torch::Tensor qkv, c10::optional<torch::Tensor> mask, torch::Te
                            ws.data_ptr<float>(), OPT_F(dbias), (int)B, (int)S, (int)heads, p, (uint64_t)seed,
                            q8.data_ptr<uint8_t>(), amax_in.data_ptr<float>(), sinv.data_ptr<float>(),
                            amax_track.data_ptr<float>(), (int)qfmt, cur_stream(), keep_mask_ptr(kmask, B, S, heads),
-                           delta_ready);
+                           delta_ready, q8_only);
 }
 
 // C[M,N] (+)= A·B with fused epilogue. la=0: A [M,K]; la=1: A [K,M]. lb=0: B [N,K]; lb=1: B [K,N].
@@ -421,7 +423,8 @@ void gemm8(torch::Tensor A, int64_t fa, torch::Tensor sa, torch::Tensor B, int64
            torch::Tensor C, int64_t epi, c10::optional<torch::Tensor> bias, c10::optional<torch::Tensor> aux,
            c10::optional<torch::Tensor> C2, double p, int64_t seed, c10::optional<torch::Tensor> dbias,
            c10::optional<torch::Tensor> q8, c10::optional<torch::Tensor> q8_amax, c10::optional<torch::Tensor> q8_sinv,
-           c10::optional<torch::Tensor> q8_track, int64_t q8fmt, c10::optional<torch::Tensor> rd, int64_t rd_seq) {
+           c10::optional<torch::Tensor> q8_track, int64_t q8fmt, c10::optional<torch::Tensor> rd, int64_t rd_seq,
+           bool q8_only) {
   uint8_t* q8p = nullptr;
   float *q8s = nullptr, *q8t = nullptr;
   const float* q8a = nullptr;
@@ -475,7 +478,7 @@ void gemm8(torch::Tensor A, int64_t fa, torch::Tensor sa, torch::Tensor B, int64
                     B.stride(0), (int)fb, sb.data_ptr<float>(), (int)M, (int)N, (int)K, BF(C), C.stride(0),
                     bias.has_value() ? CBF(*bias) : nullptr, aux.has_value() ? CBF(*aux) : nullptr,
                     aux.has_value() ? aux->stride(0) : 0, C2.has_value() ? BF(*C2) : nullptr, p, (uint64_t)seed, dbp,
-                    cur_stream(), q8p, q8a, q8s, q8t, (int)q8fmt, rdp, (int)rd_seq);
+                    cur_stream(), q8p, q8a, q8s, q8t, (int)q8fmt, rdp, (int)rd_seq, q8_only ? 1 : 0);
 }
 
 // C[M][N] fp32 += sdy·sx · dY8ᵀ · X8 (fp8 TT weight gradient): dY8 uint8 [T][M] (format fdy), X8 uint8 [T][N] (e4m3),
@@ -965,18 +968,23 @@ bool gemm2_supported(int64_t la, int64_t lb, int64_t epi, int64_t M, int64_t N, 
 PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
   m.doc() = "gfx950 HIP kernels for huggingface_sagemaker_tensorflow_distributed_amd";
   hsd::register_comm(m);
-  m.def("adam_step", &adam_step);
+  m.def("adam_step", &adam_step, py::arg("p"), py::arg("m"), py::arg("v"), py::arg("g"), py::arg("out"),
+        py::arg("decay"), py::arg("step"), py::arg("eps"), py::arg("b1"), py::arg("b2"), py::arg("gscale"),
+        py::arg("lr_wd"), py::arg("coef") = py::none(), py::arg("out_lo") = py::none(), py::arg("zero_grad") = false);
   m.def("ln_fwd_q8", &ln_fwd_q8);
   m.def("stream_wait", &stream_wait);
   m.def("gemm2_on", &gemm2_on);
-  m.def("ln_bwd_q8", &ln_bwd_q8);
+  m.def("ln_bwd_q8", &ln_bwd_q8, py::arg("dout"), py::arg("z"), py::arg("mean"), py::arg("rstd"), py::arg("gamma"),
+        py::arg("dz"), py::arg("dy"), py::arg("dgamma"), py::arg("dbeta"), py::arg("dbias"), py::arg("p"),
+        py::arg("seed"), py::arg("q8"), py::arg("amax_in"), py::arg("sinv"), py::arg("amax_track"), py::arg("qfmt"),
+        py::arg("q8_only") = false);
   m.def("attn_fwd_q8", &attn_fwd_q8, py::arg("qkv"), py::arg("mask"), py::arg("out"), py::arg("lse2"), py::arg("B"),
         py::arg("S"), py::arg("heads"), py::arg("p"), py::arg("seed"), py::arg("q8"), py::arg("amax_in"),
         py::arg("sinv"), py::arg("amax_track"), py::arg("kmask") = py::none());
   m.def("attn_bwd_q8", &attn_bwd_q8, py::arg("qkv"), py::arg("mask"), py::arg("o"), py::arg("dout"), py::arg("lse2"),
         py::arg("dqkv"), py::arg("ws"), py::arg("B"), py::arg("S"), py::arg("heads"), py::arg("p"), py::arg("seed"),
         py::arg("dbias"), py::arg("q8"), py::arg("amax_in"), py::arg("sinv"), py::arg("amax_track"), py::arg("qfmt"),
-        py::arg("kmask") = py::none(), py::arg("delta_ready") = false);
+        py::arg("kmask") = py::none(), py::arg("delta_ready") = false, py::arg("q8_only") = false);
   m.def("attn_q8_supported", [](int64_t S) { return S > 128 && hsd::attn_streaming((int)S); });
   m.def("ln_fwd", &ln_fwd);
   m.def("ln_bwd", &ln_bwd);
@@ -1030,7 +1038,7 @@ PYBIND11_MODULE(TORCH_EXTENSION_NAME, m) {
         py::arg("C2") = py::none(), py::arg("p") = 0.0, py::arg("seed") = 0, py::arg("dbias") = py::none(),
         py::arg("q8") = py::none(), py::arg("q8_amax") = py::none(),
         py::arg("q8_sinv") = py::none(), py::arg("q8_track") = py::none(), py::arg("q8fmt") = 0,
-        py::arg("rd") = py::none(), py::arg("rd_seq") = 0);
+        py::arg("rd") = py::none(), py::arg("rd_seq") = 0, py::arg("q8_only") = false);
   m.def("gemm8_supported", &hsd::gemm8_supported);
   m.def("attn_fwd", &attn_fwd, py::arg("qkv"), py::arg("mask"), py::arg("out"), py::arg("lse2"), py::arg("B"),
         py::arg("S"), py::arg("heads"), py::arg("p"), py::arg("seed"), py::arg("kmask") = py::none());

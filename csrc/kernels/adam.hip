@@ -26,16 +26,19 @@ __device__ __forceinline__ f32x4 load_grad(const void* __restrict__ g_, int64_t 
 // kLo (fp32 compute, ops/hip32.py): `out` / `out_lo` receive the bf16 hi / lo halves of the updated weight (hi =
 // bf16(θ), lo = bf16(θ - hi), exactly split2's), which the split-product GEMMs read directly -- the weights are split
 // once per optimizer step instead of at every use in forward and backward.
+// zero_g: the kernel also clears the gradient it consumed (16-B stores of the slot it just read), so the next step
+// needs no separate memset pass over the whole gradient buffer ahead of its forward (optim/adam.py: set by the
+// Trainer's eager steps; the store then skips its zero_grad once).
 // U chunks of 4 elements per thread per trip, all U x 4 loads issued before the first use (a one-chunk trip
 // leaves ~4 loads in flight per thread, too few to cover HBM latency at the occupancy a CU holds). Every
 // byte is touched once per step, so loads and stores are non-temporal (no L2 / MALL pollution).
 template <bool kGradBf16, bool kWriteBf16, int U, bool kLo = false>
 __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float* __restrict__ m,
-                                                   float* __restrict__ v, const void* __restrict__ g_,
+                                                   float* __restrict__ v, void* __restrict__ g_,
                                                    bf16_t* __restrict__ out, const uint8_t* __restrict__ decay,
                                                    int64_t n4, float step, float eps, float b1, float b2,
                                                    float gscale, float lr_wd, const float* __restrict__ coef,
-                                                   bf16_t* __restrict__ out_lo) {
+                                                   bf16_t* __restrict__ out_lo, int zero_g) {
   if (coef != nullptr) {  // HIP-graph replays: this step's scalars live on the device (train/graph.py)
     step = coef[0];
     eps = coef[1];
@@ -71,6 +74,10 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
       __builtin_nontemporal_store(pp[u], reinterpret_cast<f32x4*>(p) + i);
       __builtin_nontemporal_store(mm[u], reinterpret_cast<f32x4*>(m) + i);
       __builtin_nontemporal_store(vv[u], reinterpret_cast<f32x4*>(v) + i);
+      if (zero_g) {
+        if constexpr (kGradBf16) __builtin_nontemporal_store(u32x2{0u, 0u}, reinterpret_cast<u32x2*>(g_) + i);
+        else __builtin_nontemporal_store(f32x4{0.f, 0.f, 0.f, 0.f}, reinterpret_cast<f32x4*>(g_) + i);
+      }
       if constexpr (kWriteBf16) {
         u32x2 o;
         o.x = pack_bf2(pp[u][0], pp[u][1]);
@@ -87,9 +94,10 @@ __global__ __launch_bounds__(256) void adam_kernel(float* __restrict__ p, float*
   }
 }
 
-void launch_adam(float* p, float* m, float* v, const void* g, bool grad_bf16, bf16_t* out_bf16,
+void launch_adam(float* p, float* m, float* v, void* g, bool grad_bf16, bf16_t* out_bf16,
                  const uint8_t* decay, int64_t n, float step, float eps, float b1, float b2, float gscale,
-                 float lr_wd, const float* coef, hipStream_t stream, bf16_t* out_lo) {
+                 float lr_wd, const float* coef, hipStream_t stream, bf16_t* out_lo, bool zero_grad) {
+  const int zg = zero_grad ? 1 : 0;
   int64_t n4 = n / 4;  // n is a multiple of 1024 (FlatParamStore)
   int threads = 256;
   int64_t blocks = (n4 + threads - 1) / threads;
@@ -97,15 +105,15 @@ void launch_adam(float* p, float* m, float* v, const void* g, bool grad_bf16, bf
   // two 16-B chunks per thread per trip (1 and 4 measured slower: profiles/bench_adam_r2.json)
 #define HSD_ADAM(GB, WB)                                                                                            \
   hipLaunchKernelGGL((adam_kernel<GB, WB, 2>), dim3((unsigned)blocks), dim3(threads), 0, stream, p, m, v, g,      \
-                     out_bf16, decay, n4, step, eps, b1, b2, gscale, lr_wd, coef, nullptr)
+                     out_bf16, decay, n4, step, eps, b1, b2, gscale, lr_wd, coef, nullptr, zg)
   if (out_lo != nullptr) {
     if (out_bf16 == nullptr) abort();
     if (grad_bf16)
       hipLaunchKernelGGL((adam_kernel<true, true, 2, true>), dim3((unsigned)blocks), dim3(threads), 0, stream, p, m, v,
-                         g, out_bf16, decay, n4, step, eps, b1, b2, gscale, lr_wd, coef, out_lo);
+                         g, out_bf16, decay, n4, step, eps, b1, b2, gscale, lr_wd, coef, out_lo, zg);
     else
       hipLaunchKernelGGL((adam_kernel<false, true, 2, true>), dim3((unsigned)blocks), dim3(threads), 0, stream, p, m,
-                         v, g, out_bf16, decay, n4, step, eps, b1, b2, gscale, lr_wd, coef, out_lo);
+                         v, g, out_bf16, decay, n4, step, eps, b1, b2, gscale, lr_wd, coef, out_lo, zg);
     HSD_CHECK_LAUNCH();
     return;
   }

@@ -405,9 +405,9 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_kv_kernel(const bf16_t* __re
   float qs = 0.f, qm = 0.f;
   if (q8b != nullptr) qs = fmt_scale(qfmt, *q8o.amax_in);
   store_rows(stg_w, dv0, dv1, 1.0f, rowbase + 2 * H, ld, lane, dbias ? bsum + (4 + wave) * D : nullptr,
-             q8b ? q8b + 2 * H : nullptr, qfmt, qs, &qm);
+             q8b ? q8b + 2 * H : nullptr, qfmt, qs, &qm, q8o.only != 0);
   store_rows(stg_w, dk0, dk1, scale, rowbase + H, ld, lane, dbias ? bsum + wave * D : nullptr,
-             q8b ? q8b + H : nullptr, qfmt, qs, &qm);
+             q8b ? q8b + H : nullptr, qfmt, qs, &qm, q8o.only != 0);
   if (q8b != nullptr) wave_amax_track(qm, q8o.amax_track);
   if (dbias) {
     __syncthreads();
@@ -554,7 +554,7 @@ __global__ __launch_bounds__(256, 2) void attnS_bwd_q_kernel(const bf16_t* __res
     if (blockIdx.x == 0 && blockIdx.y == 0 && tid == 0) *q8o.sinv = 1.0f / qs;
   }
   store_rows(Kb + wave * 32 * D, dq0, dq1, scale, dqkv + qoff, ld, lane, dbias ? bsum + wave * D : nullptr,
-             q8o.q != nullptr ? q8o.q + qoff : nullptr, qfmt, qs, &qm);
+             q8o.q != nullptr ? q8o.q + qoff : nullptr, qfmt, qs, &qm, q8o.only != 0);
   if (q8o.q != nullptr) wave_amax_track(qm, q8o.amax_track);
   if (dbias) {
     __syncthreads();
@@ -629,9 +629,9 @@ void launch_attnS_fwd_q8(const bf16_t* qkv, const float* mask, bf16_t* out, floa
 void launch_attnS_bwd_q8(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
                          bf16_t* dqkv, float* delta_ws, float* dbias, int B, int S, int heads, double p, uint64_t seed,
                          uint8_t* q8, const float* amax_in, float* sinv, float* amax_track, int qfmt, hipStream_t st,
-                         const uint32_t* kmask, bool delta_ready) {
+                         const uint32_t* kmask, bool delta_ready, bool q8_only) {
   launch_attnS_bwd(qkv, mask, o, dout, lse2, dqkv, delta_ws, dbias, B, S, heads, p, seed, st,
-                   Q8Out{q8, amax_in, sinv, amax_track}, qfmt, kmask, delta_ready);
+                   Q8Out{q8, amax_in, sinv, amax_track, q8_only ? 1 : 0}, qfmt, kmask, delta_ready);
 }
 
 }  // namespace hsd

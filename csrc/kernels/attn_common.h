@@ -76,7 +76,7 @@ __device__ __forceinline__ void dma_img(bf16_t* img, const bf16_t* __restrict__ 
 __device__ __forceinline__ void store_rows(bf16_t* stg, const f32x16& a0, const f32x16& a1, float scale,
                                            bf16_t* __restrict__ dst, int64_t ld, int lane,
                                            float* colsum_lds = nullptr, uint8_t* __restrict__ q8dst = nullptr,
-                                           int qfmt = 0, float qs = 0.f, float* qm = nullptr) {
+                                           int qfmt = 0, float qs = 0.f, float* qm = nullptr, bool q8only = false) {
   const int r = lane & 31, h = lane >> 5;
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
@@ -94,7 +94,8 @@ __device__ __forceinline__ void store_rows(bf16_t* stg, const f32x16& a0, const 
   for (int it = 0; it < 4; ++it) {
     const int row = (lane >> 3) + 8 * it, c = lane & 7;
     const u32x4 v = *reinterpret_cast<const u32x4*>(stg + stoff(row, c * 8));
-    *reinterpret_cast<u32x4*>(dst + (int64_t)row * ld + c * 8) = v;
+    // q8only: the fp8 copy is the only form the consumers read (the bf16 row is not stored)
+    if (!(q8only && q8dst != nullptr)) *reinterpret_cast<u32x4*>(dst + (int64_t)row * ld + c * 8) = v;
     if (q8dst != nullptr) {
       *qm = absmax8(v, *qm);
       *reinterpret_cast<u32x2*>(q8dst + (int64_t)row * ld + c * 8) = qfmt == 0 ? quant8<0>(v, qs) : quant8<1>(v, qs);

@@ -13,6 +13,7 @@ struct Q8Out {
   const float* amax_in;
   float* sinv;
   float* amax_track;
+  int only;  // 1: the producer skips the bf16 values this fp8 copy duplicates (the LN backward's dy)
 };
 
 constexpr float kE4M3Max = 448.0f, kE5M2Max = 57344.0f;

@@ -30,7 +30,7 @@ void launch_gemm8(int epi, const uint8_t* A, int64_t lda, int fa, const float* s
                   int fb, const float* sb, int M, int N, int K, bf16_t* C, int64_t ldc, const bf16_t* bias,
                   const bf16_t* aux, int64_t ldaux, bf16_t* C2, double p_drop, uint64_t seed, float* dbias,
                   hipStream_t st, uint8_t* q8, const float* q8_amax, float* q8_sinv, float* q8_track, int q8_fmt,
-                  float* rd, int rd_seq) {
+                  float* rd, int rd_seq, int q8_only) {
   if (!gemm8_supported(epi, M, N, K)) abort();
   // the kernel's LDS-DMA reads 2-B aligned rows (every fp8 operand of the step: [rows][K] with K % 128 == 0)
   if (lda % 2 || ldb % 2) abort();
@@ -39,6 +39,7 @@ void launch_gemm8(int epi, const uint8_t* A, int64_t lda, int fa, const float* s
   p.rd_seq = rd_seq;
   if (epi == E2_STORE_RDOT && (rd == nullptr || rd_seq <= 0 || M % rd_seq)) abort();
   p.q8 = q8; p.q8_amax = q8_amax; p.q8_sinv = q8_sinv; p.q8_track = q8_track; p.q8_fmt = q8_fmt;
+  p.q8_only = q8 != nullptr && q8_only;
   p.A = reinterpret_cast<const bf16_t*>(A); p.lda = lda;
   p.B = reinterpret_cast<const bf16_t*>(B); p.ldb = ldb;
   p.M = M; p.N = N; p.K = K; p.C = C; p.ldc = ldc;

@@ -51,6 +51,9 @@ struct G2Params {
   float* q8_sinv;
   float* q8_track;
   int q8_fmt;
+  // Q8 epilogues: 1 = the fp8 copy is the output's only consumer-visible form; the bf16 output it duplicates (C2 of the
+  // two-output GELU epilogue, else C) is not stored (its consumers all take the fp8 copy: ops/hip.py, the FFN block)
+  int q8_only;
   // persistent kernels: dynamic tile queue (tq_* below; one ring slot per launch), nullptr = static tile walk
   int* tq;
   // E2_F32_SLAB with one K-split: C[m][n] += acc in place (ldc; each element has one owner) instead of a slab
@@ -385,6 +388,7 @@ __device__ __forceinline__ void epilogue_bf16(f32x4 (&acc)[MB][BN / 64], const G
   float csum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
   float qs = 0.f, qm = 0.f;
   if constexpr (Q8) qs = fmt_scale(p.q8_fmt, *p.q8_amax);
+  const bool q8_only = Q8 && __builtin_amdgcn_readfirstlane(p.q8_only) != 0;
   // aux (residual / GELU' operand) chunks of the NEXT pass are loaded right after this pass's staging writes, i.e.
   // BEFORE this pass's stores: the vector-memory counter retires loads and stores in issue order, so a load issued
   // after the previous pass's stores made its consumer wait for all of them (s_waitcnt vmcnt(0) per pass)
@@ -457,13 +461,16 @@ __device__ __forceinline__ void epilogue_bf16(f32x4 (&acc)[MB][BN / 64], const G
       const int64_t co = (int64_t)m * p.ldc + n;
       u32x4 o = sv[it], o2;
       epi_chunk<EPI>(o, o2, xv[it], m, n, p, csum, xw);
+      // Q8 with q8_only: the bf16 twin of the fp8 copy is not written (o2 of a two-output epilogue, else o)
+      const bool st_o = !(Q8 && !epi_two_out(EPI) && q8_only);
+      const bool st_o2 = !(Q8 && q8_only);
       if (p.nt_store) {
         const uint32_t bo = (uint32_t)(((int64_t)(m - mw) * p.ldc + n) * 2);
-        st16nt(rc, bo, o);
-        if constexpr (epi_two_out(EPI)) st16nt(rc2, bo, o2);
+        if (st_o) st16nt(rc, bo, o);
+        if constexpr (epi_two_out(EPI)) if (st_o2) st16nt(rc2, bo, o2);
       } else {
-        st16(C + co, o, 0);
-        if constexpr (epi_two_out(EPI)) st16(p.C2 + co, o2, 0);
+        if (st_o) st16(C + co, o, 0);
+        if constexpr (epi_two_out(EPI)) if (st_o2) st16(p.C2 + co, o2, 0);
       }
       if constexpr (Q8) {
         const u32x4 src = epi_two_out(EPI) ? o2 : o;

@@ -9,10 +9,10 @@ typedef uint16_t bf16_t;
 struct DropoutParams;
 
 // adam.hip
-void launch_adam(float* p, float* m, float* v, const void* g, bool grad_bf16, bf16_t* out_bf16,
+void launch_adam(float* p, float* m, float* v, void* g, bool grad_bf16, bf16_t* out_bf16,
                  const uint8_t* decay, int64_t n, float step, float eps, float b1, float b2, float gscale,
                  float lr_wd, const float* coef, hipStream_t stream,
-                 bf16_t* out_lo = nullptr);
+                 bf16_t* out_lo = nullptr, bool zero_grad = false);
 
 }  // namespace hsd
 
@@ -27,7 +27,7 @@ void launch_ln_fwd_q8(const bf16_t* y, const bf16_t* gamma, const bf16_t* beta, 
 void launch_ln_bwd_q8(const bf16_t* dout, const bf16_t* z, const float* mean, const float* rstd, const bf16_t* gamma,
                       bf16_t* dz, bf16_t* dy, const bf16_t* dres_add, float* dgamma, float* dbeta, float* dbias,
                       int rows, int H, double p, uint64_t seed, uint8_t* q8, const float* amax_in, float* sinv,
-                      float* amax_track, int qfmt, hipStream_t st);
+                      float* amax_track, int qfmt, hipStream_t st, bool q8_only = false);
 void launch_ln_bwd(const bf16_t* dout, const bf16_t* z, const float* mean, const float* rstd, const bf16_t* gamma,
                    bf16_t* dz, bf16_t* dy, const bf16_t* dres_add, float* dgamma, float* dbeta, float* dbias,
                    int rows, int H, double p, uint64_t seed, hipStream_t st);
@@ -84,7 +84,7 @@ void launch_attnS_fwd_q8(const bf16_t* qkv, const float* mask, bf16_t* out, floa
 void launch_attnS_bwd_q8(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
                          bf16_t* dqkv, float* delta_ws, float* dbias, int B, int S, int heads, double p, uint64_t seed,
                          uint8_t* q8, const float* amax_in, float* sinv, float* amax_track, int qfmt, hipStream_t st,
-                         const uint32_t* kmask = nullptr, bool delta_ready = false);
+                         const uint32_t* kmask = nullptr, bool delta_ready = false, bool q8_only = false);
 // dbias (optional): fp32 [3H] += column sums of dqkv (the fused QKV bias gradient)
 void launch_attn_bwd(const bf16_t* qkv, const float* mask, const bf16_t* o, const bf16_t* dout, const float* lse2,
                      bf16_t* dqkv, float* dq_acc, float* dbias, int B, int S, int heads, double p, uint64_t seed,
@@ -147,7 +147,8 @@ void launch_gemm8(int epi, const uint8_t* A, int64_t lda, int fa, const float* s
                   int fb, const float* sb, int M, int N, int K, bf16_t* C, int64_t ldc, const bf16_t* bias,
                   const bf16_t* aux, int64_t ldaux, bf16_t* C2, double p_drop, uint64_t seed, float* dbias,
                   hipStream_t st, uint8_t* q8 = nullptr, const float* q8_amax = nullptr, float* q8_sinv = nullptr,
-                  float* q8_track = nullptr, int q8_fmt = 0, float* rd = nullptr, int rd_seq = 0);
+                  float* q8_track = nullptr, int q8_fmt = 0, float* rd = nullptr, int rd_seq = 0,
+                  int q8_only = 0);
 void launch_fp8_quant(const bf16_t* x, int64_t n, float* amax, uint8_t* q, float* sinv, int fmt, bool compute_amax,
                       float* amax_track, hipStream_t st);
 void launch_fp8_quant_many(const int64_t* amax_desc, int n_amax, int amax_blocks, const int64_t* quant_desc,

@@ -164,7 +164,8 @@ __device__ __forceinline__ void ln_bwd_row(const u32x2 (&zw)[NCH], const u32x2 (
                                            bf16_t* __restrict__ dz_out, bf16_t* __restrict__ dy_out,
                                            const bf16_t* __restrict__ dres_add, const DropoutParams& dp,
                                            float (&acc_g)[NCH][4], float (&acc_b)[NCH][4], float (&acc_db)[NCH][4],
-                                           uint8_t* __restrict__ q8 = nullptr, float qs = 0.f, float* qm = nullptr) {
+                                           uint8_t* __restrict__ q8 = nullptr, float qs = 0.f, float* qm = nullptr,
+                                           bool q8only = false) {
   const int nq = H >> 2;
   float xh[NCH][4], g[NCH][4];
   float s1 = 0.f, s2 = 0.f;
@@ -215,7 +216,7 @@ __device__ __forceinline__ void ln_bwd_row(const u32x2 (&zw)[NCH], const u32x2 (
       u32x2 yo;
       yo.x = pack_bf2(dy[0], dy[1]);
       yo.y = pack_bf2(dy[2], dy[3]);
-      *reinterpret_cast<u32x2*>(dy_out + off) = yo;
+      if (!(QF >= 0 && q8only)) *reinterpret_cast<u32x2*>(dy_out + off) = yo;
       // bias grad sums the bf16-rounded dy that the dgrad GEMM consumes
       acc_db[i][0] += lo_bf(yo.x); acc_db[i][1] += hi_bf(yo.x);
       acc_db[i][2] += lo_bf(yo.y); acc_db[i][3] += hi_bf(yo.y);
@@ -245,8 +246,10 @@ __global__ __launch_bounds__(256) void ln_bwd_fused_kernel(const bf16_t* __restr
                                                            DropoutParams dp, Q8Out q8o) {
   dp = resolve_seed(dp);
   float qs = 0.f, qm = 0.f;
+  bool q8only = false;  // dy's bf16 values skipped: its consumers all take the fp8 copy (ops/hip.py _ln_bwd)
   if constexpr (QF >= 0) {
     qs = fmt_scale(QF, *q8o.amax_in);
+    q8only = q8o.only != 0;
     if (blockIdx.x == 0 && threadIdx.x == 0) *q8o.sinv = 1.0f / qs;
   }
   __shared__ float red[kLnWaves][3][NCH * 256];
@@ -277,7 +280,8 @@ __global__ __launch_bounds__(256) void ln_bwd_fused_kernel(const bf16_t* __restr
         mu2 = mean_in[r + 1];
         rs2 = rstd_in[r + 1];
       }
-      ln_bwd_row<NCH, QF>(za, da, mu, rs, gam, r, H, lane, dz_out, dy_out, dres_add, dp, ag, ab, ad, q8o.q, qs, &qm);
+      ln_bwd_row<NCH, QF>(za, da, mu, rs, gam, r, H, lane, dz_out, dy_out, dres_add, dp, ag, ab, ad, q8o.q, qs, &qm,
+                          q8only);
       if (!more) break;
       const bool more2 = r + 2 < r1;
       if (more2) {
@@ -286,7 +290,7 @@ __global__ __launch_bounds__(256) void ln_bwd_fused_kernel(const bf16_t* __restr
         rs = rstd_in[r + 2];
       }
       ln_bwd_row<NCH, QF>(zb, db, mu2, rs2, gam, r + 1, H, lane, dz_out, dy_out, dres_add, dp, ag, ab, ad, q8o.q, qs,
-                          &qm);
+                          &qm, q8only);
     }
   }
   if constexpr (QF >= 0) wave_amax_track(qm, q8o.amax_track);
@@ -394,9 +398,11 @@ void launch_ln_fwd_q8(const bf16_t* y, const bf16_t* gamma, const bf16_t* beta, 
 void launch_ln_bwd_q8(const bf16_t* dout, const bf16_t* z, const float* mean, const float* rstd, const bf16_t* gamma,
                       bf16_t* dz, bf16_t* dy, const bf16_t* dres_add, float* dgamma, float* dbeta, float* dbias,
                       int rows, int H, double p, uint64_t seed, uint8_t* q8, const float* amax_in, float* sinv,
-                      float* amax_track, int qfmt, hipStream_t st) {
+                      float* amax_track, int qfmt, hipStream_t st, bool q8_only) {
   DropoutParams dp = make_dropout(p, seed);
-  const Q8Out q{q8, amax_in, sinv, amax_track};
+  // dy's bf16 values may be skipped only when dz is its own buffer (no dropout: dz IS dy, the residual gradient)
+  if (q8_only && dz == nullptr) abort();
+  const Q8Out q{q8, amax_in, sinv, amax_track, q8_only ? 1 : 0};
   int nch = (H / 4 + 63) / 64;
   if (nch <= 1) ln_bwd_t<1>(dout, z, mean, rstd, gamma, dz, dy, dres_add, dgamma, dbeta, dbias, rows, H, dp, st, q, qfmt);
   else if (nch <= 2) ln_bwd_t<2>(dout, z, mean, rstd, gamma, dz, dy, dres_add, dgamma, dbeta, dbias, rows, H, dp, st, q, qfmt);

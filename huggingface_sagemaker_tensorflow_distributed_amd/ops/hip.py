@@ -244,11 +244,12 @@ def _empty(shape, like, dtype=None):
 
 
 # ------------------------------------------------------------------------------------------ optimizer
-def adam_step(p, m, v, g, out, decay, step, eps, b1, b2, gscale, lr_wd, coef=None, out_lo=None):
+def adam_step(p, m, v, g, out, decay, step, eps, b1, b2, gscale, lr_wd, coef=None, out_lo=None, zero_grad=False):
     """``coef``: optional fp32 [4] device tensor (step, eps, grad_scale, lr*wd) read by the kernel instead of the
     host scalars (captured HIP-graph steps, train/graph.py). ``out_lo``: with ``out``, the kernel writes the updated
-    weights' bf16 hi / lo halves (fp32 compute: the split-product GEMMs' operands, ops/hip32.py)."""
-    _C.adam_step(p, m, v, g, out, decay, step, eps, b1, b2, gscale, lr_wd, coef, out_lo)
+    weights' bf16 hi / lo halves (fp32 compute: the split-product GEMMs' operands, ops/hip32.py). ``zero_grad``: the
+    kernel also clears ``g`` after reading it."""
+    _C.adam_step(p, m, v, g, out, decay, step, eps, b1, b2, gscale, lr_wd, coef, out_lo, zero_grad)
 
 
 # ------------------------------------------------------------------------------------------ linear
@@ -674,6 +675,24 @@ def _site_ready(w, state_attr: str, wattr: str):
     return st if st is not None and getattr(st, "_hsd_cal", False) else None
 
 
+def _dequant8(q8, fmt: int, like: torch.Tensor) -> torch.Tensor:
+    """bf16 values of an fp8 copy (q, sinv): the fallback for a consumer that needs the bf16 twin a ``q8_only``
+    epilogue did not store (a path change between forward and backward, a retained-graph second backward)."""
+    q, sinv = q8
+    f8 = torch.float8_e5m2 if fmt == FP8_E5M2 else torch.float8_e4m3fn
+    return (q.view(f8).to(torch.float32) * sinv).to(like.dtype).view(like.shape)
+
+
+def _fp8_fwd_ok(w, epi, M: int, K: int) -> bool:
+    """The forward GEMM of ``w`` on an [M, K] input runs on the fp8 kernel (gemm_fwd's first branch)."""
+    return _fp8_w(w, "_hsd_q") is not None and _C.gemm8_supported(epi, M, w.shape[0], K)
+
+
+def _fp8_dgrad_ok(w, epi, M: int) -> bool:
+    """The dgrad of ``w`` for an [M, N_out] incoming gradient runs on the fp8 kernel (gemm_dgrad's first branch)."""
+    return _fp8_w(w, "_hsd_qt") is not None and _C.gemm8_supported(epi, M, w.shape[1], w.shape[0])
+
+
 def _take_q8(x):
     """The fp8 copy a producer wrote for activation ``x`` (:class:`_Q8Handoff`), or None."""
     return _Q8_HANDOFF.take(x)
@@ -695,21 +714,26 @@ def _q8_kw(q8):
     return {"q8": q, "q8_amax": st[0:1], "q8_sinv": sinv, "q8_track": st[1:2], "q8fmt": fmt}
 
 
-def gemm_fwd(x, w, epi, bias=None, aux=None, out2=None, p=0.0, seed=0, xq=None, q8_for=None):
+def gemm_fwd(x, w, epi, bias=None, aux=None, out2=None, p=0.0, seed=0, xq=None, q8_for=None, q8_only=False):
     """y[T, N] = x[T, K] · w[N, K]ᵀ with epilogue (gemm2 8-phase kernel; 128-tile kernel for odd shapes;
     gemm8 fp8 kernel when fp8 is on and the weight has an fp8 copy). ``xq``: x's fp8 copy (q, sinv) already
     written by its producer. ``q8_for``: the weight of the fp8 GEMM that consumes the output (``out2`` for the
-    two-output GELU epilogue): on the fp8 path the epilogue writes that GEMM's fp8 input copy too."""
+    two-output GELU epilogue): on the fp8 path the epilogue writes that GEMM's fp8 input copy too. ``q8_only``: the
+    caller's consumers of ``out2`` all take that fp8 copy, so its bf16 values are not stored when the copy is written
+    (returned ``y`` then carries ``_hsd_q8_only = True``; ``out2``'s contents are undefined)."""
     y = torch.empty((x.shape[0], w.shape[0]), dtype=x.dtype, device=x.device)
     wq = _fp8_w(w, "_hsd_q")
     if wq is not None and _C.gemm8_supported(epi, x.shape[0], w.shape[0], x.shape[1]):
         qx, sx = xq if xq is not None else quant_fp8(x, FP8_E4M3, getattr(w, "_hsd_fp8_x", None))
         q8 = _q8_out(y, q8_for, "_hsd_fp8_x", "_hsd_q", FP8_E4M3) \
             if q8_for is not None and epi in (EPI_BIAS_GELU, EPI_BIAS_GELU_D) and out2 is not None else None
+        only = bool(q8_only and q8 is not None)
         _C.gemm8(qx, FP8_E4M3, sx, wq, FP8_E4M3, w._hsd_qs, y, epi, bias, aux, out2, float(p), _s64(seed), None,
-                 **_q8_kw(q8))
+                 **_q8_kw(q8), q8_only=only)
         if q8 is not None:
             _Q8_HANDOFF.put(out2, q8[0], q8[1])
+        if only:
+            y._hsd_q8_only = True
         return y
     if _nt_ok(x.shape[0], w.shape[0], x.shape[1], epi):
         _C.gemm2(x, w, y, 0, 0, epi, bias, aux, out2, float(p), _s64(seed), 0, None, None)  # 0: auto split-K
@@ -749,11 +773,13 @@ def gemm_dgrad_rd(dy, w, o, rd, seq, dyq=None):
     return gemm_dgrad(dy, w, dyq=dyq), False
 
 
-def gemm_dgrad(dy, w, epi=EPI_STORE, aux=None, dbias=None, dyq=None, q8_for=None):
+def gemm_dgrad(dy, w, epi=EPI_STORE, aux=None, dbias=None, dyq=None, q8_for=None, q8_only=False):
     """dx[T, K] = dy[T, N] · w[N, K]  (NT kernel on the transposed weight wᵀ [K, N]).
 
     ``dbias`` (DGELU only): fp32 [K] buffer that receives the column sums of dx (the bias gradient of
-    the layer that produced ``aux``) from the epilogue; returns ``(dx, fused)``-style via attribute."""
+    the layer that produced ``aux``) from the epilogue; returns ``(dx, fused)``-style via attribute.
+    ``q8_only``: every consumer of dx takes the fp8 copy written for ``q8_for``, so dx's bf16 values are not stored
+    when that copy is written (dx then carries ``_hsd_q8_only = True`` and its contents are undefined)."""
     dx = torch.empty((dy.shape[0], w.shape[1]), dtype=dy.dtype, device=dy.device)
     wqt = _fp8_w(w, "_hsd_qt")
     if wqt is not None and _C.gemm8_supported(epi, dy.shape[0], w.shape[1], dy.shape[1]):
@@ -763,8 +789,12 @@ def gemm_dgrad(dy, w, epi=EPI_STORE, aux=None, dbias=None, dyq=None, q8_for=None
         # q8_for: the next fp8 dgrad's weight -- the epilogue writes its dy copy (the GELU'-product output)
         q8 = _q8_out(dx, q8_for, "_hsd_fp8_g", "_hsd_qt", fmt) \
             if q8_for is not None and epi in (EPI_MUL, EPI_DGELU) else None
+        # the bias-gradient column sums read dx when they are not fused: then dx's bf16 values must exist
+        only = bool(q8_only and q8 is not None and (dbias is None or fuse))
         _C.gemm8(qdy, fmt, sdy, wqt, FP8_E4M3, w._hsd_qs, dx, epi, None, aux, None, 0.0, 0, dbias if fuse else None,
-                 **_q8_kw(q8))
+                 **_q8_kw(q8), q8_only=only)
+        if only:
+            dx._hsd_q8_only = True
         if dbias is not None and not fuse:
             _C.colsum(dx, dbias)
         if q8 is not None:
@@ -798,6 +828,9 @@ def gemm_dgrad(dy, w, epi=EPI_STORE, aux=None, dbias=None, dyq=None, q8_for=None
 # HSD_FP8_WGRAD=0 keeps the weight gradients bf16 under --fp8.
 _FP8_WGRAD = _os.environ.get("HSD_FP8_WGRAD", "1") == "1"
 WGRAD8_CALLS = [0]  # fp8 weight-gradient launches (tests)
+# fp8 FFN: epilogues whose bf16 output is only ever read through its fp8 copy skip the bf16 store (tests switch it off
+# to compare against the path that writes both)
+_Q8_ONLY = True
 
 
 def _wgrad8_ok(dyq, xq, N, K, T) -> bool:
@@ -846,16 +879,17 @@ def _ln_fwd(z, w, b, eps, q8_for=None):
     return out, mean, rstd
 
 
-def _ln_bwd(dout2, z, mean, rstd, ln_w, dz, dy, g_lnw, g_lnb, g_b, p, seed, consumer_w):
+def _ln_bwd(dout2, z, mean, rstd, ln_w, dz, dy, g_lnw, g_lnb, g_b, p, seed, consumer_w, q8_only=False):
     """LN backward into dy (and dz with dropout); returns dy's fp8 copy (q, sinv) when ``consumer_w``'s dgrad runs
-    fp8 on a calibrated site (quantised in the same pass), else None."""
+    fp8 on a calibrated site (quantised in the same pass), else None. ``q8_only`` (dropout on, so dz is its own
+    buffer): every consumer of dy takes that fp8 copy, and dy's bf16 values are not stored."""
     st = _site_ready(consumer_w, "_hsd_fp8_g", "_hsd_qt")
     rows, H = z.shape
     if st is not None and H <= 1024 and _C.gemm8_supported(EPI_STORE, rows, consumer_w.shape[1], H):
         q = torch.empty((rows, H), dtype=torch.uint8, device=z.device)
         sinv = torch.empty(1, dtype=torch.float32, device=z.device)
         _C.ln_bwd_q8(dout2, z, mean, rstd, ln_w, dz, dy, g_lnw.buf, g_lnb.buf, g_b.buf, p, _s64(seed) if p > 0 else 0,
-                     q, st[0:1], sinv, st[1:2], _FP8["grad_fmt"])
+                     q, st[0:1], sinv, st[1:2], _FP8["grad_fmt"], q8_only=bool(q8_only and p > 0 and dz is not None))
         return q, sinv
     _C.ln_bwd(dout2, z, mean, rstd, ln_w, dz, dy, None, g_lnw.buf, g_lnb.buf, g_b.buf, p, _s64(seed) if p > 0 else 0)
     return None
@@ -907,13 +941,18 @@ class _AttnBlock(torch.autograd.Function):
         g_lnw, g_lnb, g_ow, g_ob = _Grad(ln_w), _Grad(ln_b), _Grad(out_w), _Grad(out_b)
         dy = torch.empty_like(z)
         dz = torch.empty_like(z) if p_h > 0 else None
-        dyq = _ln_bwd(dout2, z, mean, rstd, ln_w, dz, dy, g_lnw, g_lnb, g_ob, p_h, seed_h, out_w)
-        if dz is None:
-            dz = dy
-        r_lnw, r_lnb, r_ob = g_lnw.done(), g_lnb.done(), g_ob.done()
         # the fp8 copies are released after the first backward (a retained-graph second backward runs bf16)
         hq, actq = ctx.q8 or (None, None)
         ctx.q8 = None
+        T, H = z.shape
+        # dy's consumers (the out-projection weight gradient with the context's fp8 copy, its dgrad) both fp8: the LN
+        # backward stores only dy's fp8 copy
+        dy_q8 = bool(_Q8_ONLY and _FP8["on"] and _FP8_WGRAD and actq is not None and _C.gemm8_wgrad_supported(H, H, T)
+                     and _fp8_dgrad_ok(out_w, EPI_STORE, T))
+        dyq = _ln_bwd(dout2, z, mean, rstd, ln_w, dz, dy, g_lnw, g_lnb, g_ob, p_h, seed_h, out_w, q8_only=dy_q8)
+        if dz is None:
+            dz = dy
+        r_lnw, r_lnb, r_ob = g_lnw.done(), g_lnb.done(), g_ob.done()
         r_ow = wgrad_done(g_ow, dy, actx, dyq, actq)
         dq_acc = _attn_ws(B, S, heads, actx.device)
         delta_ready = False
@@ -932,9 +971,13 @@ class _AttnBlock(torch.autograd.Function):
             # ... and so does dqkv's fp8 copy for the fp8 QKV dgrad
             q = torch.empty(dqkv.shape, dtype=torch.uint8, device=dqkv.device)
             sinv = torch.empty(1, dtype=torch.float32, device=dqkv.device)
+            # dqkv's consumers (the QKV weight gradient with h's fp8 copy, the QKV dgrad) both fp8: only its fp8 copy
+            dq_only = bool(_Q8_ONLY and _FP8_WGRAD and hq is not None
+                           and _C.gemm8_wgrad_supported(qkv_w.shape[0], qkv_w.shape[1], dqkv.shape[0])
+                           and _fp8_dgrad_ok(qkv_w, EPI_RES, dqkv.shape[0]))
             _C.attn_bwd_q8(qkv, mb if has_mask else None, actx, dctx, lse, dqkv, dq_acc, B, S, heads, p_a,
                            _s64(seed_a), g_qb.buf, q, st[0:1], sinv, st[1:2], _FP8["grad_fmt"],
-                           km if ctx.has_km else None, delta_ready)
+                           km if ctx.has_km else None, delta_ready, q8_only=dq_only)
             dqq = (q, sinv)
         else:
             _C.attn_bwd(qkv, mb if has_mask else None, actx, dctx, lse, dqkv, dq_acc, B, S, heads, p_a, _s64(seed_a),
@@ -968,12 +1011,24 @@ class _FFNBlock(torch.autograd.Function):
         # epilogue is then a product (no erf/exp per element in backward)
         keep_grad = _nt_ok(h2d.shape[0], w1.shape[0], h2d.shape[1], EPI_BIAS_GELU_D) and \
             _nt_ok(h2d.shape[0], w1.shape[0], w2.shape[0], EPI_MUL)
-        pre = gemm_fwd(h2d, w1, EPI_BIAS_GELU_D if keep_grad else EPI_BIAS_GELU, bias=b1, out2=act, xq=xq, q8_for=w2)
+        T, H, I = h2d.shape[0], h2d.shape[1], w1.shape[0]
+        # fp8: the activation's bf16 values are not stored when both of its consumers take its fp8 copy -- the FFN2
+        # forward (fp8 kernel) and the W2 weight gradient (fp8 TT kernel, with the LN backward's fp8 copy of dy on a
+        # calibrated site): 2·T·I bytes of epilogue stores less per layer
+        act_q8 = bool(_Q8_ONLY and _FP8["on"] and _FP8_WGRAD and _fp8_fwd_ok(w2, EPI_BIAS_DROP_RES, T, I)
+                      and _site_ready(w2, "_hsd_fp8_g", "_hsd_qt") is not None and H <= 1024
+                      and _C.gemm8_supported(EPI_STORE, T, I, H) and _C.gemm8_wgrad_supported(H, I, T))
+        pre = gemm_fwd(h2d, w1, EPI_BIAS_GELU_D if keep_grad else EPI_BIAS_GELU, bias=b1, out2=act, xq=xq, q8_for=w2,
+                       q8_only=act_q8)
         actq = _take_q8(act)
+        act_missing = getattr(pre, "_hsd_q8_only", False)
+        if act_missing and actq is None:
+            raise RuntimeError("FFN forward: the activation's fp8 copy was not handed over")
         z = gemm_fwd(act, w2, EPI_BIAS_DROP_RES, bias=b2, aux=h2d, p=p, seed=seed, xq=actq)
         out, mean, rstd = _ln_fwd(z, ln_w, ln_b, eps, q8_for=q8_next)
         ctx.save_for_backward(h2d, w1, b1, w2, b2, ln_w, ln_b, pre, act, z, mean, rstd)
         ctx.cfg = (float(p), seed, keep_grad)
+        ctx.act_missing = act_missing
         ctx.q8 = (xq, actq) if _FP8_WGRAD else (None, None)
         return out.view(h.shape)
 
@@ -985,18 +1040,33 @@ class _FFNBlock(torch.autograd.Function):
         g_lnw, g_lnb, g_w2, g_b2 = _Grad(ln_w), _Grad(ln_b), _Grad(w2), _Grad(b2)
         dy = torch.empty_like(z)
         dz = torch.empty_like(z) if p > 0 else None
-        dyq = _ln_bwd(dout2, z, mean, rstd, ln_w, dz, dy, g_lnw, g_lnb, g_b2, p, seed, w2)
+        # the fp8 copies are released after the first backward (a retained-graph second backward runs bf16), unless
+        # the forward did not store the activation's bf16 values: then its fp8 copy stays for any later backward
+        hq, actq = ctx.q8 or (None, None)
+        if not ctx.act_missing:
+            ctx.q8 = None
+        T, H, I = h2d.shape[0], h2d.shape[1], w1.shape[0]
+        # dy's consumers (the W2 weight gradient with the activation's fp8 copy, the W2 dgrad) both fp8: the LN
+        # backward stores only dy's fp8 copy
+        dy_q8 = bool(_Q8_ONLY and _FP8["on"] and _FP8_WGRAD and actq is not None and _C.gemm8_wgrad_supported(H, I, T)
+                     and _fp8_dgrad_ok(w2, EPI_MUL if keep_grad else EPI_DGELU, T))
+        dyq = _ln_bwd(dout2, z, mean, rstd, ln_w, dz, dy, g_lnw, g_lnb, g_b2, p, seed, w2, q8_only=dy_q8)
         if dz is None:
             dz = dy
         r_lnw, r_lnb, r_b2 = g_lnw.done(), g_lnb.done(), g_b2.done()
-        # the fp8 copies are released after the first backward (a retained-graph second backward runs bf16)
-        hq, actq = ctx.q8 or (None, None)
-        ctx.q8 = None
+        if ctx.act_missing and not _wgrad8_ok(dyq, actq, H, I, T):
+            act = _dequant8(actq, FP8_E4M3, act)  # the W2 weight gradient runs bf16 after all
         r_w2 = wgrad_done(g_w2, dy, act, dyq, actq)
         g_w1, g_b1 = _Grad(w1), _Grad(b1)
+        # fp8: da's bf16 values are not stored when its consumers (the W1 weight gradient with the forward's fp8 copy
+        # of h, the W1 dgrad) both run on the fp8 kernels from the epilogue's fp8 copy
+        da_q8 = bool(_Q8_ONLY and _FP8["on"] and _FP8_WGRAD and hq is not None and _C.gemm8_wgrad_supported(I, H, T)
+                     and ctx.needs_input_grad[0] and _fp8_dgrad_ok(w1, EPI_RES, T))
         da = gemm_dgrad(dy, w2, EPI_MUL if keep_grad else EPI_DGELU, aux=pre, dbias=g_b1.buf, dyq=dyq,
-                        q8_for=w1 if ctx.needs_input_grad[0] else None)
+                        q8_for=w1 if ctx.needs_input_grad[0] else None, q8_only=da_q8)
         daq = _take_q8(da)
+        if getattr(da, "_hsd_q8_only", False) and daq is None:
+            raise RuntimeError("FFN backward: the GELU-gradient product's fp8 copy was not handed over")
         r_b1 = g_b1.done()
         r_w1 = wgrad_done(g_w1, da, h2d, daq, hq)
         dh = gemm_dgrad(da, w1, EPI_RES, aux=dz, dyq=daq) if ctx.needs_input_grad[0] else None

@@ -130,11 +130,13 @@ class FusedAdam:
     def overlap_enabled(self) -> bool:
         return bool(getattr(self, "_ranges", None))
 
-    def begin_step(self, grad_scale: float) -> None:
-        """Fix this step's coefficients before backward (the slices are stepped during it)."""
+    def begin_step(self, grad_scale: float, zero_grad: bool = False) -> None:
+        """Fix this step's coefficients before backward (the slices are stepped during it). ``zero_grad``: each slice's
+        Adam also clears the gradients it read (:meth:`step`)."""
         self.step_count += 1
         step, eps_eff = self._coeffs()
         self._coef = (step, eps_eff, float(grad_scale))
+        self._zero = bool(zero_grad) and self.store.grad.is_cuda
         self._done = [False] * len(self._ranges)
         self._began = True
 
@@ -159,7 +161,8 @@ class FusedAdam:
         out, out_lo = s.adam_outputs(st, e)
         dm = self._decay_mask[st // ALIGN:(e + ALIGN - 1) // ALIGN] if self._decay_mask is not None else None
         hip.adam_step(s.master[st:e], self.exp_avg[st:e], self.exp_avg_sq[st:e], s.grad[st:e], out, dm, step,
-                      eps_eff, self.beta1, self.beta2, gscale, self.lr * self.weight_decay, self._kernel_coef(), out_lo)
+                      eps_eff, self.beta1, self.beta2, gscale, self.lr * self.weight_decay, self._kernel_coef(), out_lo,
+                      zero_grad=getattr(self, "_zero", False))
         if self._tsub is not None:
             s.refresh_transposed_subset(self._tsub[b])
         self._done[b] = True
@@ -174,13 +177,18 @@ class FusedAdam:
         for b in range(len(self._ranges)):  # slices no gradient reached (unused parameters)
             self.step_range(b)
         self._began = False
+        self._zero = False
         if self._tsub is None:
             self.store.refresh_transposed()
         else:
             self.store.refresh_fp8()
 
     @torch.no_grad()
-    def step(self, grad_scale: float = 1.0) -> None:
+    def step(self, grad_scale: float = 1.0, zero_grad: bool = False) -> None:
+        """``zero_grad`` (GPU): the kernel clears each gradient after reading it, so the caller (the Trainer) can skip
+        its next :meth:`FlatParamStore.zero_grad` -- the memset pass over the whole gradient buffer moves into the
+        optimizer's own pass (which, overlapped with backward, runs under the weight-gradient GEMMs). With the overlap,
+        :meth:`begin_step` decides it."""
         if getattr(self, "_began", False):
             self._finish_overlapped(grad_scale)
             return
@@ -195,7 +203,7 @@ class FusedAdam:
             out, out_lo = s.adam_outputs(0, s.numel)
             hip.adam_step(s.master, self.exp_avg, self.exp_avg_sq, s.grad, out,
                           self._decay_mask, step, eps_eff, self.beta1, self.beta2, float(grad_scale),
-                          self.lr * self.weight_decay, self._kernel_coef(), out_lo)
+                          self.lr * self.weight_decay, self._kernel_coef(), out_lo, zero_grad=zero_grad)
             s.refresh_transposed()
             return
         # reference path (CPU): identical math on flat buffers

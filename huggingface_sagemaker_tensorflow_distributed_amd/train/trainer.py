@@ -28,6 +28,7 @@ import torch
 from .. import ops
 from ..obs.profiler import range as prange
 from ..parallel import backend
+from ..optim.adam import FusedAdam
 from ..parallel.collectives import allreduce_sums, params_in_sync
 
 logger = logging.getLogger(__name__)
@@ -99,6 +100,10 @@ class _Meter:
 
 
 class Trainer:
+    # eager GPU steps: the fused Adam clears each gradient slice it consumes, replacing the memset ahead of the next
+    # step's forward (False: a separate zero_grad every step)
+    zero_grad_in_optimizer = True
+
     def __init__(self, model, store, optimizer, bucketer=None, device=None, grad_accum: int = 1,
                  check_sync: int = 0, log_every: int = 50, step_watchdog: float = 0.0, hip_graph: bool = False,
                  lr_schedule: str = "constant", lr_warmup_steps: int = 0, eval_hip_graph="auto"):
@@ -123,6 +128,7 @@ class Trainer:
         self._seed = None
         self._graph_replay = True  # tests: False = graph-mode seeding with eager kernels
         self._opt_overlap = None  # LocalOverlap (one process) | "engine" (DP ranks) | None
+        self._grads_clear = False  # the last eager step's optimizer left the gradient buffer zeroed
         # learning-rate schedule: the reference's Keras Adam uses a constant rate (scripts/train.py:113); linear =
         # warmup to the base rate, then linear decay to 0 over the steps fit() is asked to run
         if lr_schedule not in ("constant", "linear"):
@@ -243,15 +249,21 @@ class Trainer:
             self.model.rng.new_step(0)
         else:
             self.model.rng.new_step(self.global_step)
-        self.store.zero_grad()
+        if self._grads_clear:
+            self._grads_clear = False  # the previous step's Adam cleared every gradient it read (stream-ordered)
+        else:
+            self.store.zero_grad()
         k = len(micro_batches)
         if self.bucketer is not None:
             self.bucketer.begin(micro_steps=k)
         if self.lr_schedule != "constant" or self.lr_warmup_steps:
             self.optimizer.lr = self.lr_at(self.global_step)
         ov = self._opt_overlap
+        # the optimizer clears the gradients it consumes (no memset pass at the next step's start): eager steps with
+        # the fused GPU Adam only (captured steps keep their own memset node)
+        zg = self.zero_grad_in_optimizer and self.device.type == "cuda" and isinstance(self.optimizer, FusedAdam)
         if ov is not None:
-            self.optimizer.begin_step(grad_scale=1.0 / (self.world * k))
+            self.optimizer.begin_step(grad_scale=1.0 / (self.world * k), zero_grad=zg)
             if ov != "engine":
                 ov.begin()
         loss = None
@@ -272,8 +284,12 @@ class Trainer:
                 ov.join()
         self._phase = "optimizer"
         with prange("optimizer"):
-            self.optimizer.step(grad_scale=1.0 / (self.world * k))
+            if zg:
+                self.optimizer.step(grad_scale=1.0 / (self.world * k), zero_grad=True)
+            else:
+                self.optimizer.step(grad_scale=1.0 / (self.world * k))
         self._phase = "idle"
+        self._grads_clear = zg
         self.global_step += 1
         if self.check_sync and self.global_step % self.check_sync == 0:
             if not params_in_sync(self.store):
@@ -286,6 +302,7 @@ class Trainer:
         self.model.rng.new_step(0)
         if self.lr_schedule != "constant" or self.lr_warmup_steps:
             self.optimizer.lr = self.lr_at(self.global_step)
+        self._grads_clear = False  # the captured step keeps its own memset node and leaves gradients in place
         self._phase = "graph-step"
         with prange("graph-step"):
             loss, logits = self._full_graph_for(mb).run(mb)

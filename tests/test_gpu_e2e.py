@@ -139,6 +139,7 @@ def test_optimizer_overlapped_with_backward_uses_final_gradients(gpu, monkeypatc
          "--dtype", "bf16", "--log_every", "0", "--hip_graph", "false", "--seed", "3"])
     parts = build(args, "train")
     tr, st, opt = parts["trainer"], parts["store"], parts["optimizer"]
+    tr.zero_grad_in_optimizer = False  # the replay below reads the step's final gradients after the step
     assert tr._opt_overlap is not None and len(opt._ranges) > 10
     for step in range(3):
         p0, m0, v0 = st.master.clone(), opt.exp_avg.clone(), opt.exp_avg_sq.clone()
@@ -155,6 +156,42 @@ def test_optimizer_overlapped_with_backward_uses_final_gradients(gpu, monkeypatc
         assert len(tracked) == 48
         for p in tracked:
             assert torch.equal(p._hsd_wt, p.detach().t())
+
+
+@pytest.mark.parametrize("overlap", ["1", "0"])
+def test_optimizer_clears_the_gradients_it_consumed(gpu, monkeypatch, overlap):
+    """Eager GPU steps: the fused Adam clears each gradient slice it reads and the next step skips its memset. After
+    every step the whole gradient buffer is zero, and the losses track a trainer that zeroes with a separate memset
+    (same init, same batches; not bitwise: the backward's fp32 atomics sum in a run-dependent order)."""
+    from huggingface_sagemaker_tensorflow_distributed_amd import data as hdata
+    from huggingface_sagemaker_tensorflow_distributed_amd.train.runner import build
+    from huggingface_sagemaker_tensorflow_distributed_amd.utils.args import build_parser
+
+    ds = hdata.synthetic_classification(8 * 4, 128, 30522, seed=0)
+    batches = [{k: torch.from_numpy(v[8 * i:8 * (i + 1)]).long().to(gpu) for k, v in
+                (("input_ids", ds.input_ids), ("attention_mask", ds.attention_mask), ("labels", ds.labels))}
+               for i in range(4)]
+    monkeypatch.setenv("HSD_OPT_OVERLAP", overlap)
+    losses = {}
+    for zero_in_opt in (True, False):
+        args, _ = build_parser("train").parse_known_args(
+            ["--model_name_or_path", "bert-base-uncased", "--train_batch_size", "8", "--learning_rate", "1e-4",
+             "--dtype", "bf16", "--log_every", "0", "--hip_graph", "false", "--seed", "3",
+             "--gradient_accumulation_steps", "2"])
+        parts = build(args, "train")
+        tr, st = parts["trainer"], parts["store"]
+        tr.zero_grad_in_optimizer = zero_in_opt
+        assert (tr._opt_overlap is not None) == (overlap == "1")
+        out = []
+        for step in range(4):
+            out.append(float(tr.train_step([batches[(2 * step + j) % 4] for j in range(2)])))
+            torch.cuda.synchronize()
+            if zero_in_opt:
+                assert tr._grads_clear and int(torch.count_nonzero(st.grad)) == 0
+        losses[zero_in_opt] = out
+    a, b = losses[True], losses[False]
+    for x, y in zip(a, b):
+        assert abs(x - y) <= 2e-3 * max(1.0, abs(y)), (a, b)
 
 
 def test_two_layer_bert_learns_the_marker_task(gpu, tmp_path):

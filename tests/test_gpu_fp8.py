@@ -226,6 +226,38 @@ def test_ln_bwd_q8_equals_ln_bwd_then_quant(gpu, rows, H, p, fmt):
             assert torch.equal(x, y), i
 
 
+@pytest.mark.parametrize("rows,H,fmt", [(4096, 768, 0), (2048, 1024, 1)])
+def test_ln_bwd_q8_only_skips_dy(gpu, rows, H, fmt):
+    """LN backward with q8_only (dropout on): dy's bf16 buffer is left untouched, every other output (dz, the fp8 copy,
+    its scale and amax, dgamma / dbeta / the bias gradient summed from the rounded dy) as when dy is stored."""
+    hip = _hip()
+    C = hip._C
+    torch.manual_seed(7)
+    z = torch.randn(rows, H, device=gpu).bfloat16()
+    dout = torch.randn(rows, H, device=gpu).bfloat16()
+    w = (1 + 0.1 * torch.randn(H, device=gpu)).bfloat16()
+    mean = z.float().mean(1)
+    rstd = torch.rsqrt(z.float().var(1, unbiased=False) + 1e-12)
+    res = {}
+    for only in (False, True):
+        dz = torch.empty_like(z)
+        dy = torch.full_like(z, 3.0)
+        dg, db, dbias = (torch.zeros(H, device=gpu) for _ in range(3))
+        st = torch.tensor([5.0, 0.0], device=gpu)
+        q = torch.empty(rows, H, dtype=torch.uint8, device=gpu)
+        sinv = torch.empty(1, device=gpu)
+        C.ln_bwd_q8(dout, z, mean, rstd, w, dz, dy, dg, db, dbias, 0.1, 11, q, st[0:1], sinv, st[1:2], fmt,
+                    q8_only=only)
+        torch.cuda.synchronize()
+        res[only] = (dz, dy, dg, db, dbias, q, sinv, st)
+    a, b = res[False], res[True]
+    assert bool((b[1] == 3.0).all()) and not bool((a[1] == 3.0).all())
+    for i in (0, 5, 6, 7):
+        assert torch.equal(a[i], b[i]), i
+    for i in (2, 3, 4):
+        torch.testing.assert_close(b[i], a[i], rtol=1e-5, atol=1e-4)
+
+
 @pytest.mark.parametrize("B,S,H,p", [(32, 128, 768, 0.1), (8, 512, 1024, 0.0)])
 def test_embed_fwd_q8_equals_embed_then_quant(gpu, B, S, H, p):
     """The embedding forward (gather + LayerNorm + dropout) writing its output's fp8 copy == the same kernel, then the
@@ -287,9 +319,9 @@ def test_fp8_fused_ln_quant_in_the_step(gpu):
         def __getattr__(self, k):
             f = getattr(orig_C, k)
             if k in calls:
-                def w(*a):
+                def w(*a, **kw):
                     calls[k] += 1
-                    return f(*a)
+                    return f(*a, **kw)
                 return w
             return f
 
@@ -375,6 +407,40 @@ def test_attention_q8_equals_attention_then_quant(gpu, S, p, fmt, use_km):
             assert torch.equal(x, y), i
 
 
+@pytest.mark.parametrize("S,fmt", [(512, 0), (384, 1)])
+def test_attention_bwd_q8_only_skips_dqkv(gpu, S, fmt):
+    """Streaming attention backward with q8_only: dqkv's bf16 buffer untouched, its fp8 copy, scale, amax and the
+    fused QKV bias gradient as when dqkv is stored."""
+    hip = _hip()
+    C = hip._C
+    torch.manual_seed(15)
+    B, heads = 2, 16
+    H = heads * 64
+    qkv = (torch.randn(B * S, 3 * H, device=gpu) * 0.5).bfloat16()
+    mb = torch.zeros(B, S, device=gpu)
+    mb[1, S - 37:] = -10000.0
+    out = torch.empty(B * S, H, device=gpu, dtype=torch.bfloat16)
+    lse = torch.empty(B * heads * S, device=gpu)
+    C.attn_fwd(qkv, mb, out, lse, B, S, heads, 0.1, 9)
+    dout = torch.randn_like(out)
+    res = {}
+    for only in (False, True):
+        dqkv = torch.full_like(qkv, 3.0)
+        ws = hip._attn_ws(B, S, heads, gpu)
+        db = torch.zeros(3 * H, device=gpu)
+        gst = torch.tensor([3.0, 0.0], device=gpu)
+        gq, gs = torch.empty(B * S, 3 * H, dtype=torch.uint8, device=gpu), torch.empty(1, device=gpu)
+        C.attn_bwd_q8(qkv, mb, out, dout, lse, dqkv, ws, B, S, heads, 0.1, 9, db, gq, gst[0:1], gs, gst[1:2], fmt,
+                      q8_only=only)
+        torch.cuda.synchronize()
+        res[only] = (dqkv, gq, gs, gst, db)
+    a, b = res[False], res[True]
+    assert bool((b[0] == 3.0).all()) and not bool((a[0] == 3.0).all())
+    for i in (1, 2, 3):
+        assert torch.equal(a[i], b[i]), i
+    torch.testing.assert_close(b[4], a[4], rtol=1e-5, atol=1e-4)
+
+
 @pytest.mark.parametrize("M,N,K,epi,fmt", [(8192, 4096, 1024, 8, 0), (8192, 1024, 4096, 9, 1), (5000, 3072, 768, 9, 0)])
 def test_gemm8_epilogue_q8_equals_gemm8_then_quant(gpu, M, N, K, epi, fmt):
     """The fp8 GEMM's epilogue writing the fp8 copy of its output (GELU output for the FFN1 forward, the GELU'-product
@@ -412,6 +478,85 @@ def test_gemm8_epilogue_q8_equals_gemm8_then_quant(gpu, M, N, K, epi, fmt):
     assert torch.equal(a[2], b[2]) and torch.equal(a[3], b[3]) and torch.equal(a[4], b[4])
     if a[5] is not None:
         torch.testing.assert_close(b[5], a[5], rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("M,N,K,epi,fmt", [(8192, 4096, 1024, 8, 0), (8192, 1024, 4096, 9, 1)])
+def test_gemm8_epilogue_q8_only_skips_the_bf16_twin(gpu, M, N, K, epi, fmt):
+    """q8_only: the fp8 epilogue does not store the bf16 output its fp8 copy duplicates (C2 of the GELU epilogue, C of
+    the GELU'-product one); every other output (the fp8 copy, its scale / amax, GELU', the bias-gradient column sums)
+    is bit-identical to the epilogue that stores both, and the skipped buffer keeps its previous contents."""
+    hip = _hip()
+    C = hip._C
+    torch.manual_seed(9)
+    x = torch.randn(M, K, device=gpu).bfloat16()
+    w = (torch.randn(N, K, device=gpu) * 0.05).bfloat16()
+    qx, sx = hip.quant_fp8(x, 0)
+    qw, sw = hip.quant_fp8(w, 0)
+    bias = (torch.randn(N, device=gpu) * 0.1).bfloat16()
+    aux = torch.randn(M, N, device=gpu).bfloat16()
+    res = {}
+    for only in (False, True):
+        y = torch.full((M, N), 7.0, device=gpu, dtype=torch.bfloat16)
+        y2 = torch.full_like(y, 7.0) if epi == 8 else None
+        db = torch.zeros(N, device=gpu) if epi == 9 else None
+        st = torch.tensor([1.5, 0.0], device=gpu)
+        q, sinv = torch.empty(M, N, dtype=torch.uint8, device=gpu), torch.empty(1, device=gpu)
+        C.gemm8(qx, 0, sx, qw, 0, sw, y, epi, bias if epi == 8 else None, aux if epi == 9 else None, y2, 0.0, 0, db,
+                q8=q, q8_amax=st[0:1], q8_sinv=sinv, q8_track=st[1:2], q8fmt=fmt, q8_only=only)
+        torch.cuda.synchronize()
+        res[only] = (y, y2, q, sinv, st, db)
+    a, b = res[False], res[True]
+    assert torch.equal(a[2], b[2]) and torch.equal(a[3], b[3]) and torch.equal(a[4], b[4])
+    skipped = b[1] if epi == 8 else b[0]
+    assert bool((skipped == 7.0).all())
+    if epi == 8:
+        assert torch.equal(a[0], b[0])  # GELU' is still stored
+    else:
+        torch.testing.assert_close(b[5], a[5], rtol=1e-4, atol=1e-3)
+
+
+@pytest.mark.parametrize("drop", [0.0, 0.1])
+def test_fp8_step_q8_only_equals_writing_both(gpu, drop):
+    """roberta-large (2 layers) MLM, calibrated fp8 step with fp8 weight gradients: skipping the bf16 twins of the fp8
+    copies (hip._Q8_ONLY: the FFN epilogues; with dropout also the LayerNorm backwards' dy) leaves the loss and every
+    gradient as with both written (the bias gradients' column atomics aside, which sum in a run-dependent order)."""
+    from huggingface_sagemaker_tensorflow_distributed_amd import data as hdata
+    from huggingface_sagemaker_tensorflow_distributed_amd.models import build_model, resolve_config
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel import FlatParamStore
+
+    hip = _hip()
+    cfg = resolve_config("roberta-large").replace(num_hidden_layers=2, hidden_dropout_prob=drop,
+                                                  attention_probs_dropout_prob=drop)
+    ds = hdata.synthetic_mlm(8, 256, cfg.vocab_size, seed=4)
+    ids = torch.from_numpy(ds.input_ids).long().to(gpu)
+    am = torch.from_numpy(ds.attention_mask).long().to(gpu)
+    labels = torch.from_numpy(ds.labels).long().to(gpu)
+    m = build_model(cfg, task="masked-lm", seed=0).to(gpu)
+    store = FlatParamStore(m, gpu, compute_dtype=torch.bfloat16, fp8=True)
+    hip.set_fp8(True)
+    prev = hip._Q8_ONLY
+    out = {}
+    try:
+        for step, only in enumerate((False, False, False, True)):
+            hip._Q8_ONLY = only
+            n0 = hip.WGRAD8_CALLS[0]
+            m.train()
+            m.rng.new_step(0)
+            store.zero_grad()
+            loss, _ = m(ids, attention_mask=am, labels=labels)
+            loss.backward()
+            torch.cuda.synchronize()
+            out[only] = (float(loss), store.grad.float().clone())
+            if step < 2:
+                store.refresh_fp8()
+            if only:
+                assert hip.WGRAD8_CALLS[0] - n0 == 8
+    finally:
+        hip._Q8_ONLY = prev
+        hip.set_fp8(False)
+    (l0, g0), (l1, g1) = out[False], out[True]
+    assert abs(l0 - l1) <= 1e-6 * abs(l0)  # the MLM loss sums by atomics
+    torch.testing.assert_close(g1, g0, rtol=1e-4, atol=1e-6)
 
 
 @pytest.mark.parametrize("M,N,T", [(768, 256, 384), (2304, 768, 4096), (512, 1024, 1152), (1024, 4096, 2048)])

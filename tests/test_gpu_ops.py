@@ -200,6 +200,31 @@ def test_adam_kernel_matches_reference(gpu):
     torch.testing.assert_close(out.float(), pr.bfloat16().float())
 
 
+@pytest.mark.parametrize("gdt", [torch.float32, torch.bfloat16])
+def test_adam_kernel_zero_grad_clears_what_it_read(gpu, gdt):
+    """zero_grad=True: the same weights / moments / bf16 copy bit for bit, and the gradient slice left at zero (the
+    slice only: the elements around it untouched)."""
+    hip = _hip()
+    torch.manual_seed(6)
+    n = 64 * 1024
+    base = [torch.randn(n, device=gpu), torch.randn(n, device=gpu).abs() * 0.1, torch.randn(n, device=gpu).abs() * 0.1]
+    gfull = torch.randn(n + 2048, device=gpu).to(gdt)
+    res = {}
+    for zg in (False, True):
+        p, m, v = (t.clone() for t in base)
+        g = gfull.clone()
+        out = torch.empty(n, device=gpu, dtype=torch.bfloat16)
+        hip.adam_step(p, m, v, g[1024:1024 + n], out, None, 1e-3, 1e-7, 0.9, 0.999, 0.5, 0.0, zero_grad=zg)
+        torch.cuda.synchronize()
+        res[zg] = (p, m, v, out, g)
+    for a, b in zip(res[False][:4], res[True][:4]):
+        assert torch.equal(a, b)
+    g0, g1 = res[False][4], res[True][4]
+    assert torch.equal(g0, gfull)
+    assert bool((g1[1024:1024 + n] == 0).all())
+    assert torch.equal(g1[:1024], gfull[:1024]) and torch.equal(g1[1024 + n:], gfull[1024 + n:])
+
+
 @pytest.mark.parametrize("S,H,heads", [(128, 256, 4), (256, 256, 4), (128, 1024, 16), (512, 1024, 16)])
 @pytest.mark.parametrize("p", [0.0, 0.1])
 def test_fused_blocks_vs_reference(gpu, p, S, H, heads):
