@@ -73,6 +73,11 @@ _WGRAD_AUTO_MAX_TOKENS = int(_os.environ.get("HSD_WGRAD_STREAM_MAX_TOKENS", "131
 _SIDE = {}
 _STASH = []
 _JOIN_QUEUED = [False]
+# callbacks run right after each weight-gradient fork (main -> side stream) outside captures, with the side stream:
+# work that must follow everything queued on the compute stream so far can be ordered behind the side stream's
+# position instead of recording an event of its own on the compute stream (optim/adam.py LocalOverlap: each event
+# recorded on the compute stream costs ~3 us on it, tools/fork_cost.py)
+_FORK_LISTENERS = []
 # HIP-graph capture (train/graph.py): the capture stream the side stream forks from and joins back to (autograd's
 # end-of-backward callback runs with the device's default stream current, not the capture stream), and whether this
 # capture forked it.
@@ -191,15 +196,34 @@ def _end_of_backward() -> None:
     join_side_streams()
 
 
+def _launch_wgrad(s, g: "_Grad", dy, x, dyq, xq):
+    """g += dyᵀ·x on the side stream ``s`` (already ordered after dy / x); the g.done() result."""
+    N, K, T = dy.shape[1], x.shape[1], dy.shape[0]
+    if g.buf is g.mg and _wgrad8_ok(dyq, xq, N, K, T):
+        _wgrad8(g.buf, dyq, xq, N, K, T, s)
+        return None
+    if g.buf is g.mg and _C.gemm2_supported(1, 1, 7, N, K, T):
+        # the common case without any Python stream plumbing: TT GEMM (+ split-K reduce) launched on the side stream
+        sp = _C.gemm2_splits(N, K, T)
+        _C.gemm2_on(s.cuda_stream, dy, x, g.buf, 1, 1, 7, None, None, None, 0.0, 0, sp,
+                    _workspace(sp * N * K, dy.device, s), None)
+        return None
+    with torch.cuda.stream(s):
+        gemm_wgrad_(g, dy, x, dyq, xq)
+        return g.done()
+
+
 def wgrad_done(g: "_Grad", dy: torch.Tensor, x: torch.Tensor, dyq=None, xq=None):
     """``g += dyᵀ·x`` then ``g.done()`` — on the wgrad side stream when the gradient lands in the flat
     fp32 main_grad buffer (training with a FlatParamStore) and the step is small enough, synchronously otherwise.
-    ``dyq`` / ``xq``: the producers' fp8 copies (q, sinv) of dy / x: with both, the fp8 TT kernel runs instead."""
+    ``dyq`` / ``xq``: the producers' fp8 copies (q, sinv) of dy / x: with both, the fp8 TT kernel runs instead.
+    (One fork per weight gradient: deferring the first weight gradient of each block half to the second one's fork,
+    one compute-stream event instead of two, measured 0.8 % slower at bert-large B = 8 and 0.2 % at the headline --
+    the side stream starts later -- profiles/r6/fork_merge_defer_ab_r6.log.)"""
     s = side_stream(dy.device) if (g.mg is not None and g.buf is g.mg and _use_side_stream(dy.shape[0])) else None
     if s is None:
         gemm_wgrad_(g, dy, x, dyq, xq)
         return g.done()
-    N, K, T = dy.shape[1], x.shape[1], dy.shape[0]
     parent = _CAPTURE["parent"]
     if parent is not None:
         _CAPTURE["forked"] = True  # a branch of the graph capture, forked from the capture stream itself
@@ -214,24 +238,12 @@ def wgrad_done(g: "_Grad", dy: torch.Tensor, x: torch.Tensor, dyq=None, xq=None)
             _C.stream_wait(s.cuda_stream, src)
             with torch.cuda.stream(s):
                 _C.cu_hog(1, _SIDE_DELAY_US)
-    if g.buf is g.mg and _wgrad8_ok(dyq, xq, N, K, T):
-        _C.stream_wait(s.cuda_stream, src)
-        _wgrad8(g.buf, dyq, xq, N, K, T, s)
-        r = None
-    elif g.buf is g.mg and _C.gemm2_supported(1, 1, 7, N, K, T):
-        _C.stream_wait(s.cuda_stream, src)
-        # the common case without any Python stream plumbing: TT GEMM (+ split-K reduce) launched on the side stream
-        sp = _C.gemm2_splits(N, K, T)
-        _C.gemm2_on(s.cuda_stream, dy, x, g.buf, 1, 1, 7, None, None, None, 0.0, 0, sp,
-                    _workspace(sp * N * K, dy.device, s), None)
-        r = None
-    else:
-        _C.stream_wait(s.cuda_stream, src)
-        with torch.cuda.stream(s):
-            gemm_wgrad_(g, dy, x, dyq, xq)
-            r = g.done()
     _STASH.append((dy, x, dyq, xq))
-    return r
+    _C.stream_wait(s.cuda_stream, src)
+    if parent is None:
+        for f in _FORK_LISTENERS:
+            f(s)
+    return _launch_wgrad(s, g, dy, x, dyq, xq)
 
 
 def _wgrad_(g: _Grad, dy2d: torch.Tensor, x2d: torch.Tensor) -> None:

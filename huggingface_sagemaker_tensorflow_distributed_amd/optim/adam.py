@@ -236,6 +236,9 @@ class LocalOverlap:
     post-accumulate hooks) and, when the last one is queued, runs the slice's Adam on a side stream that first
     waits for everything queued so far on the compute (and wgrad) streams."""
 
+    # False: every slice records its own event on the compute stream (the round-5 behaviour), for A/B runs
+    defer_to_fork = True
+
     def __init__(self, opt: FusedAdam, bucket_mb: Optional[float] = None):
         store = opt.store
         # 16 MiB slices: bert-large S=512 B=8 +0.6 % over 32 (more of the optimizer under the backward), the headline
@@ -260,12 +263,47 @@ class LocalOverlap:
         self._hog = (int(os.environ.get("HSD_HOG_CUS", "0")), float(os.environ.get("HSD_HOG_US", "400")),
                      int(os.environ.get("HSD_HOG_POINTS", "7")))
         self._hogs = 0
+        # slices whose gradients are final, waiting for the next weight-gradient fork (eager steps): a slice must
+        # follow every compute-stream kernel that wrote its gradients or READ its weights (the block's last dgrad is
+        # queued after the block's last fork), and the NEXT fork's side-stream position is after all of them. Ordering
+        # the slice behind that position (an event recorded on the side stream) instead of recording an event on the
+        # compute stream per slice takes ~3 us per slice off the compute stream's critical path (tools/fork_cost.py).
+        self._deferred: List[int] = []
+        self._forked = False  # a weight-gradient fork happened in this backward
+        from ..ops import hip
+
+        if self._on_fork not in hip._FORK_LISTENERS:
+            hip._FORK_LISTENERS.append(self._on_fork)
         opt.enable_overlap(self.ranges, on_ready=self.mark_ready)
 
     def begin(self) -> None:
         self.pending = list(self.count)
         self.sync = True
         self._hogs = 0
+        self._deferred = []
+        self._forked = False
+
+    def _launch(self, blocks: List[int]) -> None:
+        with torch.cuda.stream(self.stream):
+            for b in blocks:
+                if self._hog[0] > 0 and self._hogs < self._hog[2]:
+                    from ..ops import hip
+
+                    self._hogs += 1
+                    hip._C.cu_hog(self._hog[0], self._hog[1])
+                self.opt.step_range(b)
+
+    def _on_fork(self, side) -> None:
+        """A weight-gradient fork just made ``side`` wait for the compute stream: the deferred slices follow it."""
+        if side.device != self.stream.device:
+            return
+        self._forked = True
+        if self._deferred:
+            from ..ops import hip
+
+            hip.stream_wait(self.stream, side)
+            blocks, self._deferred = self._deferred, []
+            self._launch(blocks)
 
     def mark_ready(self, i: int) -> None:
         if not self.sync:  # accumulation micro-step: gradients are not final yet
@@ -273,6 +311,9 @@ class LocalOverlap:
         b = self.owner[i]
         self.pending[b] -= 1
         if self.pending[b] == 0:
+            if self.parent is None and self._forked and self.defer_to_fork:
+                self._deferred.append(b)  # launched behind the next weight-gradient fork (or at join)
+                return
             from ..ops import hip
 
             cur = self.parent if self.parent is not None else torch.cuda.current_stream(self.stream.device)
@@ -280,13 +321,17 @@ class LocalOverlap:
             side = hip.side_stream(self.stream.device)
             if side is not None and hip.side_stream_waitable():
                 hip.stream_wait(self.stream, side)
-            with torch.cuda.stream(self.stream):
-                if self._hog[0] > 0 and self._hogs < self._hog[2]:
-                    self._hogs += 1
-                    hip._C.cu_hog(self._hog[0], self._hog[1])
-                self.opt.step_range(b)
+            self._launch([b])
 
     def join(self) -> None:
         from ..ops import hip
 
-        hip.stream_wait(torch.cuda.current_stream(self.stream.device), self.stream)
+        cur = torch.cuda.current_stream(self.stream.device)
+        if self._deferred:
+            # slices ready after the backward's last fork: behind the compute stream, which has joined the side
+            # stream by now (Trainer.train_step joins the side streams before this)
+            hip.stream_wait(self.stream, cur)
+            blocks, self._deferred = self._deferred, []
+            self._launch(blocks)
+        self._forked = False
+        hip.stream_wait(cur, self.stream)

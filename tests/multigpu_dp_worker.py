@@ -37,6 +37,7 @@ def main(out):
     comp = os.environ.get("HSD_MGPU_COMPRESSION", "none")
     buck = GradBucketer(store, bucket_mb=1.0, compression=comp) if world > 1 else None
     tr = Trainer(model, store, opt, buck, dev, hip_graph=os.environ.get("HSD_MGPU_GRAPH", "0") == "1")
+    tr.zero_grad_in_optimizer = False  # the first step's reduced gradient is read back after the step
     if world > 1:
         broadcast_parameters(store, opt)
     g = torch.Generator().manual_seed(1234)

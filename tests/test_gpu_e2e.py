@@ -174,8 +174,10 @@ def test_optimizer_clears_the_gradients_it_consumed(gpu, monkeypatch, overlap):
     monkeypatch.setenv("HSD_OPT_OVERLAP", overlap)
     losses = {}
     for zero_in_opt in (True, False):
+        # a small learning rate: at 1e-4 this tiny-batch run is unstable (loss 0.8 -> 2.8 in a step) and run-to-run
+        # atomics noise grows to 2e-3 within 4 steps with or without the zeroing
         args, _ = build_parser("train").parse_known_args(
-            ["--model_name_or_path", "bert-base-uncased", "--train_batch_size", "8", "--learning_rate", "1e-4",
+            ["--model_name_or_path", "bert-base-uncased", "--train_batch_size", "8", "--learning_rate", "2e-5",
              "--dtype", "bf16", "--log_every", "0", "--hip_graph", "false", "--seed", "3",
              "--gradient_accumulation_steps", "2"])
         parts = build(args, "train")
@@ -190,6 +192,7 @@ def test_optimizer_clears_the_gradients_it_consumed(gpu, monkeypatch, overlap):
                 assert tr._grads_clear and int(torch.count_nonzero(st.grad)) == 0
         losses[zero_in_opt] = out
     a, b = losses[True], losses[False]
+    assert a[0] == b[0]
     for x, y in zip(a, b):
         assert abs(x - y) <= 2e-3 * max(1.0, abs(y)), (a, b)
 
