@@ -850,11 +850,16 @@ def _wgrad8_ok(dyq, xq, N, K, T) -> bool:
             and _C.gemm8_wgrad_supported(N, K, T))
 
 
+# token splits of the fp8 weight gradient (0: the kernel's cost model, which assumes the whole GPU; A/B switch)
+_WGRAD8_SPLITS = 0
+
+
 def _wgrad8(buf, dyq, xq, N, K, T, stream=None) -> None:
     """buf[N, K] += dequant(dyq)ᵀ · dequant(xq) on ``stream`` (None: the current stream)."""
-    ws = _workspace(_C.gemm8_wgrad_ws_numel(N, K, T, 0), buf.device, stream)
+    sp = _WGRAD8_SPLITS
+    ws = _workspace(_C.gemm8_wgrad_ws_numel(N, K, T, sp), buf.device, stream)
     _C.gemm8_wgrad(stream.cuda_stream if stream is not None else 0, dyq[0], _FP8["grad_fmt"], dyq[1], xq[0],
-                   FP8_E4M3, xq[1], buf, 0, ws)
+                   FP8_E4M3, xq[1], buf, sp, ws)
     WGRAD8_CALLS[0] += 1
 
 
