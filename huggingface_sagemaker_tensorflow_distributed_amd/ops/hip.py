@@ -850,13 +850,17 @@ def _wgrad8_ok(dyq, xq, N, K, T) -> bool:
             and _C.gemm8_wgrad_supported(N, K, T))
 
 
-# token splits of the fp8 weight gradient (0: the kernel's cost model, which assumes the whole GPU; A/B switch)
-_WGRAD8_SPLITS = 0
+# Side-stream fp8 weight gradients take 2 token splits instead of the kernel's cost model, which plans for a GPU of its
+# own (4-16 splits at roberta-large T = 32,768: every CU busy, one fp32 M x N slab written and re-read per split). The
+# side stream shares the GPU with the dgrad chain: roberta-large MLM fp8 +3.1 % (1,101-1,107 vs 1,068-1,072 seq/s; 3
+# splits, and the model's count halved, in between; 1 split -11 %). The bf16 TT kernel is the opposite: the headline is
+# 7 % slower at half its model's splits (profiles/r6/fp8_wgrad_splits_ab_r6.log, wgrad_splits_side_stream_ab_r6.log).
+_WGRAD8_SIDE_SPLITS = 2
 
 
 def _wgrad8(buf, dyq, xq, N, K, T, stream=None) -> None:
     """buf[N, K] += dequant(dyq)ᵀ · dequant(xq) on ``stream`` (None: the current stream)."""
-    sp = _WGRAD8_SPLITS
+    sp = _WGRAD8_SIDE_SPLITS if stream is not None and T >= 2 * 128 * _WGRAD8_SIDE_SPLITS else 0
     ws = _workspace(_C.gemm8_wgrad_ws_numel(N, K, T, sp), buf.device, stream)
     _C.gemm8_wgrad(stream.cuda_stream if stream is not None else 0, dyq[0], _FP8["grad_fmt"], dyq[1], xq[0],
                    FP8_E4M3, xq[1], buf, sp, ws)
