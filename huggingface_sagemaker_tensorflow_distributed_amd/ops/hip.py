@@ -125,6 +125,25 @@ def stream_wait(dst, src) -> None:
                    src.cuda_stream if hasattr(src, "cuda_stream") else int(src or 0))
 
 
+# A/B: > 0 = the side stream may use only this fraction of the CUs (0.5 / 0.75), so the compute stream's memory-bound
+# kernels and persistent GEMMs always find CUs without a weight-gradient workgroup on them
+_SIDE_CU_FRACTION = 0.0
+
+
+def _cu_mask_words(n_cu: int, frac: float):
+    """CU-mask words selecting ``frac`` of ``n_cu`` CUs: in every 16 consecutive CU ids the first 16·frac, so each
+    block of 32 ids (one XCD if ids are XCD-major) and each residue mod 8 (one XCD if ids interleave) get their share."""
+    keep = int(round(16 * frac))
+    words = []
+    for w in range((n_cu + 31) // 32):
+        v = 0
+        for b in range(32):
+            if (w * 32 + b) < n_cu and (b % 16) < keep:
+                v |= 1 << b
+        words.append(v)
+    return words
+
+
 def side_stream(device) -> Optional[torch.cuda.Stream]:
     """The device's wgrad side stream (created on first use), or None when HSD_WGRAD_STREAM=0."""
     if _WGRAD_MODE in ("0", "off", "false"):
@@ -132,7 +151,12 @@ def side_stream(device) -> Optional[torch.cuda.Stream]:
     key = device.index if device.index is not None else torch.cuda.current_device()
     s = _SIDE.get(key)
     if s is None:
-        s = torch.cuda.Stream(device=key)
+        if 0.0 < _SIDE_CU_FRACTION < 1.0:
+            n_cu = torch.cuda.get_device_properties(key).multi_processor_count
+            ptr = _C.cu_masked_stream(key, _cu_mask_words(n_cu, _SIDE_CU_FRACTION))
+            s = torch.cuda.ExternalStream(ptr, device=torch.device("cuda", key))
+        else:
+            s = torch.cuda.Stream(device=key)
         _SIDE[key] = s
     return s
 
@@ -855,6 +879,8 @@ def _wgrad8_ok(dyq, xq, N, K, T) -> bool:
 # side stream shares the GPU with the dgrad chain: roberta-large MLM fp8 +3.1 % (1,101-1,107 vs 1,068-1,072 seq/s; 3
 # splits, and the model's count halved, in between; 1 split -11 %). The bf16 TT kernel is the opposite: the headline is
 # 7 % slower at half its model's splits (profiles/r6/fp8_wgrad_splits_ab_r6.log, wgrad_splits_side_stream_ab_r6.log).
+# (Splits for ~64 / 128 / 192 workgroups per GEMM instead of a fixed 2: -3 % / within noise / -1 %,
+# profiles/r6/fp8_wgrad_side_wgs_ab_r6.log.)
 _WGRAD8_SIDE_SPLITS = 2
 
 
