@@ -125,25 +125,6 @@ def stream_wait(dst, src) -> None:
                    src.cuda_stream if hasattr(src, "cuda_stream") else int(src or 0))
 
 
-# A/B: > 0 = the side stream may use only this fraction of the CUs (0.5 / 0.75), so the compute stream's memory-bound
-# kernels and persistent GEMMs always find CUs without a weight-gradient workgroup on them
-_SIDE_CU_FRACTION = 0.0
-
-
-def _cu_mask_words(n_cu: int, frac: float):
-    """CU-mask words selecting ``frac`` of ``n_cu`` CUs: in every 16 consecutive CU ids the first 16·frac, so each
-    block of 32 ids (one XCD if ids are XCD-major) and each residue mod 8 (one XCD if ids interleave) get their share."""
-    keep = int(round(16 * frac))
-    words = []
-    for w in range((n_cu + 31) // 32):
-        v = 0
-        for b in range(32):
-            if (w * 32 + b) < n_cu and (b % 16) < keep:
-                v |= 1 << b
-        words.append(v)
-    return words
-
-
 def side_stream(device) -> Optional[torch.cuda.Stream]:
     """The device's wgrad side stream (created on first use), or None when HSD_WGRAD_STREAM=0."""
     if _WGRAD_MODE in ("0", "off", "false"):
@@ -151,12 +132,9 @@ def side_stream(device) -> Optional[torch.cuda.Stream]:
     key = device.index if device.index is not None else torch.cuda.current_device()
     s = _SIDE.get(key)
     if s is None:
-        if 0.0 < _SIDE_CU_FRACTION < 1.0:
-            n_cu = torch.cuda.get_device_properties(key).multi_processor_count
-            ptr = _C.cu_masked_stream(key, _cu_mask_words(n_cu, _SIDE_CU_FRACTION))
-            s = torch.cuda.ExternalStream(ptr, device=torch.device("cuda", key))
-        else:
-            s = torch.cuda.Stream(device=key)
+        # (a CU-masked side stream -- hipExtStreamCreateWithCUMask, half or 3/4 of the CUs, so the compute stream always
+        # finds CUs free of weight-gradient workgroups -- measured 18-47 % slower: profiles/r6/side_stream_cu_mask_rejected_r6.log)
+        s = torch.cuda.Stream(device=key)
         _SIDE[key] = s
     return s
 
