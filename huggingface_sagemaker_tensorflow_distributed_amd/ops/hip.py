@@ -132,8 +132,9 @@ def side_stream(device) -> Optional[torch.cuda.Stream]:
     key = device.index if device.index is not None else torch.cuda.current_device()
     s = _SIDE.get(key)
     if s is None:
-        # (a CU-masked side stream -- hipExtStreamCreateWithCUMask, half or 3/4 of the CUs, so the compute stream always
-        # finds CUs free of weight-gradient workgroups -- measured 18-47 % slower: profiles/r6/side_stream_cu_mask_rejected_r6.log)
+        # (a CU-masked side stream -- hipExtStreamCreateWithCUMask, half or 3/4 of the CUs, so the compute stream
+        # always finds CUs free of weight-gradient workgroups -- measured 18-47 % slower:
+        # profiles/r6/side_stream_cu_mask_rejected_r6.log)
         s = torch.cuda.Stream(device=key)
         _SIDE[key] = s
     return s
