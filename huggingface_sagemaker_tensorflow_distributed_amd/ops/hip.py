@@ -208,6 +208,8 @@ def _launch_wgrad(s, g: "_Grad", dy, x, dyq, xq):
     if g.buf is g.mg and _C.gemm2_supported(1, 1, 7, N, K, T):
         # the common case without any Python stream plumbing: TT GEMM (+ split-K reduce) launched on the side stream
         sp = _C.gemm2_splits(N, K, T)
+        # (fp32 atomics per K-split instead of slabs + one reduce pass: headline -5.7 %, bert-large B = 64 -13.5 %,
+        # profiles/r6/wgrad_atomic_rejected_r6.log)
         _C.gemm2_on(s.cuda_stream, dy, x, g.buf, 1, 1, 7, None, None, None, 0.0, 0, sp,
                     _workspace(sp * N * K, dy.device, s), None)
         return None
