@@ -33,6 +33,9 @@ from ..parallel.flat_params import ALIGN, FlatParamStore
 
 
 class FusedAdam:
+    # overlapped steps re-quantise each slice's fp8 weights right after its update (False: one pass at the end; A/B)
+    per_slice_fp8 = True
+
     def __init__(self, store: FlatParamStore, lr: float = 1e-3, betas=(0.9, 0.999), eps: Optional[float] = None,
                  weight_decay: float = 0.0, eps_mode: str = "keras", decoupled: bool = True):
         if eps_mode not in ("keras", "torch"):
@@ -123,6 +126,9 @@ class FusedAdam:
         # each slice's Wᵀ copies are refreshed right after its update (fp8 weight copies, which need the whole
         # step's amax, are still re-quantised once at the end)
         self._tsub = self.store.transposed_subsets(self._ranges) if self.store.master.is_cuda else None
+        # ... and each slice's fp8 weight copies right after that (fp8 runs): the per-weight amax / quantise passes
+        # leave the end of the step, where they ran alone (~0.5 ms per roberta-large step)
+        self._f8sub = self.store.fp8_subsets(self._ranges) if self._tsub is not None and self.per_slice_fp8 else None
         if on_ready is not None:
             self.store.ready_callback = on_ready
 
@@ -165,6 +171,8 @@ class FusedAdam:
                       zero_grad=getattr(self, "_zero", False))
         if self._tsub is not None:
             s.refresh_transposed_subset(self._tsub[b])
+        if self._f8sub is not None:
+            s.refresh_fp8_subset(self._f8sub[b])
         self._done[b] = True
 
     @torch.no_grad()
@@ -180,6 +188,8 @@ class FusedAdam:
         self._zero = False
         if self._tsub is None:
             self.store.refresh_transposed()
+        elif self._f8sub is not None:
+            self.store.finish_fp8_step()
         else:
             self.store.refresh_fp8()
 

@@ -248,13 +248,73 @@ class FlatParamStore:
         from ..ops import hip
 
         ad, ab, qd, qb = self._fp8_desc
+        self._roll_fp8_act()
+        self.fp8_amax.zero_()
+        hip._C.fp8_quant_many(ad, ab, qd, qb, self.fp8_amax, self.fp8_sinv, 0)
+        # the slots are left zero (stream-ordered after the quantise pass read them): per-slice passes
+        # (refresh_fp8_subset) accumulate into them next
+        self.fp8_amax.zero_()
+
+    def _roll_fp8_act(self) -> None:
         # roll the activation amax history: next step scales with this step's amax (sites not used this
         # step keep their previous value)
         prev, cur = self.fp8_act[..., 0], self.fp8_act[..., 1]
         prev.copy_(torch.where(cur > 0, cur, prev))
         cur.zero_()
-        self.fp8_amax.zero_()
+
+    def fp8_subsets(self, ranges) -> list:
+        """Per flat-buffer slice ``[start, end)``: the fp8 amax / quantise descriptor tables of the fp8 weights inside
+        it (or ``None``), so an optimizer that steps slices separately re-quantises each slice's weights (W8 and W8ᵀ,
+        after the slice's Wᵀ refresh) right after its update, under the backward, instead of in one pass over every
+        weight at the end of the step (:meth:`refresh_fp8_subset`, :meth:`finish_fp8_step`)."""
+        if self._fp8_desc is None:
+            return [None] * len(ranges)
+        from ..ops import hip
+
+        per_block = hip._C.fp8_elems_per_block()
+        ad, _ab, qd, _qb = self._fp8_desc
+        arows, qrows = ad.cpu().tolist(), qd.cpu().tolist()
+        base = self.compute.data_ptr()
+        esize = self.compute.element_size()
+        out = []
+        for st, e in ranges:
+            a_sub, q_sub, ab, qb = [], [], 0, 0
+            for t, (src, dst, n, slot, _b) in enumerate(arows):
+                off = (src - base) // esize
+                if not (st <= off < e):
+                    continue
+                nb = (n + per_block - 1) // per_block
+                a_sub.append([src, dst, n, slot, ab])
+                ab += nb
+                for qr in qrows[2 * t:2 * t + 2]:
+                    q_sub.append([qr[0], qr[1], qr[2], qr[3], qb])
+                    qb += nb
+            if a_sub:
+                out.append((torch.tensor(a_sub, dtype=torch.int64, device=self.device), ab,
+                            torch.tensor(q_sub, dtype=torch.int64, device=self.device), qb))
+            else:
+                out.append(None)
+        return out
+
+    @torch.no_grad()
+    def refresh_fp8_subset(self, sub) -> None:
+        """Re-quantise one slice's fp8 weights (a :meth:`fp8_subsets` entry) on the current stream; their amax slots
+        were zeroed by the previous :meth:`finish_fp8_step` (or the store's construction)."""
+        if sub is None:
+            return
+        from ..ops import hip
+
+        ad, ab, qd, qb = sub
         hip._C.fp8_quant_many(ad, ab, qd, qb, self.fp8_amax, self.fp8_sinv, 0)
+
+    @torch.no_grad()
+    def finish_fp8_step(self) -> None:
+        """End of a step whose slices re-quantised their own fp8 weights: roll the activation amax history and zero
+        the weight amax slots for the next step's per-slice passes."""
+        if self._fp8_desc is None:
+            return
+        self._roll_fp8_act()
+        self.fp8_amax.zero_()
 
     def transposed_subsets(self, ranges) -> list:
         """Per flat-buffer slice ``[start, end)``: the batched-transpose descriptor table of the weights inside it

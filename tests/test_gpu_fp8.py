@@ -664,3 +664,39 @@ def test_gemm8_row_dot_epilogue(gpu, B_, S, heads, K, fa):
         outs.append((ws, dqkv, gq))
     assert torch.equal(outs[0][0], rd)
     assert torch.equal(outs[0][1], outs[1][1]) and torch.equal(outs[0][2], outs[1][2])
+
+
+def test_fp8_weight_copies_requantised_per_slice_match_one_pass(gpu, monkeypatch):
+    """Overlapped optimizer slices re-quantise their own fp8 weights (W8, W8ᵀ, scale) right after each update
+    (FlatParamStore.fp8_subsets / refresh_fp8_subset): after every step the copies equal one refresh_fp8 pass over all
+    weights from the same bf16 copies, bit for bit."""
+    from huggingface_sagemaker_tensorflow_distributed_amd import data as hdata
+    from huggingface_sagemaker_tensorflow_distributed_amd.models import build_model, resolve_config
+    from huggingface_sagemaker_tensorflow_distributed_amd.optim import FusedAdam
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel import FlatParamStore
+    from huggingface_sagemaker_tensorflow_distributed_amd.train.trainer import Trainer
+
+    hip = _hip()
+    monkeypatch.setenv("HSD_OPT_BUCKET_MB", "4")
+    cfg = resolve_config("roberta-large").replace(num_hidden_layers=2)
+    ds = hdata.synthetic_mlm(8, 256, cfg.vocab_size, seed=5)
+    batch = {"input_ids": torch.from_numpy(ds.input_ids).long().to(gpu),
+             "attention_mask": torch.from_numpy(ds.attention_mask).long().to(gpu),
+             "labels": torch.from_numpy(ds.labels).long().to(gpu)}
+    m = build_model(cfg, task="masked-lm", seed=0).to(gpu)
+    hip.set_fp8(True)
+    try:
+        store = FlatParamStore(m, gpu, compute_dtype=torch.bfloat16, fp8=True)
+        opt = FusedAdam(store, lr=1e-4)
+        tr = Trainer(m, store, opt, None, gpu)
+        assert opt._f8sub is not None and sum(x is not None for x in opt._f8sub) >= 2
+        for _ in range(3):
+            tr.train_step([batch])
+            torch.cuda.synchronize()
+            q, qt, si = store.fp8_w.clone(), store.fp8_wt.clone(), store.fp8_sinv.clone()
+            store.refresh_fp8()
+            torch.cuda.synchronize()
+            assert torch.equal(q, store.fp8_w) and torch.equal(qt, store.fp8_wt) and torch.equal(si, store.fp8_sinv)
+            assert int(torch.count_nonzero(store.fp8_amax)) == 0
+    finally:
+        hip.set_fp8(False)
