@@ -146,6 +146,48 @@ def test_optimizer_overlap_on_engine_stream(gpu, monkeypatch):
         assert torch.equal(out, store.compute)
 
 
+def test_engine_optimizer_slices_clear_gradients(gpu, monkeypatch):
+    """DP form of the gradient zeroing: the engine-stream Adam slices clear every gradient they consumed, so after each
+    step the whole buffer is zero and the next step skips its memset; the losses track the same steps with a memset
+    per step (world-of-one communicator; not bitwise: fp32 atomics in the backward)."""
+    from huggingface_sagemaker_tensorflow_distributed_amd import data as hdata
+    from huggingface_sagemaker_tensorflow_distributed_amd.parallel import GradBucketer
+    from huggingface_sagemaker_tensorflow_distributed_amd.train.runner import build
+    from huggingface_sagemaker_tensorflow_distributed_amd.train.trainer import Trainer
+    from huggingface_sagemaker_tensorflow_distributed_amd.utils.args import build_parser
+
+    monkeypatch.setenv("HSD_OPT_OVERLAP", "1")
+    ds = hdata.synthetic_classification(16, 128, 30522, seed=0)
+    batches = [{k: torch.from_numpy(v[8 * i:8 * (i + 1)]).long().to(gpu) for k, v in
+                (("input_ids", ds.input_ids), ("attention_mask", ds.attention_mask), ("labels", ds.labels))}
+               for i in range(2)]
+    C = _C()
+    losses = {}
+    for zero_in_opt in (True, False):
+        args, _ = build_parser("train").parse_known_args(
+            ["--model_name_or_path", "bert-base-uncased", "--train_batch_size", "8", "--dtype", "bf16",
+             "--learning_rate", "2e-5", "--log_every", "0", "--hip_graph", "false", "--seed", "3"])
+        parts = build(args, "train")
+        model, store, opt = parts["model"], parts["store"], parts["optimizer"]
+        eng = C.CommEngine(0, 1, C.CommEngine.unique_id(), gpu.index, True)
+        buck = GradBucketer(store, bucket_mb=4, engine=eng)
+        tr = Trainer(model, store, opt, buck, gpu)
+        tr.zero_grad_in_optimizer = zero_in_opt
+        assert tr._opt_overlap == "engine"
+        out = []
+        for step in range(3):
+            out.append(float(tr.train_step([batches[step % 2]])))
+            torch.cuda.synchronize()
+            if zero_in_opt:
+                assert tr._grads_clear and int(torch.count_nonzero(store.grad)) == 0
+        losses[zero_in_opt] = out
+        buck.detach()
+    a, b = losses[True], losses[False]
+    assert a[0] == b[0]
+    for x, y in zip(a, b):
+        assert abs(x - y) <= 2e-3 * max(1.0, abs(y)), (a, b)
+
+
 @pytest.mark.parametrize("mode,dtype", [(1, torch.bfloat16), (2, torch.float16)])
 def test_comm_engine_wire_compression(gpu, mode, dtype):
     """set_compression (Horovod's hvd.Compression.fp16): each fp32 bucket is cast to 16 bits on the comm stream,
