@@ -1491,12 +1491,15 @@ static WgradPlan wgrad_plan(int M, int N, int K) {
   const bool can_small = N % SBN_HOST == 0 && M % 8 == 0 && K % 64 == 0 && force != 0;
   const bool can_big = N % 256 == 0 && force != 1;
   // small steps (<= 8,192 tokens), whose weight gradients run on the side stream under the backward: the fewest K-splits
-  // of the 128 x 128 kernel that still give 192 workgroups, so a weight gradient takes no more CUs and slab traffic
+  // of the 128 x 128 kernel that still give 384 workgroups, so a weight gradient takes no more CUs and slab traffic
   // than it needs beside the critical path (the latency cost model below minimises its own time instead). Measured
-  // (profiles/wgrad_min_grid_ab_r4.log): bert-large S=512 B=8 504-505 -> 524-526 seq/s, bert-base B=64 +1.8 %.
+  // (profiles/wgrad_min_grid_ab_r4.log): bert-large S=512 B=8 504-505 -> 524-526 seq/s, bert-base B=64 +1.8 % at a
+  // 192-workgroup target; re-swept in round 6 with the optimizer slices behind the weight-gradient forks
+  // (profiles/r6/bl8_knob_sweep_r6.log, profiles/r6/wgrad_min_grid_small_steps_r6.log): 384 is +1.2-1.4 % at
+  // bert-large B = 8 (552.6-554.2 vs 546.4-547.7) and ahead at bert-base B = 32 too; 256, 512 and 768 are 2 % slower.
   // HSD_WGRAD_MIN_GRID sets the workgroup target (0 = the cost model at every size).
   const int grid_knob = HSD_KNOB("HSD_WGRAD_MIN_GRID", kKnobUnset);
-  const int min_grid = grid_knob != kKnobUnset ? grid_knob : (K <= 8192 ? 192 : 0);
+  const int min_grid = grid_knob != kKnobUnset ? grid_knob : (K <= 8192 ? 384 : 0);
   if (min_grid > 0 && can_small) {
     const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
     int sp = 1;
