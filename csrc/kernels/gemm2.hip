@@ -1497,9 +1497,10 @@ static WgradPlan wgrad_plan(int M, int N, int K) {
   // 192-workgroup target; re-swept in round 6 with the optimizer slices behind the weight-gradient forks
   // (profiles/r6/bl8_knob_sweep_r6.log, profiles/r6/wgrad_min_grid_small_steps_r6.log): 384 is +1.2-1.4 % at
   // bert-large B = 8 (552.6-554.2 vs 546.4-547.7) and ahead at bert-base B = 32 too; 256, 512 and 768 are 2 % slower.
+  // Both are 4,096-token steps: below that (the graph-replayed small batches) the measured 192 stays.
   // HSD_WGRAD_MIN_GRID sets the workgroup target (0 = the cost model at every size).
   const int grid_knob = HSD_KNOB("HSD_WGRAD_MIN_GRID", kKnobUnset);
-  const int min_grid = grid_knob != kKnobUnset ? grid_knob : (K <= 8192 ? 384 : 0);
+  const int min_grid = grid_knob != kKnobUnset ? grid_knob : (K <= 8192 ? (K >= 4096 ? 384 : 192) : 0);
   if (min_grid > 0 && can_small) {
     const int tiles = ((M + 127) / 128) * ((N + 127) / 128);
     int sp = 1;
