@@ -162,10 +162,13 @@ def test_gemm_nt_split_policy(monkeypatch):
     monkeypatch.delenv("HSD_G2_SMALL")
     assert C.gemm2_splits(2304, 768, 131072) == 9        # headline wgrads: 256^2 tiles, one wave of 256 CUs
     assert C.gemm2_splits(768, 768, 131072) == 28
-    # small steps (<= 8,192 tokens): the fewest 128^2 K-splits giving 192 workgroups
-    assert C.gemm2_splits(1024, 1024, 4096) == 3
-    assert C.gemm2_splits(3072, 1024, 4096) == 1         # 192 tiles: one split, accumulated in place
-    assert C.gemm2_splits(2304, 768, 8192) == 2          # 108 tiles -> 216 workgroups
+    # small steps (4,096-8,192 tokens): the fewest 128^2 K-splits giving 384 workgroups (profiles/r6/
+    # wgrad_min_grid_small_steps_r6.log); below 4,096 tokens 192
+    assert C.gemm2_splits(1024, 1024, 4096) == 6
+    assert C.gemm2_splits(3072, 1024, 4096) == 2         # 192 tiles -> 384 workgroups
+    assert C.gemm2_splits(2304, 768, 8192) == 4          # 108 tiles -> 432 workgroups
+    assert C.gemm2_splits(1024, 1024, 2048) == 3         # 64 tiles -> 192 workgroups
+    assert C.gemm2_splits(3072, 1024, 2048) == 1         # 192 tiles: one split, accumulated in place
     monkeypatch.setenv("HSD_WGRAD_MIN_GRID", "0")        # the latency cost model at every size
     assert C.gemm2_splits(1024, 1024, 4096) == 4         # 128^2 tiles x 4 splits (256^2 would need 13+)
 
